@@ -1,0 +1,195 @@
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE implementation.
+
+Runs only in the build container (it imports /root/reference, which does not exist on the GPU
+box).  Inputs and weights are regenerated from the portable counter hash in ``s2v_amd.synth``,
+so only outputs (full tensors for small cases, fixed-index probes for large ones) are stored.
+
+Import shims (neither touches arithmetic; both documented in SURVEY.md §8c):
+  * ``torchsummary`` is imported but unused by models/__init__.py:6 -> empty stub module;
+  * ``basicsr.archs.arch_util.default_init_weights`` (models/base_blocks.py:9) -> the reference's
+    own vendored copy third_part/GPEN/sr_model/arch_util.py (only used for init, which the
+    synthetic state_dict overwrites).
+
+Usage:  python tests/golden/make_golden.py [--only lnet,enet,dnet,ops]
+"""
+import argparse
+import importlib.util
+import json
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, REPO)
+import s2v_import  # noqa: E402,F401
+from s2v_amd import synth  # noqa: E402
+from s2v_amd.models import arch  # noqa: E402
+
+
+def _install_ref_shims():
+    ts = types.ModuleType("torchsummary")
+    ts.summary = lambda *a, **k: None
+    sys.modules.setdefault("torchsummary", ts)
+    spec = importlib.util.spec_from_file_location(
+        "_ref_arch_util", os.path.join(REF, "third_part/GPEN/sr_model/arch_util.py"))
+    au = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(au)
+    for name in ("basicsr", "basicsr.archs"):
+        sys.modules.setdefault(name, types.ModuleType(name))
+    sys.modules["basicsr.archs.arch_util"] = au
+    sys.modules["basicsr"].archs = sys.modules["basicsr.archs"]
+    sys.modules["basicsr.archs"].arch_util = au
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+
+
+def _manifest(module):
+    return {k: list(v.shape) for k, v in module.state_dict().items()}
+
+
+def _check_keys(name, ref_mod, mine):
+    a, b = _manifest(ref_mod), _manifest(mine)
+    if a != b:
+        missing = sorted(set(a) - set(b))[:10]
+        extra = sorted(set(b) - set(a))[:10]
+        diff = [k for k in a if k in b and a[k] != b[k]][:10]
+        raise SystemExit(f"{name}: state_dict layout mismatch missing={missing} extra={extra} shape={diff}")
+    with open(os.path.join(HERE, f"{name}_keys.json"), "w") as f:
+        json.dump(a, f, indent=0, sort_keys=True)
+    print(f"{name}: {len(a)} state_dict entries match the reference layout")
+
+
+def _load_synth(ref_mod):
+    sd = synth.synth_torch_state_dict(ref_mod)
+    missing, unexpected = ref_mod.load_state_dict(sd, strict=True), None
+    return sd
+
+
+def _probe(t: torch.Tensor, key: str):
+    flat = t.detach().reshape(-1).double().numpy()
+    idx = synth.probe_indices(flat.size, 4096, key)
+    return {"idx": idx, "val": flat[idx].astype(np.float32),
+            "stats": np.array([flat.mean(), flat.std(), np.abs(flat).max(), flat.size], dtype=np.float64)}
+
+
+def _save(name, arrays):
+    path = os.path.join(HERE, f"{name}.npz")
+    np.savez_compressed(path, **arrays)
+    print(f"wrote {path} ({os.path.getsize(path) / 1e6:.2f} MB)")
+
+
+def gen_lnet():
+    from models.LNet import LNet
+    ref = LNet().eval()
+    _check_keys("lnet", ref, arch.LNetParams())
+    _load_synth(ref)
+    acts = {}
+    hooks = [
+        ref.audio_encoder.register_forward_hook(lambda m, i, o: acts.__setitem__("audio_feat", o)),
+        ref.decoder.final.model[0].register_forward_hook(lambda m, i, o: acts.__setitem__("logits", o)),
+        ref.encoder.register_forward_hook(lambda m, i, o: acts.__setitem__("enc", [t.clone() for t in o])),
+        ref.decoder.res2.register_forward_hook(lambda m, i, o: acts.__setitem__("res2", o)),
+    ]
+    mel, face, _ = synth.lipsync_inputs("golden.lnet", 2, 96)
+    with torch.no_grad():
+        out = ref(torch.from_numpy(mel), torch.from_numpy(face))
+    for h in hooks:
+        h.remove()
+    arrays = {"out": out.numpy(), "logits": acts["logits"].numpy(),
+              "audio_feat": acts["audio_feat"].reshape(2, -1).numpy()}
+    for i, t in enumerate(acts["enc"]):
+        p = _probe(t, f"lnet.enc{i}")
+        arrays.update({f"enc{i}_idx": p["idx"], f"enc{i}_val": p["val"], f"enc{i}_stats": p["stats"]})
+    p = _probe(acts["res2"], "lnet.res2")
+    arrays.update({"res2_idx": p["idx"], "res2_val": p["val"], "res2_stats": p["stats"]})
+    _save("lnet_b2_96", arrays)
+
+
+def gen_enet():
+    from models.LNet import LNet
+    from models.ENet import ENet
+    ref = ENet(lnet=LNet()).eval()
+    _check_keys("enet", ref, arch.ENetParams(lnet=arch.LNetParams()))
+    _load_synth(ref)
+    acts = {}
+    ref.final_linear.register_forward_hook(lambda m, i, o: acts.__setitem__("style", o))
+    for size, full in ((256, True), (384, False)):
+        mel, face, gt = synth.lipsync_inputs(f"golden.enet{size}", 1, size)
+        with torch.no_grad():
+            out, low = ref(torch.from_numpy(mel), torch.from_numpy(face), torch.from_numpy(gt))
+        arrays = {"low": low.numpy(), "style": acts["style"].numpy()}
+        if full:
+            arrays["out"] = out.numpy()
+        else:
+            p = _probe(out, "enet.out")
+            arrays.update({"out_idx": p["idx"], "out_val": p["val"], "out_stats": p["stats"]})
+        _save(f"enet_b1_{size}", arrays)
+
+
+def gen_dnet():
+    from models.DNet import DNet
+    ref = DNet().eval()
+    _check_keys("dnet", ref, arch.DNetParams())
+    _load_synth(ref)
+    acts = {}
+    ref.mapping_net.register_forward_hook(lambda m, i, o: acts.__setitem__("descriptor", o))
+    for size, batch, full in ((128, 2, True), (256, 1, False)):
+        src, coeff = synth.dnet_inputs(f"golden.dnet{size}", batch, size)
+        with torch.no_grad():
+            out = ref(torch.from_numpy(src), torch.from_numpy(coeff))
+        arrays = {"descriptor": acts["descriptor"].reshape(batch, -1).numpy(),
+                  "flow": out["flow_field"].numpy()}
+        for k in ("warp_image", "fake_image"):
+            if full:
+                arrays[k] = out[k].numpy()
+            else:
+                p = _probe(out[k], f"dnet.{k}")
+                arrays.update({f"{k}_idx": p["idx"], f"{k}_val": p["val"], f"{k}_stats": p["stats"]})
+        _save(f"dnet_b{batch}_{size}", arrays)
+
+
+def gen_ops():
+    """GPEN native-op CPU fallbacks (op/fused_act.py:92-96, op/upfirdn2d.py:149-193) and the
+    flow_util warp (futils/flow_util.py:3-56) on small shapes."""
+    sys.path.insert(0, os.path.join(REF, "third_part/GPEN/face_model"))
+    from op.fused_act import fused_leaky_relu
+    from op.upfirdn2d import upfirdn2d
+    from futils import flow_util
+    arrays = {}
+    x = torch.from_numpy(synth.hash_array("golden.fba.x", (2, 8, 5, 7)))
+    b = torch.from_numpy(synth.hash_array("golden.fba.b", (8,)))
+    arrays["fba_out"] = fused_leaky_relu(x, b, 0.2, 2 ** 0.5).numpy()
+    x2 = torch.from_numpy(synth.hash_array("golden.fba.x2", (3, 16)))
+    b2 = torch.from_numpy(synth.hash_array("golden.fba.b2", (16,)))
+    arrays["fba2_out"] = fused_leaky_relu(x2, b2, 0.2, 2 ** 0.5).numpy()
+    k = torch.tensor([1.0, 3.0, 3.0, 1.0])
+    k = k[None, :] * k[:, None]
+    k = k / k.sum()
+    xi = torch.from_numpy(synth.hash_array("golden.ufd.x", (2, 3, 9, 11)))
+    for name, (up, down, pad) in {"up2": (2, 1, (2, 1)), "blur22": (1, 1, (2, 2)),
+                                  "blur11": (1, 1, (1, 1)), "down2": (1, 2, (1, 1))}.items():
+        arrays[f"ufd_{name}"] = upfirdn2d(xi, k * (4 if up == 2 else 1), up=up, down=down, pad=pad).numpy()
+    flow = torch.from_numpy(synth.hash_array("golden.flow", (2, 2, 16, 16), -3.0, 3.0))
+    src = torch.from_numpy(synth.hash_array("golden.flow.src", (2, 3, 64, 64)))
+    deform = flow_util.convert_flow_to_deformation(flow)
+    arrays["warp"] = flow_util.warp_image(src, deform).numpy()
+    flow_same = torch.from_numpy(synth.hash_array("golden.flow2", (1, 2, 32, 32), -2.0, 2.0))
+    src2 = torch.from_numpy(synth.hash_array("golden.flow2.src", (1, 3, 32, 32)))
+    arrays["warp_same"] = flow_util.warp_image(src2, flow_util.convert_flow_to_deformation(flow_same)).numpy()
+    _save("ops", arrays)
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="lnet,enet,dnet,ops")
+    args = ap.parse_args()
+    torch.set_num_threads(os.cpu_count() or 8)
+    _install_ref_shims()
+    os.chdir("/tmp")
+    for part in args.only.split(","):
+        globals()[f"gen_{part}"]()

@@ -1,0 +1,35 @@
+"""Shared test helpers: synthetic reference-layout state dicts and comparison utilities."""
+import functools
+
+import numpy as np
+import torch
+
+import s2v_import  # noqa: F401
+from s2v_amd import synth
+from s2v_amd.models import arch
+
+
+@functools.lru_cache(maxsize=None)
+def synth_sd(net: str):
+    """Synthetic state_dict (CPU tensors) in the reference layout for 'lnet'|'enet'|'dnet'."""
+    mod = {"lnet": lambda: arch.LNetParams(), "enet": lambda: arch.ENetParams(lnet=arch.LNetParams()),
+           "dnet": lambda: arch.DNetParams()}[net]()
+    return synth.synth_torch_state_dict(mod)
+
+
+def max_abs(a, b):
+    a = a.detach().cpu().double().numpy() if isinstance(a, torch.Tensor) else np.asarray(a, np.float64)
+    b = b.detach().cpu().double().numpy() if isinstance(b, torch.Tensor) else np.asarray(b, np.float64)
+    assert a.shape == b.shape, (a.shape, b.shape)
+    d = np.abs(a - b)
+    return float(d.max()), float(d.mean())
+
+
+def check_probe(t, g, name, atol, rtol=0.0):
+    flat = t.detach().cpu().reshape(-1).double().numpy()
+    idx, val = g[f"{name}_idx"], g[f"{name}_val"].astype(np.float64)
+    got = flat[idx]
+    err = np.abs(got - val)
+    lim = atol + rtol * np.abs(val)
+    assert (err <= lim).all(), f"{name}: max err {err.max():.3e} (limit {lim.max():.3e})"
+    return float(err.max())
