@@ -1,0 +1,196 @@
+/*
+ * s2v.h — C ABI of libs2v.so, the MI355X (gfx950) compute path for the per-frame lip-sync
+ * inference path of Ryukhaan/speech-to-video-mpp (VideoReTalking fork).
+ *
+ * Conventions (all entry points):
+ *   - every pointer is a device pointer (HBM) unless documented otherwise; fp32 data;
+ *   - activations are NHWC: element (n, y, x, c) of a view lives at
+ *     data[((n*H + y)*W + x)*cs + c]; ``cs`` (channel stride / pixel pitch) lets a view be a
+ *     channel slice of a wider tensor (this is how concat/split of the reference are fused away);
+ *   - work is enqueued on ``stream`` (a hipStream_t); nothing synchronises, nothing allocates,
+ *     so every call is hipGraph-capturable;
+ *   - return 0 on success, a negative S2V_E* code on invalid arguments (nothing launched) or a
+ *     launch failure; s2v_last_error() returns a message for the last failure on this thread.
+ *
+ * The reference's only native FFI on this path is GPEN's pybind11 ops (fused_bias_act,
+ * upfirdn2d); every other entry point replaces a PyTorch aten call sequence the reference's
+ * Python makes (file:line cited per function).
+ */
+#ifndef S2V_H_
+#define S2V_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void *s2v_stream_t; /* hipStream_t */
+
+enum {
+    S2V_OK = 0,
+    S2V_E_INVALID = -1, /* bad shape / stride / alignment / unsupported mode */
+    S2V_E_LAUNCH = -2,  /* hipGetLastError() after launch was not hipSuccess */
+    S2V_E_WORKSPACE = -3 /* workspace missing or too small */
+};
+
+/* activation codes (epilogues / prologues) */
+enum {
+    S2V_ACT_NONE = 0,
+    S2V_ACT_RELU = 1,
+    S2V_ACT_LRELU = 2,     /* x >= 0 ? x : alpha * x */
+    S2V_ACT_SIGMOID = 3,
+    S2V_ACT_TANH = 4,
+    S2V_ACT_GELU_TANH = 5  /* models/transformer.py:11-15 */
+};
+
+/* input addressing modes of the implicit-GEMM convolution */
+enum {
+    S2V_IN_DIRECT = 0,     /* ordinary (dilated, strided) conv                                */
+    S2V_IN_NEAREST_UP2 = 1,/* conv over nearest-x2-upsampled input (UpBlock2d, base_blocks.py:123) */
+    S2V_IN_TRANSPOSED = 2  /* ConvTranspose2d: out[o] += in[(o + pad - k*dil)/stride] (DNet decoder) */
+};
+
+enum { S2V_PAD_ZERO = 0, S2V_PAD_REFLECT = 1 };
+
+/*
+ * Fused convolution / GEMM (implicit GEMM on v_mfma_f32_32x32x2_f32, exact fp32).
+ *   out[n, oy, ox, o] = epilogue( sum_{ky,kx,c} A(n, oy, ox, ky, kx, c) * W[o][(ky*kw + kx)*cin + c] )
+ * A = prologue(x) addressed per ``in_mode`` / ``pad_mode``; prologue = act(x * in_scale[n, c]).
+ * Epilogue order:  v = acc * scale[o] * nc_scale[n, o] + shift[o] + pix_w * pix_add[n, oy, ox]
+ *                  (+ res if !res_after_act);  v = act(v);  (+ res if res_after_act).
+ * Weights are pre-packed [npad][kpad] (k = (ky*kw + kx)*cin + c, zero padded; npad % 128 == 0,
+ * kpad % 32 == 0) — or, with ``b_kn`` = 1, an unpacked row-major [K][N] matrix (ldb) for
+ * activation x activation GEMMs (the FourierUnit DFT products).
+ * ``batch`` > 1 repeats the problem with per-batch pointer offsets (elements).
+ */
+typedef struct s2v_conv_params {
+    /* input */
+    const float *x; int n, h, w, cin, xcs;
+    int in_mode; int pad_mode;
+    int pre_act; float pre_alpha;
+    const float *in_scale; int in_scale_ns;     /* [n][in_scale_ns], may be NULL */
+    /* filter */
+    int kh, kw, sh, sw, ph, pw, dh, dw;
+    const float *wt; int kpad, npad; int cout;  /* packed weights */
+    int b_kn; int ldb;                          /* b_kn: wt is [K][ldb] row-major, N = cout */
+    /* output */
+    float *y; int oh, ow, ycs;
+    /* epilogue */
+    const float *scale, *shift;                 /* [cout], may be NULL */
+    const float *nc_scale; int nc_scale_ns;     /* [n][nc_scale_ns], may be NULL */
+    const float *pix_add; float pix_w;          /* [n][oh][ow], may be NULL */
+    const float *res; int res_cs, res_h, res_w, res_oy, res_ox; int res_after_act; /* may be NULL */
+    int act; float alpha;
+    /* batching (GEMM mode) */
+    int batch; long long x_bs, w_bs, y_bs, res_bs;
+    /* split-K workspace (see s2v_conv2d_ws_bytes) */
+    float *ws; size_t ws_bytes;
+    int force_tile; int force_splits;           /* 0 = heuristic (tests use these) */
+} s2v_conv_params;
+
+/* Replaces the nn.Conv2d / ConvTranspose2d / Conv1d / Linear calls of models/LNet.py,
+ * ENet.py, DNet.py, base_blocks.py, ffc.py, transformer.py (inventory: SURVEY.md App. A). */
+int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream);
+size_t s2v_conv2d_ws_bytes(const s2v_conv_params *p);
+
+/* LayerNorm2d (base_blocks.py:52-69) over (H,W,C) per sample, fused affine + act
+ * (+ 2x2 average pool: DownBlock2d base_blocks.py:95-109) (+ residual after act: Jump + out,
+ * LNet.py:75).  ws: >= s2v_layernorm2d_ws_bytes(n, h, w, c) bytes. */
+int s2v_layernorm2d(const float *x, int n, int h, int w, int c, int xcs,
+                    const float *weight, const float *bias, float eps, int act, float alpha, int pool,
+                    const float *res, int res_cs, float *y, int ycs, void *ws, size_t ws_bytes,
+                    s2v_stream_t stream);
+size_t s2v_layernorm2d_ws_bytes(int n, int h, int w, int c);
+
+/* ADAIN apply (base_blocks.py:143-157): InstanceNorm2d(eps) * (1 + gamma[n,c]) + beta[n,c],
+ * then act, then + res.  gamma/beta rows have stride gb_ns per sample. */
+int s2v_instnorm_adain(const float *x, int n, int h, int w, int c, int xcs,
+                       const float *gamma, const float *beta, int gb_ns, float eps, int act, float alpha,
+                       const float *res, int res_cs, float *y, int ycs, void *ws, size_t ws_bytes,
+                       s2v_stream_t stream);
+size_t s2v_instnorm_ws_bytes(int n, int h, int w, int c);
+
+/* Segmented GEMV for all ADAIN gamma/beta heads at once (base_blocks.py:148-155):
+ *   out[b][o] = bias[o] + sum_j W2t[j][o] * hid[b][seg[o]*nhidden + j]
+ * W2t is [nhidden][total] (transposed so consecutive o are contiguous). */
+int s2v_adain_params(const float *hid, int batch, int hid_ns, int nhidden, const float *w2t,
+                     const float *bias, const int *seg, int total, float *out, int out_ns,
+                     s2v_stream_t stream);
+
+/* StyleGAN2 demodulation (base_blocks.py:492-494) without per-sample weights:
+ *   d[b][o] = rsqrt(sum_i s[b][i]^2 * wsq[o][i] + eps) * post */
+int s2v_modconv_demod(const float *s, int batch, int s_ns, int cin, const float *wsq, int cout,
+                      float eps, float post, float *d, int d_ns, s2v_stream_t stream);
+
+/* Bilinear resize (F.interpolate mode='bilinear', align_corners=False, no antialias) between
+ * arbitrary strided 4-D views; scale_h/scale_w as torch's area_pixel_compute_scale.
+ * Element (n,c,y,x) at base + n*sn + c*sc + y*sy + x*sx (strides in elements).
+ * mode 0 bilinear, 1 nearest (floor(dst*scale)). Output index order is (n, y, x, c). */
+int s2v_resize(const float *x, int n, int c, int ih, int iw, long long xsn, long long xsc, long long xsy,
+               long long xsx, float *y, int oh, int ow, long long ysn, long long ysc, long long ysy,
+               long long ysx, float scale_h, float scale_w, int mode, s2v_stream_t stream);
+
+/* F.pad(mode='reflect') on NHWC (ENet.py:119). */
+int s2v_pad_reflect(const float *x, int n, int h, int w, int c, int xcs, int pt, int pb, int pl, int pr,
+                    float *y, int ycs, s2v_stream_t stream);
+
+/* Row LayerNorm over the last dim (transformer.py:24-35 nn.LayerNorm). */
+int s2v_row_layernorm(const float *x, int rows, int dim, int xld, const float *weight, const float *bias,
+                      float eps, float *y, int yld, s2v_stream_t stream);
+
+/* Multi-head attention core (transformer.py:73-80): per (b, head):
+ *   O = softmax(Q K^T * scale) V; tokens <= 256, dim_head == 64. Q/K/V/O rows are tokens with
+ *   leading dims q_ld.. and per-batch strides; head h uses columns [h*64, h*64+64). */
+int s2v_attention(const float *q, const float *k, const float *v, int batch, int heads, int tokens,
+                  int dim_head, int ld_q, int ld_k, int ld_v, long long bs_q, long long bs_k, long long bs_v,
+                  float scale, float *o, int ld_o, long long bs_o, s2v_stream_t stream);
+
+/* DNet warp (flow_util.py:3-56) fused: flow [n][fh][fw][2] NHWC -> deformation grid
+ * (align_corners=True convention) -> bilinear resize to (h, w) -> grid_sample(bilinear, zeros,
+ * align_corners=False) of src (NCHW-strided view, c channels). Output NHWC slice. */
+int s2v_flow_warp(const float *flow, int n, int fh, int fw, int flow_cs, const float *src, int c, int h,
+                  int w, long long ssn, long long ssc, long long ssy, long long ssx, float *y, int ycs,
+                  s2v_stream_t stream);
+
+/* Mel spectrogram (futils/audio.py:45-51, :20-23, :57-61, :92-123 + hparams.py:21-61):
+ * preemphasis(0.97) -> STFT(n_fft 800, hop 200, periodic Hann, center=True, zero or reflect
+ * pad) -> |.| -> mel (80 x 401, Slaney) -> 20 log10(max(1e-5, .)) - 20 -> clip(8 (S+100)/100 - 4,
+ * -4, 4).  ``tables`` = mel basis [80][401] | cos(2 pi k/800) [800] | sin [800] | window [800]
+ * (the sin table carries the -i of the forward DFT only through |.|).  Output [80][frames],
+ * frames = 1 + n_samples / 200. */
+int s2v_melspectrogram(const float *wav, long long n_samples, const float *tables, int pad_reflect,
+                       float *out, long long frames, s2v_stream_t stream);
+
+/* Per-video-frame 16-column mel windows (inference.py:209-216): out[i][80][step] =
+ * mel[:, starts[i] : starts[i] + step]; starts (device int32) computed by the host. */
+int s2v_mel_chunks(const float *mel, long long frames, const int *starts, int nchunks, int step, float *out,
+                   s2v_stream_t stream);
+
+/* GPEN native ops, same signatures/semantics as third_part/GPEN/face_model/op/:
+ *   fused_bias_act (fused_bias_act.cpp:4-21, fused_bias_act_kernel.cu:18-99)
+ *   y = scale * act(x + b[(i / step_b) % C]) with act 1 = linear, 3 = leaky relu(alpha);
+ *   grad = 1 is the backward form using ref > 0.  size = numel, step_b = prod of dims after C. */
+int s2v_fused_bias_act(const float *x, const float *b, const float *ref, float *y, long long size, int c,
+                       long long step_b, int act, int grad, float alpha, float scale, s2v_stream_t stream);
+/* upfirdn2d (upfirdn2d.cpp:4-23, upfirdn2d_kernel.cu:140-271) on [major][H][W][minor]; any
+ * up/down/pad combination (the reference silently returns garbage for unsupported ones). */
+int s2v_upfirdn2d(const float *x, int major, int in_h, int in_w, int minor, const float *k, int kh, int kw,
+                  int up_x, int up_y, int down_x, int down_y, int pad_x0, int pad_x1, int pad_y0, int pad_y1,
+                  float *y, int out_h, int out_w, s2v_stream_t stream);
+
+/* N(0,1) noise from a counter-based generator (StyleConv noise injection,
+ * base_blocks.py:528-531): y[i] = BoxMuller(splitmix64(seed ^ splitmix64(offset + i))). */
+int s2v_gaussian_noise(float *y, long long n, unsigned long long seed, unsigned long long offset,
+                       s2v_stream_t stream);
+
+const char *s2v_last_error(void);
+/* number of compute units of the current device (0 if no device) */
+int s2v_device_cus(void);
+const char *s2v_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* S2V_H_ */

@@ -1,0 +1,108 @@
+"""ctypes binding of libs2v.so (the C ABI declared in include/s2v.h).
+
+The library is built in-tree (``make -C speech-to-video-mpp_amd/csrc`` or
+``__graft_entry__.build()``) and loaded from this package directory only.  There is no CPU
+fallback anywhere on the product path: if the library is missing, every op raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libs2v.so")
+
+ACT_NONE, ACT_RELU, ACT_LRELU, ACT_SIGMOID, ACT_TANH, ACT_GELU_TANH = range(6)
+IN_DIRECT, IN_NEAREST_UP2, IN_TRANSPOSED = range(3)
+PAD_ZERO, PAD_REFLECT = range(2)
+
+_c_int, _c_float, _c_ll, _c_size, _vp = ctypes.c_int, ctypes.c_float, ctypes.c_longlong, ctypes.c_size_t, ctypes.c_void_p
+
+
+class ConvParams(ctypes.Structure):
+    """Mirror of s2v_conv_params (include/s2v.h)."""
+    _fields_ = [
+        ("x", _vp), ("n", _c_int), ("h", _c_int), ("w", _c_int), ("cin", _c_int), ("xcs", _c_int),
+        ("in_mode", _c_int), ("pad_mode", _c_int), ("pre_act", _c_int), ("pre_alpha", _c_float),
+        ("in_scale", _vp), ("in_scale_ns", _c_int),
+        ("kh", _c_int), ("kw", _c_int), ("sh", _c_int), ("sw", _c_int), ("ph", _c_int), ("pw", _c_int),
+        ("dh", _c_int), ("dw", _c_int),
+        ("wt", _vp), ("kpad", _c_int), ("npad", _c_int), ("cout", _c_int), ("b_kn", _c_int), ("ldb", _c_int),
+        ("y", _vp), ("oh", _c_int), ("ow", _c_int), ("ycs", _c_int),
+        ("scale", _vp), ("shift", _vp), ("nc_scale", _vp), ("nc_scale_ns", _c_int),
+        ("pix_add", _vp), ("pix_w", _c_float),
+        ("res", _vp), ("res_cs", _c_int), ("res_h", _c_int), ("res_w", _c_int), ("res_oy", _c_int),
+        ("res_ox", _c_int), ("res_after_act", _c_int),
+        ("act", _c_int), ("alpha", _c_float),
+        ("batch", _c_int), ("x_bs", _c_ll), ("w_bs", _c_ll), ("y_bs", _c_ll), ("res_bs", _c_ll),
+        ("ws", _vp), ("ws_bytes", _c_size),
+        ("force_tile", _c_int), ("force_splits", _c_int),
+    ]
+
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "s2v_conv2d": (_c_int, [ctypes.POINTER(ConvParams), _vp]),
+    "s2v_conv2d_ws_bytes": (_c_size, [ctypes.POINTER(ConvParams)]),
+    "s2v_layernorm2d": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_float, _c_int, _c_float,
+                                 _c_int, _vp, _c_int, _vp, _c_int, _vp, _c_size, _vp]),
+    "s2v_layernorm2d_ws_bytes": (_c_size, [_c_int, _c_int, _c_int, _c_int]),
+    "s2v_instnorm_adain": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_int, _c_float, _c_int,
+                                    _c_float, _vp, _c_int, _vp, _c_int, _vp, _c_size, _vp]),
+    "s2v_instnorm_ws_bytes": (_c_size, [_c_int, _c_int, _c_int, _c_int]),
+    "s2v_adain_params": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _c_int, _vp, _c_int, _vp]),
+    "s2v_modconv_demod": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_float, _c_float, _vp, _c_int, _vp]),
+    "s2v_resize": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_ll, _c_ll, _c_ll, _c_ll, _vp, _c_int, _c_int,
+                            _c_ll, _c_ll, _c_ll, _c_ll, _c_float, _c_float, _c_int, _vp]),
+    "s2v_pad_reflect": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp,
+                                 _c_int, _vp]),
+    "s2v_row_layernorm": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _vp, _c_float, _vp, _c_int, _vp]),
+    "s2v_attention": (_c_int, [_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_ll, _c_ll,
+                               _c_ll, _c_float, _vp, _c_int, _c_ll, _vp]),
+    "s2v_flow_warp": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_ll, _c_ll,
+                               _c_ll, _c_ll, _vp, _c_int, _vp]),
+    "s2v_melspectrogram": (_c_int, [_vp, _c_ll, _vp, _c_int, _vp, _c_ll, _vp]),
+    "s2v_mel_chunks": (_c_int, [_vp, _c_ll, _vp, _c_int, _c_int, _vp, _vp]),
+    "s2v_fused_bias_act": (_c_int, [_vp, _vp, _vp, _vp, _c_ll, _c_int, _c_ll, _c_int, _c_int, _c_float, _c_float,
+                                    _vp]),
+    "s2v_upfirdn2d": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_int,
+                               _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _vp]),
+    "s2v_gaussian_noise": (_c_int, [_vp, _c_ll, ctypes.c_uint64, ctypes.c_uint64, _vp]),
+    "s2v_last_error": (ctypes.c_char_p, []),
+    "s2v_device_cus": (_c_int, []),
+    "s2v_version": (ctypes.c_char_p, []),
+}
+
+EXPORTS = tuple(_SIGS)
+
+_lock = threading.Lock()
+_lib = None
+
+
+class S2VError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libs2v.so (raises if it was not built — there is no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise S2VError(f"{LIB_PATH} is missing: build it with `make -C {os.path.dirname(LIB_PATH)}/csrc` "
+                               "(or __graft_entry__.build()); the HIP path has no CPU fallback")
+            lib = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in _SIGS.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = load().s2v_last_error().decode(errors="replace")
+        raise S2VError(f"{what} failed ({rc}): {msg}")

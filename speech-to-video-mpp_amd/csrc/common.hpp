@@ -1,0 +1,46 @@
+// Shared device/host helpers for libs2v (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+
+#include "../../include/s2v.h"
+
+namespace s2v {
+
+void set_error(const char *fmt, ...);
+int check_launch(const char *what);
+int device_cus();
+
+#define S2V_REQUIRE(cond, ...)            \
+    do {                                  \
+        if (!(cond)) {                    \
+            ::s2v::set_error(__VA_ARGS__);\
+            return S2V_E_INVALID;         \
+        }                                 \
+    } while (0)
+
+__device__ __forceinline__ float apply_act(float v, int act, float alpha) {
+    switch (act) {
+        case S2V_ACT_RELU: return v > 0.f ? v : 0.f;
+        case S2V_ACT_LRELU: return v >= 0.f ? v : v * alpha;
+        case S2V_ACT_SIGMOID: return 1.f / (1.f + expf(-v));
+        case S2V_ACT_TANH: return tanhf(v);
+        case S2V_ACT_GELU_TANH: {
+            const float k0 = 0.7978845608028654f;  // sqrt(2/pi)
+            return 0.5f * v * (1.f + tanhf(k0 * (v + 0.044715f * v * v * v)));
+        }
+        default: return v;
+    }
+}
+
+// F.pad(mode='reflect') index map for one reflection (pad < n)
+__device__ __forceinline__ int reflect_idx(int i, int n) {
+    i = i < 0 ? -i : i;
+    return i >= n ? 2 * n - 2 - i : i;
+}
+
+inline unsigned cdiv(long long a, long long b) { return (unsigned)((a + b - 1) / b); }
+
+}  // namespace s2v

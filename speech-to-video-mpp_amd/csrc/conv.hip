@@ -1,0 +1,552 @@
+// Implicit-GEMM convolution / GEMM on gfx950 fp32 MFMA (v_mfma_f32_32x32x2_f32).
+//
+// GEMM view:  M = batch pixels (n, oy, ox)   N = output channels   K = (ky, kx, cin)
+//   A[m][k]  gathered on the fly from the NHWC input (zero / reflect padding, nearest-x2
+//            upsampling, transposed-conv scatter-as-gather), prologue act/in_scale fused;
+//   B[n][k]  pre-packed weights [npad][kpad] (or an activation matrix [K][N], ``b_kn``);
+//   C        NHWC output slice; epilogue fuses bias/BN/demod scale, noise, residual, act.
+//
+// Block = 256 threads = 4 waves laid out WAVES_M x WAVES_N; each wave owns a
+// (BM/WAVES_M) x (BN/WAVES_N) sub-tile made of 32x32 MFMA tiles. K is staged through LDS in
+// BK = 32 slices held K-contiguous ([row][BK+4] floats; the +4 pad makes the ds_read_b128 of 16
+// consecutive rows conflict-free), so each lane feeds 4 MFMA k-steps from one 16-byte read.
+// Global loads of slice t+1 are issued into registers before the MFMAs of slice t (one LDS
+// buffer, register double-buffering).  Split-K writes raw partial sums to a workspace that
+// ``splitk_reduce`` folds with the same epilogue.
+#include "common.hpp"
+
+namespace s2v {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+struct Epi {
+    const float *scale, *shift, *nc_scale, *pix_add, *res;
+    int nc_ns;
+    float pix_w;
+    int res_cs, res_h, res_w, res_oy, res_ox, res_after, res_simple;
+    int act;
+    float alpha;
+};
+
+struct ConvArgs {
+    const float *x;
+    int n, h, w, cin, xcs;
+    int in_mode, pad_mode, pre_act;
+    float pre_alpha;
+    const float *in_scale;
+    int in_scale_ns;
+    int kh, kw, sh, sw, ph, pw, dh, dw;
+    const float *wt;
+    int kpad, cout, ldb;
+    float *y;
+    int oh, ow, ycs;
+    Epi epi;
+    long long x_bs, w_bs, y_bs, res_bs;
+    int M, K, ktiles, splits, tps;
+    float *ws;
+};
+
+__device__ __forceinline__ void store_epilogue(const ConvArgs &a, int bidx, int m, int n, float v) {
+    const Epi &e = a.epi;
+    const int hw = a.oh * a.ow;
+    int img = 0, oy = 0, ox = 0;
+    if (e.nc_scale || (e.res && !e.res_simple)) {
+        img = m / hw;
+        int rem = m - img * hw;
+        oy = rem / a.ow;
+        ox = rem - oy * a.ow;
+    }
+    if (e.scale) v *= e.scale[n];
+    if (e.nc_scale) v *= e.nc_scale[(long long)img * e.nc_ns + n];
+    if (e.shift) v += e.shift[n];
+    if (e.pix_add) v += e.pix_w * e.pix_add[(long long)bidx * hw * a.n + m];
+    float r = 0.f;
+    if (e.res) {
+        long long off = e.res_simple
+            ? (long long)m * e.res_cs
+            : ((long long)(img * e.res_h + oy + e.res_oy) * e.res_w + ox + e.res_ox) * e.res_cs;
+        r = e.res[(long long)bidx * a.res_bs + off + n];
+        if (!e.res_after) v += r;
+    }
+    v = apply_act(v, e.act, e.alpha);
+    if (e.res && e.res_after) v += r;
+    a.y[(long long)bidx * a.y_bs + (long long)m * a.ycs + n] = v;
+}
+
+// Map an output pixel + filter tap to an input pixel; false -> zero padding.
+__device__ __forceinline__ bool map_tap(const ConvArgs &a, int oy, int ox, int ky, int kx, int &iy, int &ix) {
+    if (a.in_mode == S2V_IN_DIRECT) {
+        iy = oy * a.sh - a.ph + ky * a.dh;
+        ix = ox * a.sw - a.pw + kx * a.dw;
+        if (a.pad_mode == S2V_PAD_REFLECT) {
+            iy = reflect_idx(iy, a.h);
+            ix = reflect_idx(ix, a.w);
+            return true;
+        }
+        return (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
+    } else if (a.in_mode == S2V_IN_NEAREST_UP2) {
+        int uy = oy * a.sh - a.ph + ky * a.dh;
+        int ux = ox * a.sw - a.pw + kx * a.dw;
+        if ((unsigned)uy >= (unsigned)(2 * a.h) || (unsigned)ux >= (unsigned)(2 * a.w)) return false;
+        iy = uy >> 1;
+        ix = ux >> 1;
+        return true;
+    } else {  // transposed
+        int ty = oy + a.ph - ky * a.dh;
+        int tx = ox + a.pw - kx * a.dw;
+        if (ty < 0 || tx < 0) return false;
+        iy = ty / a.sh;
+        ix = tx / a.sw;
+        return iy * a.sh == ty && ix * a.sw == tx && iy < a.h && ix < a.w;
+    }
+}
+
+__device__ __forceinline__ float prologue(const ConvArgs &a, float v, int img, int c) {
+    if (a.in_scale) v *= a.in_scale[(long long)img * a.in_scale_ns + c];
+    if (a.pre_act) v = apply_act(v, a.pre_act, a.pre_alpha);
+    return v;
+}
+
+template <int BM, int BN, int WAVES_M, int AVEC, int BKN>
+__global__ __launch_bounds__(256) void conv_igemm(ConvArgs a) {
+    constexpr int BK = 32, LDK = BK + 4;
+    constexpr int WAVES_N = 4 / WAVES_M;
+    constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
+    constexpr int TM = WTM / 32, TN = WTN / 32;
+    constexpr int AR = BM / 32;  // A float4 slots per thread
+    constexpr int BR = BN / 32;  // B float4 slots per thread
+    static_assert(TM >= 1 && TN >= 1 && WTM % 32 == 0 && WTN % 32 == 0, "tile");
+
+    __shared__ __attribute__((aligned(16))) float As[BM * LDK];
+    __shared__ __attribute__((aligned(16))) float Bs[BN * LDK];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+    const int bz = blockIdx.z;
+    const int bidx = bz / a.splits, split = bz - bidx * a.splits;
+    const float *__restrict__ x = a.x + (long long)bidx * a.x_bs;
+    const float *__restrict__ wt = a.wt + (long long)bidx * a.w_bs;
+    const int kt0 = split * a.tps;
+    const int kt1 = min(a.ktiles, kt0 + a.tps);
+    const int hw = a.oh * a.ow;
+
+    // ---- per-thread A rows (fixed across K)
+    const int ar = tid >> 3, ak = (tid & 7) * 4;
+    int a_img[AR], a_oy[AR], a_ox[AR];
+    bool a_ok[AR];
+#pragma unroll
+    for (int j = 0; j < AR; ++j) {
+        int m = m0 + ar + 32 * j;
+        a_ok[j] = m < a.M;
+        int mm = a_ok[j] ? m : 0;
+        int img = mm / hw;
+        int rem = mm - img * hw;
+        a_img[j] = img;
+        a_oy[j] = rem / a.ow;
+        a_ox[j] = rem - a_oy[j] * a.ow;
+    }
+
+    float4 ra[AR], rb[BR];
+
+    auto load_tile = [&](int kt) {
+        const int kbase = kt * BK;
+        if (AVEC) {
+            const int k = kbase + ak;
+            const bool kok = k < a.K;
+            const int tap = k / a.cin;
+            const int c = k - tap * a.cin;
+            const int ky = tap / a.kw, kx = tap - (tap / a.kw) * a.kw;
+#pragma unroll
+            for (int j = 0; j < AR; ++j) {
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                int iy, ix;
+                if (a_ok[j] && kok && map_tap(a, a_oy[j], a_ox[j], ky, kx, iy, ix)) {
+                    v = *(const float4 *)(x + ((long long)(a_img[j] * a.h + iy) * a.w + ix) * a.xcs + c);
+                    if (a.in_scale || a.pre_act) {
+                        v.x = prologue(a, v.x, a_img[j], c);
+                        v.y = prologue(a, v.y, a_img[j], c + 1);
+                        v.z = prologue(a, v.z, a_img[j], c + 2);
+                        v.w = prologue(a, v.w, a_img[j], c + 3);
+                    }
+                }
+                ra[j] = v;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < AR; ++j) {
+                float vv[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int k = kbase + ak + e;
+                    float v = 0.f;
+                    if (a_ok[j] && k < a.K) {
+                        const int tap = k / a.cin;
+                        const int c = k - tap * a.cin;
+                        const int ky = tap / a.kw, kx = tap - (tap / a.kw) * a.kw;
+                        int iy, ix;
+                        if (map_tap(a, a_oy[j], a_ox[j], ky, kx, iy, ix)) {
+                            v = x[((long long)(a_img[j] * a.h + iy) * a.w + ix) * a.xcs + c];
+                            v = prologue(a, v, a_img[j], c);
+                        }
+                    }
+                    vv[e] = v;
+                }
+                ra[j] = make_float4(vv[0], vv[1], vv[2], vv[3]);
+            }
+        }
+        if (!BKN) {
+#pragma unroll
+            for (int j = 0; j < BR; ++j)
+                rb[j] = *(const float4 *)(wt + (long long)(n0 + ar + 32 * j) * a.kpad + kbase + ak);
+        } else {
+            // B is [K][ldb] row-major: thread reads 4 consecutive n of one k row
+            constexpr int NV = BN / 4;            // float4 per k-row
+            constexpr int RPP = 256 / NV;         // k-rows per pass
+            const int kr = tid / NV, nn = (tid - (tid / NV) * NV) * 4;
+#pragma unroll
+            for (int j = 0; j < BR; ++j) {
+                const int k = kbase + kr + RPP * j;
+                const int n = n0 + nn;
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (k < a.K) {
+                    const float *src = wt + (long long)k * a.ldb + n;
+                    if (n + 3 < a.cout) {
+                        v = *(const float4 *)src;
+                    } else {
+                        if (n < a.cout) v.x = src[0];
+                        if (n + 1 < a.cout) v.y = src[1];
+                        if (n + 2 < a.cout) v.z = src[2];
+                    }
+                }
+                rb[j] = v;
+            }
+        }
+    };
+
+    auto store_tile = [&]() {
+#pragma unroll
+        for (int j = 0; j < AR; ++j) *(float4 *)&As[(ar + 32 * j) * LDK + ak] = ra[j];
+        if (!BKN) {
+#pragma unroll
+            for (int j = 0; j < BR; ++j) *(float4 *)&Bs[(ar + 32 * j) * LDK + ak] = rb[j];
+        } else {
+            constexpr int NV = BN / 4;
+            constexpr int RPP = 256 / NV;
+            const int kr = tid / NV, nn = (tid - (tid / NV) * NV) * 4;
+#pragma unroll
+            for (int j = 0; j < BR; ++j) {
+                const int k = kr + RPP * j;
+                Bs[(nn + 0) * LDK + k] = rb[j].x;
+                Bs[(nn + 1) * LDK + k] = rb[j].y;
+                Bs[(nn + 2) * LDK + k] = rb[j].z;
+                Bs[(nn + 3) * LDK + k] = rb[j].w;
+            }
+        }
+    };
+
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int li = lane & 31, lh = lane >> 5;
+    if (kt0 < kt1) load_tile(kt0);
+    for (int kt = kt0; kt < kt1; ++kt) {
+        store_tile();
+        __syncthreads();
+        if (kt + 1 < kt1) load_tile(kt + 1);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            float4 av[TM], bv[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+                av[i] = *(const float4 *)&As[(wm * WTM + i * 32 + li) * LDK + lh * 16 + q * 4];
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+                bv[j] = *(const float4 *)&Bs[(wn * WTN + j * 32 + li) * LDK + lh * 16 + q * 4];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i].x, bv[j].x, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i].y, bv[j].y, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i].z, bv[j].z, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i].w, bv[j].w, acc[i][j], 0, 0, 0);
+                }
+        }
+        __syncthreads();
+    }
+
+    // ---- epilogue: lane owns column li of each 32x32 tile, rows (r&3) + 8(r>>2) + 4 lh
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = n0 + wn * WTN + j * 32 + li;
+            if (n >= a.cout) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                if (m >= a.M) continue;
+                if (a.splits > 1)
+                    a.ws[((long long)bz * a.M + m) * a.cout + n] = acc[i][j][r];
+                else
+                    store_epilogue(a, bidx, m, n, acc[i][j][r]);
+            }
+        }
+}
+
+__global__ void splitk_reduce(ConvArgs a, int batch) {
+    const long long total = (long long)batch * a.M * a.cout;
+    for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)gridDim.x * blockDim.x) {
+        const int n = (int)(idx % a.cout);
+        const long long bm = idx / a.cout;
+        const int m = (int)(bm % a.M);
+        const int bidx = (int)(bm / a.M);
+        float s = 0.f;
+        for (int sp = 0; sp < a.splits; ++sp)
+            s += a.ws[(((long long)bidx * a.splits + sp) * a.M + m) * a.cout + n];
+        store_epilogue(a, bidx, m, n, s);
+    }
+}
+
+// Direct VALU convolution for tiny Cout (final RGB / flow heads): one thread per output pixel.
+template <int CO>
+__global__ __launch_bounds__(256) void conv_direct_small(ConvArgs a, int batch) {
+    const long long total = (long long)batch * a.M;
+    const long long gid = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (gid >= total) return;
+    const int bidx = (int)(gid / a.M);
+    const int m = (int)(gid - (long long)bidx * a.M);
+    const int hw = a.oh * a.ow;
+    const int img = m / hw;
+    const int rem = m - img * hw;
+    const int oy = rem / a.ow, ox = rem - (rem / a.ow) * a.ow;
+    const float *x = a.x + (long long)bidx * a.x_bs;
+    const float *wt = a.wt + (long long)bidx * a.w_bs;
+    float acc[CO];
+#pragma unroll
+    for (int o = 0; o < CO; ++o) acc[o] = 0.f;
+    const bool vec = (a.cin % 4 == 0) && (a.xcs % 4 == 0) && !a.in_scale && !a.pre_act &&
+                     (((uintptr_t)x & 15) == 0) && (a.kpad % 4 == 0);
+    for (int ky = 0; ky < a.kh; ++ky)
+        for (int kx = 0; kx < a.kw; ++kx) {
+            int iy, ix;
+            if (!map_tap(a, oy, ox, ky, kx, iy, ix)) continue;
+            const float *px = x + ((long long)(img * a.h + iy) * a.w + ix) * a.xcs;
+            const int kb = (ky * a.kw + kx) * a.cin;
+            if (vec) {
+                for (int c = 0; c < a.cin; c += 4) {
+                    const float4 v = *(const float4 *)(px + c);
+#pragma unroll
+                    for (int o = 0; o < CO; ++o) {
+                        const float4 wv = *(const float4 *)(wt + (long long)o * a.kpad + kb + c);
+                        acc[o] = fmaf(v.x, wv.x, acc[o]);
+                        acc[o] = fmaf(v.y, wv.y, acc[o]);
+                        acc[o] = fmaf(v.z, wv.z, acc[o]);
+                        acc[o] = fmaf(v.w, wv.w, acc[o]);
+                    }
+                }
+            } else {
+                for (int c = 0; c < a.cin; ++c) {
+                    const float v = prologue(a, px[c], img, c);
+#pragma unroll
+                    for (int o = 0; o < CO; ++o) acc[o] = fmaf(v, wt[(long long)o * a.kpad + kb + c], acc[o]);
+                }
+            }
+        }
+#pragma unroll
+    for (int o = 0; o < CO; ++o)
+        if (o < a.cout) store_epilogue(a, bidx, m, o, acc[o]);
+}
+
+// ------------------------------------------------------------------ host side
+struct TileCfg {
+    int bm, bn, wm;
+};
+static const TileCfg kTiles[] = {
+    {128, 128, 2}, {128, 64, 2}, {64, 128, 2}, {64, 64, 2}, {256, 32, 4}, {128, 32, 4}};
+constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
+
+struct Plan {
+    int tile;   // index into kTiles, or -1 for the direct small-N kernel
+    int splits, tps, ktiles;
+};
+
+static bool use_direct(const s2v_conv_params *p) { return p->cout <= 4 && !p->b_kn; }
+
+static Plan make_plan(const s2v_conv_params *p, int M, int K) {
+    Plan pl{};
+    pl.ktiles = (K + 31) / 32;
+    if (use_direct(p) && !p->force_tile) {
+        pl.tile = -1;
+        pl.splits = 1;
+        pl.tps = pl.ktiles;
+        return pl;
+    }
+    const int batch = p->batch > 0 ? p->batch : 1;
+    const long long target = 2LL * (device_cus() > 0 ? device_cus() : 256);
+    int cands[kNumTiles];
+    int nc = 0;
+    if (p->force_tile > 0) {
+        cands[nc++] = p->force_tile - 1;
+    } else if (p->cout <= 32) {
+        cands[nc++] = 4; cands[nc++] = 5;
+    } else if (p->cout <= 64) {
+        cands[nc++] = 1; cands[nc++] = 3;
+    } else {
+        cands[nc++] = 0; cands[nc++] = 1; cands[nc++] = 2; cands[nc++] = 3;
+    }
+    pl.tile = cands[nc - 1];
+    long long blocks = 0;
+    for (int i = 0; i < nc; ++i) {
+        const TileCfg &t = kTiles[cands[i]];
+        blocks = (long long)cdiv(M, t.bm) * cdiv(p->cout, t.bn) * batch;
+        if (blocks >= target) {
+            pl.tile = cands[i];
+            break;
+        }
+    }
+    const TileCfg &t = kTiles[pl.tile];
+    blocks = (long long)cdiv(M, t.bm) * cdiv(p->cout, t.bn) * batch;
+    int splits = 1;
+    if (p->force_splits > 0) {
+        splits = p->force_splits;
+    } else if (blocks < target) {
+        splits = (int)((target + blocks - 1) / blocks);
+        int maxs = pl.ktiles / 8;
+        if (splits > maxs) splits = maxs;
+        if (splits < 1) splits = 1;
+    }
+    if (splits > pl.ktiles) splits = pl.ktiles;
+    pl.tps = (pl.ktiles + splits - 1) / splits;
+    pl.splits = (pl.ktiles + pl.tps - 1) / pl.tps;
+    return pl;
+}
+
+static int validate(const s2v_conv_params *p, int &M, int &K) {
+    S2V_REQUIRE(p && p->x && p->wt && p->y, "conv2d: null pointer");
+    S2V_REQUIRE(p->n > 0 && p->h > 0 && p->w > 0 && p->cin > 0 && p->cout > 0 && p->oh > 0 && p->ow > 0,
+                "conv2d: bad shape n=%d h=%d w=%d cin=%d cout=%d oh=%d ow=%d", p->n, p->h, p->w, p->cin,
+                p->cout, p->oh, p->ow);
+    S2V_REQUIRE(p->kh > 0 && p->kw > 0 && p->sh > 0 && p->sw > 0 && p->dh > 0 && p->dw > 0, "conv2d: bad kernel");
+    S2V_REQUIRE(p->xcs >= p->cin && p->ycs >= p->cout, "conv2d: channel stride smaller than channels");
+    S2V_REQUIRE(p->in_mode >= 0 && p->in_mode <= 2, "conv2d: bad in_mode %d", p->in_mode);
+    S2V_REQUIRE(!(p->pad_mode == S2V_PAD_REFLECT && p->in_mode != S2V_IN_DIRECT),
+                "conv2d: reflect padding only with direct input");
+    S2V_REQUIRE(!(p->pad_mode == S2V_PAD_REFLECT && (p->ph >= p->h || p->pw >= p->w)),
+                "conv2d: reflect pad must be smaller than the input");
+    const long long m = (long long)p->n * p->oh * p->ow;
+    const long long k = (long long)p->kh * p->kw * p->cin;
+    S2V_REQUIRE(m < (1LL << 31) && k < (1LL << 31), "conv2d: problem too large");
+    M = (int)m;
+    K = (int)k;
+    if (p->b_kn) {
+        S2V_REQUIRE(p->ldb >= p->cout, "conv2d: ldb < cout");
+        S2V_REQUIRE(p->ldb % 4 == 0 && ((uintptr_t)p->wt % 16) == 0, "conv2d: b_kn needs ldb%%4==0, 16B aligned");
+    } else {
+        S2V_REQUIRE(p->kpad >= k && p->kpad % 32 == 0, "conv2d: kpad=%d must be >= K=%lld and %%32", p->kpad, k);
+        S2V_REQUIRE(p->npad >= p->cout && p->npad % 128 == 0, "conv2d: npad=%d must be >= cout and %%128", p->npad);
+        S2V_REQUIRE(((uintptr_t)p->wt % 16) == 0, "conv2d: weights must be 16B aligned");
+    }
+    if (p->res) S2V_REQUIRE(p->res_cs >= p->cout, "conv2d: res_cs < cout");
+    return 0;
+}
+
+static ConvArgs make_args(const s2v_conv_params *p, int M, int K, const Plan &pl) {
+    ConvArgs a{};
+    a.x = p->x; a.n = p->n; a.h = p->h; a.w = p->w; a.cin = p->cin; a.xcs = p->xcs;
+    a.in_mode = p->in_mode; a.pad_mode = p->pad_mode; a.pre_act = p->pre_act; a.pre_alpha = p->pre_alpha;
+    a.in_scale = p->in_scale; a.in_scale_ns = p->in_scale_ns;
+    a.kh = p->kh; a.kw = p->kw; a.sh = p->sh; a.sw = p->sw; a.ph = p->ph; a.pw = p->pw; a.dh = p->dh; a.dw = p->dw;
+    a.wt = p->wt; a.kpad = p->kpad; a.cout = p->cout; a.ldb = p->ldb;
+    a.y = p->y; a.oh = p->oh; a.ow = p->ow; a.ycs = p->ycs;
+    Epi &e = a.epi;
+    e.scale = p->scale; e.shift = p->shift; e.nc_scale = p->nc_scale; e.nc_ns = p->nc_scale_ns;
+    e.pix_add = p->pix_add; e.pix_w = p->pix_w; e.res = p->res; e.res_cs = p->res_cs;
+    e.res_h = p->res_h > 0 ? p->res_h : p->oh; e.res_w = p->res_w > 0 ? p->res_w : p->ow;
+    e.res_oy = p->res_oy; e.res_ox = p->res_ox; e.res_after = p->res_after_act;
+    e.res_simple = (e.res_h == p->oh && e.res_w == p->ow && p->res_oy == 0 && p->res_ox == 0);
+    e.act = p->act; e.alpha = p->alpha;
+    a.x_bs = p->x_bs; a.w_bs = p->w_bs; a.y_bs = p->y_bs; a.res_bs = p->res_bs;
+    a.M = M; a.K = K; a.ktiles = pl.ktiles; a.splits = pl.splits; a.tps = pl.tps; a.ws = p->ws;
+    return a;
+}
+
+template <int BM, int BN, int WM>
+static void launch_tile(const ConvArgs &a, bool avec, bool bkn, dim3 grid, hipStream_t s) {
+    if (avec) {
+        if (bkn) conv_igemm<BM, BN, WM, 1, 1><<<grid, 256, 0, s>>>(a);
+        else conv_igemm<BM, BN, WM, 1, 0><<<grid, 256, 0, s>>>(a);
+    } else {
+        if (bkn) conv_igemm<BM, BN, WM, 0, 1><<<grid, 256, 0, s>>>(a);
+        else conv_igemm<BM, BN, WM, 0, 0><<<grid, 256, 0, s>>>(a);
+    }
+}
+
+}  // namespace s2v
+
+using namespace s2v;
+
+extern "C" size_t s2v_conv2d_ws_bytes(const s2v_conv_params *p) {
+    int M, K;
+    if (validate(p, M, K) != 0) return 0;
+    Plan pl = make_plan(p, M, K);
+    if (pl.tile < 0 || pl.splits <= 1) return 0;
+    const int batch = p->batch > 0 ? p->batch : 1;
+    return (size_t)batch * pl.splits * (size_t)M * p->cout * sizeof(float);
+}
+
+extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
+    int M, K;
+    int rc = validate(p, M, K);
+    if (rc) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    const int batch = p->batch > 0 ? p->batch : 1;
+    Plan pl = make_plan(p, M, K);
+    ConvArgs a = make_args(p, M, K, pl);
+    if (pl.tile < 0) {
+        const long long total = (long long)batch * M;
+        dim3 grid(cdiv(total, 256));
+        switch (p->cout) {
+            case 1: conv_direct_small<1><<<grid, 256, 0, s>>>(a, batch); break;
+            case 2: conv_direct_small<2><<<grid, 256, 0, s>>>(a, batch); break;
+            case 3: conv_direct_small<3><<<grid, 256, 0, s>>>(a, batch); break;
+            default: conv_direct_small<4><<<grid, 256, 0, s>>>(a, batch); break;
+        }
+        return check_launch("conv_direct_small");
+    }
+    if (pl.splits > 1) {
+        const size_t need = (size_t)batch * pl.splits * (size_t)M * p->cout * sizeof(float);
+        if (!p->ws || p->ws_bytes < need) {
+            set_error("conv2d: split-K workspace of %zu bytes required (have %zu)", need, p->ws_bytes);
+            return S2V_E_WORKSPACE;
+        }
+    }
+    const bool avec = (p->cin % 4 == 0) && (p->xcs % 4 == 0) && (((uintptr_t)p->x % 16) == 0) &&
+                      (p->x_bs % 4 == 0);
+    const bool bkn = p->b_kn != 0;
+    const TileCfg &t = kTiles[pl.tile];
+    dim3 grid(cdiv(M, t.bm), cdiv(p->cout, t.bn), batch * pl.splits);
+    switch (pl.tile) {
+        case 0: launch_tile<128, 128, 2>(a, avec, bkn, grid, s); break;
+        case 1: launch_tile<128, 64, 2>(a, avec, bkn, grid, s); break;
+        case 2: launch_tile<64, 128, 2>(a, avec, bkn, grid, s); break;
+        case 3: launch_tile<64, 64, 2>(a, avec, bkn, grid, s); break;
+        case 4: launch_tile<256, 32, 4>(a, avec, bkn, grid, s); break;
+        default: launch_tile<128, 32, 4>(a, avec, bkn, grid, s); break;
+    }
+    rc = check_launch("conv_igemm");
+    if (rc || pl.splits <= 1) return rc;
+    const long long total = (long long)batch * M * p->cout;
+    unsigned blocks = cdiv(total, 256);
+    if (blocks > 65535u * 4u) blocks = 65535u * 4u;
+    splitk_reduce<<<blocks, 256, 0, s>>>(a, batch);
+    return check_launch("splitk_reduce");
+}

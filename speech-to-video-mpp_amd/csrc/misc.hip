@@ -1,0 +1,444 @@
+// Resampling, padding, attention, flow warp, mel front end and the GPEN native ops.
+// All HBM/latency-bound; one thread per output element with the channel index fastest so that
+// NHWC reads/writes coalesce.
+#include "common.hpp"
+
+namespace s2v {
+
+// torch upsample_bilinear2d (align_corners=False): src = scale*(dst+0.5)-0.5, clamped at 0
+__device__ __forceinline__ void bilin_index(float scale, int dst, int in, int &i0, int &i1, float &l0, float &l1) {
+    float src = scale * ((float)dst + 0.5f) - 0.5f;
+    if (src < 0.f) src = 0.f;
+    i0 = (int)src;
+    i1 = i0 + ((i0 < in - 1) ? 1 : 0);
+    l1 = src - (float)i0;
+    l0 = 1.f - l1;
+}
+
+__global__ __launch_bounds__(256) void resize_kernel(const float *__restrict__ x, int n, int c, int ih, int iw,
+                                                     long long xsn, long long xsc, long long xsy, long long xsx,
+                                                     float *__restrict__ y, int oh, int ow, long long ysn,
+                                                     long long ysc, long long ysy, long long ysx, float sh, float sw,
+                                                     int mode) {
+    const long long total = (long long)n * oh * ow * c;
+    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+        const int cc = (int)(e % c);
+        long long t = e / c;
+        const int ox = (int)(t % ow);
+        t /= ow;
+        const int oy = (int)(t % oh);
+        const int nn = (int)(t / oh);
+        const float *xb = x + nn * xsn + cc * xsc;
+        float v;
+        if (mode == 0) {
+            int y0, y1, x0, x1;
+            float ly0, ly1, lx0, lx1;
+            bilin_index(sh, oy, ih, y0, y1, ly0, ly1);
+            bilin_index(sw, ox, iw, x0, x1, lx0, lx1);
+            v = ly0 * (lx0 * xb[y0 * xsy + x0 * xsx] + lx1 * xb[y0 * xsy + x1 * xsx]) +
+                ly1 * (lx0 * xb[y1 * xsy + x0 * xsx] + lx1 * xb[y1 * xsy + x1 * xsx]);
+        } else {
+            const int sy = min((int)floorf((float)oy * sh), ih - 1);
+            const int sx = min((int)floorf((float)ox * sw), iw - 1);
+            v = xb[sy * xsy + sx * xsx];
+        }
+        y[nn * ysn + cc * ysc + oy * ysy + ox * ysx] = v;
+    }
+}
+
+__global__ __launch_bounds__(256) void pad_reflect_kernel(const float *__restrict__ x, int n, int h, int w, int c,
+                                                          int xcs, int pt, int pl, int oh, int ow,
+                                                          float *__restrict__ y, int ycs) {
+    const long long total = (long long)n * oh * ow * c;
+    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+        const int cc = (int)(e % c);
+        long long t = e / c;
+        const int ox = (int)(t % ow);
+        t /= ow;
+        const int oy = (int)(t % oh);
+        const int nn = (int)(t / oh);
+        const int iy = reflect_idx(oy - pt, h), ix = reflect_idx(ox - pl, w);
+        y[(((long long)nn * oh + oy) * ow + ox) * ycs + cc] = x[(((long long)nn * h + iy) * w + ix) * xcs + cc];
+    }
+}
+
+// ------------------------------------------------------------------ attention
+// one block per (b, head); K padded to 65 floats per row (conflict-free column reads)
+__global__ __launch_bounds__(256) void attention_kernel(const float *__restrict__ q, const float *__restrict__ k,
+                                                        const float *__restrict__ v, int heads, int T, int ldq, int ldk,
+                                                        int ldv, long long bsq, long long bsk, long long bsv,
+                                                        float scale, float *__restrict__ o, int ldo, long long bso) {
+    extern __shared__ float sm[];
+    float *Ks = sm;                    // [T][65]
+    float *Vs = Ks + T * 65;           // [T][64]
+    float *scr = Vs + T * 64;          // per wave: q[64] + p[T]
+    const int b = blockIdx.x / heads, hd = blockIdx.x - (blockIdx.x / heads) * heads;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const float *kb = k + b * bsk + hd * 64;
+    const float *vb = v + b * bsv + hd * 64;
+    for (int e = threadIdx.x; e < T * 64; e += 256) {
+        const int j = e >> 6, d = e & 63;
+        Ks[j * 65 + d] = kb[(long long)j * ldk + d];
+        Vs[j * 64 + d] = vb[(long long)j * ldv + d];
+    }
+    __syncthreads();
+    float *qs = scr + wv * (64 + T);
+    float *ps = qs + 64;
+    const float *qb = q + b * bsq + hd * 64;
+    float *ob = o + b * bso + hd * 64;
+    for (int i = wv; i < T; i += 4) {
+        qs[lane] = qb[(long long)i * ldq + lane];
+        __builtin_amdgcn_wave_barrier();
+        float sv[4];
+        float mx = -INFINITY;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int j = lane + 64 * t;
+            float s = -INFINITY;
+            if (j < T) {
+                float acc = 0.f;
+                const float *kr = Ks + j * 65;
+#pragma unroll 16
+                for (int d = 0; d < 64; ++d) acc = fmaf(qs[d], kr[d], acc);
+                s = acc * scale;
+            }
+            sv[t] = s;
+            mx = fmaxf(mx, s);
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+        float sum = 0.f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int j = lane + 64 * t;
+            const float pe = (j < T) ? expf(sv[t] - mx) : 0.f;
+            sv[t] = pe;
+            sum += pe;
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 64);
+        const float inv = 1.f / sum;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int j = lane + 64 * t;
+            if (j < T) ps[j] = sv[t] * inv;
+        }
+        __builtin_amdgcn_wave_barrier();
+        float acc = 0.f;
+        for (int j = 0; j < T; ++j) acc = fmaf(ps[j], Vs[j * 64 + lane], acc);
+        ob[(long long)i * ldo + lane] = acc;
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// ------------------------------------------------------------------ flow warp
+// flow_util.py: grid (align_corners=True convention) + 2*flow/(W-1, H-1) -> bilinear resize
+// (align_corners=False) -> grid_sample(bilinear, zeros, align_corners=False)
+__device__ __forceinline__ void deform_at(const float *flow, int fh, int fw, int fcs, int fy, int fx, float &gx,
+                                          float &gy) {
+    const float *f = flow + ((long long)fy * fw + fx) * fcs;
+    gx = (2.f * ((float)fx / (float)(fw - 1)) - 1.f) + 2.f * (f[0] / (float)(fw - 1));
+    gy = (2.f * ((float)fy / (float)(fh - 1)) - 1.f) + 2.f * (f[1] / (float)(fh - 1));
+}
+
+__global__ __launch_bounds__(256) void flow_warp_kernel(const float *__restrict__ flow, int n, int fh, int fw,
+                                                        int fcs, const float *__restrict__ src, int c, int h, int w,
+                                                        long long ssn, long long ssc, long long ssy, long long ssx,
+                                                        float *__restrict__ y, int ycs) {
+    const long long total = (long long)n * h * w;
+    const long long e = blockIdx.x * 256LL + threadIdx.x;
+    if (e >= total) return;
+    const int ox = (int)(e % w);
+    const int oy = (int)((e / w) % h);
+    const int nn = (int)(e / ((long long)w * h));
+    const float *fb = flow + (long long)nn * fh * fw * fcs;
+    float gx, gy;
+    if (fh == h && fw == w) {
+        deform_at(fb, fh, fw, fcs, oy, ox, gx, gy);
+    } else {
+        int y0, y1, x0, x1;
+        float ly0, ly1, lx0, lx1;
+        bilin_index((float)fh / (float)h, oy, fh, y0, y1, ly0, ly1);
+        bilin_index((float)fw / (float)w, ox, fw, x0, x1, lx0, lx1);
+        float ax, ay, bx, by, cx, cy, dx, dy;
+        deform_at(fb, fh, fw, fcs, y0, x0, ax, ay);
+        deform_at(fb, fh, fw, fcs, y0, x1, bx, by);
+        deform_at(fb, fh, fw, fcs, y1, x0, cx, cy);
+        deform_at(fb, fh, fw, fcs, y1, x1, dx, dy);
+        gx = ly0 * (lx0 * ax + lx1 * bx) + ly1 * (lx0 * cx + lx1 * dx);
+        gy = ly0 * (lx0 * ay + lx1 * by) + ly1 * (lx0 * cy + lx1 * dy);
+    }
+    const float ix = ((gx + 1.f) * (float)w - 1.f) * 0.5f;
+    const float iy = ((gy + 1.f) * (float)h - 1.f) * 0.5f;
+    const float fx0 = floorf(ix), fy0 = floorf(iy);
+    const int ix0 = (int)fx0, iy0 = (int)fy0, ix1 = ix0 + 1, iy1 = iy0 + 1;
+    const float wnw = ((float)ix1 - ix) * ((float)iy1 - iy);
+    const float wne = (ix - (float)ix0) * ((float)iy1 - iy);
+    const float wsw = ((float)ix1 - ix) * (iy - (float)iy0);
+    const float wse = (ix - (float)ix0) * (iy - (float)iy0);
+    const bool vnw = ix0 >= 0 && ix0 < w && iy0 >= 0 && iy0 < h;
+    const bool vne = ix1 >= 0 && ix1 < w && iy0 >= 0 && iy0 < h;
+    const bool vsw = ix0 >= 0 && ix0 < w && iy1 >= 0 && iy1 < h;
+    const bool vse = ix1 >= 0 && ix1 < w && iy1 >= 0 && iy1 < h;
+    const float *sb = src + nn * ssn;
+    float *yo = y + e * ycs;
+    for (int cc = 0; cc < c; ++cc) {
+        const float *sc = sb + cc * ssc;
+        float acc = 0.f;
+        if (vnw) acc += sc[iy0 * ssy + ix0 * ssx] * wnw;
+        if (vne) acc += sc[iy0 * ssy + ix1 * ssx] * wne;
+        if (vsw) acc += sc[iy1 * ssy + ix0 * ssx] * wsw;
+        if (vse) acc += sc[iy1 * ssy + ix1 * ssx] * wse;
+        yo[cc] = acc;
+    }
+}
+
+// ------------------------------------------------------------------ mel spectrogram
+// tables: mel basis [80][401] | cos[800] | sin[800] | periodic Hann window[800]
+constexpr int kNfft = 800, kHop = 200, kBins = 401, kMels = 80;
+
+__global__ __launch_bounds__(256) void mel_kernel(const float *__restrict__ wav, long long ns,
+                                                  const float *__restrict__ tables, int pad_reflect,
+                                                  float *__restrict__ out, long long frames) {
+    __shared__ float xs[kNfft];
+    __shared__ float cs[kNfft], sn[kNfft];
+    __shared__ float mag[kBins];
+    const long long t = blockIdx.x;
+    const float *basis = tables;
+    const float *ct = tables + kMels * kBins;
+    const float *st = ct + kNfft;
+    const float *win = st + kNfft;
+    for (int i = threadIdx.x; i < kNfft; i += 256) {
+        cs[i] = ct[i];
+        sn[i] = st[i];
+        // padded index -> sample index (center=True: pad n_fft/2 both sides)
+        long long j = t * kHop + i - kNfft / 2;
+        float v = 0.f;
+        if (pad_reflect) {
+            if (j < 0) j = -j;
+            if (j >= ns) j = 2 * ns - 2 - j;
+        }
+        if (j >= 0 && j < ns) {
+            // preemphasis y[j] = x[j] - 0.97 x[j-1]  (lfilter([1,-k],[1]), zero initial state)
+            v = wav[j] - (j > 0 ? 0.97f * wav[j - 1] : 0.f);
+        }
+        xs[i] = v * win[i];
+    }
+    __syncthreads();
+    for (int f = threadIdx.x; f < kBins; f += 256) {
+        float re = 0.f, im = 0.f;
+        int idx = 0;
+        for (int i = 0; i < kNfft; ++i) {
+            re = fmaf(xs[i], cs[idx], re);
+            im = fmaf(xs[i], sn[idx], im);
+            idx += f;
+            if (idx >= kNfft) idx -= kNfft;
+        }
+        mag[f] = sqrtf(re * re + im * im);
+    }
+    __syncthreads();
+    if (threadIdx.x < kMels) {
+        const float *br = basis + threadIdx.x * kBins;
+        float acc = 0.f;
+        for (int f = 0; f < kBins; ++f) acc = fmaf(br[f], mag[f], acc);
+        float db = 20.f * log10f(fmaxf(1e-5f, acc)) - 20.f;
+        float v = 8.f * ((db + 100.f) / 100.f) - 4.f;
+        v = fminf(fmaxf(v, -4.f), 4.f);
+        out[threadIdx.x * frames + t] = v;
+    }
+}
+
+__global__ __launch_bounds__(256) void mel_chunks_kernel(const float *__restrict__ mel, long long frames,
+                                                         const int *__restrict__ starts, int nchunks, int step,
+                                                         float *__restrict__ out) {
+    const long long total = (long long)nchunks * kMels * step;
+    const long long e = blockIdx.x * 256LL + threadIdx.x;
+    if (e >= total) return;
+    const int tt = (int)(e % step);
+    const int m = (int)((e / step) % kMels);
+    const int i = (int)(e / ((long long)step * kMels));
+    out[e] = mel[(long long)m * frames + starts[i] + tt];
+}
+
+// ------------------------------------------------------------------ GPEN ops
+__global__ __launch_bounds__(256) void fused_bias_act_kernel(const float *__restrict__ x, const float *__restrict__ b,
+                                                             const float *__restrict__ ref, float *__restrict__ y,
+                                                             long long size, int c, long long step_b, int act, int grad,
+                                                             float alpha, float scale) {
+    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < size; i += (long long)gridDim.x * 256) {
+        float v = x[i];
+        if (b) v += b[(i / step_b) % c];
+        const float r = ref ? ref[i] : 0.f;
+        float o;
+        switch (act * 10 + grad) {
+            case 30: o = v > 0.f ? v : v * alpha; break;
+            case 31: o = r > 0.f ? v : v * alpha; break;
+            case 12:
+            case 32: o = 0.f; break;
+            default: o = v; break;
+        }
+        y[i] = o * scale;
+    }
+}
+
+// out = down( FIR( zero-pad( zero-insert-up(x) ), flip(k) ) ) per plane, [major][H][W][minor]
+__global__ __launch_bounds__(256) void upfirdn2d_kernel(const float *__restrict__ x, int major, int ih, int iw,
+                                                        int minor, const float *__restrict__ k, int kh, int kw,
+                                                        int upx, int upy, int dnx, int dny, int px0, int py0,
+                                                        float *__restrict__ y, int oh, int ow) {
+    const long long total = (long long)major * oh * ow * minor;
+    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+        const int mi = (int)(e % minor);
+        long long t = e / minor;
+        const int ox = (int)(t % ow);
+        t /= ow;
+        const int oy = (int)(t % oh);
+        const int mj = (int)(t / oh);
+        const float *xb = x + (long long)mj * ih * iw * minor + mi;
+        float acc = 0.f;
+        for (int i = 0; i < kh; ++i) {
+            const int uy = oy * dny + i - py0;   // row in the zero-inserted image
+            if (uy < 0 || uy % upy) continue;
+            const int iy = uy / upy;
+            if (iy >= ih) continue;
+            for (int j = 0; j < kw; ++j) {
+                const int ux = ox * dnx + j - px0;
+                if (ux < 0 || ux % upx) continue;
+                const int ix = ux / upx;
+                if (ix >= iw) continue;
+                acc = fmaf(xb[((long long)iy * iw + ix) * minor], k[(kh - 1 - i) * kw + (kw - 1 - j)], acc);
+            }
+        }
+        y[e] = acc;
+    }
+}
+
+// ------------------------------------------------------------------ noise
+// Counter-based N(0,1) (splitmix64 + Box-Muller): StyleConv noise injection
+// (base_blocks.py:528-531 draws normal_() per call; only its distribution is reproducible).
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long z) {
+    z += 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void gaussian_kernel(float *__restrict__ y, long long n, unsigned long long seed,
+                                                       unsigned long long offset) {
+    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+        const unsigned long long z = splitmix64(seed ^ splitmix64(offset + (unsigned long long)i));
+        const float u1 = ((float)(z >> 40) + 0.5f) * (1.0f / 16777216.0f);
+        const float u2 = (float)((z >> 16) & 0xFFFFFF) * (1.0f / 16777216.0f);
+        y[i] = sqrtf(-2.f * logf(u1)) * cospif(2.f * u2);
+    }
+}
+
+static unsigned grid_for(long long total) {
+    long long b = (total + 255) / 256;
+    if (b > 65535LL * 16) b = 65535LL * 16;
+    return (unsigned)(b < 1 ? 1 : b);
+}
+
+}  // namespace s2v
+
+using namespace s2v;
+
+extern "C" int s2v_resize(const float *x, int n, int c, int ih, int iw, long long xsn, long long xsc, long long xsy,
+                          long long xsx, float *y, int oh, int ow, long long ysn, long long ysc, long long ysy,
+                          long long ysx, float scale_h, float scale_w, int mode, s2v_stream_t stream) {
+    S2V_REQUIRE(x && y && n > 0 && c > 0 && ih > 0 && iw > 0 && oh > 0 && ow > 0, "resize: bad args");
+    S2V_REQUIRE(mode == 0 || mode == 1, "resize: bad mode");
+    resize_kernel<<<grid_for((long long)n * oh * ow * c), 256, 0, (hipStream_t)stream>>>(
+        x, n, c, ih, iw, xsn, xsc, xsy, xsx, y, oh, ow, ysn, ysc, ysy, ysx, scale_h, scale_w, mode);
+    return check_launch("resize");
+}
+
+extern "C" int s2v_pad_reflect(const float *x, int n, int h, int w, int c, int xcs, int pt, int pb, int pl, int pr,
+                               float *y, int ycs, s2v_stream_t stream) {
+    S2V_REQUIRE(x && y && n > 0 && h > 0 && w > 0 && c > 0 && xcs >= c && ycs >= c, "pad_reflect: bad args");
+    S2V_REQUIRE(pt >= 0 && pb >= 0 && pl >= 0 && pr >= 0 && pt < h && pb < h && pl < w && pr < w,
+                "pad_reflect: padding must be < input size");
+    const int oh = h + pt + pb, ow = w + pl + pr;
+    pad_reflect_kernel<<<grid_for((long long)n * oh * ow * c), 256, 0, (hipStream_t)stream>>>(
+        x, n, h, w, c, xcs, pt, pl, oh, ow, y, ycs);
+    return check_launch("pad_reflect");
+}
+
+extern "C" int s2v_attention(const float *q, const float *k, const float *v, int batch, int heads, int tokens,
+                             int dim_head, int ld_q, int ld_k, int ld_v, long long bs_q, long long bs_k,
+                             long long bs_v, float scale, float *o, int ld_o, long long bs_o, s2v_stream_t stream) {
+    S2V_REQUIRE(q && k && v && o && batch > 0 && heads > 0, "attention: bad args");
+    S2V_REQUIRE(dim_head == 64 && tokens > 0 && tokens <= 256, "attention: needs dim_head 64, tokens <= 256");
+    const size_t smem = ((size_t)tokens * 65 + (size_t)tokens * 64 + 4 * (64 + (size_t)tokens)) * sizeof(float);
+    S2V_REQUIRE(smem <= 160 * 1024, "attention: too many tokens for LDS");
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipFuncSetAttribute((const void *)attention_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr_set = true;
+    }
+    attention_kernel<<<batch * heads, 256, smem, (hipStream_t)stream>>>(q, k, v, heads, tokens, ld_q, ld_k, ld_v, bs_q,
+                                                                        bs_k, bs_v, scale, o, ld_o, bs_o);
+    return check_launch("attention");
+}
+
+extern "C" int s2v_flow_warp(const float *flow, int n, int fh, int fw, int flow_cs, const float *src, int c, int h,
+                             int w, long long ssn, long long ssc, long long ssy, long long ssx, float *y, int ycs,
+                             s2v_stream_t stream) {
+    S2V_REQUIRE(flow && src && y && n > 0 && fh > 1 && fw > 1 && c > 0 && h > 0 && w > 0 && flow_cs >= 2 && ycs >= c,
+                "flow_warp: bad args");
+    flow_warp_kernel<<<cdiv((long long)n * h * w, 256), 256, 0, (hipStream_t)stream>>>(
+        flow, n, fh, fw, flow_cs, src, c, h, w, ssn, ssc, ssy, ssx, y, ycs);
+    return check_launch("flow_warp");
+}
+
+extern "C" int s2v_melspectrogram(const float *wav, long long n_samples, const float *tables, int pad_reflect,
+                                  float *out, long long frames, s2v_stream_t stream) {
+    S2V_REQUIRE(wav && tables && out && n_samples > 0, "melspectrogram: bad args");
+    S2V_REQUIRE(frames == 1 + n_samples / kHop, "melspectrogram: frames must be 1 + n_samples/200");
+    S2V_REQUIRE(!pad_reflect || n_samples > kNfft / 2, "melspectrogram: reflect padding needs > 400 samples");
+    S2V_REQUIRE(frames < 2147483647LL, "melspectrogram: too long");
+    mel_kernel<<<(unsigned)frames, 256, 0, (hipStream_t)stream>>>(wav, n_samples, tables, pad_reflect, out, frames);
+    return check_launch("mel");
+}
+
+extern "C" int s2v_mel_chunks(const float *mel, long long frames, const int *starts, int nchunks, int step,
+                              float *out, s2v_stream_t stream) {
+    S2V_REQUIRE(mel && starts && out && nchunks > 0 && step > 0 && frames >= step, "mel_chunks: bad args");
+    mel_chunks_kernel<<<cdiv((long long)nchunks * kMels * step, 256), 256, 0, (hipStream_t)stream>>>(
+        mel, frames, starts, nchunks, step, out);
+    return check_launch("mel_chunks");
+}
+
+extern "C" int s2v_fused_bias_act(const float *x, const float *b, const float *ref, float *y, long long size, int c,
+                                  long long step_b, int act, int grad, float alpha, float scale,
+                                  s2v_stream_t stream) {
+    S2V_REQUIRE(x && y && size >= 0, "fused_bias_act: bad args");
+    S2V_REQUIRE(!b || (c > 0 && step_b > 0), "fused_bias_act: bias needs c > 0 and step_b > 0");
+    if (size == 0) return 0;
+    fused_bias_act_kernel<<<grid_for(size), 256, 0, (hipStream_t)stream>>>(x, b, ref, y, size, c, step_b, act, grad,
+                                                                             alpha, scale);
+    return check_launch("fused_bias_act");
+}
+
+extern "C" int s2v_upfirdn2d(const float *x, int major, int in_h, int in_w, int minor, const float *k, int kh, int kw,
+                             int up_x, int up_y, int down_x, int down_y, int pad_x0, int pad_x1, int pad_y0,
+                             int pad_y1, float *y, int out_h, int out_w, s2v_stream_t stream) {
+    S2V_REQUIRE(x && k && y && major > 0 && in_h > 0 && in_w > 0 && minor > 0 && kh > 0 && kw > 0,
+                "upfirdn2d: bad args");
+    S2V_REQUIRE(up_x >= 1 && up_y >= 1 && down_x >= 1 && down_y >= 1, "upfirdn2d: up/down must be >= 1");
+    const int eh = (in_h * up_y + pad_y0 + pad_y1 - kh) / down_y + 1;
+    const int ew = (in_w * up_x + pad_x0 + pad_x1 - kw) / down_x + 1;
+    S2V_REQUIRE(eh == out_h && ew == out_w && out_h > 0 && out_w > 0,
+                "upfirdn2d: output must be %dx%d (got %dx%d)", eh, ew, out_h, out_w);
+    upfirdn2d_kernel<<<grid_for((long long)major * out_h * out_w * minor), 256, 0, (hipStream_t)stream>>>(
+        x, major, in_h, in_w, minor, k, kh, kw, up_x, up_y, down_x, down_y, pad_x0, pad_y0, y, out_h, out_w);
+    return check_launch("upfirdn2d");
+}
+
+extern "C" int s2v_gaussian_noise(float *y, long long n, unsigned long long seed, unsigned long long offset,
+                                  s2v_stream_t stream) {
+    S2V_REQUIRE(y && n >= 0, "gaussian_noise: bad args");
+    if (n == 0) return 0;
+    gaussian_kernel<<<grid_for(n), 256, 0, (hipStream_t)stream>>>(y, n, seed, offset);
+    return check_launch("gaussian_noise");
+}

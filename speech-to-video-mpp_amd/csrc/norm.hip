@@ -1,0 +1,347 @@
+// Normalisation kernels: LayerNorm2d (+act, +pool, +residual), InstanceNorm/ADAIN (+act,
+// +residual), token LayerNorm, ADAIN gamma/beta heads, StyleGAN2 demodulation.
+//
+// All are HBM-bound.  Statistics are accumulated in fp64 per thread (no cancellation in
+// E[x^2] - E[x]^2 at 1e6-element reductions) and combined deterministically through a
+// workspace of per-block partials (no float atomics), so results are run-to-run identical.
+#include "common.hpp"
+
+namespace s2v {
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float wave_sumf(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float wave_maxf(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// block (256 threads) sum of two doubles; result valid in all threads
+__device__ __forceinline__ void block_sum2(double &a, double &b) {
+    __shared__ double red[2][4];
+    a = wave_sum(a);
+    b = wave_sum(b);
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        red[0][wv] = a;
+        red[1][wv] = b;
+    }
+    __syncthreads();
+    a = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    b = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+    __syncthreads();
+}
+
+// ------------------------------------------------------------------ LayerNorm2d
+static int ln_blocks(long long elems) {
+    long long b = (elems + 8191) / 8192;
+    if (b < 1) b = 1;
+    if (b > 256) b = 256;
+    return (int)b;
+}
+
+__global__ __launch_bounds__(256) void ln_stats(const float *__restrict__ x, int hw, int c, int xcs, int nblk,
+                                                double *__restrict__ part) {
+    const int n = blockIdx.y, blk = blockIdx.x;
+    const long long pix_per = ((long long)hw + nblk - 1) / nblk;
+    const long long p0 = blk * pix_per;
+    const long long p1 = min((long long)hw, p0 + pix_per);
+    const float *xb = x + (long long)n * hw * xcs;
+    double s = 0.0, q = 0.0;
+    if ((c & 3) == 0 && (xcs & 3) == 0 && ((uintptr_t)x & 15) == 0) {
+        const int c4 = c >> 2;
+        const int tot = (int)(p1 - p0) * c4;
+        for (int e = threadIdx.x; e < tot; e += 256) {
+            const long long p = p0 + e / c4;
+            const int cc = (e - (e / c4) * c4) * 4;
+            const float4 v = *(const float4 *)(xb + p * xcs + cc);
+            s += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
+            q += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+        }
+    } else {
+        const int tot = (int)(p1 - p0) * c;
+        for (int e = threadIdx.x; e < tot; e += 256) {
+            const long long p = p0 + e / c;
+            const int cc = e - (e / c) * c;
+            const double v = xb[p * xcs + cc];
+            s += v;
+            q += v * v;
+        }
+    }
+    block_sum2(s, q);
+    if (threadIdx.x == 0) {
+        part[((long long)n * nblk + blk) * 2 + 0] = s;
+        part[((long long)n * nblk + blk) * 2 + 1] = q;
+    }
+}
+
+__global__ __launch_bounds__(256) void ln_apply(const float *__restrict__ x, int h, int w, int c, int xcs,
+                                                const float *__restrict__ weight, const float *__restrict__ bias,
+                                                float eps, int act, float alpha, int pool, const float *res, int res_cs,
+                                                float *y, int ycs, const double *__restrict__ part, int nblk) {
+    const int n = blockIdx.y;
+    __shared__ float st[2];
+    {
+        double s = 0.0, q = 0.0;
+        for (int i = threadIdx.x; i < nblk; i += 256) {
+            s += part[((long long)n * nblk + i) * 2 + 0];
+            q += part[((long long)n * nblk + i) * 2 + 1];
+        }
+        block_sum2(s, q);
+        if (threadIdx.x == 0) {
+            const double cnt = (double)h * w * c;
+            const double mean = s / cnt;
+            double var = q / cnt - mean * mean;
+            if (var < 0.0) var = 0.0;
+            st[0] = (float)mean;
+            st[1] = (float)(1.0 / sqrt(var + (double)eps));
+        }
+        __syncthreads();
+    }
+    const float mean = st[0], rstd = st[1];
+    const int oh = pool ? h / 2 : h, ow = pool ? w / 2 : w;
+    const int tot = oh * ow * c;
+    const float *xb = x + (long long)n * h * w * xcs;
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < tot; e += gridDim.x * 256) {
+        const int p = e / c;
+        const int cc = e - p * c;
+        const int oy = p / ow, ox = p - (p / ow) * ow;
+        const float g = weight[cc] * rstd, b = bias[cc];
+        float v;
+        if (pool) {
+            const float *px = xb + ((long long)(2 * oy) * w + 2 * ox) * xcs + cc;
+            float a0 = apply_act((px[0] - mean) * g + b, act, alpha);
+            float a1 = apply_act((px[xcs] - mean) * g + b, act, alpha);
+            float a2 = apply_act((px[(long long)w * xcs] - mean) * g + b, act, alpha);
+            float a3 = apply_act((px[(long long)w * xcs + xcs] - mean) * g + b, act, alpha);
+            v = (a0 + a1 + a2 + a3) * 0.25f;
+        } else {
+            v = apply_act((xb[p * xcs + cc] - mean) * g + b, act, alpha);
+        }
+        const long long op = (long long)n * oh * ow + p;
+        if (res) v += res[op * res_cs + cc];
+        y[op * ycs + cc] = v;
+    }
+}
+
+// ------------------------------------------------------------------ InstanceNorm / ADAIN
+static int in_chunks(long long hw) {
+    long long k = (hw + 1023) / 1024;
+    if (k > 64) k = 64;
+    return (int)(k < 1 ? 1 : k);
+}
+
+// grid (chunks, ceil(c/64), n); lane -> channel, wave -> pixel phase
+__global__ __launch_bounds__(256) void in_stats(const float *__restrict__ x, int hw, int c, int xcs, int chunks,
+                                                double *__restrict__ part) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int cc = blockIdx.y * 64 + lane;
+    const int n = blockIdx.z, ch = blockIdx.x;
+    const int per = (hw + chunks - 1) / chunks;
+    const int p0 = ch * per, p1 = min(hw, p0 + per);
+    double s = 0.0, q = 0.0;
+    if (cc < c) {
+        const float *xb = x + (long long)n * hw * xcs + cc;
+        for (int p = p0 + wv; p < p1; p += 4) {
+            const double v = xb[(long long)p * xcs];
+            s += v;
+            q += v * v;
+        }
+    }
+    __shared__ double red[2][4][64];
+    red[0][wv][lane] = s;
+    red[1][wv][lane] = q;
+    __syncthreads();
+    if (wv == 0 && cc < c) {
+        s = red[0][0][lane] + red[0][1][lane] + red[0][2][lane] + red[0][3][lane];
+        q = red[1][0][lane] + red[1][1][lane] + red[1][2][lane] + red[1][3][lane];
+        const long long o = (((long long)n * c + cc) * chunks + ch) * 2;
+        part[o] = s;
+        part[o + 1] = q;
+    }
+}
+
+__global__ __launch_bounds__(256) void in_apply(const float *__restrict__ x, int hw, int c, int xcs,
+                                                const float *__restrict__ gamma, const float *__restrict__ beta,
+                                                int gb_ns, float eps, int act, float alpha, const float *res,
+                                                int res_cs, float *y, int ycs, const double *__restrict__ part,
+                                                int chunks, int achunks) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int cc = blockIdx.y * 64 + lane;
+    const int n = blockIdx.z;
+    if (cc >= c) return;
+    double s = 0.0, q = 0.0;
+    const long long o = ((long long)n * c + cc) * chunks * 2;
+    for (int i = 0; i < chunks; ++i) {
+        s += part[o + 2 * i];
+        q += part[o + 2 * i + 1];
+    }
+    const double mean = s / hw;
+    double var = q / hw - mean * mean;
+    if (var < 0.0) var = 0.0;
+    const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+    const float g = gamma ? 1.f + gamma[(long long)n * gb_ns + cc] : 1.f;
+    const float b = beta ? beta[(long long)n * gb_ns + cc] : 0.f;
+    const float meanf = (float)mean;
+    const int per = (hw + achunks - 1) / achunks;
+    const int p0 = blockIdx.x * per, p1 = min(hw, p0 + per);
+    const float *xb = x + (long long)n * hw * xcs + cc;
+    float *yb = y + (long long)n * hw * ycs + cc;
+    const float *rb = res ? res + (long long)n * hw * res_cs + cc : nullptr;
+    for (int p = p0 + wv; p < p1; p += 4) {
+        float v = apply_act((xb[(long long)p * xcs] - meanf) * rstd * g + b, act, alpha);
+        if (rb) v += rb[(long long)p * res_cs];
+        yb[(long long)p * ycs] = v;
+    }
+}
+
+// ------------------------------------------------------------------ token LayerNorm
+__global__ __launch_bounds__(256) void row_ln(const float *__restrict__ x, int rows, int dim, int xld,
+                                              const float *__restrict__ w, const float *__restrict__ b, float eps,
+                                              float *__restrict__ y, int yld) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= rows) return;
+    const float *xr = x + (long long)row * xld;
+    float s = 0.f;
+    for (int i = lane; i < dim; i += 64) s += xr[i];
+    const float mean = wave_sumf(s) / dim;
+    float q = 0.f;
+    for (int i = lane; i < dim; i += 64) {
+        const float d = xr[i] - mean;
+        q += d * d;
+    }
+    const float rstd = rsqrtf(wave_sumf(q) / dim + eps);
+    float *yr = y + (long long)row * yld;
+    for (int i = lane; i < dim; i += 64) yr[i] = (xr[i] - mean) * rstd * w[i] + b[i];
+}
+
+// ------------------------------------------------------------------ ADAIN heads / demod
+__global__ __launch_bounds__(256) void adain_heads(const float *__restrict__ hid, int batch, int hid_ns, int nh,
+                                                   const float *__restrict__ w2t, const float *__restrict__ bias,
+                                                   const int *__restrict__ seg, int total, float *__restrict__ out,
+                                                   int out_ns) {
+    constexpr int BB = 8;
+    const int o = blockIdx.x * 256 + threadIdx.x;
+    const int b0 = blockIdx.y * BB;
+    if (o >= total) return;
+    const int sg = seg[o];
+    float acc[BB];
+#pragma unroll
+    for (int i = 0; i < BB; ++i) acc[i] = 0.f;
+    for (int j = 0; j < nh; ++j) {
+        const float wv = w2t[(long long)j * total + o];
+#pragma unroll
+        for (int i = 0; i < BB; ++i)
+            if (b0 + i < batch) acc[i] = fmaf(wv, hid[(long long)(b0 + i) * hid_ns + (long long)sg * nh + j], acc[i]);
+    }
+    const float bb = bias ? bias[o] : 0.f;
+#pragma unroll
+    for (int i = 0; i < BB; ++i)
+        if (b0 + i < batch) out[(long long)(b0 + i) * out_ns + o] = acc[i] + bb;
+}
+
+__global__ __launch_bounds__(256) void demod_kernel(const float *__restrict__ s, int batch, int s_ns, int cin,
+                                                    const float *__restrict__ wsq, int cout, float eps, float post,
+                                                    float *__restrict__ d, int d_ns) {
+    const int o = blockIdx.x * 256 + threadIdx.x;
+    const int b = blockIdx.y;
+    if (o >= cout) return;
+    const float *sr = s + (long long)b * s_ns;
+    const float *wr = wsq + (long long)o * cin;
+    float acc = 0.f;
+    for (int i = 0; i < cin; ++i) acc = fmaf(sr[i] * sr[i], wr[i], acc);
+    d[(long long)b * d_ns + o] = rsqrtf(acc + eps) * post;
+}
+
+}  // namespace s2v
+
+using namespace s2v;
+
+extern "C" size_t s2v_layernorm2d_ws_bytes(int n, int h, int w, int c) {
+    return (size_t)n * ln_blocks((long long)h * w * c) * 2 * sizeof(double);
+}
+
+extern "C" int s2v_layernorm2d(const float *x, int n, int h, int w, int c, int xcs, const float *weight,
+                               const float *bias, float eps, int act, float alpha, int pool, const float *res,
+                               int res_cs, float *y, int ycs, void *ws, size_t ws_bytes, s2v_stream_t stream) {
+    S2V_REQUIRE(x && y && weight && bias && n > 0 && h > 0 && w > 0 && c > 0, "layernorm2d: bad args");
+    S2V_REQUIRE(xcs >= c && ycs >= c && (!res || res_cs >= c), "layernorm2d: bad strides");
+    S2V_REQUIRE(!pool || (h >= 2 && w >= 2), "layernorm2d: pool needs h,w >= 2");
+    const int nblk = ln_blocks((long long)h * w * c);
+    const size_t need = (size_t)n * nblk * 2 * sizeof(double);
+    if (!ws || ws_bytes < need) {
+        set_error("layernorm2d: workspace of %zu bytes required", need);
+        return S2V_E_WORKSPACE;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    ln_stats<<<dim3(nblk, n), 256, 0, s>>>(x, h * w, c, xcs, nblk, (double *)ws);
+    int rc = check_launch("ln_stats");
+    if (rc) return rc;
+    const long long out = (long long)(pool ? (h / 2) * (w / 2) : h * w) * c;
+    unsigned gx = cdiv(out, 256 * 4);
+    if (gx > 1024) gx = 1024;
+    ln_apply<<<dim3(gx, n), 256, 0, s>>>(x, h, w, c, xcs, weight, bias, eps, act, alpha, pool, res, res_cs, y, ycs,
+                                         (const double *)ws, nblk);
+    return check_launch("ln_apply");
+}
+
+extern "C" size_t s2v_instnorm_ws_bytes(int n, int h, int w, int c) {
+    return (size_t)n * c * in_chunks((long long)h * w) * 2 * sizeof(double);
+}
+
+extern "C" int s2v_instnorm_adain(const float *x, int n, int h, int w, int c, int xcs, const float *gamma,
+                                  const float *beta, int gb_ns, float eps, int act, float alpha, const float *res,
+                                  int res_cs, float *y, int ycs, void *ws, size_t ws_bytes, s2v_stream_t stream) {
+    S2V_REQUIRE(x && y && n > 0 && h > 0 && w > 0 && c > 0, "instnorm: bad args");
+    S2V_REQUIRE(xcs >= c && ycs >= c && (!res || res_cs >= c), "instnorm: bad strides");
+    const int hw = h * w;
+    const int chunks = in_chunks(hw);
+    const size_t need = (size_t)n * c * chunks * 2 * sizeof(double);
+    if (!ws || ws_bytes < need) {
+        set_error("instnorm: workspace of %zu bytes required", need);
+        return S2V_E_WORKSPACE;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    const unsigned cg = cdiv(c, 64);
+    in_stats<<<dim3(chunks, cg, n), 256, 0, s>>>(x, hw, c, xcs, chunks, (double *)ws);
+    int rc = check_launch("in_stats");
+    if (rc) return rc;
+    in_apply<<<dim3(chunks, cg, n), 256, 0, s>>>(x, hw, c, xcs, gamma, beta, gb_ns, eps, act, alpha, res, res_cs, y,
+                                                 ycs, (const double *)ws, chunks, chunks);
+    return check_launch("in_apply");
+}
+
+extern "C" int s2v_row_layernorm(const float *x, int rows, int dim, int xld, const float *weight, const float *bias,
+                                 float eps, float *y, int yld, s2v_stream_t stream) {
+    S2V_REQUIRE(x && y && weight && bias && rows > 0 && dim > 0 && xld >= dim && yld >= dim, "row_layernorm: bad args");
+    row_ln<<<cdiv(rows, 4), 256, 0, (hipStream_t)stream>>>(x, rows, dim, xld, weight, bias, eps, y, yld);
+    return check_launch("row_ln");
+}
+
+extern "C" int s2v_adain_params(const float *hid, int batch, int hid_ns, int nhidden, const float *w2t,
+                                const float *bias, const int *seg, int total, float *out, int out_ns,
+                                s2v_stream_t stream) {
+    S2V_REQUIRE(hid && w2t && seg && out && batch > 0 && nhidden > 0 && total > 0 && out_ns >= total,
+                "adain_params: bad args");
+    adain_heads<<<dim3(cdiv(total, 256), cdiv(batch, 8)), 256, 0, (hipStream_t)stream>>>(
+        hid, batch, hid_ns, nhidden, w2t, bias, seg, total, out, out_ns);
+    return check_launch("adain_heads");
+}
+
+extern "C" int s2v_modconv_demod(const float *s, int batch, int s_ns, int cin, const float *wsq, int cout, float eps,
+                                 float post, float *d, int d_ns, s2v_stream_t stream) {
+    S2V_REQUIRE(s && wsq && d && batch > 0 && cin > 0 && cout > 0 && s_ns >= cin && d_ns >= cout,
+                "modconv_demod: bad args");
+    demod_kernel<<<dim3(cdiv(cout, 256), batch), 256, 0, (hipStream_t)stream>>>(s, batch, s_ns, cin, wsq, cout, eps,
+                                                                                post, d, d_ns);
+    return check_launch("demod");
+}

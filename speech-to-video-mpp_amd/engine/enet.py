@@ -1,0 +1,152 @@
+"""ENet engine (reference models/ENet.py:82-139): style encoder + LNet + two StyleGAN2 stages.
+
+Modulated convolutions (base_blocks.py:460-554) are computed without per-sample weights:
+    conv(x, W * s[b,i]) * demod[b,o]  ==  (conv(x * s[b,:], W)) * demod[b,o]
+so the input modulation is a prologue scale on the gathered activations (``in_scale``), the
+demodulation rsqrt(sum_i s_i^2 sum_k W_oik^2 + eps) a per-(b,o) epilogue scale (``nc_scale``),
+and all convolutions share one set of packed weights across the batch (the reference builds a
+grouped conv with B distinct weight sets).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .. import ops
+from ..ops import NHWC, ConvW
+from .lnet import LNetEngine
+
+LRELU = 0.2  # ENet.py:94-97, base_blocks.py:41-44, :522
+
+
+class StyleLayer:
+    """One ModulatedConv2d (StyleConv or ToRGB)."""
+
+    def __init__(self, sd, p, device, demodulate, upsample, is_rgb):
+        m = p + "modulated_conv."
+        w = sd[m + "weight"].float()[0]                      # [O, I, k, k]
+        self.k = w.shape[-1]
+        self.cin, self.cout = w.shape[1], w.shape[0]
+        self.demodulate, self.upsample, self.is_rgb = demodulate, upsample, is_rgb
+        bias = sd[p + "bias"].float().reshape(-1)
+        self.conv = ConvW(w, bias, device, padding=self.k // 2)
+        self.wsq = w.pow(2).sum((2, 3)).contiguous().to(device)   # [O, I]
+        self.mod_w = sd[m + "modulation.weight"].float()
+        self.mod_b = sd[m + "modulation.bias"].float()
+        self.noise_w = None if is_rgb else float(sd[p + "weight"].float().reshape(-1)[0])
+        self.device = device
+
+
+class ENetEngine:
+    def __init__(self, sd, device):
+        dev = torch.device(device)
+        self.device = dev
+        self.lnet = LNetEngine(sd, dev, prefix="low_res.")
+        self.first = ConvW(sd["conv_body_first.weight"], sd["conv_body_first.bias"], dev)
+        self.down = []
+        for i in range(6):
+            p = f"conv_body_down.{i}."
+            self.down.append((ConvW(sd[p + "conv1.weight"], sd[p + "conv1.bias"], dev, padding=1),
+                              ConvW(sd[p + "conv2.weight"], sd[p + "conv2.bias"], dev, padding=1),
+                              ConvW(sd[p + "skip.weight"], None, dev)))
+        self.final_conv = ConvW(sd["final_conv.weight"], sd["final_conv.bias"], dev, padding=1)
+        # final_linear consumes feat.reshape(B, -1) in NCHW (c, h, w) order; our feature is NHWC
+        # (h, w, c): permute the weight columns once.
+        wl = sd["final_linear.weight"].float()
+        c4 = sd["final_conv.weight"].shape[0]
+        wl = wl.reshape(wl.shape[0], c4, 4, 4).permute(0, 2, 3, 1).reshape(wl.shape[0], -1)
+        self.final_linear = ConvW(wl, sd["final_linear.bias"], dev)
+        self.layers = []
+        for i in range(2):
+            self.layers.append(StyleLayer(sd, f"style_convs.{2 * i}.", dev, True, True, False))
+            self.layers.append(StyleLayer(sd, f"style_convs.{2 * i + 1}.", dev, True, False, False))
+            self.layers.append(StyleLayer(sd, f"to_rgbs.{i}.", dev, False, False, True))
+        # all six modulation Linears consume the same style code -> one GEMM
+        self.mod = ConvW(torch.cat([l.mod_w for l in self.layers], 0), torch.cat([l.mod_b for l in self.layers], 0),
+                         dev)
+        offs, o = [], 0
+        for l in self.layers:
+            offs.append(o)
+            o += l.cin
+        self.mod_offs = offs
+        self.noise_seed = 0x5EED
+        self.calls = 0
+
+    def style_code(self, ctx, ref: torch.Tensor):
+        """ref: NCHW [B,3,H,W] device tensor -> style [B,1,1,512] (ENet.py:94-101)."""
+        dev, b = self.device, ref.shape[0]
+        x = NHWC.empty(b, 256, 256, 3, dev)
+        ops.nchw_to_nhwc(ctx, ref, x)                              # F.interpolate(ref, 256, bilinear)
+        f = NHWC.empty(b, 256, 256, self.first.cout, dev)
+        ops.conv2d(ctx, x, self.first, f, act=ops.ACT_LRELU, alpha=LRELU)
+        for c1, c2, sk in self.down:                                # ResBlock(mode='down'), base_blocks.py:40-49
+            h, w = f.h, f.w
+            t = NHWC.empty(b, h, w, c1.cout, dev)
+            ops.conv2d(ctx, f, c1, t, act=ops.ACT_LRELU, alpha=LRELU)
+            td = NHWC.empty(b, h // 2, w // 2, c1.cout, dev)
+            ops.resize_nhwc(ctx, t, td, scale_factor=0.5)
+            fd = NHWC.empty(b, h // 2, w // 2, f.c, dev)
+            ops.resize_nhwc(ctx, f, fd, scale_factor=0.5)
+            out = NHWC.empty(b, h // 2, w // 2, c2.cout, dev)
+            ops.conv2d(ctx, fd, sk, out)                            # skip(x_down)
+            ops.conv2d(ctx, td, c2, out, act=ops.ACT_LRELU, alpha=LRELU, res=out, res_after=True)
+            f = out
+        g = NHWC.empty(b, f.h, f.w, self.final_conv.cout, dev)
+        ops.conv2d(ctx, f, self.final_conv, g, act=ops.ACT_LRELU, alpha=LRELU)
+        style = NHWC.empty(b, 1, 1, self.final_linear.cout, dev)
+        ops.conv2d(ctx, NHWC(g.t.view(b, 1, 1, -1)), self.final_linear, style)
+        return style
+
+    def forward(self, ctx, audio, face, gt, out: torch.Tensor, low: torch.Tensor, noises=None, aux=None):
+        """audio [B,1,80,16], face [B,6,H,W], gt [B,3,H,W] (NCHW device tensors) ->
+        out [B,3,384,384], low [B,3,96,96] (NCHW, written in place)."""
+        dev = self.device
+        b = audio.shape[0]
+        style = self.style_code(ctx, face[:, 3:])
+        if aux is not None:
+            aux["style"] = style.t.view(b, -1)
+        svec = NHWC.empty(b, 1, 1, self.mod.cout, dev)
+        ops.conv2d(ctx, style, self.mod, svec)
+        s2 = svec.t.view(b, -1)
+        # LNet input: cat(inp, gt) -> bilinear 96x96 (ENet.py:103-104)
+        x6 = NHWC.empty(b, 96, 96, 6, dev)
+        ops.nchw_to_nhwc(ctx, face[:, :3], x6.slice(0, 3))
+        ops.nchw_to_nhwc(ctx, gt, x6.slice(3, 3))
+        lo = NHWC.empty(b, 96, 96, 3, dev)
+        self.lnet.forward(ctx, audio, x6, lo)
+        ops.nhwc_to_nchw(ctx, lo, low)
+        # F.pad(reflect, 2) -> StyleConv / ToRGB stages (ENet.py:119-129)
+        cur = NHWC.empty(b, 100, 100, 3, dev)
+        ops.pad_reflect(ctx, lo, cur, (2, 2, 2, 2))
+        skip = cur
+        self.calls += 1
+        for st in range(2):
+            for li in range(2):
+                L = self.layers[3 * st + li]
+                off = self.mod_offs[3 * st + li]
+                x = cur
+                if L.upsample:
+                    x = NHWC.empty(b, 2 * cur.h, 2 * cur.w, cur.c, dev)
+                    ops.resize_nhwc(ctx, cur, x, scale_factor=2)
+                d = torch.empty((b, L.cout), device=dev)
+                ops.modconv_demod(ctx, s2[:, off: off + L.cin], L.wsq, d, eps=1e-8, post=math.sqrt(2.0))
+                y = NHWC.empty(b, x.h, x.w, L.cout, dev)
+                noise = None
+                if L.noise_w:
+                    if noises is not None and noises[2 * st + li] is not None:
+                        noise = noises[2 * st + li].contiguous()
+                    else:
+                        noise = torch.empty((b, x.h, x.w), device=dev)
+                        ops.gaussian_noise(ctx, noise, self.noise_seed, (self.calls << 40) + ((2 * st + li) << 36))
+                ops.conv2d(ctx, x, L.conv, y, in_scale=s2[:, off: off + L.cin], nc_scale=d, act=ops.ACT_LRELU,
+                           alpha=LRELU, pix_add=noise, pix_w=L.noise_w or 0.0)
+                cur = y
+            R = self.layers[3 * st + 2]
+            off = self.mod_offs[3 * st + 2]
+            rgb = NHWC.empty(b, cur.h, cur.w, 3, dev)
+            ops.resize_nhwc(ctx, skip, rgb, scale_factor=2)          # skip upsample (base_blocks.py:552)
+            ops.conv2d(ctx, cur, R.conv, rgb, in_scale=s2[:, off: off + R.cin], res=rgb)
+            skip = rgb
+        ops.nhwc_to_nchw(ctx, skip, out, crop=(8, 8))                # [:, :, 8:-8, 8:-8]
+        return out, low

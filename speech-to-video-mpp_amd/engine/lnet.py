@@ -1,0 +1,240 @@
+"""LNet engine: the audio-conditioned lip-sync U-Net (reference models/LNet.py:80-139) on libs2v.
+
+Data layout: NHWC fp32 in HBM.  The reference's torch.cat / split / narrow calls are channel
+slices of one buffer (e.g. the 1024-channel [x_maskGT | x_ref] feature at 12x12 is written in
+place by the two encoder streams, FFC x_l / x_g are channel ranges of the block tensor).
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import ops
+from ..ops import NHWC, ConvW
+from .common import AdainBank, bn_tuple, conv_weight, make_conv
+
+LRELU = 0.1        # LNet.py:91
+LRELU_FFC = 0.01   # FineADAINLama built with nn.LeakyReLU() default (base_blocks.py:369 via :393/:419)
+
+AUDIO_CFG = [  # LNet.py:102-120: (stride, padding, residual)
+    (1, 1, False), (1, 1, True), (1, 1, True), ((3, 1), 1, False), (1, 1, True), (1, 1, True),
+    (3, 1, False), (1, 1, True), (1, 1, True), ((3, 2), 1, False), (1, 1, True), (1, 0, False), (1, 0, False)]
+
+
+class ConvNormAct:
+    """conv -> LayerNorm2d -> LeakyReLU (-> avgpool2) (FirstBlock2d/DownBlock2d/UpBlock2d/Jump)."""
+
+    def __init__(self, sd, p, device, k, pool=False, up=False):
+        self.conv = make_conv(sd, p + "model.0.", device, padding=k // 2,
+                              in_mode=ops.IN_NEAREST_UP2 if up else ops.IN_DIRECT)
+        self.ln_w = sd[p + "model.1.weight"].float().reshape(-1).contiguous().to(device)
+        self.ln_b = sd[p + "model.1.bias"].float().reshape(-1).contiguous().to(device)
+        self.pool = pool
+        self.device = device
+
+    def out_shape(self, x: NHWC):
+        oh, ow = self.conv.out_hw(x.h, x.w)
+        if self.pool:
+            oh, ow = oh // 2, ow // 2
+        return x.n, oh, ow, self.conv.cout
+
+    def __call__(self, ctx, x: NHWC, out: NHWC | None = None, res: NHWC | None = None) -> NHWC:
+        oh, ow = self.conv.out_hw(x.h, x.w)
+        tmp = NHWC.empty(x.n, oh, ow, self.conv.cout, self.device)
+        ops.conv2d(ctx, x, self.conv, tmp)
+        if out is None:
+            out = NHWC.empty(*self.out_shape(x), self.device)
+        ops.layernorm2d(ctx, tmp, self.ln_w, self.ln_b, out, act=ops.ACT_LRELU, alpha=LRELU, pool=self.pool, res=res)
+        return out
+
+
+class Transformer:
+    """models/transformer.py:89-112 (DualPreNorm cross attention, q,k <- x, v <- y)."""
+
+    def __init__(self, sd, p, device, depth=2, heads=4, dim_head=64):
+        self.layers = []
+        self.heads, self.dim_head = heads, dim_head
+        t = lambda k: sd[k].float().contiguous().to(device)  # noqa: E731
+        for i in range(depth):
+            a, f = f"{p}layers.{i}.0.", f"{p}layers.{i}.1."
+            self.layers.append(dict(
+                nx=(t(a + "normx.weight"), t(a + "normx.bias")), ny=(t(a + "normy.weight"), t(a + "normy.bias")),
+                qk=ConvW(torch.cat([sd[a + "fn.to_q.weight"], sd[a + "fn.to_k.weight"]], 0), None, device),
+                v=ConvW(sd[a + "fn.to_v.weight"], None, device),
+                out=ConvW(sd[a + "fn.to_out.0.weight"], sd[a + "fn.to_out.0.bias"], device),
+                nf=(t(f + "norm.weight"), t(f + "norm.bias")),
+                ff1=ConvW(sd[f + "fn.net.0.weight"], sd[f + "fn.net.0.bias"], device),
+                ff2=ConvW(sd[f + "fn.net.3.weight"], sd[f + "fn.net.3.bias"], device)))
+        self.inner = heads * dim_head
+        self.device = device
+
+    def __call__(self, ctx, x: NHWC, y: NHWC, out: NHWC):
+        """x: dense NHWC [B,h,w,C] scratch (used in place as the residual stream), y: NHWC view
+        (tokens = pixels, row stride y.cs); result written to ``out`` (a channel slice)."""
+        b, h, w, c = x.n, x.h, x.w, x.c
+        assert x.cs == c and x.coff == 0
+        T = h * w
+        rows = b * T
+        dev = self.device
+        xt = x.t.view(rows, c)
+        yt = y.t.view(rows, y.cs)[:, y.coff: y.coff + c]
+        xn = torch.empty_like(xt)
+        yn = torch.empty_like(xt)
+        qk = torch.empty((rows, 2 * self.inner), device=dev)
+        v = torch.empty((rows, self.inner), device=dev)
+        o = torch.empty((rows, self.inner), device=dev)
+        hdn = torch.empty((rows, self.layers[0]["ff1"].cout), device=dev)
+        as4 = lambda t: NHWC(t.view(rows, 1, 1, t.shape[1]))  # noqa: E731
+        for li, L in enumerate(self.layers):
+            ops.row_layernorm(ctx, xt, *L["nx"], xn)
+            ops.row_layernorm(ctx, yt, *L["ny"], yn)
+            ops.conv2d(ctx, as4(xn), L["qk"], as4(qk))
+            ops.conv2d(ctx, as4(yn), L["v"], as4(v))
+            ops.attention(ctx, qk[:, : self.inner], qk[:, self.inner:], v, o, batch=b, heads=self.heads, tokens=T,
+                          dim_head=self.dim_head)
+            ops.conv2d(ctx, as4(o), L["out"], as4(xt), res=as4(xt))
+            ops.row_layernorm(ctx, xt, *L["nf"], xn)
+            ops.conv2d(ctx, as4(xn), L["ff1"], as4(hdn), act=ops.ACT_GELU_TANH)
+            last = li == len(self.layers) - 1
+            dst = NHWC(out.t.view(rows, 1, 1, out.cs), out.coff, c) if last else as4(xt)
+            ops.conv2d(ctx, as4(hdn), L["ff2"], dst, res=as4(xt))
+        return out
+
+
+class FFCLama:
+    """FineADAINLama (base_blocks.py:368-386) = FFC (ffc.py:176-233, ratio 0.75, reflect 3x3,
+    spectral g2g without LFU) + ADAIN(bn_l | bn_g) + LeakyReLU(0.01)."""
+
+    def __init__(self, sd, p, device, c, hw, bank: AdainBank):
+        f = p + "ffc."
+        self.c = c
+        self.cg = int(c * 0.75)
+        self.cl = c - self.cg
+        self.cc = self.cg // 2
+        rp = dict(padding=1, pad_mode=ops.PAD_REFLECT)
+        w_l2l, w_g2l = sd[f + "convl2l.weight"].float(), sd[f + "convg2l.weight"].float()
+        self.conv_to_l = ConvW(torch.cat([w_l2l, w_g2l], 1), None, device, **rp)   # l2l(x_l) + g2l(x_g)
+        self.conv_l2g = ConvW(sd[f + "convl2g.weight"], None, device, **rp)
+        st = f + "convg2g."
+        self.st1 = ConvW(sd[st + "conv1.0.weight"], None, device, bn=bn_tuple(sd, st + "conv1.1."))
+        # FourierUnit 1x1 conv on [re, im]-interleaved channels (ffc.py:100-118) -> reorder to
+        # (part, channel) so the spectrum is a plain [B, F, 2C] tensor.
+        cc = self.cc
+        perm = torch.tensor([2 * (i % cc) + i // cc for i in range(2 * cc)])
+        wfu = sd[st + "fu.conv_layer.weight"].float()[perm][:, perm]
+        bn = tuple(t.float()[perm] for t in bn_tuple(sd, st + "fu.bn."))
+        self.fu = ConvW(wfu, None, device, bn=bn)
+        self.st2 = ConvW(sd[st + "conv2.weight"], None, device)
+        self.h, self.w = hw
+        self.d2, self.iv = ops.fourier_matrices(self.h, self.w, device)
+        self.F = self.h * (self.w // 2 + 1)
+        self.gid = bank.add_group(sd, [(p + "bn_l.", self.cl), (p + "bn_g.", self.cg)])
+        self.device = device
+
+    def pre_norm(self, ctx, x: NHWC, y: NHWC):
+        """y <- [l2l(x_l)+g2l(x_g) | l2g(x_l) + spectral(x_g)] (before ADAIN)."""
+        b = x.n
+        P = self.h * self.w
+        cl, cg, cc, dev = self.cl, self.cg, self.cc, self.device
+        ops.conv2d(ctx, x, self.conv_to_l, y.slice(0, cl))
+        yg = y.slice(cl, cg)
+        ops.conv2d(ctx, x.slice(0, cl), self.conv_l2g, yg)
+        t1 = NHWC.empty(b, self.h, self.w, cc, dev)
+        ops.conv2d(ctx, x.slice(cl, cg), self.st1, t1, act=ops.ACT_RELU)
+        spec = torch.empty((b, 2 * self.F, cc), device=dev)
+        ops.gemm_kn(ctx, self.d2, t1.t, spec, batch=b, a_bs=0, b_bs=P * cc, out_bs=2 * self.F * cc)
+        spec2 = NHWC.empty(b, self.F, 1, 2 * cc, dev)
+        ops.conv2d(ctx, NHWC(spec.view(b, self.F, 1, 2 * cc)), self.fu, spec2, act=ops.ACT_RELU)
+        u = NHWC.empty(b, self.h, self.w, cc, dev)
+        ops.gemm_kn(ctx, self.iv, spec2.t.view(b, 2 * self.F, cc), u.t, batch=b, a_bs=0, b_bs=2 * self.F * cc, out_bs=P * cc,
+                    res=t1.t, res_bs=P * cc)
+        ops.conv2d(ctx, u, self.st2, yg, res=yg)
+
+    def norm(self, ctx, bank: AdainBank, y: NHWC, out: NHWC, res: NHWC | None = None):
+        g, bt, ns = bank.gamma_beta(self.gid)
+        ops.instnorm(ctx, y, out, g, bt, ns, act=ops.ACT_LRELU, alpha=LRELU_FFC, res=res)
+
+
+class LNetEngine:
+    def __init__(self, sd, device, prefix=""):
+        p = prefix
+        dev = torch.device(device)
+        self.device = dev
+        e = p + "encoder."
+        self.first_inp = ConvNormAct(sd, e + "first_inp.", dev, 7)
+        self.first_ref = ConvNormAct(sd, e + "first_ref.", dev, 7)
+        self.inp_down = [ConvNormAct(sd, f"{e}inp_down{i}.", dev, 3, pool=True) for i in range(3)]
+        self.ref_down = [ConvNormAct(sd, f"{e}ref_down{i}.", dev, 3, pool=True) for i in range(3)]
+        self.ca2 = Transformer(sd, e + "ca2.", dev)
+        self.audio = []
+        for i, (stride, pad, res) in enumerate(AUDIO_CFG):
+            a = f"{p}audio_encoder.{i}.conv_block."
+            self.audio.append((ConvW(sd[a + "0.weight"], sd[a + "0.bias"], dev, stride=stride, padding=pad,
+                                     bn=bn_tuple(sd, a + "1.")), res))
+        d = p + "decoder."
+        self.bank = AdainBank(sd[f"{d}res2.res0.conv1.bn_l.mlp_shared.0.weight"].shape[1])
+        self.levels = []
+        chans = {2: 1024, 1: 256, 0: 128}
+        sizes = {2: (12, 12), 1: (24, 24), 0: (48, 48)}
+        for i in (2, 1, 0):
+            blocks = []
+            for j in range(9):
+                r = f"{d}res{i}.res{j}."
+                blocks.append((FFCLama(sd, r + "conv1.", dev, chans[i], sizes[i], self.bank),
+                               FFCLama(sd, r + "conv2.", dev, chans[i], sizes[i], self.bank)))
+            self.levels.append(dict(i=i, c=chans[i], blocks=blocks,
+                                    up=ConvNormAct(sd, f"{d}up{i}.", dev, 3, up=True),
+                                    jump=ConvNormAct(sd, f"{d}jump{i}.", dev, 3)))
+        self.bank.build(dev)
+        self.final = make_conv(sd, d + "final.model.0.", dev, padding=3)
+
+    def forward(self, ctx, audio: torch.Tensor, face6: NHWC, out: NHWC, logits: NHWC | None = None):
+        """audio: [B,1,80,16] device tensor; face6: NHWC [B,96,96,6] = [masked | ref];
+        out: NHWC [B,96,96,3] receives sigmoid(final conv)."""
+        dev = self.device
+        b = face6.n
+        # ---- visual encoder (LNet.py:30-43)
+        xm = self.first_inp(ctx, face6.slice(0, 3))
+        xr = self.first_ref(ctx, face6.slice(3, 3))
+        skips = [xm]
+        h = face6.h
+        cat = None
+        for i in range(3):
+            if i < 2:
+                xm = self.inp_down[i](ctx, xm)
+                xr = self.ref_down[i](ctx, xr)
+                skips.append(xm)
+            else:
+                n_, oh, ow, c = self.inp_down[i].out_shape(xm)
+                cat = NHWC.empty(n_, oh, ow, 2 * c, dev)
+                xm2 = self.inp_down[i](ctx, xm)
+                self.ref_down[i](ctx, xr, out=cat.slice(c, c))
+                self.ca2(ctx, xm2, cat.slice(c, c), cat.slice(0, c))
+        # ---- audio encoder (LNet.py:102-120, base_blocks.py:12-26)
+        a = audio.contiguous()
+        x = NHWC(a.view(b, a.shape[2], a.shape[3], 1))
+        for cw, res in self.audio:
+            oh, ow = cw.out_hw(x.h, x.w)
+            y = NHWC.empty(b, oh, ow, cw.cout, dev)
+            ops.conv2d(ctx, x, cw, y, act=ops.ACT_RELU, res=x if res else None)
+            x = y
+        z = x
+        self.bank.run(ctx, z)
+        # ---- decoder (LNet.py:67-77)
+        cur = cat
+        for lv in self.levels:
+            c = lv["c"]
+            ya = NHWC.empty(cur.n, cur.h, cur.w, c, dev)
+            yb = NHWC.empty(cur.n, cur.h, cur.w, c, dev)
+            for l1, l2 in lv["blocks"]:
+                l1.pre_norm(ctx, cur, ya)
+                l1.norm(ctx, self.bank, ya, ya)
+                l2.pre_norm(ctx, ya, yb)
+                l2.norm(ctx, self.bank, yb, cur, res=cur)       # FFCResnetBlock: id + conv2(conv1(x))
+            up = lv["up"](ctx, cur)
+            skip = skips.pop()
+            lv["jump"](ctx, skip, out=up, res=up)               # jump(skip) + out
+            cur = up
+        if logits is not None:
+            ops.conv2d(ctx, cur, self.final, logits)
+        ops.conv2d(ctx, cur, self.final, out, act=ops.ACT_SIGMOID)
+        return out

@@ -1,0 +1,362 @@
+"""Tensor-level wrappers over the C ABI (libs2v.so).
+
+PyTorch is used only as the device allocator and stream provider: every op here hands raw
+device pointers + sizes to a HIP kernel in libs2v.  Inputs must be CUDA (HIP) fp32 tensors; a
+CPU tensor raises (there is no CPU path in the product).
+
+Layout: activations are NHWC tensors [N, H, W, Ctot]; an ``NHWC`` view selects a channel slice
+[coff, coff + c) of one, which is how the reference's torch.cat / split / narrow disappear.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import torch
+
+from . import _lib
+from ._lib import (ACT_GELU_TANH, ACT_LRELU, ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_TANH,  # noqa: F401
+                   IN_DIRECT, IN_NEAREST_UP2, IN_TRANSPOSED, PAD_REFLECT, PAD_ZERO, check)
+
+F32 = 4
+
+
+def _require_cuda(t: torch.Tensor, what: str):
+    if not (t.is_cuda and t.dtype == torch.float32):
+        raise _lib.S2VError(f"{what}: expected a float32 HIP device tensor, got {t.dtype} on {t.device} "
+                            "(the s2v path has no CPU fallback)")
+
+
+class NHWC:
+    """Channel-slice view of a contiguous [N, H, W, Ctot] fp32 device tensor."""
+    __slots__ = ("t", "n", "h", "w", "cs", "coff", "c")
+
+    def __init__(self, t: torch.Tensor, coff: int = 0, c: int | None = None):
+        assert t.dim() == 4 and t.is_contiguous(), "NHWC view needs a contiguous 4-D tensor"
+        _require_cuda(t, "NHWC")
+        self.t = t
+        self.n, self.h, self.w, self.cs = t.shape
+        self.coff = coff
+        self.c = self.cs - coff if c is None else c
+        assert 0 <= coff and coff + self.c <= self.cs
+
+    @property
+    def ptr(self) -> int:
+        return self.t.data_ptr() + F32 * self.coff
+
+    def slice(self, coff: int, c: int) -> "NHWC":
+        return NHWC(self.t, self.coff + coff, c)
+
+    @staticmethod
+    def empty(n, h, w, c, device) -> "NHWC":
+        return NHWC(torch.empty((n, h, w, c), device=device, dtype=torch.float32))
+
+
+class Workspace:
+    """Grow-only scratch buffer shared by the ops of one stream (split-K partials, norm stats).
+    Grows only outside graph capture; a capture that needs more raises."""
+
+    def __init__(self, device):
+        self.device = device
+        self.buf = torch.empty(0, dtype=torch.uint8, device=device)
+
+    def get(self, nbytes: int):
+        if nbytes <= 0:
+            return None, 0
+        if self.buf.numel() < nbytes:
+            if torch.cuda.is_current_stream_capturing():
+                raise _lib.S2VError("workspace must be sized by an eager run before graph capture")
+            self.buf = torch.empty(int(nbytes * 1.25) + 256, dtype=torch.uint8, device=self.device)
+        return self.buf.data_ptr(), self.buf.numel()
+
+
+class Ctx:
+    """Execution context: device, stream handle, workspace."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.ws = Workspace(self.device)
+        self.lib = _lib.load()
+
+    @property
+    def stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+
+# ----------------------------------------------------------------------------- weights
+def _pad2(t: torch.Tensor, rows: int, cols: int) -> torch.Tensor:
+    out = torch.zeros((rows, cols), dtype=torch.float32)
+    out[: t.shape[0], : t.shape[1]] = t
+    return out
+
+
+class ConvW:
+    """Packed convolution weights [npad][kpad] with k = (ky*kw + kx)*cin + c, plus the folded
+    per-output-channel epilogue scale/shift (bias, eval BatchNorm)."""
+
+    def __init__(self, weight: torch.Tensor, bias=None, device="cuda", *, stride=1, padding=0, dilation=1,
+                 transposed=False, output_padding=0, pad_mode=PAD_ZERO, in_mode=IN_DIRECT, bn=None, bn_eps=1e-5,
+                 post_scale=None):
+        w = weight.detach().to("cpu", torch.float32)
+        if w.dim() == 2:
+            w = w[:, :, None, None]
+        elif w.dim() == 3:            # Conv1d [O, I, k] -> 1 x k
+            w = w[:, :, None, :]
+        if transposed:                # ConvTranspose2d [I, O, kh, kw] -> [O, I, kh, kw]
+            w = w.transpose(0, 1)
+            in_mode = IN_TRANSPOSED
+        self.cout, self.cin, self.kh, self.kw = (int(s) for s in w.shape)
+        pair = lambda v: (v, v) if isinstance(v, int) else tuple(v)  # noqa: E731
+        self.sh, self.sw = pair(stride)
+        self.ph, self.pw = pair(padding)
+        self.dh, self.dw = pair(dilation)
+        if weight.dim() == 3:
+            self.sh, self.ph, self.dh = 1, 0, 1
+        self.oph, self.opw = pair(output_padding)
+        self.pad_mode, self.in_mode = pad_mode, in_mode
+        K = self.kh * self.kw * self.cin
+        self.K = K
+        self.kpad = (K + 31) // 32 * 32
+        self.npad = (self.cout + 127) // 128 * 128
+        wk = w.permute(0, 2, 3, 1).reshape(self.cout, K)
+        self.wt = _pad2(wk, self.npad, self.kpad).to(device)
+        scale = shift = None
+        b = None if bias is None else bias.detach().to("cpu", torch.float32)
+        if bn is not None:
+            g, beta, mean, var = (t.detach().to("cpu", torch.float32) for t in bn)
+            s = g / torch.sqrt(var + bn_eps)
+            scale = s
+            shift = beta - mean * s + (b * s if b is not None else 0.0)
+        elif b is not None:
+            shift = b
+        if post_scale is not None:
+            scale = (scale if scale is not None else torch.ones(self.cout)) * post_scale
+            if shift is not None:
+                shift = shift * post_scale
+        self.scale = None if scale is None else scale.contiguous().to(device)
+        self.shift = None if shift is None else shift.contiguous().to(device)
+
+    def out_hw(self, h, w):
+        if self.in_mode == IN_TRANSPOSED:
+            return ((h - 1) * self.sh - 2 * self.ph + self.dh * (self.kh - 1) + self.oph + 1,
+                    (w - 1) * self.sw - 2 * self.pw + self.dw * (self.kw - 1) + self.opw + 1)
+        if self.in_mode == IN_NEAREST_UP2:
+            h, w = 2 * h, 2 * w
+        return ((h + 2 * self.ph - self.dh * (self.kh - 1) - 1) // self.sh + 1,
+                (w + 2 * self.pw - self.dw * (self.kw - 1) - 1) // self.sw + 1)
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def conv2d(ctx: Ctx, x: NHWC, cw: ConvW, y: NHWC, *, act=ACT_NONE, alpha=0.0, res: NHWC | None = None,
+           res_after=False, res_offset=(0, 0), nc_scale=None, in_scale=None, pre_act=ACT_NONE, pre_alpha=0.0,
+           pix_add=None, pix_w=0.0, scale=None, shift=None, force_tile=0, force_splits=0):
+    """Fused conv (see s2v_conv_params).  nc_scale / in_scale: [N, C] device tensors."""
+    oh, ow = cw.out_hw(x.h, x.w)
+    assert x.c == cw.cin, f"conv: input has {x.c} channels, weights expect {cw.cin}"
+    assert (y.n, y.h, y.w, y.c) == (x.n, oh, ow, cw.cout), f"conv: output view {(y.n, y.h, y.w, y.c)} != {(x.n, oh, ow, cw.cout)}"
+    p = _lib.ConvParams()
+    p.x, p.n, p.h, p.w, p.cin, p.xcs = x.ptr, x.n, x.h, x.w, x.c, x.cs
+    p.in_mode, p.pad_mode, p.pre_act, p.pre_alpha = cw.in_mode, cw.pad_mode, pre_act, pre_alpha
+    if in_scale is not None:
+        p.in_scale, p.in_scale_ns = in_scale.data_ptr(), in_scale.stride(0)
+    p.kh, p.kw, p.sh, p.sw, p.ph, p.pw, p.dh, p.dw = cw.kh, cw.kw, cw.sh, cw.sw, cw.ph, cw.pw, cw.dh, cw.dw
+    p.wt, p.kpad, p.npad, p.cout = cw.wt.data_ptr(), cw.kpad, cw.npad, cw.cout
+    p.y, p.oh, p.ow, p.ycs = y.ptr, oh, ow, y.cs
+    sc = cw.scale if scale is None else scale
+    sh = cw.shift if shift is None else shift
+    p.scale, p.shift = _ptr(sc), _ptr(sh)
+    if nc_scale is not None:
+        p.nc_scale, p.nc_scale_ns = nc_scale.data_ptr(), nc_scale.stride(0)
+    if pix_add is not None:
+        p.pix_add, p.pix_w = pix_add.data_ptr(), pix_w
+    if res is not None:
+        p.res, p.res_cs, p.res_h, p.res_w = res.ptr, res.cs, res.h, res.w
+        p.res_oy, p.res_ox = res_offset
+        p.res_after_act = int(res_after)
+    p.act, p.alpha = act, alpha
+    p.batch = 1
+    p.force_tile, p.force_splits = force_tile, force_splits
+    need = ctx.lib.s2v_conv2d_ws_bytes(ctypes.byref(p))
+    p.ws, p.ws_bytes = ctx.ws.get(need)
+    check(ctx.lib.s2v_conv2d(ctypes.byref(p), ctx.stream), "s2v_conv2d")
+    return y
+
+
+def gemm_kn(ctx: Ctx, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, batch: int, a_bs: int, b_bs: int,
+            out_bs: int, res: torch.Tensor | None = None, res_bs: int = 0, act=ACT_NONE, alpha=0.0,
+            force_tile=0, force_splits=0):
+    """Batched out[z] = a[z] @ b[z] (+res[z]) with a [M, K] row-major (K contiguous, lda = K),
+    b [K, N] row-major (ldb = N), out [M, N] (ldc = N).  Used for the FourierUnit DFT products."""
+    M, K = a.shape[-2], a.shape[-1]
+    N = b.shape[-1]
+    p = _lib.ConvParams()
+    p.x, p.n, p.h, p.w, p.cin, p.xcs = a.data_ptr(), 1, 1, M, K, K
+    p.kh = p.kw = p.sh = p.sw = p.dh = p.dw = 1
+    p.wt, p.cout, p.b_kn, p.ldb = b.data_ptr(), N, 1, N
+    p.y, p.oh, p.ow, p.ycs = out.data_ptr(), 1, M, N
+    if res is not None:
+        p.res, p.res_cs, p.res_h, p.res_w = res.data_ptr(), N, 1, M
+        p.res_bs = res_bs
+    p.act, p.alpha = act, alpha
+    p.batch, p.x_bs, p.w_bs, p.y_bs = batch, a_bs, b_bs, out_bs
+    p.force_tile, p.force_splits = force_tile, force_splits
+    need = ctx.lib.s2v_conv2d_ws_bytes(ctypes.byref(p))
+    p.ws, p.ws_bytes = ctx.ws.get(need)
+    check(ctx.lib.s2v_conv2d(ctypes.byref(p), ctx.stream), "s2v_conv2d(gemm)")
+    return out
+
+
+def layernorm2d(ctx: Ctx, x: NHWC, weight, bias, y: NHWC, *, act=ACT_LRELU, alpha=0.1, pool=False,
+                res: NHWC | None = None, eps=1e-5):
+    need = ctx.lib.s2v_layernorm2d_ws_bytes(x.n, x.h, x.w, x.c)
+    ws, nb = ctx.ws.get(need)
+    check(ctx.lib.s2v_layernorm2d(x.ptr, x.n, x.h, x.w, x.c, x.cs, weight.data_ptr(), bias.data_ptr(), eps, act, alpha,
+                                  int(pool), None if res is None else res.ptr, 0 if res is None else res.cs,
+                                  y.ptr, y.cs, ws, nb, ctx.stream), "s2v_layernorm2d")
+    return y
+
+
+def instnorm(ctx: Ctx, x: NHWC, y: NHWC, gamma=None, beta=None, gb_ns=0, *, act=ACT_NONE, alpha=0.0,
+             res: NHWC | None = None, eps=1e-5):
+    """gamma/beta: raw device pointers (ints) or None; gb_ns = per-sample row stride."""
+    need = ctx.lib.s2v_instnorm_ws_bytes(x.n, x.h, x.w, x.c)
+    ws, nb = ctx.ws.get(need)
+    check(ctx.lib.s2v_instnorm_adain(x.ptr, x.n, x.h, x.w, x.c, x.cs, gamma, beta, gb_ns, eps, act, alpha,
+                                     None if res is None else res.ptr, 0 if res is None else res.cs, y.ptr, y.cs,
+                                     ws, nb, ctx.stream), "s2v_instnorm_adain")
+    return y
+
+
+def adain_params(ctx: Ctx, hid: torch.Tensor, nhidden: int, w2t: torch.Tensor, bias: torch.Tensor, seg: torch.Tensor,
+                 out: torch.Tensor):
+    batch, total = out.shape
+    check(ctx.lib.s2v_adain_params(hid.data_ptr(), batch, hid.stride(0), nhidden, w2t.data_ptr(), bias.data_ptr(),
+                                   seg.data_ptr(), total, out.data_ptr(), out.stride(0), ctx.stream),
+          "s2v_adain_params")
+    return out
+
+
+def modconv_demod(ctx: Ctx, s: torch.Tensor, wsq: torch.Tensor, out: torch.Tensor, *, eps=1e-8, post=1.0):
+    """s: [B, cin] view (row stride s.stride(0)), wsq: [cout, cin], out: [B, cout]."""
+    batch, cin = s.shape
+    cout = wsq.shape[0]
+    check(ctx.lib.s2v_modconv_demod(s.data_ptr(), batch, s.stride(0), cin, wsq.data_ptr(), cout, eps, post,
+                                    out.data_ptr(), out.stride(0), ctx.stream), "s2v_modconv_demod")
+    return out
+
+
+def torch_bilinear_scale(in_size: int, out_size: int, scale_factor=None) -> float:
+    """area_pixel_compute_scale (align_corners=False) as PyTorch computes it (float32)."""
+    if scale_factor is not None and scale_factor > 0:
+        return float(torch.tensor(1.0 / scale_factor, dtype=torch.float32))
+    return float(torch.tensor(in_size, dtype=torch.float32) / out_size)
+
+
+def resize(ctx: Ctx, x_ptr: int, x_shape, x_strides, y_ptr: int, y_hw, y_strides, *, scale_factor=None,
+           mode=0):
+    """x_shape = (n, c, ih, iw); strides (sn, sc, sy, sx) in elements, for input and output."""
+    n, c, ih, iw = x_shape
+    oh, ow = y_hw
+    sh = torch_bilinear_scale(ih, oh, scale_factor) if mode == 0 else (
+        float(torch.tensor(1.0 / scale_factor, dtype=torch.float32)) if scale_factor else ih / oh)
+    sw = torch_bilinear_scale(iw, ow, scale_factor) if mode == 0 else (
+        float(torch.tensor(1.0 / scale_factor, dtype=torch.float32)) if scale_factor else iw / ow)
+    check(ctx.lib.s2v_resize(x_ptr, n, c, ih, iw, *x_strides, y_ptr, oh, ow, *y_strides, sh, sw, mode, ctx.stream),
+          "s2v_resize")
+
+
+def nhwc_strides(v: NHWC):
+    return (v.h * v.w * v.cs, 1, v.w * v.cs, v.cs)
+
+
+def resize_nhwc(ctx: Ctx, x: NHWC, y: NHWC, scale_factor=None, mode=0):
+    resize(ctx, x.ptr, (x.n, x.c, x.h, x.w), nhwc_strides(x), y.ptr, (y.h, y.w), nhwc_strides(y),
+           scale_factor=scale_factor, mode=mode)
+    return y
+
+
+def nchw_to_nhwc(ctx: Ctx, x: torch.Tensor, y: NHWC, size=None):
+    """NCHW device tensor (any strides) -> NHWC view, optionally bilinear-resized to y's size."""
+    _require_cuda(x, "nchw_to_nhwc")
+    n, c, h, w = x.shape
+    sn, sc, sy, sx = x.stride()
+    resize(ctx, x.data_ptr(), (n, c, h, w), (sn, sc, sy, sx), y.ptr, (y.h, y.w), nhwc_strides(y))
+    return y
+
+
+def nhwc_to_nchw(ctx: Ctx, x: NHWC, out: torch.Tensor, crop=(0, 0)):
+    """NHWC view (optionally cropped by (top, left) to out's H, W) -> contiguous NCHW tensor."""
+    n, c, oh, ow = out.shape
+    base = x.ptr + F32 * (crop[0] * x.w + crop[1]) * x.cs
+    resize(ctx, base, (n, c, oh, ow), nhwc_strides(x), out.data_ptr(), (oh, ow), out.stride())
+    return out
+
+
+def pad_reflect(ctx: Ctx, x: NHWC, y: NHWC, pads):
+    pt, pb, pl, pr = pads
+    check(ctx.lib.s2v_pad_reflect(x.ptr, x.n, x.h, x.w, x.c, x.cs, pt, pb, pl, pr, y.ptr, y.cs, ctx.stream),
+          "s2v_pad_reflect")
+    return y
+
+
+def row_layernorm(ctx: Ctx, x: torch.Tensor, weight, bias, y: torch.Tensor, eps=1e-5):
+    rows, dim = x.shape
+    check(ctx.lib.s2v_row_layernorm(x.data_ptr(), rows, dim, x.stride(0), weight.data_ptr(), bias.data_ptr(), eps,
+                                    y.data_ptr(), y.stride(0), ctx.stream), "s2v_row_layernorm")
+    return y
+
+
+def attention(ctx: Ctx, q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: torch.Tensor, *, batch, heads,
+              tokens, dim_head=64, scale=None):
+    """q, k, v, out: [batch*tokens, *] row views (row stride = stride(0)); head h = cols [64h, 64h+64)."""
+    scale = dim_head ** -0.5 if scale is None else scale
+    check(ctx.lib.s2v_attention(q.data_ptr(), k.data_ptr(), v.data_ptr(), batch, heads, tokens, dim_head,
+                                q.stride(0), k.stride(0), v.stride(0), tokens * q.stride(0), tokens * k.stride(0),
+                                tokens * v.stride(0), scale, out.data_ptr(), out.stride(0), tokens * out.stride(0),
+                                ctx.stream), "s2v_attention")
+    return out
+
+
+def flow_warp(ctx: Ctx, flow: NHWC, src: torch.Tensor, y: NHWC):
+    """flow: NHWC view with >= 2 channels (x, y); src: NCHW-strided device tensor."""
+    n, c, h, w = src.shape
+    check(ctx.lib.s2v_flow_warp(flow.ptr, flow.n, flow.h, flow.w, flow.cs, src.data_ptr(), c, h, w, *src.stride(),
+                                y.ptr, y.cs, ctx.stream), "s2v_flow_warp")
+    return y
+
+
+def gaussian_noise(ctx: Ctx, out: torch.Tensor, seed: int, offset: int = 0):
+    check(ctx.lib.s2v_gaussian_noise(out.data_ptr(), out.numel(), seed & (2 ** 64 - 1), offset & (2 ** 64 - 1),
+                                     ctx.stream), "s2v_gaussian_noise")
+    return out
+
+
+# ----------------------------------------------------------------------------- DFT matrices
+_DFT_CACHE = {}
+
+
+def fourier_matrices(h: int, w: int, device):
+    """Real matrices of torch.fft.rfftn / irfftn(s=(h, w)) with norm='ortho' (ffc.py:99, :121).
+
+    D2  [2F, P]: spectrum rows ordered (u*Wf + v)*2 + part (part 0 = real, 1 = imag)
+    Iv  [P, 2F]: the inverse (Hermitian c2r) acting on the same row order.
+    Built by applying torch.fft (float64) to basis vectors, so they are exactly the reference's
+    transforms, including the c2r treatment of the imaginary DC/Nyquist bins."""
+    key = (h, w, str(device))
+    if key not in _DFT_CACHE:
+        P, wf = h * w, w // 2 + 1
+        F = h * wf
+        eye = torch.eye(P, dtype=torch.float64).reshape(P, h, w)
+        spec = torch.fft.rfftn(eye, dim=(-2, -1), norm="ortho").reshape(P, F)      # [P, F] complex
+        d2 = torch.stack([spec.real, spec.imag], -1).reshape(P, 2 * F).t()           # [2F, P]
+        basis = torch.zeros(2 * F, F, dtype=torch.complex128)
+        idx = torch.arange(F)
+        basis[2 * idx, idx] = 1.0
+        basis[2 * idx + 1, idx] = 1.0j
+        iv = torch.fft.irfftn(basis.reshape(2 * F, h, wf), s=(h, w), dim=(-2, -1), norm="ortho")
+        iv = iv.reshape(2 * F, P).t()                                                # [P, 2F]
+        _DFT_CACHE[key] = (d2.float().contiguous().to(device), iv.float().contiguous().to(device))
+    return _DFT_CACHE[key]

@@ -1,0 +1,138 @@
+"""End-to-end parity of the HIP models (s2v_amd.models, drop-in for reference models/) against
+the reference outputs stored in tests/golden/ (and the CPU oracle for larger batches).
+
+Tolerances (fp32 everywhere; reference fp32-vs-fp64 spread 5e-4..7e-4):
+  LNet  [0,1] output  max|d| <= 2e-3, mean|d| <= 1e-4;  pre-sigmoid logits max|d| <= 5e-3
+  ENet  output (unclamped, |x| <= ~9)  max|d| <= 1e-2, mean|d| <= 5e-4;  low as LNet
+  DNet  fake/warp  max|d| <= 2e-3 (tanh-saturated regions amplify nothing);  flow max|d| <= 1e-3
+"""
+import numpy as np
+import pytest
+import torch
+
+import s2v_import  # noqa: F401
+from helpers import synth_sd, max_abs, check_probe
+from s2v_amd import synth
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _model(name):
+    from s2v_amd import models
+    m = {"lnet": models.LNet, "enet": models.ENet, "dnet": models.DNet}[name]()
+    m.load_state_dict(synth_sd(name), strict=True)
+    return m.eval()
+
+
+@pytest.fixture(scope="module")
+def lnet():
+    return _model("lnet")
+
+
+@pytest.fixture(scope="module")
+def enet():
+    return _model("enet")
+
+
+@pytest.fixture(scope="module")
+def dnet():
+    return _model("dnet")
+
+
+def test_lnet_matches_reference(lnet, golden):
+    g = golden("lnet_b2_96")
+    mel, face, _ = synth.lipsync_inputs("golden.lnet", 2, 96)
+    out = lnet(torch.from_numpy(mel).to(DEV), torch.from_numpy(face).to(DEV))
+    m, mean = max_abs(out, g["out"])
+    assert m <= 2e-3 and mean <= 1e-4, (m, mean)
+
+
+def test_lnet_intermediates(lnet, golden):
+    """Audio feature and pre-sigmoid logits through the engine directly."""
+    from s2v_amd import ops
+    from s2v_amd.ops import NHWC
+    g = golden("lnet_b2_96")
+    eng, ctx = lnet._engine(torch.device(DEV))
+    mel, face, _ = synth.lipsync_inputs("golden.lnet", 2, 96)
+    x6 = NHWC.empty(2, 96, 96, 6, DEV)
+    ops.nchw_to_nhwc(ctx, torch.from_numpy(face).to(DEV), x6)
+    out = NHWC.empty(2, 96, 96, 3, DEV)
+    logits = NHWC.empty(2, 96, 96, 3, DEV)
+    eng.forward(ctx, torch.from_numpy(mel).to(DEV), x6, out, logits=logits)
+    lg = logits.t.permute(0, 3, 1, 2).cpu()
+    m, mean = max_abs(lg, g["logits"])
+    assert m <= 5e-3 and mean <= 3e-4, (m, mean)
+    z = eng.bank  # audio feature is the bank's input; compare via the stored params' source
+    assert z.params.shape == (2, z.total)
+
+
+def test_lnet_5d_input_fold(lnet):
+    mel, face, _ = synth.lipsync_inputs("lnet.5d", 4, 96)
+    m = torch.from_numpy(mel).to(DEV)
+    f = torch.from_numpy(face).to(DEV)
+    flat = lnet(m, f)
+    # [B, T, 1, 80, 16] / [B, 6, T, H, W] with B=2, T=2 (LNet.py:124-127)
+    m5 = torch.stack([m[:2], m[2:]], 1)
+    f5 = torch.stack([f[:2], f[2:]], 2)
+    out5 = lnet(m5, f5)
+    assert out5.shape == (2, 3, 2, 96, 96)
+    assert (out5[:, :, 0] - flat[:2]).abs().max() < 1e-6 and (out5[:, :, 1] - flat[2:]).abs().max() < 1e-6
+
+
+def test_enet_matches_reference(enet, golden):
+    for size in (256, 384):
+        g = golden(f"enet_b1_{size}")
+        mel, face, gt = synth.lipsync_inputs(f"golden.enet{size}", 1, size)
+        out, low = enet(torch.from_numpy(mel).to(DEV), torch.from_numpy(face).to(DEV), torch.from_numpy(gt).to(DEV))
+        m, mean = max_abs(low, g["low"])
+        assert m <= 2e-3 and mean <= 1e-4, ("low", size, m, mean)
+        if "out" in g.files:
+            m, mean = max_abs(out, g["out"])
+            assert m <= 1e-2 and mean <= 5e-4, ("out", size, m, mean)
+        else:
+            check_probe(out, g, "out", atol=1e-2)
+
+
+def test_enet_batch16_vs_oracle(enet):
+    """Full-size bench workload batch (B=16, 256x256 crops) against the CPU oracle on 2 frames of
+    it, and batch-invariance (frames are independent) on the rest."""
+    from oracle import nets
+    mel, face, gt = synth.lipsync_inputs("enet.b16", 16, 256)
+    out, low = enet(torch.from_numpy(mel).to(DEV), torch.from_numpy(face).to(DEV), torch.from_numpy(gt).to(DEV))
+    sd = synth_sd("enet")
+    with torch.no_grad():
+        ro, rl = nets.enet_forward(sd, torch.from_numpy(mel[:2]), torch.from_numpy(face[:2]), torch.from_numpy(gt[:2]))
+    m, mean = max_abs(out[:2], ro)
+    assert m <= 1e-2 and mean <= 5e-4, (m, mean)
+    out2, _ = enet(torch.from_numpy(mel[8:10]).to(DEV), torch.from_numpy(face[8:10]).to(DEV),
+                   torch.from_numpy(gt[8:10]).to(DEV))
+    assert (out2 - out[8:10]).abs().max() < 1e-4
+
+
+def test_dnet_matches_reference(dnet, golden):
+    for size, batch in ((128, 2), (256, 1)):
+        g = golden(f"dnet_b{batch}_{size}")
+        src, coeff = synth.dnet_inputs(f"golden.dnet{size}", batch, size)
+        out = dnet(torch.from_numpy(src).to(DEV), torch.from_numpy(coeff).to(DEV))
+        assert max_abs(out["flow_field"], g["flow"])[0] <= 1e-3
+        for k in ("warp_image", "fake_image"):
+            if k in g.files:
+                m, mean = max_abs(out[k], g[k])
+                assert m <= 2e-3 and mean <= 1e-4, (k, m, mean)
+            else:
+                check_probe(out[k], g, k, atol=2e-3)
+
+
+def test_dnet_warp_stage(dnet):
+    src, coeff = synth.dnet_inputs("dnet.stage", 1, 128)
+    full = dnet(torch.from_numpy(src).to(DEV), torch.from_numpy(coeff).to(DEV))
+    warp = dnet(torch.from_numpy(src).to(DEV), torch.from_numpy(coeff).to(DEV), stage="warp")
+    assert "fake_image" not in warp
+    assert torch.equal(warp["warp_image"], full["warp_image"])
+
+
+def test_cpu_inputs_fail_loudly(lnet):
+    mel, face, _ = synth.lipsync_inputs("cpu", 1, 96)
+    with pytest.raises(RuntimeError):
+        lnet(torch.from_numpy(mel), torch.from_numpy(face))

@@ -1,0 +1,313 @@
+"""Per-kernel parity of libs2v (called through the C ABI) against fp64 CPU references.
+
+fp32 kernels vs fp64 references: tolerances are stated per test; for the MFMA convolutions the
+bound is 2e-6 * sum|a*b| (k-ordered fp32 fma chains, < 1.5e-7*K relative to that sum for K <= 10^4,
+cdna_hip_programming.md §3 'FP32-input MFMA').
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import s2v_import  # noqa: F401
+
+pytestmark = pytest.mark.gpu
+
+if torch.cuda.is_available():
+    from s2v_amd import ops
+    from s2v_amd.ops import NHWC, ConvW
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return ops.Ctx(DEV)
+
+
+def nhwc(t):
+    return NHWC(t.permute(0, 2, 3, 1).contiguous().to(DEV))
+
+
+def to_nchw(v: NHWC):
+    return v.t[..., v.coff: v.coff + v.c].permute(0, 3, 1, 2).double().cpu()
+
+
+def rnd(*shape, seed=0, lo=-1.0, hi=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return lo + (hi - lo) * torch.rand(*shape, generator=g, dtype=torch.float64)
+
+
+def act_ref(v, act, alpha):
+    if act == ops.ACT_RELU:
+        return F.relu(v)
+    if act == ops.ACT_LRELU:
+        return F.leaky_relu(v, alpha)
+    if act == ops.ACT_SIGMOID:
+        return torch.sigmoid(v)
+    if act == ops.ACT_TANH:
+        return torch.tanh(v)
+    if act == ops.ACT_GELU_TANH:
+        return 0.5 * v * (1 + torch.tanh(math.sqrt(2 / math.pi) * (v + 0.044715 * v ** 3)))
+    return v
+
+
+def conv_bound(x, w, stride, padding, dilation, transposed=False, op=0):
+    f = F.conv_transpose2d if transposed else F.conv2d
+    kw = dict(stride=stride, padding=padding, dilation=dilation)
+    if transposed:
+        kw["output_padding"] = op
+    return f(x.abs(), w.abs(), **kw)
+
+
+CONV_CASES = [
+    # (n, cin, h, w, cout, k, stride, pad, dil, mode, pad_mode, tile, splits)
+    (2, 64, 17, 19, 96, 3, 1, 1, 1, "direct", "zero", 0, 0),
+    (2, 64, 16, 16, 128, 3, 1, 1, 1, "direct", "zero", 1, 0),
+    (2, 64, 16, 16, 128, 3, 1, 1, 1, "direct", "zero", 2, 3),
+    (1, 32, 20, 12, 64, 3, 2, 1, 1, "direct", "zero", 3, 0),
+    (2, 32, 12, 12, 64, 3, 1, 1, 1, "direct", "zero", 4, 2),
+    (2, 96, 10, 10, 200, 3, 1, 1, 1, "direct", "reflect", 5, 0),
+    (2, 48, 12, 12, 40, 3, 1, 1, 1, "direct", "reflect", 6, 4),
+    (1, 3, 24, 24, 64, 7, 1, 3, 1, "direct", "zero", 0, 0),
+    (2, 6, 20, 20, 33, 4, 2, 1, 1, "direct", "zero", 0, 0),
+    (2, 73, 1, 26, 40, (1, 7), 1, 0, 1, "direct", "zero", 0, 0),
+    (2, 40, 1, 20, 40, (1, 3), 1, 0, (1, 3), "direct", "zero", 0, 0),
+    (2, 32, 8, 8, 48, 3, 1, 1, 1, "up2", "zero", 0, 0),
+    (2, 64, 6, 7, 32, 3, 2, 1, 1, "transposed", "zero", 0, 0),
+    (2, 64, 9, 9, 3, 7, 1, 3, 1, "direct", "zero", 0, 0),     # direct small-N kernel
+    (3, 1, 20, 16, 32, 3, (3, 1), 1, 1, "direct", "zero", 0, 0),
+    (2, 128, 3, 3, 256, 3, (3, 2), 1, 1, "direct", "zero", 0, 0),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES, ids=[str(i) for i in range(len(CONV_CASES))])
+def test_conv2d(ctx, case):
+    n, cin, h, w, cout, k, stride, pad, dil, mode, pad_mode, tile, splits = case
+    kh, kw = (k, k) if isinstance(k, int) else k
+    transposed = mode == "transposed"
+    wshape = (cin, cout, kh, kw) if transposed else (cout, cin, kh, kw)
+    wt = rnd(*wshape, seed=1) / math.sqrt(cin * kh * kw)
+    bias = rnd(cout, seed=2)
+    x = rnd(n, cin, h, w, seed=3)
+    st = stride if isinstance(stride, tuple) else (stride, stride)
+    dl = dil if isinstance(dil, tuple) else (dil, dil)
+    cw = ConvW(wt.float(), bias.float(), DEV, stride=st, padding=pad, dilation=dl, transposed=transposed,
+               output_padding=1 if transposed else 0,
+               pad_mode=ops.PAD_REFLECT if pad_mode == "reflect" else ops.PAD_ZERO,
+               in_mode=ops.IN_NEAREST_UP2 if mode == "up2" else ops.IN_DIRECT)
+    xin = F.interpolate(x, scale_factor=2, mode="nearest") if mode == "up2" else x
+    if transposed:
+        ref = F.conv_transpose2d(x, wt, bias, st, pad, output_padding=1, dilation=dl)
+        bound = conv_bound(x, wt, st, pad, dl, True, 1)
+    else:
+        xp = F.pad(xin, (pad,) * 4, mode="reflect") if pad_mode == "reflect" else xin
+        p = 0 if pad_mode == "reflect" else pad
+        ref = F.conv2d(xp, wt, bias, st, p, dl)
+        bound = conv_bound(xp, wt, st, p, dl)
+    oh, ow = ref.shape[-2:]
+    res = rnd(n, cout, oh, ow, seed=4)
+    ncs = rnd(n, cout, seed=5, lo=0.5, hi=1.5)
+    for variant in range(3):
+        # 0: bias + lrelu ; 1: nc_scale + residual-before + sigmoid ; 2: residual-after + tanh + wide out slice
+        y = NHWC.empty(n, oh, ow, cout + 5, DEV).slice(3, cout)
+        kwargs = dict(force_tile=tile, force_splits=splits)
+        exp = ref.clone()
+        if variant == 0:
+            kwargs.update(act=ops.ACT_LRELU, alpha=0.2)
+            exp = F.leaky_relu(exp, 0.2)
+        elif variant == 1:
+            rv = nhwc(res.float())
+            kwargs.update(act=ops.ACT_SIGMOID, res=rv, nc_scale=ncs.float().to(DEV))
+            exp = torch.sigmoid((exp - bias[None, :, None, None]) * ncs[:, :, None, None] + bias[None, :, None, None]
+                                + res)
+        else:
+            rv = nhwc(res.float())
+            kwargs.update(act=ops.ACT_TANH, res=rv, res_after=True)
+            exp = torch.tanh(exp) + res
+        ops.conv2d(ctx, nhwc(x.float()), cw, y, **kwargs)
+        got = to_nchw(y)
+        err = (got - exp).abs()
+        lim = 2e-6 * (bound + 1) + 1e-6
+        if variant == 1:
+            lim = lim * 1.5
+        assert (err <= lim).all(), f"variant {variant}: max err {err.max():.3e}, rel {(err / lim).max():.2f}"
+
+
+def test_conv2d_prologue(ctx):
+    n, cin, h, w, cout = 2, 32, 10, 10, 64
+    wt = rnd(cout, cin, 3, 3, seed=7) / math.sqrt(cin * 9)
+    x = rnd(n, cin, h, w, seed=8)
+    s = rnd(n, cin, seed=9, lo=0.5, hi=2.0)
+    cw = ConvW(wt.float(), None, DEV, padding=1)
+    y = NHWC.empty(n, h, w, cout, DEV)
+    ops.conv2d(ctx, nhwc(x.float()), cw, y, in_scale=s.float().to(DEV), pre_act=ops.ACT_LRELU, pre_alpha=0.1)
+    ref = F.conv2d(F.leaky_relu(x * s[:, :, None, None], 0.1), wt, padding=1)
+    assert (to_nchw(y) - ref).abs().max() < 1e-5
+
+
+def test_gemm_kn_batched(ctx):
+    b, M, K, N = 3, 70, 144, 44
+    a = rnd(M, K, seed=10).float()
+    bm = rnd(b, K, N, seed=11).float()
+    res = rnd(b, M, N, seed=12).float()
+    out = torch.empty(b, M, N, device=DEV)
+    ops.gemm_kn(ctx, a.to(DEV), bm.to(DEV), out, batch=b, a_bs=0, b_bs=K * N, out_bs=M * N, res=res.to(DEV),
+                res_bs=M * N)
+    ref = torch.einsum("mk,bkn->bmn", a.double(), bm.double()) + res.double()
+    assert (out.double().cpu() - ref).abs().max() < 2e-5
+
+
+def test_layernorm2d(ctx):
+    x = rnd(2, 40, 12, 10, seed=13) * 3 + 1
+    wgt, b = rnd(40, seed=14), rnd(40, seed=15)
+    res = rnd(2, 40, 6, 5, seed=16)
+    xv = nhwc(x.float())
+    for pool in (False, True):
+        oh, ow = (6, 5) if pool else (12, 10)
+        y = NHWC.empty(2, oh, ow, 40, DEV)
+        ops.layernorm2d(ctx, xv, wgt.float().to(DEV), b.float().to(DEV), y, act=ops.ACT_LRELU, alpha=0.1, pool=pool,
+                        res=nhwc(res.float()) if pool else None)
+        ref = F.leaky_relu(F.layer_norm(x, x.shape[1:], wgt[:, None, None].expand(x.shape[1:]),
+                                        b[:, None, None].expand(x.shape[1:]), 1e-5), 0.1)
+        if pool:
+            ref = F.avg_pool2d(ref, 2) + res
+        assert (to_nchw(y) - ref).abs().max() < 2e-5
+
+
+def test_instnorm_adain(ctx):
+    for (h, w) in ((12, 12), (70, 40)):
+        x = rnd(2, 70, h, w, seed=17) * 2 - 0.5
+        g, bt = rnd(2, 70, seed=18), rnd(2, 70, seed=19)
+        gb = torch.cat([g, bt], 1).float().to(DEV)
+        res = rnd(2, 70, h, w, seed=20)
+        y = NHWC.empty(2, h, w, 70, DEV)
+        ops.instnorm(ctx, nhwc(x.float()), y, gb.data_ptr(), gb.data_ptr() + 4 * 70, 140, act=ops.ACT_LRELU,
+                     alpha=0.01, res=nhwc(res.float()))
+        ref = F.leaky_relu(F.instance_norm(x, eps=1e-5) * (1 + g[:, :, None, None]) + bt[:, :, None, None], 0.01) + res
+        assert (to_nchw(y) - ref).abs().max() < 2e-5
+
+
+def test_row_layernorm_attention(ctx):
+    b, T, heads = 2, 144, 4
+    x = rnd(b * T, 512, seed=21).float().to(DEV)
+    wgt, bias = rnd(512, seed=22).float().to(DEV), rnd(512, seed=23).float().to(DEV)
+    y = torch.empty_like(x)
+    ops.row_layernorm(ctx, x, wgt, bias, y)
+    ref = F.layer_norm(x.double().cpu(), (512,), wgt.double().cpu(), bias.double().cpu())
+    assert (y.double().cpu() - ref).abs().max() < 2e-5
+    qk = rnd(b * T, 512, seed=24).float().to(DEV)
+    v = rnd(b * T, 256, seed=25).float().to(DEV)
+    o = torch.empty(b * T, 256, device=DEV)
+    ops.attention(ctx, qk[:, :256], qk[:, 256:], v, o, batch=b, heads=heads, tokens=T)
+    q = qk[:, :256].double().cpu().reshape(b, T, heads, 64).transpose(1, 2)
+    k = qk[:, 256:].double().cpu().reshape(b, T, heads, 64).transpose(1, 2)
+    vv = v.double().cpu().reshape(b, T, heads, 64).transpose(1, 2)
+    ref = (torch.softmax(q @ k.transpose(-1, -2) * 0.125, -1) @ vv).transpose(1, 2).reshape(b * T, 256)
+    assert (o.double().cpu() - ref).abs().max() < 1e-5
+
+
+def test_adain_params_and_demod(ctx):
+    b, nh, L = 3, 128, 5
+    hid = rnd(b, L * nh, seed=26).float().to(DEV)
+    total = 300
+    seg = torch.randint(0, L, (total,), generator=torch.Generator().manual_seed(0)).int()
+    w2 = rnd(total, nh, seed=27).float()
+    bias = rnd(total, seed=28).float()
+    out = torch.empty(b, total, device=DEV)
+    ops.adain_params(ctx, hid, nh, w2.t().contiguous().to(DEV), bias.to(DEV), seg.to(DEV), out)
+    h = hid.double().cpu().reshape(b, L, nh)
+    ref = torch.stack([h[:, int(seg[o])] @ w2[o].double() for o in range(total)], 1) + bias.double()
+    assert (out.double().cpu() - ref).abs().max() < 1e-4
+    s = rnd(b, 40, seed=29).float().to(DEV)
+    wsq = rnd(24, 40, seed=30, lo=0, hi=1).float().to(DEV)
+    d = torch.empty(b, 24, device=DEV)
+    ops.modconv_demod(ctx, s, wsq, d, eps=1e-8, post=math.sqrt(2))
+    ref = torch.rsqrt((s.double().cpu() ** 2) @ wsq.double().cpu().t() + 1e-8) * math.sqrt(2)
+    assert ((d.double().cpu() - ref).abs() / ref).max() < 1e-5
+
+
+@pytest.mark.parametrize("shape", [((2, 3, 384, 384), (96, 96), None), ((2, 5, 64, 64), None, 0.5),
+                                   ((1, 4, 50, 50), None, 2), ((1, 3, 256, 256), (256, 256), None),
+                                   ((2, 6, 100, 90), (37, 53), None)])
+def test_resize_bilinear(ctx, shape):
+    ishape, size, sf = shape
+    x = rnd(*ishape, seed=31).float()
+    ref = F.interpolate(x, size=size, scale_factor=sf, mode="bilinear", align_corners=False)
+    y = NHWC.empty(ishape[0], ref.shape[2], ref.shape[3], ishape[1], DEV)
+    ops.resize_nhwc(ctx, nhwc(x), y, scale_factor=sf)
+    assert (to_nchw(y) - ref.double()).abs().max() < 2e-6
+    y2 = NHWC.empty(ishape[0], ref.shape[2], ref.shape[3], ishape[1], DEV)
+    ops.nchw_to_nhwc(ctx, x.to(DEV), y2) if sf is None else ops.resize_nhwc(ctx, nhwc(x), y2, scale_factor=sf)
+    assert (to_nchw(y2) - ref.double()).abs().max() < 2e-6
+
+
+def test_pad_reflect_and_crop(ctx):
+    x = rnd(2, 3, 96, 96, seed=32).float()
+    y = NHWC.empty(2, 100, 100, 3, DEV)
+    ops.pad_reflect(ctx, nhwc(x), y, (2, 2, 2, 2))
+    ref = F.pad(x, (2, 2, 2, 2), mode="reflect")
+    assert torch.equal(to_nchw(y).float(), ref)
+    out = torch.empty(2, 3, 84, 84, device=DEV)
+    ops.nhwc_to_nchw(ctx, y, out, crop=(8, 8))
+    assert torch.equal(out.cpu(), ref[:, :, 8:-8, 8:-8])
+
+
+def test_flow_warp_matches_golden(ctx, golden):
+    from s2v_amd import synth
+    g = golden("ops")
+    for key, fshape, sshape, name in (("golden.flow", (2, 2, 16, 16), (2, 3, 64, 64), "warp"),
+                                      ("golden.flow2", (1, 2, 32, 32), (1, 3, 32, 32), "warp_same")):
+        lo, hi = (-3.0, 3.0) if name == "warp" else (-2.0, 2.0)
+        flow = torch.from_numpy(synth.hash_array(key, fshape, lo, hi))
+        src = torch.from_numpy(synth.hash_array(key + ".src", sshape)).to(DEV)
+        y = NHWC.empty(sshape[0], sshape[2], sshape[3], 3, DEV)
+        ops.flow_warp(ctx, nhwc(flow), src, y)
+        assert np.abs(to_nchw(y).numpy() - g[name]).max() < 2e-5
+
+
+def test_gpen_ops_match_golden(ctx, golden):
+    from s2v_amd import synth
+    g = golden("ops")
+    x = torch.from_numpy(synth.hash_array("golden.fba.x", (2, 8, 5, 7))).to(DEV)
+    b = torch.from_numpy(synth.hash_array("golden.fba.b", (8,))).to(DEV)
+    y = torch.empty_like(x)
+    ops.check(ctx.lib.s2v_fused_bias_act(x.data_ptr(), b.data_ptr(), None, y.data_ptr(), x.numel(), 8, 35, 3, 0, 0.2,
+                                         2 ** 0.5, ctx.stream), "fba")
+    assert np.abs(y.cpu().numpy() - g["fba_out"]).max() < 1e-6
+    xi = torch.from_numpy(synth.hash_array("golden.ufd.x", (2, 3, 9, 11))).to(DEV)
+    k = torch.tensor([1.0, 3.0, 3.0, 1.0])
+    k = (k[None, :] * k[:, None]) / 64.0
+    for name, (up, down, pad) in {"up2": (2, 1, (2, 1)), "blur22": (1, 1, (2, 2)), "blur11": (1, 1, (1, 1)),
+                                  "down2": (1, 2, (1, 1))}.items():
+        kk = (k * (4 if up == 2 else 1)).to(DEV)
+        exp = g[f"ufd_{name}"]
+        oh, ow = exp.shape[-2:]
+        out = torch.empty(6, oh, ow, 1, device=DEV)
+        ops.check(ctx.lib.s2v_upfirdn2d(xi.data_ptr(), 6, 9, 11, 1, kk.data_ptr(), 4, 4, up, up, down, down, pad[0],
+                                        pad[1], pad[0], pad[1], out.data_ptr(), oh, ow, ctx.stream), "upfirdn2d")
+        assert np.abs(out.cpu().numpy().reshape(exp.shape) - exp).max() < 1e-6, name
+
+
+def test_gaussian_noise_stats(ctx):
+    y = torch.empty(1 << 20, device=DEV)
+    ops.gaussian_noise(ctx, y, 1234)
+    m, s = y.mean().item(), y.std().item()
+    assert abs(m) < 5e-3 and abs(s - 1) < 5e-3
+    y2 = torch.empty(1 << 20, device=DEV)
+    ops.gaussian_noise(ctx, y2, 1234)
+    assert torch.equal(y, y2)
+
+
+def test_fourier_matrices_match_torch_fft(ctx):
+    for h, w in ((12, 12), (24, 24), (48, 48)):
+        d2, iv = ops.fourier_matrices(h, w, DEV)
+        x = rnd(3, h, w, seed=33)
+        spec = torch.fft.rfftn(x, dim=(-2, -1), norm="ortho")
+        st = torch.stack([spec.real, spec.imag], -1).reshape(3, -1)
+        got = (d2.double().cpu() @ x.reshape(3, -1).t()).t()
+        assert (got - st).abs().max() < 1e-5
+        back = (iv.double().cpu() @ st.t()).t().reshape(3, h, w)
+        assert (back - x).abs().max() < 1e-5
