@@ -373,7 +373,7 @@ extern "C" int s2v_attention(const float *q, const float *k, const float *v, int
     S2V_REQUIRE(smem <= 160 * 1024, "attention: too many tokens for LDS");
     static bool attr_set = false;
     if (!attr_set) {
-        hipFuncSetAttribute((const void *)attention_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void *)attention_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
     attention_kernel<<<batch * heads, 256, smem, (hipStream_t)stream>>>(q, k, v, heads, tokens, ld_q, ld_k, ld_v, bs_q,
