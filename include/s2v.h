@@ -94,6 +94,9 @@ typedef struct s2v_conv_params {
  * ENet.py, DNet.py, base_blocks.py, ffc.py, transformer.py (inventory: SURVEY.md App. A). */
 int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream);
 size_t s2v_conv2d_ws_bytes(const s2v_conv_params *p);
+/* The launch plan s2v_conv2d would use: out6 = {BM, BN, WAVES_M, AVEC, B_KN, splits} of the
+ * conv_igemm<BM,BN,WAVES_M,AVEC,B_KN> instance, or {0, CO, 0, 0, 0, 1} for conv_direct_small<CO>. */
+int s2v_conv2d_plan(const s2v_conv_params *p, int *out6);
 
 /* LayerNorm2d (base_blocks.py:52-69) over (H,W,C) per sample, fused affine + act
  * (+ 2x2 average pool: DownBlock2d base_blocks.py:95-109) (+ residual after act: Jump + out,

@@ -503,6 +503,23 @@ extern "C" size_t s2v_conv2d_ws_bytes(const s2v_conv_params *p) {
     return (size_t)batch * pl.splits * (size_t)M * p->cout * sizeof(float);
 }
 
+extern "C" int s2v_conv2d_plan(const s2v_conv_params *p, int *out6) {
+    int M, K;
+    int rc = validate(p, M, K);
+    if (rc) return rc;
+    Plan pl = make_plan(p, M, K);
+    if (pl.tile < 0) {
+        out6[0] = 0; out6[1] = p->cout < 4 ? p->cout : 4; out6[2] = 0; out6[3] = 0; out6[4] = 0; out6[5] = 1;
+        return 0;
+    }
+    const TileCfg &t = kTiles[pl.tile];
+    out6[0] = t.bm; out6[1] = t.bn; out6[2] = t.wm;
+    out6[3] = (p->cin % 4 == 0) && (p->xcs % 4 == 0) && (((uintptr_t)p->x % 16) == 0) && (p->x_bs % 4 == 0);
+    out6[4] = p->b_kn != 0;
+    out6[5] = pl.splits;
+    return 0;
+}
+
 extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
     int M, K;
     int rc = validate(p, M, K);

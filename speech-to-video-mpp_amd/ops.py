@@ -20,6 +20,10 @@ from ._lib import (ACT_GELU_TANH, ACT_LRELU, ACT_NONE, ACT_RELU, ACT_SIGMOID, AC
 
 F32 = 4
 
+# Optional per-launch observer (bench.py's live roofline): called as hook(ctx, params, flops, launch)
+# where launch() performs the conv; the hook may bracket it with events.
+CONV_HOOK = None
+
 
 def _require_cuda(t: torch.Tensor, what: str):
     if not (t.is_cuda and t.dtype == torch.float32):
@@ -181,6 +185,13 @@ def conv2d(ctx: Ctx, x: NHWC, cw: ConvW, y: NHWC, *, act=ACT_NONE, alpha=0.0, re
     p.force_tile, p.force_splits = force_tile, force_splits
     need = ctx.lib.s2v_conv2d_ws_bytes(ctypes.byref(p))
     p.ws, p.ws_bytes = ctx.ws.get(need)
+    if CONV_HOOK is not None:
+        # algorithmic MACs: a transposed conv only counts real (non-inserted-zero) taps
+        taps = cw.kh * cw.kw
+        pix = x.n * x.h * x.w if cw.in_mode == IN_TRANSPOSED else x.n * oh * ow
+        flops = 2.0 * pix * taps * cw.cin * cw.cout
+        CONV_HOOK(ctx, p, flops, lambda: check(ctx.lib.s2v_conv2d(ctypes.byref(p), ctx.stream), "s2v_conv2d"))
+        return y
     check(ctx.lib.s2v_conv2d(ctypes.byref(p), ctx.stream), "s2v_conv2d")
     return y
 
@@ -205,8 +216,27 @@ def gemm_kn(ctx: Ctx, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, ba
     p.force_tile, p.force_splits = force_tile, force_splits
     need = ctx.lib.s2v_conv2d_ws_bytes(ctypes.byref(p))
     p.ws, p.ws_bytes = ctx.ws.get(need)
+    if CONV_HOOK is not None:   # DFT products: executed work, not reference-algorithmic FLOPs
+        CONV_HOOK(ctx, p, 0.0, lambda: check(ctx.lib.s2v_conv2d(ctypes.byref(p), ctx.stream), "s2v_conv2d(gemm)"))
+        return out
     check(ctx.lib.s2v_conv2d(ctypes.byref(p), ctx.stream), "s2v_conv2d(gemm)")
     return out
+
+
+def conv_symbol(ctx: Ctx, p) -> str:
+    """Kernel symbol (as rocprofv3 reports it, demangled) the launch of ``p`` runs."""
+    out = (ctypes.c_int * 6)()
+    check(ctx.lib.s2v_conv2d_plan(ctypes.byref(p), out), "s2v_conv2d_plan")
+    bm, bn, wm, avec, bkn, splits = list(out)
+    if bm == 0:
+        return f"void s2v::conv_direct_small<{bn}>(s2v::ConvArgs, int)"
+    return f"void s2v::conv_igemm<{bm}, {bn}, {wm}, {avec}, {bkn}>(s2v::ConvArgs)"
+
+
+def conv_splits(ctx: Ctx, p) -> int:
+    out = (ctypes.c_int * 6)()
+    check(ctx.lib.s2v_conv2d_plan(ctypes.byref(p), out), "s2v_conv2d_plan")
+    return out[5]
 
 
 def layernorm2d(ctx: Ctx, x: NHWC, weight, bias, y: NHWC, *, act=ACT_LRELU, alpha=0.1, pool=False,
