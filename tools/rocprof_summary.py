@@ -9,7 +9,7 @@ import sys
 def rows_from_db(path):
     db = sqlite3.connect(path)
     q = "select name, total_calls, total_duration, average, percentage from top_kernels order by total_duration desc"
-    return [(n, int(c), t / 1e3, a / 1e3, p) for n, c, t, a, p in db.execute(q)]
+    return [(n, int(c), t, a, p) for n, c, t, a, p in db.execute(q)]  # top_kernels reports microseconds
 
 
 def main():
