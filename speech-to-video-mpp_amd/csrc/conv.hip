@@ -18,6 +18,7 @@
 namespace s2v {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float f4 __attribute__((ext_vector_type(4)));   // register-native 16-byte vector
 
 struct Epi {
     const float *scale, *shift, *nc_scale, *pix_add, *res;
@@ -107,18 +108,180 @@ __device__ __forceinline__ float prologue(const ConvArgs &a, float v, int img, i
     return v;
 }
 
-template <int BM, int BN, int WAVES_M, int AVEC, int BKN>
-__global__ __launch_bounds__(256) void conv_igemm(ConvArgs a) {
+// Branch-light activation for the epilogue hot path: NONE / RELU / LRELU are one select; the
+// transcendental ones go through an out-of-line call so 64 unrolled copies stay small.
+__device__ __noinline__ float act_complex(float v, int act) { return apply_act(v, act, 0.f); }
+
+__device__ __forceinline__ float fast_act(float v, int act, float slope) {
+    if (act > S2V_ACT_LRELU) return act_complex(v, act);
+    return v >= 0.f ? v : v * slope;
+}
+
+// A operand loaders.  AMODE 0: direct conv, zero padding, no prologue, cin % 32 == 0 (a whole
+// K-slice lies in one filter tap: the tap offset is tile-uniform).  AMODE 1: any input mode,
+// cin % 4 == 0 (one tap per float4).  AMODE 2: anything (scalar gather).
+template <int AR, int AMODE>
+struct ARows {
+    long long base[AR];  // AMODE 0: element offset of (img, iy0, ix0) (may point outside the image)
+    int iy0[AR], ix0[AR];
+    int img[AR], oy[AR], ox[AR];
+    bool ok[AR];
+};
+
+template <int AR, int AMODE>
+__device__ __forceinline__ void a_rows_init(const ConvArgs &a, int m0, int ar, ARows<AR, AMODE> &R) {
+    const int hw = a.oh * a.ow;
+#pragma unroll
+    for (int j = 0; j < AR; ++j) {
+        const int m = m0 + ar + 32 * j;
+        R.ok[j] = m < a.M;
+        const int mm = R.ok[j] ? m : 0;
+        const int img = mm / hw;
+        const int rem = mm - img * hw;
+        const int oy = rem / a.ow;
+        const int ox = rem - oy * a.ow;
+        R.img[j] = img;
+        R.oy[j] = oy;
+        R.ox[j] = ox;
+        R.iy0[j] = oy * a.sh - a.ph;
+        R.ix0[j] = ox * a.sw - a.pw;
+        R.base[j] = ((long long)(img * a.h + R.iy0[j]) * a.w + R.ix0[j]) * a.xcs;
+    }
+}
+
+template <int AR, int AMODE>
+__device__ __forceinline__ void load_a(const ConvArgs &a, const float *__restrict__ x, int kt, int ak,
+                                       const ARows<AR, AMODE> &R, f4 (&ra)[AR]) {
+    const int kbase = kt * 32;
+    if (AMODE == 0) {
+        // tile-uniform tap (scalar math)
+        const int tap = kbase / a.cin;
+        const int c = kbase - tap * a.cin + ak;
+        const int ky = tap / a.kw, kx = tap - (tap / a.kw) * a.kw;
+        const int dy = ky * a.dh, dx = kx * a.dw;
+        const long long toff = ((long long)dy * a.w + dx) * a.xcs + c;
+#pragma unroll
+        for (int j = 0; j < AR; ++j) {
+            const bool ok = R.ok[j] && (unsigned)(R.iy0[j] + dy) < (unsigned)a.h &&
+                            (unsigned)(R.ix0[j] + dx) < (unsigned)a.w;
+            f4 v = {0.f, 0.f, 0.f, 0.f};
+            if (ok) v = *(const f4 *)(x + R.base[j] + toff);
+            ra[j] = v;
+        }
+    } else if (AMODE == 1) {
+        const int k = kbase + ak;
+        const bool kok = k < a.K;
+        const int tap = k / a.cin;
+        const int c = k - tap * a.cin;
+        const int ky = tap / a.kw, kx = tap - (tap / a.kw) * a.kw;
+#pragma unroll
+        for (int j = 0; j < AR; ++j) {
+            f4 v = {0.f, 0.f, 0.f, 0.f};
+            int iy, ix;
+            if (R.ok[j] && kok && map_tap(a, R.oy[j], R.ox[j], ky, kx, iy, ix)) {
+                v = *(const f4 *)(x + ((long long)(R.img[j] * a.h + iy) * a.w + ix) * a.xcs + c);
+                if (a.in_scale || a.pre_act) {
+                    v.x = prologue(a, v.x, R.img[j], c);
+                    v.y = prologue(a, v.y, R.img[j], c + 1);
+                    v.z = prologue(a, v.z, R.img[j], c + 2);
+                    v.w = prologue(a, v.w, R.img[j], c + 3);
+                }
+            }
+            ra[j] = v;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < AR; ++j) {
+            float vv[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int k = kbase + ak + e;
+                float v = 0.f;
+                if (R.ok[j] && k < a.K) {
+                    const int tap = k / a.cin;
+                    const int c = k - tap * a.cin;
+                    const int ky = tap / a.kw, kx = tap - (tap / a.kw) * a.kw;
+                    int iy, ix;
+                    if (map_tap(a, R.oy[j], R.ox[j], ky, kx, iy, ix)) {
+                        v = x[((long long)(R.img[j] * a.h + iy) * a.w + ix) * a.xcs + c];
+                        v = prologue(a, v, R.img[j], c);
+                    }
+                }
+                vv[e] = v;
+            }
+            ra[j] = f4{vv[0], vv[1], vv[2], vv[3]};
+        }
+    }
+}
+
+template <int BN, int BR, int BKN>
+__device__ __forceinline__ void load_b(const ConvArgs &a, const float *__restrict__ wt, int kt, int n0, int tid,
+                                       f4 (&rb)[BR]) {
+    const int kbase = kt * 32;
+    if (!BKN) {
+        const int ar = tid >> 3, ak = (tid & 7) * 4;
+        const float *p = wt + (long long)(n0 + ar) * a.kpad + kbase + ak;
+#pragma unroll
+        for (int j = 0; j < BR; ++j) rb[j] = *(const f4 *)(p + (long long)32 * j * a.kpad);
+    } else {
+        constexpr int NV = BN / 4, RPP = 256 / NV;
+        const int kr = tid / NV, nn = (tid - (tid / NV) * NV) * 4;
+#pragma unroll
+        for (int j = 0; j < BR; ++j) {
+            const int k = kbase + kr + RPP * j;
+            const int n = n0 + nn;
+            f4 v = {0.f, 0.f, 0.f, 0.f};
+            if (k < a.K) {
+                const float *src = wt + (long long)k * a.ldb + n;
+                if (n + 3 < a.cout) {
+                    v = *(const f4 *)src;
+                } else {
+                    if (n < a.cout) v.x = src[0];
+                    if (n + 1 < a.cout) v.y = src[1];
+                    if (n + 2 < a.cout) v.z = src[2];
+                }
+            }
+            rb[j] = v;
+        }
+    }
+}
+
+template <int BM, int BN, int AR, int BR, int BKN>
+__device__ __forceinline__ void store_ab(float *As, float *Bs, int tid, const f4 (&ra)[AR],
+                                         const f4 (&rb)[BR]) {
+    constexpr int LDK = 36;
+    const int ar = tid >> 3, ak = (tid & 7) * 4;
+#pragma unroll
+    for (int j = 0; j < AR; ++j) *(f4 *)&As[(ar + 32 * j) * LDK + ak] = ra[j];
+    if (!BKN) {
+#pragma unroll
+        for (int j = 0; j < BR; ++j) *(f4 *)&Bs[(ar + 32 * j) * LDK + ak] = rb[j];
+    } else {
+        constexpr int NV = BN / 4, RPP = 256 / NV;
+        const int kr = tid / NV, nn = (tid - (tid / NV) * NV) * 4;
+#pragma unroll
+        for (int j = 0; j < BR; ++j) {
+            const int k = kr + RPP * j;
+            Bs[(nn + 0) * LDK + k] = rb[j].x;
+            Bs[(nn + 1) * LDK + k] = rb[j].y;
+            Bs[(nn + 2) * LDK + k] = rb[j].z;
+            Bs[(nn + 3) * LDK + k] = rb[j].w;
+        }
+    }
+}
+
+template <int BM, int BN, int WAVES_M, int AMODE, int BKN>
+__global__ __launch_bounds__(256, 1) void conv_igemm(ConvArgs a) {
     constexpr int BK = 32, LDK = BK + 4;
     constexpr int WAVES_N = 4 / WAVES_M;
     constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
     constexpr int TM = WTM / 32, TN = WTN / 32;
-    constexpr int AR = BM / 32;  // A float4 slots per thread
-    constexpr int BR = BN / 32;  // B float4 slots per thread
+    constexpr int AR = BM / 32;
+    constexpr int BR = BN / 32;
+    constexpr int STAGE = (BM + BN) * LDK;
     static_assert(TM >= 1 && TN >= 1 && WTM % 32 == 0 && WTN % 32 == 0, "tile");
 
-    __shared__ __attribute__((aligned(16))) float As[BM * LDK];
-    __shared__ __attribute__((aligned(16))) float Bs[BN * LDK];
+    __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
@@ -130,122 +293,12 @@ __global__ __launch_bounds__(256) void conv_igemm(ConvArgs a) {
     const float *__restrict__ wt = a.wt + (long long)bidx * a.w_bs;
     const int kt0 = split * a.tps;
     const int kt1 = min(a.ktiles, kt0 + a.tps);
-    const int hw = a.oh * a.ow;
-
-    // ---- per-thread A rows (fixed across K)
     const int ar = tid >> 3, ak = (tid & 7) * 4;
-    int a_img[AR], a_oy[AR], a_ox[AR];
-    bool a_ok[AR];
-#pragma unroll
-    for (int j = 0; j < AR; ++j) {
-        int m = m0 + ar + 32 * j;
-        a_ok[j] = m < a.M;
-        int mm = a_ok[j] ? m : 0;
-        int img = mm / hw;
-        int rem = mm - img * hw;
-        a_img[j] = img;
-        a_oy[j] = rem / a.ow;
-        a_ox[j] = rem - a_oy[j] * a.ow;
-    }
 
-    float4 ra[AR], rb[BR];
+    ARows<AR, AMODE> R;
+    a_rows_init<AR, AMODE>(a, m0, ar, R);
 
-    auto load_tile = [&](int kt) {
-        const int kbase = kt * BK;
-        if (AVEC) {
-            const int k = kbase + ak;
-            const bool kok = k < a.K;
-            const int tap = k / a.cin;
-            const int c = k - tap * a.cin;
-            const int ky = tap / a.kw, kx = tap - (tap / a.kw) * a.kw;
-#pragma unroll
-            for (int j = 0; j < AR; ++j) {
-                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-                int iy, ix;
-                if (a_ok[j] && kok && map_tap(a, a_oy[j], a_ox[j], ky, kx, iy, ix)) {
-                    v = *(const float4 *)(x + ((long long)(a_img[j] * a.h + iy) * a.w + ix) * a.xcs + c);
-                    if (a.in_scale || a.pre_act) {
-                        v.x = prologue(a, v.x, a_img[j], c);
-                        v.y = prologue(a, v.y, a_img[j], c + 1);
-                        v.z = prologue(a, v.z, a_img[j], c + 2);
-                        v.w = prologue(a, v.w, a_img[j], c + 3);
-                    }
-                }
-                ra[j] = v;
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < AR; ++j) {
-                float vv[4];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int k = kbase + ak + e;
-                    float v = 0.f;
-                    if (a_ok[j] && k < a.K) {
-                        const int tap = k / a.cin;
-                        const int c = k - tap * a.cin;
-                        const int ky = tap / a.kw, kx = tap - (tap / a.kw) * a.kw;
-                        int iy, ix;
-                        if (map_tap(a, a_oy[j], a_ox[j], ky, kx, iy, ix)) {
-                            v = x[((long long)(a_img[j] * a.h + iy) * a.w + ix) * a.xcs + c];
-                            v = prologue(a, v, a_img[j], c);
-                        }
-                    }
-                    vv[e] = v;
-                }
-                ra[j] = make_float4(vv[0], vv[1], vv[2], vv[3]);
-            }
-        }
-        if (!BKN) {
-#pragma unroll
-            for (int j = 0; j < BR; ++j)
-                rb[j] = *(const float4 *)(wt + (long long)(n0 + ar + 32 * j) * a.kpad + kbase + ak);
-        } else {
-            // B is [K][ldb] row-major: thread reads 4 consecutive n of one k row
-            constexpr int NV = BN / 4;            // float4 per k-row
-            constexpr int RPP = 256 / NV;         // k-rows per pass
-            const int kr = tid / NV, nn = (tid - (tid / NV) * NV) * 4;
-#pragma unroll
-            for (int j = 0; j < BR; ++j) {
-                const int k = kbase + kr + RPP * j;
-                const int n = n0 + nn;
-                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (k < a.K) {
-                    const float *src = wt + (long long)k * a.ldb + n;
-                    if (n + 3 < a.cout) {
-                        v = *(const float4 *)src;
-                    } else {
-                        if (n < a.cout) v.x = src[0];
-                        if (n + 1 < a.cout) v.y = src[1];
-                        if (n + 2 < a.cout) v.z = src[2];
-                    }
-                }
-                rb[j] = v;
-            }
-        }
-    };
-
-    auto store_tile = [&]() {
-#pragma unroll
-        for (int j = 0; j < AR; ++j) *(float4 *)&As[(ar + 32 * j) * LDK + ak] = ra[j];
-        if (!BKN) {
-#pragma unroll
-            for (int j = 0; j < BR; ++j) *(float4 *)&Bs[(ar + 32 * j) * LDK + ak] = rb[j];
-        } else {
-            constexpr int NV = BN / 4;
-            constexpr int RPP = 256 / NV;
-            const int kr = tid / NV, nn = (tid - (tid / NV) * NV) * 4;
-#pragma unroll
-            for (int j = 0; j < BR; ++j) {
-                const int k = kr + RPP * j;
-                Bs[(nn + 0) * LDK + k] = rb[j].x;
-                Bs[(nn + 1) * LDK + k] = rb[j].y;
-                Bs[(nn + 2) * LDK + k] = rb[j].z;
-                Bs[(nn + 3) * LDK + k] = rb[j].w;
-            }
-        }
-    };
-
+    f4 ra[AR], rb[BR];
     floatx16 acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -255,20 +308,31 @@ __global__ __launch_bounds__(256) void conv_igemm(ConvArgs a) {
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
     const int li = lane & 31, lh = lane >> 5;
-    if (kt0 < kt1) load_tile(kt0);
-    for (int kt = kt0; kt < kt1; ++kt) {
-        store_tile();
+    if (kt0 < kt1) {
+        load_a<AR, AMODE>(a, x, kt0, ak, R, ra);
+        load_b<BN, BR, BKN>(a, wt, kt0, n0, tid, rb);
+        store_ab<BM, BN, AR, BR, BKN>(smem, smem + BM * LDK, tid, ra, rb);
         __syncthreads();
-        if (kt + 1 < kt1) load_tile(kt + 1);
+    }
+    int buf = 0;
+    for (int kt = kt0; kt < kt1; ++kt) {
+        // prefetch slice kt+1 into registers (the last iteration re-reads its own slice: no
+        // control flow around the staging registers); it lands while the MFMAs below run
+        const int kn = min(kt + 1, kt1 - 1);
+        load_a<AR, AMODE>(a, x, kn, ak, R, ra);
+        load_b<BN, BR, BKN>(a, wt, kn, n0, tid, rb);
+        __builtin_amdgcn_sched_barrier(0);   // keep the prefetch issue above the MFMA block
+        const float *As = smem + buf * STAGE;
+        const float *Bs = As + BM * LDK;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            float4 av[TM], bv[TN];
+            f4 av[TM], bv[TN];
 #pragma unroll
             for (int i = 0; i < TM; ++i)
-                av[i] = *(const float4 *)&As[(wm * WTM + i * 32 + li) * LDK + lh * 16 + q * 4];
+                av[i] = *(const f4 *)&As[(wm * WTM + i * 32 + li) * LDK + lh * 16 + q * 4];
 #pragma unroll
             for (int j = 0; j < TN; ++j)
-                bv[j] = *(const float4 *)&Bs[(wn * WTN + j * 32 + li) * LDK + lh * 16 + q * 4];
+                bv[j] = *(const f4 *)&Bs[(wn * WTN + j * 32 + li) * LDK + lh * 16 + q * 4];
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -279,26 +343,64 @@ __global__ __launch_bounds__(256) void conv_igemm(ConvArgs a) {
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i].w, bv[j].w, acc[i][j], 0, 0, 0);
                 }
         }
+        // the other buffer was last read before the previous barrier
+        float *Ad = smem + (buf ^ 1) * STAGE;
+        store_ab<BM, BN, AR, BR, BKN>(Ad, Ad + BM * LDK, tid, ra, rb);
         __syncthreads();
+        buf ^= 1;
     }
 
-    // ---- epilogue: lane owns column li of each 32x32 tile, rows (r&3) + 8(r>>2) + 4 lh
+    // ---- epilogue.  The lane owns column li of each 32x32 tile, rows (r&3) + 8(r>>2) + 4 lh:
+    // stage the tile through LDS with static indices, then every thread walks the tile row by
+    // row (consecutive threads -> consecutive output channels: coalesced stores).
+    constexpr int LDC = BN + 4;
+    static_assert(BM * LDC <= 2 * STAGE, "C tile must fit in the staging LDS");
+    float *Cs = smem;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int n = n0 + wn * WTN + j * 32 + li;
-            if (n >= a.cout) continue;
+        for (int j = 0; j < TN; ++j)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-                if (m >= a.M) continue;
-                if (a.splits > 1)
-                    a.ws[((long long)bz * a.M + m) * a.cout + n] = acc[i][j][r];
-                else
-                    store_epilogue(a, bidx, m, n, acc[i][j][r]);
+            for (int r = 0; r < 16; ++r)
+                Cs[(wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * LDC + wn * WTN + j * 32 + li] = acc[i][j][r];
+    __syncthreads();
+    const Epi &e = a.epi;
+    constexpr int TPR = BN < 256 ? BN : 256;   // threads per tile row
+    constexpr int RSTEP = 256 / TPR;
+    const int cn = tid % TPR;
+    const int n = n0 + cn;
+    if (n >= a.cout) return;
+    const int mlim = min(BM, a.M - m0);
+    if (a.splits > 1) {
+        float *w = a.ws + (long long)bz * a.M * a.cout;
+#pragma unroll 1
+        for (int rr = tid / TPR; rr < mlim; rr += RSTEP) w[(long long)(m0 + rr) * a.cout + n] = Cs[rr * LDC + cn];
+        return;
+    }
+    const bool simple = !e.nc_scale && !e.pix_add && (!e.res || e.res_simple);
+    if (simple) {
+        const float sc = e.scale ? e.scale[n] : 1.f;
+        const float sh = e.shift ? e.shift[n] : 0.f;
+        const float slope = e.act == S2V_ACT_RELU ? 0.f : (e.act == S2V_ACT_LRELU ? e.alpha : 1.f);
+        float *__restrict__ yb = a.y + (long long)bidx * a.y_bs + n;
+        const float *rsrc = e.res ? e.res + (long long)bidx * a.res_bs + n : nullptr;
+#pragma unroll 1
+        for (int rr = tid / TPR; rr < mlim; rr += RSTEP) {
+            const long long m = m0 + rr;
+            float v = Cs[rr * LDC + cn] * sc + sh;
+            float rv = 0.f;
+            if (rsrc) {
+                rv = rsrc[m * e.res_cs];
+                if (!e.res_after) v += rv;
             }
+            v = fast_act(v, e.act, slope);
+            if (rsrc && e.res_after) v += rv;
+            yb[m * a.ycs] = v;
         }
+    } else {
+#pragma unroll 1
+        for (int rr = tid / TPR; rr < mlim; rr += RSTEP) store_epilogue(a, bidx, m0 + rr, n, Cs[rr * LDC + cn]);
+    }
 }
 
 __global__ void splitk_reduce(ConvArgs a, int batch) {
@@ -316,14 +418,18 @@ __global__ void splitk_reduce(ConvArgs a, int batch) {
     }
 }
 
-// Direct VALU convolution for tiny Cout (final RGB / flow heads): one thread per output pixel.
+// Direct VALU convolution for tiny Cout (final RGB / flow heads, ToRGB): one thread per output
+// pixel, all CO outputs per thread.  Per filter tap the block stages W[:, tap, c0:c0+CCH] in LDS,
+// so every weight read is an LDS broadcast (all lanes read the same address).
 template <int CO>
 __global__ __launch_bounds__(256) void conv_direct_small(ConvArgs a, int batch) {
+    constexpr int CCH = 512;                  // channels staged per pass
+    __shared__ __attribute__((aligned(16))) float wsm[CO * CCH];
     const long long total = (long long)batch * a.M;
     const long long gid = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    if (gid >= total) return;
-    const int bidx = (int)(gid / a.M);
-    const int m = (int)(gid - (long long)bidx * a.M);
+    const bool live = gid < total;
+    const int bidx = live ? (int)(gid / a.M) : 0;
+    const int m = live ? (int)(gid - (long long)bidx * a.M) : 0;
     const int hw = a.oh * a.ow;
     const int img = m / hw;
     const int rem = m - img * hw;
@@ -334,33 +440,44 @@ __global__ __launch_bounds__(256) void conv_direct_small(ConvArgs a, int batch) 
 #pragma unroll
     for (int o = 0; o < CO; ++o) acc[o] = 0.f;
     const bool vec = (a.cin % 4 == 0) && (a.xcs % 4 == 0) && !a.in_scale && !a.pre_act &&
-                     (((uintptr_t)x & 15) == 0) && (a.kpad % 4 == 0);
+                     (((uintptr_t)x & 15) == 0);
     for (int ky = 0; ky < a.kh; ++ky)
         for (int kx = 0; kx < a.kw; ++kx) {
-            int iy, ix;
-            if (!map_tap(a, oy, ox, ky, kx, iy, ix)) continue;
+            int iy = 0, ix = 0;
+            const bool ok = live && map_tap(a, oy, ox, ky, kx, iy, ix);
             const float *px = x + ((long long)(img * a.h + iy) * a.w + ix) * a.xcs;
             const int kb = (ky * a.kw + kx) * a.cin;
-            if (vec) {
-                for (int c = 0; c < a.cin; c += 4) {
-                    const float4 v = *(const float4 *)(px + c);
-#pragma unroll
-                    for (int o = 0; o < CO; ++o) {
-                        const float4 wv = *(const float4 *)(wt + (long long)o * a.kpad + kb + c);
-                        acc[o] = fmaf(v.x, wv.x, acc[o]);
-                        acc[o] = fmaf(v.y, wv.y, acc[o]);
-                        acc[o] = fmaf(v.z, wv.z, acc[o]);
-                        acc[o] = fmaf(v.w, wv.w, acc[o]);
-                    }
+            for (int c0 = 0; c0 < a.cin; c0 += CCH) {
+                const int cn = min(CCH, a.cin - c0);
+                __syncthreads();
+                for (int e = threadIdx.x; e < CO * cn; e += 256) {
+                    const int o = e / cn, c = e - (e / cn) * cn;
+                    wsm[o * CCH + c] = o < a.cout ? wt[(long long)o * a.kpad + kb + c0 + c] : 0.f;
                 }
-            } else {
-                for (int c = 0; c < a.cin; ++c) {
-                    const float v = prologue(a, px[c], img, c);
+                __syncthreads();
+                if (!ok) continue;
+                if (vec) {
+                    for (int c = 0; c < cn; c += 4) {
+                        const float4 v = *(const float4 *)(px + c0 + c);
 #pragma unroll
-                    for (int o = 0; o < CO; ++o) acc[o] = fmaf(v, wt[(long long)o * a.kpad + kb + c], acc[o]);
+                        for (int o = 0; o < CO; ++o) {
+                            const float4 wv = *(const float4 *)&wsm[o * CCH + c];
+                            acc[o] = fmaf(v.x, wv.x, acc[o]);
+                            acc[o] = fmaf(v.y, wv.y, acc[o]);
+                            acc[o] = fmaf(v.z, wv.z, acc[o]);
+                            acc[o] = fmaf(v.w, wv.w, acc[o]);
+                        }
+                    }
+                } else {
+                    for (int c = 0; c < cn; ++c) {
+                        const float v = prologue(a, px[c0 + c], img, c0 + c);
+#pragma unroll
+                        for (int o = 0; o < CO; ++o) acc[o] = fmaf(v, wsm[o * CCH + c], acc[o]);
+                    }
                 }
             }
         }
+    if (!live) return;
 #pragma unroll
     for (int o = 0; o < CO; ++o)
         if (o < a.cout) store_epilogue(a, bidx, m, o, acc[o]);
@@ -397,7 +514,7 @@ static Plan make_plan(const s2v_conv_params *p, int M, int K) {
     if (p->force_tile > 0) {
         cands[nc++] = p->force_tile - 1;
     } else if (p->cout <= 32) {
-        cands[nc++] = 4; cands[nc++] = 5;
+        cands[nc++] = 5;
     } else if (p->cout <= 64) {
         cands[nc++] = 1; cands[nc++] = 3;
     } else {
@@ -480,14 +597,25 @@ static ConvArgs make_args(const s2v_conv_params *p, int M, int K, const Plan &pl
 }
 
 template <int BM, int BN, int WM>
-static void launch_tile(const ConvArgs &a, bool avec, bool bkn, dim3 grid, hipStream_t s) {
-    if (avec) {
-        if (bkn) conv_igemm<BM, BN, WM, 1, 1><<<grid, 256, 0, s>>>(a);
-        else conv_igemm<BM, BN, WM, 1, 0><<<grid, 256, 0, s>>>(a);
-    } else {
-        if (bkn) conv_igemm<BM, BN, WM, 0, 1><<<grid, 256, 0, s>>>(a);
-        else conv_igemm<BM, BN, WM, 0, 0><<<grid, 256, 0, s>>>(a);
+static void launch_tile(const ConvArgs &a, int amode, bool bkn, dim3 grid, hipStream_t s) {
+    switch (amode * 2 + (bkn ? 1 : 0)) {
+        case 0: conv_igemm<BM, BN, WM, 0, 0><<<grid, 256, 0, s>>>(a); break;
+        case 1: conv_igemm<BM, BN, WM, 0, 1><<<grid, 256, 0, s>>>(a); break;
+        case 2: conv_igemm<BM, BN, WM, 1, 0><<<grid, 256, 0, s>>>(a); break;
+        case 3: conv_igemm<BM, BN, WM, 1, 1><<<grid, 256, 0, s>>>(a); break;
+        case 4: conv_igemm<BM, BN, WM, 2, 0><<<grid, 256, 0, s>>>(a); break;
+        default: conv_igemm<BM, BN, WM, 2, 1><<<grid, 256, 0, s>>>(a); break;
     }
+}
+
+// 0: fast direct path, 1: generic float4 gather, 2: scalar gather
+static int a_mode(const s2v_conv_params *p) {
+    const bool vec = (p->cin % 4 == 0) && (p->xcs % 4 == 0) && (((uintptr_t)p->x % 16) == 0) && (p->x_bs % 4 == 0);
+    if (!vec) return 2;
+    if (p->cin % 32 == 0 && p->in_mode == S2V_IN_DIRECT && p->pad_mode == S2V_PAD_ZERO && !p->in_scale &&
+        !p->pre_act)
+        return 0;
+    return 1;
 }
 
 }  // namespace s2v
@@ -514,7 +642,7 @@ extern "C" int s2v_conv2d_plan(const s2v_conv_params *p, int *out6) {
     }
     const TileCfg &t = kTiles[pl.tile];
     out6[0] = t.bm; out6[1] = t.bn; out6[2] = t.wm;
-    out6[3] = (p->cin % 4 == 0) && (p->xcs % 4 == 0) && (((uintptr_t)p->x % 16) == 0) && (p->x_bs % 4 == 0);
+    out6[3] = a_mode(p);
     out6[4] = p->b_kn != 0;
     out6[5] = pl.splits;
     return 0;
@@ -546,18 +674,17 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
             return S2V_E_WORKSPACE;
         }
     }
-    const bool avec = (p->cin % 4 == 0) && (p->xcs % 4 == 0) && (((uintptr_t)p->x % 16) == 0) &&
-                      (p->x_bs % 4 == 0);
+    const int amode = a_mode(p);
     const bool bkn = p->b_kn != 0;
     const TileCfg &t = kTiles[pl.tile];
     dim3 grid(cdiv(M, t.bm), cdiv(p->cout, t.bn), batch * pl.splits);
     switch (pl.tile) {
-        case 0: launch_tile<128, 128, 2>(a, avec, bkn, grid, s); break;
-        case 1: launch_tile<128, 64, 2>(a, avec, bkn, grid, s); break;
-        case 2: launch_tile<64, 128, 2>(a, avec, bkn, grid, s); break;
-        case 3: launch_tile<64, 64, 2>(a, avec, bkn, grid, s); break;
-        case 4: launch_tile<256, 32, 4>(a, avec, bkn, grid, s); break;
-        default: launch_tile<128, 32, 4>(a, avec, bkn, grid, s); break;
+        case 0: launch_tile<128, 128, 2>(a, amode, bkn, grid, s); break;
+        case 1: launch_tile<128, 64, 2>(a, amode, bkn, grid, s); break;
+        case 2: launch_tile<64, 128, 2>(a, amode, bkn, grid, s); break;
+        case 3: launch_tile<64, 64, 2>(a, amode, bkn, grid, s); break;
+        case 4: launch_tile<256, 32, 4>(a, amode, bkn, grid, s); break;
+        default: launch_tile<128, 32, 4>(a, amode, bkn, grid, s); break;
     }
     rc = check_launch("conv_igemm");
     if (rc || pl.splits <= 1) return rc;
