@@ -1,0 +1,186 @@
+"""CPU tests: the C ABI library loads and exports what include/s2v.h declares, struct layout,
+state_dict layout vs the reference manifests, weight packing / folding, DFT matrices, mel host
+logic and the mel restatement cross-checks.  No GPU compute here."""
+import ctypes
+import json
+import os
+import re
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+import s2v_import  # noqa: F401
+from conftest import GOLDEN, REPO
+from s2v_amd import _lib, synth
+from s2v_amd.models import arch
+
+HEADER = os.path.join(REPO, "include", "s2v.h")
+
+
+def header_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(s2v_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    names = header_functions()
+    assert len(names) >= 20
+    for n in names:
+        assert hasattr(lib, n), f"libs2v.so does not export {n}"
+    assert set(names) == set(_lib.EXPORTS), (set(names) ^ set(_lib.EXPORTS))
+    assert lib.s2v_version().startswith(b"s2v")
+
+
+def test_invalid_arguments_are_rejected_without_a_device():
+    lib = _lib.load()
+    p = _lib.ConvParams()                       # null pointers
+    assert lib.s2v_conv2d(ctypes.byref(p), None) == -1
+    assert b"null" in lib.s2v_last_error()
+    assert lib.s2v_upfirdn2d(None, 1, 4, 4, 1, None, 4, 4, 1, 1, 1, 1, 0, 0, 0, 0, None, 1, 1, None) == -1
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="gcc not available")
+def test_conv_params_struct_layout_matches_header(tmp_path):
+    src = tmp_path / "sz.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "%s"\n'
+                   'int main(){printf("%%zu %%zu %%zu %%zu %%zu %%zu\\n", sizeof(s2v_conv_params),'
+                   'offsetof(s2v_conv_params, ws), offsetof(s2v_conv_params, x_bs),'
+                   'offsetof(s2v_conv_params, res), offsetof(s2v_conv_params, force_splits),'
+                   'offsetof(s2v_conv_params, b_kn));return 0;}' % HEADER)
+    exe = tmp_path / "sz"
+    subprocess.run(["gcc", str(src), "-o", str(exe)], check=True)
+    got = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    P = _lib.ConvParams
+    assert got == [ctypes.sizeof(P), P.ws.offset, P.x_bs.offset, P.res.offset, P.force_splits.offset, P.b_kn.offset]
+
+
+@pytest.mark.parametrize("name,ctor", [("lnet", lambda: arch.LNetParams()),
+                                       ("enet", lambda: arch.ENetParams(lnet=arch.LNetParams())),
+                                       ("dnet", lambda: arch.DNetParams())])
+def test_state_dict_layout_matches_reference(name, ctor):
+    ref = json.load(open(os.path.join(GOLDEN, f"{name}_keys.json")))
+    mine = {k: list(v.shape) for k, v in ctor().state_dict().items()}
+    assert mine == ref
+
+
+def test_public_models_share_the_layout():
+    from s2v_amd import models
+    assert set(models.ENet().state_dict()) == set(json.load(open(os.path.join(GOLDEN, "enet_keys.json"))))
+    assert set(models.DNet().state_dict()) == set(json.load(open(os.path.join(GOLDEN, "dnet_keys.json"))))
+
+
+def test_synth_is_deterministic_and_portable():
+    u = synth.hash_uniform("decoder.res2.res0.conv1.ffc.convl2l.weight", 4)
+    # fixed values: the golden fixtures were produced from exactly these numbers
+    np.testing.assert_allclose(u, synth.hash_uniform("decoder.res2.res0.conv1.ffc.convl2l.weight", 4))
+    assert np.all(np.abs(u) < 1)
+    a = synth.synth_tensor("x.running_var", (5,))
+    assert np.all(a > 0.7)
+    assert synth.synth_tensor("style_convs.0.weight", (1,))[0] == 0.0
+
+
+def test_conv_weight_packing_roundtrip():
+    from s2v_amd.ops import ConvW
+    w = torch.randn(5, 7, 3, 3)
+    cw = ConvW(w, torch.randn(5), "cpu", padding=1)
+    assert cw.kpad % 32 == 0 and cw.npad % 128 == 0
+    back = cw.wt[:5, :63].reshape(5, 3, 3, 7).permute(0, 3, 1, 2)
+    assert torch.equal(back, w)
+    assert torch.all(cw.wt[5:] == 0) and torch.all(cw.wt[:, 63:] == 0)
+    wt = torch.randn(7, 5, 3, 3)                        # ConvTranspose2d layout [in, out, k, k]
+    ct = ConvW(wt, None, "cpu", transposed=True, stride=2, padding=1, output_padding=1)
+    assert (ct.cout, ct.cin) == (5, 7) and ct.out_hw(6, 6) == (12, 12)
+    c1 = ConvW(torch.randn(4, 3, 3), None, "cpu", dilation=(1, 3))   # Conv1d k3 dil3 (DNet.py:41-42)
+    assert (c1.kh, c1.kw, c1.dw) == (1, 3, 3) and c1.out_hw(1, 20) == (1, 14)
+
+
+def test_bn_fold_matches_eval_batchnorm():
+    from s2v_amd.ops import ConvW
+    g = torch.Generator().manual_seed(0)
+    w, b = torch.randn(6, 4, 3, 3, generator=g), torch.randn(6, generator=g)
+    bn = (torch.rand(6, generator=g) + 0.5, torch.randn(6, generator=g), torch.randn(6, generator=g),
+          torch.rand(6, generator=g) + 0.5)
+    cw = ConvW(w, b, "cpu", padding=1, bn=bn)
+    x = torch.randn(2, 4, 5, 5, generator=g)
+    ref = torch.nn.functional.batch_norm(torch.nn.functional.conv2d(x, w, b, padding=1), bn[2], bn[3], bn[0], bn[1],
+                                         False, 0.0, 1e-5)
+    got = torch.nn.functional.conv2d(x, w, None, padding=1) * cw.scale[None, :, None, None] + cw.shift[None, :, None, None]
+    assert (got - ref).abs().max() < 1e-5
+
+
+def test_spectral_norm_fold_matches_torch():
+    from s2v_amd.engine.common import conv_weight
+    from torch.nn.utils import spectral_norm
+    m = spectral_norm(torch.nn.Conv2d(4, 6, 3))
+    sd = synth.synth_torch_state_dict(m)
+    m.load_state_dict(sd)
+    m.eval()
+    with torch.no_grad():
+        m(torch.zeros(1, 4, 5, 5))          # the spectral-norm pre-hook recomputes .weight
+    assert (conv_weight(sd, "") - m.weight).abs().max() < 1e-6
+
+
+def test_fourier_matrices_are_the_reference_transforms():
+    from s2v_amd.ops import fourier_matrices
+    for h, w in ((12, 12), (24, 24), (6, 10)):
+        d2, iv = fourier_matrices(h, w, "cpu")
+        x = torch.randn(3, h, w, dtype=torch.float64)
+        spec = torch.fft.rfftn(x, dim=(-2, -1), norm="ortho")
+        st = torch.stack([spec.real, spec.imag], -1).reshape(3, -1)
+        assert (d2.double() @ x.reshape(3, -1).t()).t().sub(st).abs().max() < 1e-5
+        y = torch.randn_like(st)          # arbitrary spectrum, incl. imag DC / Nyquist parts
+        ref = torch.fft.irfftn(torch.complex(y[:, 0::2], y[:, 1::2]).reshape(3, h, w // 2 + 1), s=(h, w),
+                               dim=(-2, -1), norm="ortho").reshape(3, -1)
+        assert (iv.double() @ y.t()).t().sub(ref).abs().max() < 1e-5
+
+
+def test_adain_bank_layout():
+    from s2v_amd.engine.common import AdainBank
+    sd = {}
+    for p, c in (("a.", 3), ("b.", 5)):
+        sd.update({p + "mlp_shared.0.weight": torch.randn(128, 7), p + "mlp_shared.0.bias": torch.randn(128),
+                   p + "mlp_gamma.weight": torch.randn(c, 128), p + "mlp_gamma.bias": torch.randn(c),
+                   p + "mlp_beta.weight": torch.randn(c, 128), p + "mlp_beta.bias": torch.randn(c)})
+    bank = AdainBank(7)
+    gid = bank.add_group(sd, [("a.", 3), ("b.", 5)])
+    bank.build("cpu")
+    assert bank.total == 16 and bank.groups[gid] == (0, 8)
+    assert bank.seg.tolist() == [0] * 3 + [1] * 5 + [0] * 3 + [1] * 5
+    assert torch.equal(bank.w2t[:, 3:8].t(), sd["b.mlp_gamma.weight"])
+    assert torch.equal(bank.w2t[:, 11:16].t(), sd["b.mlp_beta.weight"])
+
+
+def test_mel_chunk_starts_follow_inference_loop():
+    from s2v_amd.audio import chunk_starts
+    from oracle.audio import mel_chunk_starts
+    for T in (16, 17, 100, 3201):
+        assert chunk_starts(T) == mel_chunk_starts(T)
+    st = chunk_starts(3201)
+    assert st[:4] == [0, 3, 6, 9] and st[-1] == 3201 - 16
+    assert len(st) == 997           # 40 s at 16 kHz: the last window is clamped (inference.py:212-214)
+
+
+def test_mel_restatement_cross_checks():
+    """The NumPy restatement against independent implementations: scipy's lfilter for the
+    pre-emphasis and torch.stft for the framed, windowed STFT."""
+    from scipy import signal
+    from oracle import audio
+    from s2v_amd.audio import slaney_mel_basis
+    rng = np.random.default_rng(0)
+    wav = (0.1 * rng.standard_normal(16000)).astype(np.float32)
+    assert np.abs(audio.preemphasis(wav) - signal.lfilter([1, -0.97], [1], wav)).max() < 1e-12
+    y = audio.preemphasis(wav)
+    for mode in ("constant", "reflect"):
+        ref = torch.stft(torch.from_numpy(y), 800, 200, 800, torch.hann_window(800, periodic=True, dtype=torch.float64),
+                         center=True, pad_mode=mode, return_complex=True).abs().numpy()
+        assert np.abs(audio.stft_mag(y, mode) - ref).max() < 1e-9
+    mel = audio.melspectrogram(wav)
+    assert mel.shape == (80, 81) and mel.min() >= -4 and mel.max() <= 4
+    b = audio.mel_basis()
+    assert b.shape == (80, 401) and b.dtype == np.float32
+    assert np.array_equal(b, slaney_mel_basis())

@@ -15,9 +15,8 @@ import s2v_import  # noqa: F401
 
 pytestmark = pytest.mark.gpu
 
-if torch.cuda.is_available():
-    from s2v_amd import ops
-    from s2v_amd.ops import NHWC, ConvW
+from s2v_amd import ops  # noqa: E402  (importable without a device; launches need one)
+from s2v_amd.ops import NHWC, ConvW  # noqa: E402
 
 DEV = "cuda"
 
@@ -311,3 +310,26 @@ def test_fourier_matrices_match_torch_fft(ctx):
         assert (got - st).abs().max() < 1e-5
         back = (iv.double().cpu() @ st.t()).t().reshape(3, h, w)
         assert (back - x).abs().max() < 1e-5
+
+
+@pytest.mark.parametrize("pad_mode", ["constant", "reflect"])
+def test_melspectrogram_matches_restatement(pad_mode):
+    """Device mel vs the float64 NumPy restatement of futils/audio.py (librosa 0.9.2 semantics;
+    parity unpinned at the librosa boundary, see oracle/audio.py).  Tolerance 1e-3 in normalised
+    units (range +-4), SURVEY.md §8d."""
+    from oracle import audio as ref
+    from s2v_amd import audio
+    t = np.arange(48000) / 16000.0
+    rng = np.random.default_rng(1)
+    wav = (0.1 * rng.standard_normal(t.size) + 0.2 * (np.sin(2 * np.pi * 220 * t) + np.sin(2 * np.pi * 440 * t)
+                                                         + np.sin(2 * np.pi * 1000 * t))).astype(np.float32)
+    wav[:2000] = 0.0                                   # exercise the -100 dB floor / clip
+    got = audio.melspectrogram(torch.from_numpy(wav).to(DEV), pad_mode=pad_mode).cpu().numpy()
+    exp = ref.melspectrogram(wav, pad_mode=pad_mode)
+    assert got.shape == exp.shape == (80, 241)
+    assert np.abs(got - exp).max() < 1e-3
+    chunks = audio.mel_chunks(torch.from_numpy(exp.astype(np.float32)).to(DEV)).cpu().numpy()
+    starts = ref.mel_chunk_starts(exp.shape[1])
+    assert chunks.shape == (len(starts), 1, 80, 16)
+    for i, s in enumerate(starts):
+        assert np.array_equal(chunks[i, 0], exp[:, s: s + 16].astype(np.float32))
