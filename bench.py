@@ -88,6 +88,11 @@ def live_roofline(model, inputs):
         d["launches"] += 1
         d["split_launches"] += int(splits > 1)
     dom = max(per, key=lambda k: per[k]["ms"])
+    if os.environ.get("S2V_BENCH_VERBOSE"):
+        for k in sorted(per, key=lambda k: -per[k]["ms"]):
+            v = per[k]
+            tf = v["flops"] / max(v["ms"], 1e-9) / 1e9
+            print(f"  {v['ms']:9.3f} ms  {v['launches']:4d} launches  {tf:7.2f} TF/s  {k}", file=sys.stderr)
     d = per[dom]
     achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12
     total_ms = sum(v["ms"] for v in per.values())

@@ -168,6 +168,21 @@ __device__ __forceinline__ void load_a(const ConvArgs &a, const float *__restric
             if (ok) v = *(const f4 *)(x + R.base[j] + toff);
             ra[j] = v;
         }
+        if (a.in_scale) {   // StyleGAN2 input modulation s[n, c] (zero padding stays zero)
+#pragma unroll
+            for (int j = 0; j < AR; ++j)
+                ra[j] *= *(const f4 *)(a.in_scale + (long long)R.img[j] * a.in_scale_ns + c);
+        }
+        if (a.pre_act) {
+            const float sl = a.pre_act == S2V_ACT_RELU ? 0.f : a.pre_alpha;
+#pragma unroll
+            for (int j = 0; j < AR; ++j) {
+                ra[j].x = ra[j].x >= 0.f ? ra[j].x : ra[j].x * sl;
+                ra[j].y = ra[j].y >= 0.f ? ra[j].y : ra[j].y * sl;
+                ra[j].z = ra[j].z >= 0.f ? ra[j].z : ra[j].z * sl;
+                ra[j].w = ra[j].w >= 0.f ? ra[j].w : ra[j].w * sl;
+            }
+        }
     } else if (AMODE == 1) {
         const int k = kbase + ak;
         const bool kok = k < a.K;
@@ -612,9 +627,9 @@ static void launch_tile(const ConvArgs &a, int amode, bool bkn, dim3 grid, hipSt
 static int a_mode(const s2v_conv_params *p) {
     const bool vec = (p->cin % 4 == 0) && (p->xcs % 4 == 0) && (((uintptr_t)p->x % 16) == 0) && (p->x_bs % 4 == 0);
     if (!vec) return 2;
-    if (p->cin % 32 == 0 && p->in_mode == S2V_IN_DIRECT && p->pad_mode == S2V_PAD_ZERO && !p->in_scale &&
-        !p->pre_act)
-        return 0;
+    const bool simple_pre = (p->pre_act == S2V_ACT_NONE || p->pre_act == S2V_ACT_RELU || p->pre_act == S2V_ACT_LRELU) &&
+                            (!p->in_scale || (p->in_scale_ns % 4 == 0 && ((uintptr_t)p->in_scale % 16) == 0));
+    if (p->cin % 32 == 0 && p->in_mode == S2V_IN_DIRECT && p->pad_mode == S2V_PAD_ZERO && simple_pre) return 0;
     return 1;
 }
 

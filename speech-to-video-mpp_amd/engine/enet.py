@@ -62,13 +62,16 @@ class ENetEngine:
             self.layers.append(StyleLayer(sd, f"style_convs.{2 * i}.", dev, True, True, False))
             self.layers.append(StyleLayer(sd, f"style_convs.{2 * i + 1}.", dev, True, False, False))
             self.layers.append(StyleLayer(sd, f"to_rgbs.{i}.", dev, False, False, True))
-        # all six modulation Linears consume the same style code -> one GEMM
-        self.mod = ConvW(torch.cat([l.mod_w for l in self.layers], 0), torch.cat([l.mod_b for l in self.layers], 0),
-                         dev)
-        offs, o = [], 0
+        # all six modulation Linears consume the same style code -> one GEMM; each layer's segment
+        # is padded to a multiple of 4 so the conv prologue can read s[n, c:c+4] as one 16-byte load
+        offs, o, ws, bs = [], 0, [], []
         for l in self.layers:
             offs.append(o)
-            o += l.cin
+            pad = (-l.cin) % 4
+            ws += [l.mod_w, torch.zeros(pad, l.mod_w.shape[1])]
+            bs += [l.mod_b, torch.zeros(pad)]
+            o += l.cin + pad
+        self.mod = ConvW(torch.cat(ws, 0), torch.cat(bs, 0), dev)
         self.mod_offs = offs
         self.noise_seed = 0x5EED
         self.calls = 0
