@@ -188,6 +188,24 @@ int s2v_upfirdn2d(const float *x, int major, int in_h, int in_w, int minor, cons
 int s2v_gaussian_noise(float *y, long long n, unsigned long long seed, unsigned long long offset,
                        s2v_stream_t stream);
 
+/* Full-clip pipeline glue.  DNet fake [n,3,h,w] in [-1,1] -> uint8 reference frames
+ * (preprocessing/facing.py:190-191) and the ENet inputs built from them and the original crops src
+ * (inference.py:393-399): face6 = [masked original | ref] / 255 (rows >= h/2 of the original zeroed),
+ * gt = ref / 255.  All NCHW. */
+int s2v_lipsync_inputs(const float *src, const float *fake, int n, int h, int w, unsigned char *ref_u8,
+                       float *face6, float *gt, s2v_stream_t stream);
+/* y = uint8((clamp(x, lo, hi) + offset) * scale) with truncation (inference.py:267, :288). */
+int s2v_to_u8(const float *x, long long n, float lo, float hi, float scale, float offset, unsigned char *y,
+              s2v_stream_t stream);
+/* Elementwise over NHWC views: y = post * act(a * x [* mul] [+ add] [+ bias[c]]) — GFPGAN SFT
+ * (gfpganv1_clean_arch.py:98-106), U-Net skip adds, GPEN NoiseInjection halves (gpen_model.py:287-302). */
+int s2v_eltwise(const float *x, int xcs, const float *mul, int mcs, const float *add, int acs, const float *bias,
+                long long pixels, int c, float a, int act, float alpha, float post, float *y, int ycs,
+                s2v_stream_t stream);
+
+/* y[0:n) = value (channel padding of 3-channel images to the vectorised 4-channel layout). */
+int s2v_fill(float *y, long long n, float value, s2v_stream_t stream);
+
 const char *s2v_last_error(void);
 /* number of compute units of the current device (0 if no device) */
 int s2v_device_cus(void);

@@ -145,7 +145,8 @@ __device__ __forceinline__ void a_rows_init(const ConvArgs &a, int m0, int ar, A
         R.ox[j] = ox;
         R.iy0[j] = oy * a.sh - a.ph;
         R.ix0[j] = ox * a.sw - a.pw;
-        R.base[j] = ((long long)(img * a.h + R.iy0[j]) * a.w + R.ix0[j]) * a.xcs;
+        R.base[j] = AMODE == 3 ? (long long)img * a.h * a.w * a.xcs
+                               : ((long long)(img * a.h + R.iy0[j]) * a.w + R.ix0[j]) * a.xcs;
     }
 }
 
@@ -153,20 +154,30 @@ template <int AR, int AMODE>
 __device__ __forceinline__ void load_a(const ConvArgs &a, const float *__restrict__ x, int kt, int ak,
                                        const ARows<AR, AMODE> &R, f4 (&ra)[AR]) {
     const int kbase = kt * 32;
-    if (AMODE == 0) {
-        // tile-uniform tap (scalar math)
+    if (AMODE == 0 || AMODE == 3) {
+        // tile-uniform tap (scalar math); AMODE 3 reflects out-of-range rows/cols (FFC, ffc.py:196-204)
         const int tap = kbase / a.cin;
         const int c = kbase - tap * a.cin + ak;
         const int ky = tap / a.kw, kx = tap - (tap / a.kw) * a.kw;
         const int dy = ky * a.dh, dx = kx * a.dw;
         const long long toff = ((long long)dy * a.w + dx) * a.xcs + c;
+        if (AMODE == 0) {
 #pragma unroll
-        for (int j = 0; j < AR; ++j) {
-            const bool ok = R.ok[j] && (unsigned)(R.iy0[j] + dy) < (unsigned)a.h &&
-                            (unsigned)(R.ix0[j] + dx) < (unsigned)a.w;
-            f4 v = {0.f, 0.f, 0.f, 0.f};
-            if (ok) v = *(const f4 *)(x + R.base[j] + toff);
-            ra[j] = v;
+            for (int j = 0; j < AR; ++j) {
+                const bool ok = R.ok[j] && (unsigned)(R.iy0[j] + dy) < (unsigned)a.h &&
+                                (unsigned)(R.ix0[j] + dx) < (unsigned)a.w;
+                f4 v = {0.f, 0.f, 0.f, 0.f};
+                if (ok) v = *(const f4 *)(x + R.base[j] + toff);
+                ra[j] = v;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < AR; ++j) {
+                const int iy = reflect_idx(R.iy0[j] + dy, a.h), ix = reflect_idx(R.ix0[j] + dx, a.w);
+                f4 v = {0.f, 0.f, 0.f, 0.f};
+                if (R.ok[j]) v = *(const f4 *)(x + R.base[j] + ((long long)iy * a.w + ix) * a.xcs + c);
+                ra[j] = v;
+            }
         }
         if (a.in_scale) {   // StyleGAN2 input modulation s[n, c] (zero padding stays zero)
 #pragma unroll
@@ -498,6 +509,76 @@ __global__ __launch_bounds__(256) void conv_direct_small(ConvArgs a, int batch) 
         if (o < a.cout) store_epilogue(a, bidx, m, o, acc[o]);
 }
 
+// Small-Cout conv, channel-parallel form: TPP lanes share one output pixel, each owns 4 input
+// channels (16-byte loads; consecutive lanes read consecutive bytes of the pixel row, so a wave
+// reads 64/TPP neighbouring pixels contiguously), partial dot products are combined with
+// shuffles.  Requires cin % 4 == 0 and 16-byte aligned rows.
+template <int CO, int TPP>
+__global__ __launch_bounds__(256) void conv_small_cpar(ConvArgs a, int batch) {
+    const long long total = (long long)batch * a.M;
+    const long long gid = (blockIdx.x * 256LL + threadIdx.x) / TPP;
+    const int sub = threadIdx.x % TPP;
+    const bool live = gid < total;
+    const int bidx = live ? (int)(gid / a.M) : 0;
+    const int m = live ? (int)(gid - (long long)bidx * a.M) : 0;
+    const int hw = a.oh * a.ow;
+    const int img = m / hw;
+    const int rem = m - img * hw;
+    const int oy = rem / a.ow, ox = rem - (rem / a.ow) * a.ow;
+    const float *x = a.x + (long long)bidx * a.x_bs;
+    const float *wt = a.wt + (long long)bidx * a.w_bs;
+    float acc[CO];
+#pragma unroll
+    for (int o = 0; o < CO; ++o) acc[o] = 0.f;
+    if (live) {
+        for (int ky = 0; ky < a.kh; ++ky)
+            for (int kx = 0; kx < a.kw; ++kx) {
+                int iy, ix;
+                if (!map_tap(a, oy, ox, ky, kx, iy, ix)) continue;
+                const float *px = x + ((long long)(img * a.h + iy) * a.w + ix) * a.xcs;
+                const int kb = (ky * a.kw + kx) * a.cin;
+                for (int c = sub * 4; c < a.cin; c += TPP * 4) {
+                    f4 v = *(const f4 *)(px + c);
+                    if (a.in_scale) v *= *(const f4 *)(a.in_scale + (long long)img * a.in_scale_ns + c);
+                    if (a.pre_act) {
+                        v.x = apply_act(v.x, a.pre_act, a.pre_alpha);
+                        v.y = apply_act(v.y, a.pre_act, a.pre_alpha);
+                        v.z = apply_act(v.z, a.pre_act, a.pre_alpha);
+                        v.w = apply_act(v.w, a.pre_act, a.pre_alpha);
+                    }
+#pragma unroll
+                    for (int o = 0; o < CO; ++o) {
+                        const f4 wv = *(const f4 *)(wt + (long long)o * a.kpad + kb + c);
+                        acc[o] = fmaf(v.x, wv.x, fmaf(v.y, wv.y, fmaf(v.z, wv.z, fmaf(v.w, wv.w, acc[o]))));
+                    }
+                }
+            }
+    }
+#pragma unroll
+    for (int o = 0; o < CO; ++o)
+#pragma unroll
+        for (int off = TPP / 2; off > 0; off >>= 1) acc[o] += __shfl_xor(acc[o], off, 64);
+    if (!live || sub != 0) return;
+#pragma unroll
+    for (int o = 0; o < CO; ++o)
+        if (o < a.cout) store_epilogue(a, bidx, m, o, acc[o]);
+}
+
+template <int CO>
+static void launch_small(const ConvArgs &a, int batch, bool cpar, hipStream_t s) {
+    const long long total = (long long)batch * a.M;
+    if (!cpar) {
+        conv_direct_small<CO><<<cdiv(total, 256), 256, 0, s>>>(a, batch);
+        return;
+    }
+    const int c4 = a.cin / 4;
+    if (c4 >= 64) conv_small_cpar<CO, 64><<<cdiv(total * 64, 256), 256, 0, s>>>(a, batch);
+    else if (c4 >= 32) conv_small_cpar<CO, 32><<<cdiv(total * 32, 256), 256, 0, s>>>(a, batch);
+    else if (c4 >= 16) conv_small_cpar<CO, 16><<<cdiv(total * 16, 256), 256, 0, s>>>(a, batch);
+    else if (c4 >= 8) conv_small_cpar<CO, 8><<<cdiv(total * 8, 256), 256, 0, s>>>(a, batch);
+    else conv_small_cpar<CO, 4><<<cdiv(total * 4, 256), 256, 0, s>>>(a, batch);
+}
+
 // ------------------------------------------------------------------ host side
 struct TileCfg {
     int bm, bn, wm;
@@ -619,7 +700,8 @@ static void launch_tile(const ConvArgs &a, int amode, bool bkn, dim3 grid, hipSt
         case 2: conv_igemm<BM, BN, WM, 1, 0><<<grid, 256, 0, s>>>(a); break;
         case 3: conv_igemm<BM, BN, WM, 1, 1><<<grid, 256, 0, s>>>(a); break;
         case 4: conv_igemm<BM, BN, WM, 2, 0><<<grid, 256, 0, s>>>(a); break;
-        default: conv_igemm<BM, BN, WM, 2, 1><<<grid, 256, 0, s>>>(a); break;
+        case 5: conv_igemm<BM, BN, WM, 2, 1><<<grid, 256, 0, s>>>(a); break;
+        default: conv_igemm<BM, BN, WM, 3, 0><<<grid, 256, 0, s>>>(a); break;   // 6 (reflect, packed B)
     }
 }
 
@@ -629,6 +711,8 @@ static int a_mode(const s2v_conv_params *p) {
     if (!vec) return 2;
     const bool simple_pre = (p->pre_act == S2V_ACT_NONE || p->pre_act == S2V_ACT_RELU || p->pre_act == S2V_ACT_LRELU) &&
                             (!p->in_scale || (p->in_scale_ns % 4 == 0 && ((uintptr_t)p->in_scale % 16) == 0));
+    if (p->cin % 32 == 0 && p->in_mode == S2V_IN_DIRECT && simple_pre && !p->b_kn)
+        return p->pad_mode == S2V_PAD_ZERO ? 0 : 3;
     if (p->cin % 32 == 0 && p->in_mode == S2V_IN_DIRECT && p->pad_mode == S2V_PAD_ZERO && simple_pre) return 0;
     return 1;
 }
@@ -652,7 +736,13 @@ extern "C" int s2v_conv2d_plan(const s2v_conv_params *p, int *out6) {
     if (rc) return rc;
     Plan pl = make_plan(p, M, K);
     if (pl.tile < 0) {
-        out6[0] = 0; out6[1] = p->cout < 4 ? p->cout : 4; out6[2] = 0; out6[3] = 0; out6[4] = 0; out6[5] = 1;
+        const bool cpar = (p->cin % 4 == 0) && (p->xcs % 4 == 0) && (((uintptr_t)p->x % 16) == 0) &&
+                          (p->x_bs % 4 == 0) && (!p->in_scale || (p->in_scale_ns % 4 == 0 &&
+                                                                  ((uintptr_t)p->in_scale % 16) == 0));
+        const int c4 = p->cin / 4;
+        out6[0] = 0; out6[1] = p->cout < 4 ? p->cout : 4;
+        out6[2] = !cpar ? 0 : (c4 >= 64 ? 64 : c4 >= 32 ? 32 : c4 >= 16 ? 16 : c4 >= 8 ? 8 : 4);
+        out6[3] = 0; out6[4] = 0; out6[5] = 1;
         return 0;
     }
     const TileCfg &t = kTiles[pl.tile];
@@ -672,15 +762,16 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
     Plan pl = make_plan(p, M, K);
     ConvArgs a = make_args(p, M, K, pl);
     if (pl.tile < 0) {
-        const long long total = (long long)batch * M;
-        dim3 grid(cdiv(total, 256));
+        const bool cpar = (p->cin % 4 == 0) && (p->xcs % 4 == 0) && (((uintptr_t)p->x % 16) == 0) &&
+                          (p->x_bs % 4 == 0) && (!p->in_scale || (p->in_scale_ns % 4 == 0 &&
+                                                                  ((uintptr_t)p->in_scale % 16) == 0));
         switch (p->cout) {
-            case 1: conv_direct_small<1><<<grid, 256, 0, s>>>(a, batch); break;
-            case 2: conv_direct_small<2><<<grid, 256, 0, s>>>(a, batch); break;
-            case 3: conv_direct_small<3><<<grid, 256, 0, s>>>(a, batch); break;
-            default: conv_direct_small<4><<<grid, 256, 0, s>>>(a, batch); break;
+            case 1: launch_small<1>(a, batch, cpar, s); break;
+            case 2: launch_small<2>(a, batch, cpar, s); break;
+            case 3: launch_small<3>(a, batch, cpar, s); break;
+            default: launch_small<4>(a, batch, cpar, s); break;
         }
-        return check_launch("conv_direct_small");
+        return check_launch("conv_small");
     }
     if (pl.splits > 1) {
         const size_t need = (size_t)batch * pl.splits * (size_t)M * p->cout * sizeof(float);

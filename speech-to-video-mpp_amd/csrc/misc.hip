@@ -333,6 +333,62 @@ __global__ __launch_bounds__(256) void gaussian_kernel(float *__restrict__ y, lo
     }
 }
 
+// ------------------------------------------------------------------ pipeline glue
+// DNet fake image -> uint8 reference frame (facing.py:190-191: uint8((clamp(x,-1,1)+1)/2*255),
+// truncation like numpy's float->uint8 cast) and the ENet inputs built from it (inference.py:
+// 393-399: lower half of the original crop zeroed, [masked | ref] / 255; gt = ref).
+__global__ __launch_bounds__(256) void lipsync_inputs_kernel(const float *__restrict__ src, const float *__restrict__ fake,
+                                                            int n, int h, int w, unsigned char *__restrict__ ref_u8,
+                                                            float *__restrict__ face6, float *__restrict__ gt) {
+    const long long plane = (long long)h * w;
+    const long long total = (long long)n * 3 * plane;
+    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+        const long long p = e % plane;
+        const int c = (int)((e / plane) % 3);
+        const int b = (int)(e / (3 * plane));
+        const int y = (int)(p / w);
+        float f = fminf(fmaxf(fake[e], -1.f), 1.f);
+        const unsigned char q = (unsigned char)((f + 1.f) * 0.5f * 255.f);
+        ref_u8[e] = q;
+        const float r = (float)q / 255.f;
+        // original crop as uint8 then /255 (the reference reads frames as uint8)
+        float s = fminf(fmaxf(src[e], -1.f), 1.f);
+        const float o = (float)(unsigned char)((s + 1.f) * 0.5f * 255.f) / 255.f;
+        const long long base6 = (long long)b * 6 * plane;
+        face6[base6 + (long long)c * plane + p] = (y >= h / 2) ? 0.f : o;
+        face6[base6 + (long long)(c + 3) * plane + p] = r;
+        gt[e] = r;
+    }
+}
+
+// ENet output -> uint8 frames (inference.py:267 clamp(0,1), :288 * 255, uint8 cast truncates)
+__global__ __launch_bounds__(256) void to_u8_kernel(const float *__restrict__ x, long long n, float lo, float hi,
+                                                    float scale, float offset, unsigned char *__restrict__ y) {
+    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < n; e += (long long)gridDim.x * 256)
+        y[e] = (unsigned char)((fminf(fmaxf(x[e], lo), hi) + offset) * scale);
+}
+
+// y = post * act(x * a + mul * + add + bias[c]) over NHWC views (SFT, skip adds, noise halves)
+__global__ __launch_bounds__(256) void eltwise_kernel(const float *__restrict__ x, int xcs, const float *__restrict__ mul,
+                                                      int mcs, const float *__restrict__ add, int acs,
+                                                      const float *__restrict__ bias, long long pixels, int c, float a,
+                                                      int act, float alpha, float post, float *__restrict__ y, int ycs) {
+    const long long total = pixels * c;
+    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+        const long long p = e / c;
+        const int cc = (int)(e - p * c);
+        float v = x[p * xcs + cc] * a;
+        if (mul) v *= mul[p * mcs + cc];
+        if (add) v += add[p * acs + cc];
+        if (bias) v += bias[cc];
+        y[p * ycs + cc] = apply_act(v, act, alpha) * post;
+    }
+}
+
+__global__ __launch_bounds__(256) void fill_kernel(float *__restrict__ y, long long n, float v) {
+    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < n; e += (long long)gridDim.x * 256) y[e] = v;
+}
+
 static unsigned grid_for(long long total) {
     long long b = (total + 255) / 256;
     if (b > 65535LL * 16) b = 65535LL * 16;
@@ -441,4 +497,38 @@ extern "C" int s2v_gaussian_noise(float *y, long long n, unsigned long long seed
     if (n == 0) return 0;
     gaussian_kernel<<<grid_for(n), 256, 0, (hipStream_t)stream>>>(y, n, seed, offset);
     return check_launch("gaussian_noise");
+}
+
+extern "C" int s2v_lipsync_inputs(const float *src, const float *fake, int n, int h, int w, unsigned char *ref_u8,
+                                  float *face6, float *gt, s2v_stream_t stream) {
+    S2V_REQUIRE(src && fake && ref_u8 && face6 && gt && n > 0 && h > 1 && w > 0, "lipsync_inputs: bad args");
+    lipsync_inputs_kernel<<<grid_for((long long)n * 3 * h * w), 256, 0, (hipStream_t)stream>>>(src, fake, n, h, w,
+                                                                                               ref_u8, face6, gt);
+    return check_launch("lipsync_inputs");
+}
+
+extern "C" int s2v_to_u8(const float *x, long long n, float lo, float hi, float scale, float offset, unsigned char *y,
+                         s2v_stream_t stream) {
+    S2V_REQUIRE(x && y && n >= 0, "to_u8: bad args");
+    if (n == 0) return 0;
+    to_u8_kernel<<<grid_for(n), 256, 0, (hipStream_t)stream>>>(x, n, lo, hi, scale, offset, y);
+    return check_launch("to_u8");
+}
+
+extern "C" int s2v_eltwise(const float *x, int xcs, const float *mul, int mcs, const float *add, int acs,
+                           const float *bias, long long pixels, int c, float a, int act, float alpha, float post,
+                           float *y, int ycs, s2v_stream_t stream) {
+    S2V_REQUIRE(x && y && pixels >= 0 && c > 0 && xcs >= c && ycs >= c && (!mul || mcs >= c) && (!add || acs >= c),
+                "eltwise: bad args");
+    if (pixels == 0) return 0;
+    eltwise_kernel<<<grid_for(pixels * c), 256, 0, (hipStream_t)stream>>>(x, xcs, mul, mcs, add, acs, bias, pixels,
+                                                                           c, a, act, alpha, post, y, ycs);
+    return check_launch("eltwise");
+}
+
+extern "C" int s2v_fill(float *y, long long n, float value, s2v_stream_t stream) {
+    S2V_REQUIRE(y && n >= 0, "fill: bad args");
+    if (n == 0) return 0;
+    fill_kernel<<<grid_for(n), 256, 0, (hipStream_t)stream>>>(y, n, value);
+    return check_launch("fill");
 }

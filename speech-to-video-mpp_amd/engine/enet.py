@@ -27,6 +27,8 @@ class StyleLayer:
         m = p + "modulated_conv."
         w = sd[m + "weight"].float()[0]                      # [O, I, k, k]
         self.k = w.shape[-1]
+        if w.shape[1] == 3:                                  # 3-channel image input, carried as 4
+            w = ops.pad_cin(w, 4)
         self.cin, self.cout = w.shape[1], w.shape[0]
         self.demodulate, self.upsample, self.is_rgb = demodulate, upsample, is_rgb
         bias = sd[p + "bias"].float().reshape(-1)
@@ -34,6 +36,9 @@ class StyleLayer:
         self.wsq = w.pow(2).sum((2, 3)).contiguous().to(device)   # [O, I]
         self.mod_w = sd[m + "modulation.weight"].float()
         self.mod_b = sd[m + "modulation.bias"].float()
+        if self.mod_w.shape[0] < self.cin:                   # zero modulation for the padding channel
+            self.mod_w = torch.cat([self.mod_w, torch.zeros(self.cin - self.mod_w.shape[0], self.mod_w.shape[1])])
+            self.mod_b = torch.cat([self.mod_b, torch.zeros(self.cin - self.mod_b.shape[0])])
         self.noise_w = None if is_rgb else float(sd[p + "weight"].float().reshape(-1)[0])
         self.device = device
 
@@ -43,7 +48,8 @@ class ENetEngine:
         dev = torch.device(device)
         self.device = dev
         self.lnet = LNetEngine(sd, dev, prefix="low_res.")
-        self.first = ConvW(sd["conv_body_first.weight"], sd["conv_body_first.bias"], dev)
+        # 3-channel images are carried as 4 channels (4th = 0) so their convs use the float4 gather
+        self.first = ConvW(ops.pad_cin(sd["conv_body_first.weight"].float(), 4), sd["conv_body_first.bias"], dev)
         self.down = []
         for i in range(6):
             p = f"conv_body_down.{i}."
@@ -79,8 +85,9 @@ class ENetEngine:
     def style_code(self, ctx, ref: torch.Tensor):
         """ref: NCHW [B,3,H,W] device tensor -> style [B,1,1,512] (ENet.py:94-101)."""
         dev, b = self.device, ref.shape[0]
-        x = NHWC.empty(b, 256, 256, 3, dev)
-        ops.nchw_to_nhwc(ctx, ref, x)                              # F.interpolate(ref, 256, bilinear)
+        x = NHWC.empty(b, 256, 256, 4, dev)
+        ops.fill(ctx, x.t)
+        ops.nchw_to_nhwc(ctx, ref, x.slice(0, 3))                  # F.interpolate(ref, 256, bilinear)
         f = NHWC.empty(b, 256, 256, self.first.cout, dev)
         ops.conv2d(ctx, x, self.first, f, act=ops.ACT_LRELU, alpha=LRELU)
         for c1, c2, sk in self.down:                                # ResBlock(mode='down'), base_blocks.py:40-49
@@ -116,13 +123,13 @@ class ENetEngine:
         x6 = NHWC.empty(b, 96, 96, 6, dev)
         ops.nchw_to_nhwc(ctx, face[:, :3], x6.slice(0, 3))
         ops.nchw_to_nhwc(ctx, gt, x6.slice(3, 3))
-        lo = NHWC.empty(b, 96, 96, 3, dev)
-        self.lnet.forward(ctx, audio, x6, lo)
-        ops.nhwc_to_nchw(ctx, lo, low)
+        lo = NHWC.empty(b, 96, 96, 4, dev)          # channel 3 = sigmoid(0): finite, zero weights
+        self.lnet.forward(ctx, audio, x6, lo, pad_rgb=True)
+        ops.nhwc_to_nchw(ctx, lo.slice(0, 3), low)
         # F.pad(reflect, 2) -> StyleConv / ToRGB stages (ENet.py:119-129)
-        cur = NHWC.empty(b, 100, 100, 3, dev)
+        cur = NHWC.empty(b, 100, 100, 4, dev)
         ops.pad_reflect(ctx, lo, cur, (2, 2, 2, 2))
-        skip = cur
+        skip = cur.slice(0, 3)
         self.calls += 1
         for st in range(2):
             for li in range(2):

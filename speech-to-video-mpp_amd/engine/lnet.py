@@ -186,10 +186,15 @@ class LNetEngine:
                                     jump=ConvNormAct(sd, f"{d}jump{i}.", dev, 3)))
         self.bank.build(dev)
         self.final = make_conv(sd, d + "final.model.0.", dev, padding=3)
+        fw = conv_weight(sd, d + "final.model.0.")                 # 4-output variant (4th row zero)
+        self.final4 = ConvW(torch.cat([fw, torch.zeros((1,) + tuple(fw.shape[1:]))]),
+                            torch.cat([sd[d + "final.model.0.bias"].float(), torch.zeros(1)]), dev, padding=3)
 
-    def forward(self, ctx, audio: torch.Tensor, face6: NHWC, out: NHWC, logits: NHWC | None = None):
+    def forward(self, ctx, audio: torch.Tensor, face6: NHWC, out: NHWC, logits: NHWC | None = None,
+                pad_rgb: bool = False):
         """audio: [B,1,80,16] device tensor; face6: NHWC [B,96,96,6] = [masked | ref];
-        out: NHWC [B,96,96,3] receives sigmoid(final conv)."""
+        out: NHWC [B,96,96,3] receives sigmoid(final conv) ([B,96,96,4] with a 4th constant channel
+        when ``pad_rgb``)."""
         dev = self.device
         b = face6.n
         # ---- visual encoder (LNet.py:30-43)
@@ -236,5 +241,5 @@ class LNetEngine:
             cur = up
         if logits is not None:
             ops.conv2d(ctx, cur, self.final, logits)
-        ops.conv2d(ctx, cur, self.final, out, act=ops.ACT_SIGMOID)
+        ops.conv2d(ctx, cur, self.final4 if pad_rgb else self.final, out, act=ops.ACT_SIGMOID)
         return out

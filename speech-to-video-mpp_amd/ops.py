@@ -229,6 +229,8 @@ def conv_symbol(ctx: Ctx, p) -> str:
     check(ctx.lib.s2v_conv2d_plan(ctypes.byref(p), out), "s2v_conv2d_plan")
     bm, bn, wm, avec, bkn, splits = list(out)
     if bm == 0:
+        if wm:
+            return f"void s2v::conv_small_cpar<{bn}, {wm}>(s2v::ConvArgs, int)"
         return f"void s2v::conv_direct_small<{bn}>(s2v::ConvArgs, int)"
     return f"void s2v::conv_igemm<{bm}, {bn}, {wm}, {avec}, {bkn}>(s2v::ConvArgs)"
 
@@ -356,6 +358,19 @@ def flow_warp(ctx: Ctx, flow: NHWC, src: torch.Tensor, y: NHWC):
     check(ctx.lib.s2v_flow_warp(flow.ptr, flow.n, flow.h, flow.w, flow.cs, src.data_ptr(), c, h, w, *src.stride(),
                                 y.ptr, y.cs, ctx.stream), "s2v_flow_warp")
     return y
+
+
+def fill(ctx: Ctx, t: torch.Tensor, value: float = 0.0):
+    check(ctx.lib.s2v_fill(t.data_ptr(), t.numel(), value, ctx.stream), "s2v_fill")
+    return t
+
+
+def pad_cin(w: torch.Tensor, cin: int) -> torch.Tensor:
+    """Zero-pad a conv weight [O, I, kh, kw] along I (vectorised 4-channel image layout)."""
+    if w.shape[1] >= cin:
+        return w
+    z = torch.zeros((w.shape[0], cin - w.shape[1]) + tuple(w.shape[2:]), dtype=w.dtype)
+    return torch.cat([w, z], 1)
 
 
 def gaussian_noise(ctx: Ctx, out: torch.Tensor, seed: int, offset: int = 0):

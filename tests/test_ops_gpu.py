@@ -333,3 +333,21 @@ def test_melspectrogram_matches_restatement(pad_mode):
     assert chunks.shape == (len(starts), 1, 80, 16)
     for i, s in enumerate(starts):
         assert np.array_equal(chunks[i, 0], exp[:, s: s + 16].astype(np.float32))
+
+
+@pytest.mark.parametrize("cin,k,cout", [(64, 7, 3), (128, 1, 3), (256, 1, 3), (256, 7, 2), (12, 3, 1)])
+def test_small_cout_conv(ctx, cin, k, cout):
+    """Cout <= 4 heads (LNet/DNet final 7x7, ToRGB 1x1 with modulation, flow head): channel-parallel
+    kernel with in_scale prologue and in-place residual."""
+    n, h, w = 2, 13, 11
+    wt = rnd(cout, cin, k, k, seed=40) / math.sqrt(cin * k * k)
+    bias = rnd(cout, seed=41)
+    x = rnd(n, cin, h, w, seed=42)
+    s = rnd(n, cin, seed=43, lo=0.5, hi=1.5)
+    res = rnd(n, cout, h, w, seed=44)
+    cw = ConvW(wt.float(), bias.float(), DEV, padding=k // 2)
+    y = nhwc(res.float())
+    ops.conv2d(ctx, nhwc(x.float()), cw, y, in_scale=s.float().to(DEV), res=y)
+    ref = F.conv2d(x * s[:, :, None, None], wt, bias, padding=k // 2) + res
+    bound = conv_bound(x * s[:, :, None, None], wt, 1, k // 2, 1)
+    assert ((to_nchw(y) - ref).abs() <= 2e-6 * (bound + 1) + 1e-6).all()
