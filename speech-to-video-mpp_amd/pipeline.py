@@ -1,0 +1,172 @@
+"""Full-clip per-frame lip-sync path (BASELINE configs 3/4): wav -> mel windows, semantic 3DMM
+coefficients -> DNet expression-canonicalised reference faces -> ENet(+LNet) -> uint8 frames.
+
+Reference flow restated (host parts are plain NumPy, device parts libs2v kernels):
+  * mel + 16-column windows          inference.py:204-216            (s2v_amd.audio)
+  * DNet coefficient windows          futils/inference_utils.py:73-99, preprocessing/facing.py:176-187
+  * DNet -> uint8 stabilised frame   facing.py:189-191
+  * ENet batch inputs                 inference.py:393-399 (lower half of the crop masked, /255)
+  * ENet -> clamp(0,1)*255 -> uint8   inference.py:266-288
+
+Multi-GPU: frames are independent once the per-clip host data exists, so ranks
+take contiguous frame ranges; RCCL (torch.distributed 'nccl') carries only the broadcast of the
+per-clip host tensors (wav, semantic coefficients, expression) and the final gather of the uint8
+frames.  The helpers are backend-agnostic (gloo on CPU in the tests).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib, audio
+from .ops import Ctx
+
+
+# ----------------------------------------------------------------------------- host precompute
+def obtain_seq_index(index: int, num_frames: int):
+    """inference_utils.py:73-76: 26-frame window centred on ``index``, clamped to the clip."""
+    return [min(max(i, 0), num_frames - 1) for i in range(index - 13, index + 13)]
+
+
+def transform_semantic(semantic: np.ndarray, frame_index: int, crop_norm_ratio=None) -> np.ndarray:
+    """inference_utils.py:78-91 -> float32 [73, 26] (exp 64 | angles 3 | translation 3 | crop 3)."""
+    coeff = semantic[obtain_seq_index(frame_index, semantic.shape[0])]
+    ex, ang, trans = coeff[:, 80:144], coeff[:, 224:227], coeff[:, 254:257]
+    crop = coeff[:, 259:262].copy()
+    if crop_norm_ratio:
+        crop[:, -3] = crop[:, -3] * crop_norm_ratio
+    return np.concatenate([ex, ang, trans, crop], 1).astype(np.float32).T.copy()
+
+
+def find_crop_norm_ratio(source_coeff: np.ndarray, target_coeffs: np.ndarray):
+    """inference_utils.py:93-99 (argmin of 0.3 * exp diff + 0.7 * angle diff)."""
+    alpha = 0.3
+    exp_diff = np.mean(np.abs(target_coeffs[:, 80:144] - source_coeff[:, 80:144]), 1)
+    angle_diff = np.mean(np.abs(target_coeffs[:, 224:227] - source_coeff[:, 224:227]), 1)
+    index = np.argmin(alpha * exp_diff + (1 - alpha) * angle_diff)
+    return source_coeff[:, -3] / target_coeffs[index: index + 1, -3]
+
+
+def dnet_coefficients(semantic: np.ndarray, expression=None, one_shot: bool = False, start: int = 0,
+                      stop: int | None = None) -> np.ndarray:
+    """facing.py:176-187 for frames [start, stop) -> float32 [n, 73, 26]; ``expression`` (64,)
+    overwrites the expression rows (the 'hack_3dmm_expression' step)."""
+    stop = semantic.shape[0] if stop is None else stop
+    out = np.empty((stop - start, 73, 26), dtype=np.float32)
+    for k, idx in enumerate(range(start, stop)):
+        src = semantic[0:1] if one_shot else semantic[idx: idx + 1]
+        ratio = find_crop_norm_ratio(src, semantic)
+        out[k] = transform_semantic(semantic, idx, ratio)
+        if expression is not None:
+            out[k, :64, :] = np.asarray(expression, dtype=np.float32)[:64, None]
+    return out
+
+
+def shard_range(n: int, rank: int, world: int):
+    """Contiguous frame range of ``rank`` (sizes differ by at most one)."""
+    base, extra = divmod(n, world)
+    start = rank * base + min(rank, extra)
+    return start, start + base + (1 if rank < extra else 0)
+
+
+# ----------------------------------------------------------------------------- device path
+class LipSyncPipeline:
+    """mel windows + DNet source frames + coefficient windows -> uint8 [n, 3, 384, 384] frames."""
+
+    def __init__(self, dnet, enet, device="cuda", batch: int = 16):
+        self.dnet, self.enet = dnet, enet
+        self.device = torch.device(device)
+        self.batch = batch
+        self.ctx = Ctx(self.device)
+
+    @torch.no_grad()
+    def run_batch(self, mel: torch.Tensor, src: torch.Tensor, coeff: torch.Tensor, out_u8: torch.Tensor):
+        """mel [b,1,80,16], src [b,3,256,256] in [-1,1] (DNet input, trans_image layout), coeff
+        [b,73,26] -> out_u8 [b,3,384,384] (RGB, NCHW)."""
+        b, _, h, w = src.shape
+        fake = self.dnet(src, coeff)["fake_image"]
+        ref_u8 = torch.empty((b, 3, h, w), dtype=torch.uint8, device=self.device)
+        face6 = torch.empty((b, 6, h, w), device=self.device)
+        gt = torch.empty((b, 3, h, w), device=self.device)
+        _lib.check(self.ctx.lib.s2v_lipsync_inputs(src.contiguous().data_ptr(), fake.data_ptr(), b, h, w,
+                                                   ref_u8.data_ptr(), face6.data_ptr(), gt.data_ptr(),
+                                                   self.ctx.stream), "s2v_lipsync_inputs")
+        pred, _ = self.enet(mel, face6, gt)
+        _lib.check(self.ctx.lib.s2v_to_u8(pred.data_ptr(), pred.numel(), 0.0, 1.0, 255.0, 0.0, out_u8.data_ptr(),
+                                          self.ctx.stream), "s2v_to_u8")
+        return out_u8
+
+    @torch.no_grad()
+    def run(self, mel_chunks: torch.Tensor, src: torch.Tensor, coeffs: torch.Tensor, start: int = 0,
+            stop: int | None = None) -> torch.Tensor:
+        """Frames [start, stop): ``mel_chunks`` indexed absolutely, ``src`` / ``coeffs`` hold only
+        the frames of this range."""
+        stop = mel_chunks.shape[0] if stop is None else stop
+        n = stop - start
+        out = torch.empty((n, 3, 384, 384), dtype=torch.uint8, device=self.device)
+        for b0 in range(0, n, self.batch):
+            b1 = min(n, b0 + self.batch)
+            self.run_batch(mel_chunks[start + b0: start + b1], src[b0:b1], coeffs[b0:b1], out[b0:b1])
+        return out
+
+
+# ----------------------------------------------------------------------------- distributed helpers
+def broadcast_tensor(t: torch.Tensor | None, shape, dtype, device, src: int = 0) -> torch.Tensor:
+    """Broadcast a per-clip host tensor from ``src`` (RCCL on GPU, gloo on CPU)."""
+    import torch.distributed as dist
+    if dist.get_rank() == src:
+        buf = t.to(device=device, dtype=dtype).contiguous()
+    else:
+        buf = torch.empty(shape, dtype=dtype, device=device)
+    dist.broadcast(buf, src)
+    return buf
+
+
+def gather_frames(local: torch.Tensor, n_total: int, dst: int = 0):
+    """Gather contiguous frame shards (shard_range layout) to ``dst``; returns [n_total, ...] on
+    dst, None elsewhere.  Uses all_gather_into_tensor on equal, padded shards."""
+    import torch.distributed as dist
+    world, rank = dist.get_world_size(), dist.get_rank()
+    per = (n_total + world - 1) // world
+    pad = torch.zeros((per,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    pad[: local.shape[0]] = local
+    full = torch.empty((per * world,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    if local.dtype == torch.uint8 and local.device.type == "cpu":
+        # gloo has no uint8 all_gather_into_tensor: gather as a list
+        parts = [torch.empty_like(pad) for _ in range(world)]
+        dist.all_gather(parts, pad)
+        full = torch.cat(parts, 0)
+    else:
+        dist.all_gather_into_tensor(full, pad)
+    if rank != dst:
+        return None
+    pieces = []
+    for r in range(world):
+        s, e = shard_range(n_total, r, world)
+        pieces.append(full[r * per: r * per + (e - s)])
+    return torch.cat(pieces, 0)
+
+
+def run_sharded(pipeline: LipSyncPipeline, wav, semantic, expression, src_provider, fps: float = 25.0,
+                one_shot: bool = False):
+    """The whole clip across all ranks.  Rank 0 holds ``wav`` (float32 [S]), ``semantic`` [N, 262],
+    ``expression`` [64]; ``src_provider(start, stop)`` returns this rank's DNet source frames
+    [n,3,256,256] on its device.  Returns the uint8 frames [n_chunks, 3, 384, 384] on rank 0."""
+    import torch.distributed as dist
+    dev = pipeline.device
+    rank = dist.get_rank()
+    meta = torch.tensor([0 if wav is None else len(wav), 0 if semantic is None else semantic.shape[0]],
+                        dtype=torch.int64, device=dev)
+    dist.broadcast(meta, 0)
+    ns, nf = int(meta[0]), int(meta[1])
+    wav_t = broadcast_tensor(None if rank else torch.as_tensor(wav), (ns,), torch.float32, dev)
+    sem_t = broadcast_tensor(None if rank else torch.as_tensor(semantic), (nf, 262), torch.float32, dev)
+    exp_t = broadcast_tensor(None if rank else torch.as_tensor(expression), (64,), torch.float32, dev)
+    mel = audio.melspectrogram(wav_t)
+    chunks = audio.mel_chunks(mel, fps=fps)
+    n = min(chunks.shape[0], nf)                       # inference.py:220-222 truncation
+    start, stop = shard_range(n, dist.get_rank(), dist.get_world_size())
+    sem = sem_t.cpu().numpy()[:n]
+    coeffs = torch.from_numpy(dnet_coefficients(sem, exp_t.cpu().numpy(), one_shot, start, stop)).to(dev)
+    local = pipeline.run(chunks, src_provider(start, stop), coeffs, start, stop)
+    return gather_frames(local, n)

@@ -1,0 +1,112 @@
+"""Full-clip path on the device: the glue kernels bit-exact against the
+oracle's restatement, a ragged multi-batch run against the CPU oracle chain DNet -> uint8 ->
+ENet -> uint8, and run_sharded (RCCL, world 1) reproducing run().
+
+uint8 tolerance: the fp32 networks agree to ~1e-2 before quantisation and DNet's uint8 reference
+frame can flip by one level, so frames agree within a few levels with a tiny mean difference."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+import s2v_import  # noqa: F401
+from helpers import synth_sd
+from s2v_amd import synth
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def nets_pair():
+    from s2v_amd import models
+    d = models.DNet()
+    d.load_state_dict(synth_sd("dnet"), strict=True)
+    e = models.ENet()
+    e.load_state_dict(synth_sd("enet"), strict=True)
+    return d.eval(), e.eval()
+
+
+def test_glue_kernels_bit_exact():
+    from oracle import pipeline as OP
+    from s2v_amd import _lib
+    from s2v_amd.ops import Ctx
+    g = torch.Generator().manual_seed(3)
+    src = torch.rand((2, 3, 64, 48), generator=g) * 2.4 - 1.2           # includes out-of-range values
+    fake = torch.rand((2, 3, 64, 48), generator=g) * 2.4 - 1.2
+    ctx = Ctx(torch.device(DEV))
+    ref_u8 = torch.empty((2, 3, 64, 48), dtype=torch.uint8, device=DEV)
+    face6 = torch.empty((2, 6, 64, 48), device=DEV)
+    gt = torch.empty((2, 3, 64, 48), device=DEV)
+    _lib.check(ctx.lib.s2v_lipsync_inputs(src.to(DEV).data_ptr(), fake.to(DEV).data_ptr(), 2, 64, 48,
+                                          ref_u8.data_ptr(), face6.data_ptr(), gt.data_ptr(), ctx.stream), "li")
+    r_u8, r_face6, r_gt = OP.lipsync_inputs(src, fake)
+    assert torch.equal(ref_u8.cpu(), r_u8) and torch.equal(face6.cpu(), r_face6) and torch.equal(gt.cpu(), r_gt)
+    x = torch.rand(1000, generator=g) * 1.6 - 0.3
+    y = torch.empty(1000, dtype=torch.uint8, device=DEV)
+    _lib.check(ctx.lib.s2v_to_u8(x.to(DEV).data_ptr(), 1000, 0.0, 1.0, 255.0, 0.0, y.data_ptr(), ctx.stream), "u8")
+    assert torch.equal(y.cpu(), (x.clamp(0, 1) * 255).to(torch.uint8))
+
+
+def _clip(n_frames, seed):
+    rng = np.random.default_rng(seed)
+    semantic = rng.standard_normal((n_frames, 262)).astype(np.float32)
+    semantic[:, -3] = 1.0 + 0.1 * rng.random(n_frames)           # crop scale, away from 0
+    expression = rng.standard_normal(64).astype(np.float32)
+    wav = (0.2 * rng.standard_normal(int(16000 * n_frames / 25))).astype(np.float32)
+    src, _ = synth.dnet_inputs(f"pipeline.{seed}", n_frames, 256)
+    return wav, semantic, expression, torch.from_numpy(src)
+
+
+def _check_u8(got, ref):
+    d = (got.cpu().int() - ref.int()).abs()
+    assert d.max() <= 6 and d.float().mean() <= 0.05, (int(d.max()), float(d.float().mean()))
+
+
+def test_pipeline_ragged_batches_vs_oracle(nets_pair):
+    from oracle import pipeline as OP
+    from s2v_amd import audio, pipeline as P
+    dnet, enet = nets_pair
+    wav, semantic, expression, src = _clip(5, 1)
+    mel = audio.melspectrogram(torch.from_numpy(wav).to(DEV))
+    chunks = audio.mel_chunks(mel)
+    n = min(chunks.shape[0], 5)
+    coeffs = torch.from_numpy(P.dnet_coefficients(semantic[:n], expression))
+    pipe = P.LipSyncPipeline(dnet, enet, DEV, batch=2)                # batches 2, 2, 1
+    got = pipe.run(chunks, src[:n].to(DEV), coeffs.to(DEV), 0, n)
+    assert got.shape == (n, 3, 384, 384) and got.dtype == torch.uint8
+    with torch.no_grad():
+        ref = OP.lipsync_frames(synth_sd("dnet"), synth_sd("enet"), chunks[:n].cpu(), src[:n], coeffs)
+    _check_u8(got, ref)
+    # a sub-range with relative src/coeffs reproduces the same frames
+    part = pipe.run(chunks, src[1:4].to(DEV), coeffs[1:4].to(DEV), 1, 4)
+    assert (part.int() - got[1:4].int()).abs().max() <= 1
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_run_sharded_world1_rccl(nets_pair):
+    import torch.distributed as dist
+    from s2v_amd import audio, pipeline as P
+    dnet, enet = nets_pair
+    wav, semantic, expression, src = _clip(4, 2)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device(DEV, 0))
+    try:
+        pipe = P.LipSyncPipeline(dnet, enet, DEV, batch=16)
+        full = P.run_sharded(pipe, wav, semantic, expression, lambda s, e: src[s:e].to(DEV))
+    finally:
+        dist.destroy_process_group()
+    chunks = audio.mel_chunks(audio.melspectrogram(torch.from_numpy(wav).to(DEV)))
+    n = min(chunks.shape[0], 4)
+    coeffs = torch.from_numpy(P.dnet_coefficients(semantic[:n], expression)).to(DEV)
+    direct = pipe.run(chunks, src[:n].to(DEV), coeffs, 0, n)
+    assert full.shape == direct.shape and torch.equal(full.cpu(), direct.cpu())

@@ -1,0 +1,100 @@
+"""Host logic of the full-clip pipeline: coefficient windows, crop-norm ratio, sharding, and the
+RCCL-path helpers (broadcast + gather) exercised with world_size 2 on the gloo backend."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import s2v_import  # noqa: F401
+from s2v_amd import pipeline as P
+
+
+def test_seq_index_and_transform_semantic():
+    assert P.obtain_seq_index(0, 100)[:14] == [0] * 14 and P.obtain_seq_index(0, 100)[-1] == 12
+    assert P.obtain_seq_index(99, 100)[-1] == 99 and len(P.obtain_seq_index(50, 100)) == 26
+    sem = np.arange(5 * 262, dtype=np.float64).reshape(5, 262)
+    c = P.transform_semantic(sem, 2, 2.0)
+    assert c.shape == (73, 26) and c.dtype == np.float32
+    rows = P.obtain_seq_index(2, 5)
+    assert np.array_equal(c[:64, 0], sem[rows[0], 80:144])
+    assert np.array_equal(c[64:67, 5], sem[rows[5], 224:227])
+    assert np.array_equal(c[67:70, 7], sem[rows[7], 254:257])
+    assert c[70, 3] == sem[rows[3], 259] * 2.0 and c[72, 3] == sem[rows[3], 261]
+
+
+def test_find_crop_norm_ratio_picks_closest_frame():
+    rng = np.random.default_rng(0)
+    sem = rng.standard_normal((20, 262))
+    src = sem[7:8].copy()
+    src[:, -3] = 3.0
+    sem[7, -3] = 1.5
+    r = P.find_crop_norm_ratio(src, sem)          # frame 7 matches exp/angles exactly
+    assert np.allclose(r, [2.0])
+
+
+def test_dnet_coefficients_expression_hack_and_ranges():
+    rng = np.random.default_rng(1)
+    sem = rng.standard_normal((30, 262))
+    exp = rng.standard_normal(64)
+    full = P.dnet_coefficients(sem, exp)
+    assert full.shape == (30, 73, 26)
+    assert np.allclose(full[:, :64, :], exp.astype(np.float32)[None, :, None])
+    part = P.dnet_coefficients(sem, exp, start=11, stop=17)
+    assert np.array_equal(part, full[11:17])
+    one = P.dnet_coefficients(sem, None, one_shot=True)
+    r0 = P.find_crop_norm_ratio(sem[0:1], sem)
+    assert np.allclose(one[4], P.transform_semantic(sem, 4, r0))
+
+
+@pytest.mark.parametrize("n,world", [(1000, 8), (997, 8), (5, 8), (16, 2), (3, 1)])
+def test_shard_range_partitions(n, world):
+    ranges = [P.shard_range(n, r, world) for r in range(world)]
+    assert ranges[0][0] == 0 and ranges[-1][1] == n
+    for (a, b), (c, d) in zip(ranges, ranges[1:]):
+        assert b == c
+    sizes = [b - a for a, b in ranges]
+    assert max(sizes) - min(sizes) <= 1
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, n, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sem = torch.arange(n * 262, dtype=torch.float32).reshape(n, 262) if rank == 0 else None
+        got = P.broadcast_tensor(sem, (n, 262), torch.float32, torch.device("cpu"))
+        assert float(got[n - 1, 261]) == n * 262 - 1
+        s, e = P.shard_range(n, rank, world)
+        # per-frame stand-in for the device path: frame i -> constant (i % 251)
+        local = torch.stack([torch.full((3, 4, 4), i % 251, dtype=torch.uint8) for i in range(s, e)]) \
+            if e > s else torch.zeros((0, 3, 4, 4), dtype=torch.uint8)
+        full = P.gather_frames(local, n)
+        if rank == 0:
+            q.put([int(full[i, 0, 0, 0]) for i in range(n)])
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n", [7, 16])
+def test_broadcast_and_gather_world2_gloo(n):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, n, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    assert q.get(timeout=10) == [i % 251 for i in range(n)]
