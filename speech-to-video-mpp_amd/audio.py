@@ -102,6 +102,7 @@ def mel_chunks(mel: torch.Tensor, fps: float = 25.0, step: int = 16) -> torch.Te
     starts = torch.tensor(st, dtype=torch.int32).to(mel.device)
     out = torch.empty((len(st), 1, N_MELS, step), device=mel.device)
     ctx = _ctx(mel.device)
-    _lib.check(ctx.lib.s2v_mel_chunks(mel.contiguous().data_ptr(), T, starts.data_ptr(), len(st), step,
+    mel = mel.contiguous()
+    _lib.check(ctx.lib.s2v_mel_chunks(mel.data_ptr(), T, starts.data_ptr(), len(st), step,
                                       out.data_ptr(), ctx.stream), "s2v_mel_chunks")
     return out

@@ -88,7 +88,8 @@ class LipSyncPipeline:
         ref_u8 = torch.empty((b, 3, h, w), dtype=torch.uint8, device=self.device)
         face6 = torch.empty((b, 6, h, w), device=self.device)
         gt = torch.empty((b, 3, h, w), device=self.device)
-        _lib.check(self.ctx.lib.s2v_lipsync_inputs(src.contiguous().data_ptr(), fake.data_ptr(), b, h, w,
+        src = src.contiguous()
+        _lib.check(self.ctx.lib.s2v_lipsync_inputs(src.data_ptr(), fake.data_ptr(), b, h, w,
                                                    ref_u8.data_ptr(), face6.data_ptr(), gt.data_ptr(),
                                                    self.ctx.stream), "s2v_lipsync_inputs")
         pred, _ = self.enet(mel, face6, gt)
@@ -103,6 +104,9 @@ class LipSyncPipeline:
         the frames of this range."""
         stop = mel_chunks.shape[0] if stop is None else stop
         n = stop - start
+        if not (0 <= start <= stop <= mel_chunks.shape[0]) or src.shape[0] != n or coeffs.shape[0] != n:
+            raise ValueError(f"frames [{start}, {stop}) need {n} src frames / coefficient windows and "
+                             f"mel windows up to {stop} (got {src.shape[0]}, {coeffs.shape[0]}, {mel_chunks.shape[0]})")
         out = torch.empty((n, 3, 384, 384), dtype=torch.uint8, device=self.device)
         for b0 in range(0, n, self.batch):
             b1 = min(n, b0 + self.batch)

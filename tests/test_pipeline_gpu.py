@@ -40,13 +40,15 @@ def test_glue_kernels_bit_exact():
     ref_u8 = torch.empty((2, 3, 64, 48), dtype=torch.uint8, device=DEV)
     face6 = torch.empty((2, 6, 64, 48), device=DEV)
     gt = torch.empty((2, 3, 64, 48), device=DEV)
-    _lib.check(ctx.lib.s2v_lipsync_inputs(src.to(DEV).data_ptr(), fake.to(DEV).data_ptr(), 2, 64, 48,
+    src_d, fake_d = src.to(DEV), fake.to(DEV)          # keep the device copies alive across the launch
+    _lib.check(ctx.lib.s2v_lipsync_inputs(src_d.data_ptr(), fake_d.data_ptr(), 2, 64, 48,
                                           ref_u8.data_ptr(), face6.data_ptr(), gt.data_ptr(), ctx.stream), "li")
     r_u8, r_face6, r_gt = OP.lipsync_inputs(src, fake)
     assert torch.equal(ref_u8.cpu(), r_u8) and torch.equal(face6.cpu(), r_face6) and torch.equal(gt.cpu(), r_gt)
     x = torch.rand(1000, generator=g) * 1.6 - 0.3
     y = torch.empty(1000, dtype=torch.uint8, device=DEV)
-    _lib.check(ctx.lib.s2v_to_u8(x.to(DEV).data_ptr(), 1000, 0.0, 1.0, 255.0, 0.0, y.data_ptr(), ctx.stream), "u8")
+    x_d = x.to(DEV)
+    _lib.check(ctx.lib.s2v_to_u8(x_d.data_ptr(), 1000, 0.0, 1.0, 255.0, 0.0, y.data_ptr(), ctx.stream), "u8")
     assert torch.equal(y.cpu(), (x.clamp(0, 1) * 255).to(torch.uint8))
 
 
@@ -55,14 +57,16 @@ def _clip(n_frames, seed):
     semantic = rng.standard_normal((n_frames, 262)).astype(np.float32)
     semantic[:, -3] = 1.0 + 0.1 * rng.random(n_frames)           # crop scale, away from 0
     expression = rng.standard_normal(64).astype(np.float32)
-    wav = (0.2 * rng.standard_normal(int(16000 * n_frames / 25))).astype(np.float32)
+    # the last 16-column window ends ~5 video frames before the audio does (inference.py:209-216)
+    wav = (0.2 * rng.standard_normal(int(16000 * (n_frames + 5) / 25))).astype(np.float32)
     src, _ = synth.dnet_inputs(f"pipeline.{seed}", n_frames, 256)
     return wav, semantic, expression, torch.from_numpy(src)
 
 
 def _check_u8(got, ref):
     d = (got.cpu().int() - ref.int()).abs()
-    assert d.max() <= 6 and d.float().mean() <= 0.05, (int(d.max()), float(d.float().mean()))
+    within1 = float((d <= 1).float().mean())          # <= 1 LSB on >= 99.9 % of pixels
+    assert within1 >= 0.999 and d.max() <= 6, (within1, int(d.max()), float(d.float().mean()))
 
 
 def test_pipeline_ragged_batches_vs_oracle(nets_pair):
@@ -73,6 +77,7 @@ def test_pipeline_ragged_batches_vs_oracle(nets_pair):
     mel = audio.melspectrogram(torch.from_numpy(wav).to(DEV))
     chunks = audio.mel_chunks(mel)
     n = min(chunks.shape[0], 5)
+    assert n == 5
     coeffs = torch.from_numpy(P.dnet_coefficients(semantic[:n], expression))
     pipe = P.LipSyncPipeline(dnet, enet, DEV, batch=2)                # batches 2, 2, 1
     got = pipe.run(chunks, src[:n].to(DEV), coeffs.to(DEV), 0, n)
@@ -81,6 +86,8 @@ def test_pipeline_ragged_batches_vs_oracle(nets_pair):
         ref = OP.lipsync_frames(synth_sd("dnet"), synth_sd("enet"), chunks[:n].cpu(), src[:n], coeffs)
     _check_u8(got, ref)
     # a sub-range with relative src/coeffs reproduces the same frames
+    with pytest.raises(ValueError):
+        pipe.run(chunks, src[:2].to(DEV), coeffs[:3].to(DEV), 0, 2)
     part = pipe.run(chunks, src[1:4].to(DEV), coeffs[1:4].to(DEV), 1, 4)
     assert (part.int() - got[1:4].int()).abs().max() <= 1
 
