@@ -34,7 +34,7 @@ def hash_uniform(key: str, n: int) -> np.ndarray:
     return 2.0 * u - 1.0
 
 
-_NOISE_WEIGHT = re.compile(r"(^|\.)style_convs\.\d+\.weight$")
+_NOISE_WEIGHT = re.compile(r"(^|\.)(style_convs\.\d+|style_conv1)\.weight$")
 _TRANSPOSED = ("conv_s.weight", "conv_1.weight")  # DNet ADAINDecoderBlock ConvTranspose2d
 
 
@@ -52,6 +52,8 @@ def synth_tensor(key: str, shape, gain: float = 1.3, noise_weight: float = 0.0) 
     if leaf == "num_batches_tracked":
         return np.zeros(shape, dtype=np.int64)
     u = hash_uniform(key, n).reshape(shape)
+    if ".noises.noise" in key or key.endswith("constant_input.weight"):
+        return (u * np.sqrt(3.0)).astype(np.float32)     # torch.randn buffers / parameters: unit variance
     if leaf == "running_mean":
         v = 0.1 * u
     elif leaf == "running_var":
@@ -74,6 +76,41 @@ def synth_tensor(key: str, shape, gain: float = 1.3, noise_weight: float = 0.0) 
     else:
         v = 0.1 * u
     return v.astype(np.float32)
+
+
+def blur_kernel(factor: int = 1) -> np.ndarray:
+    """gpen_model.py:26-35 make_kernel([1, 3, 3, 1]) (x factor^2 for the upsampling blurs)."""
+    k = np.array([1.0, 3.0, 3.0, 1.0])
+    k = np.outer(k, k)
+    return (k / k.sum() * factor ** 2).astype(np.float32)
+
+
+_GPEN_STYLE_MLP = re.compile(r"^generator\.style\.\d+\.weight$")
+
+
+def synth_equal_tensor(key: str, shape, noise_weight: float = 0.0, lr_mlp: float = 0.01) -> np.ndarray:
+    """GPEN (equalized learning rate, gpen_model.py:94-167): parameters are stored as N(0,1)
+    draws (divided by lr_mul for the style MLP) and scaled at run time, so synthetic weights are
+    unit-variance uniforms; blur kernels are the fixed make_kernel buffers."""
+    shape = tuple(int(s) for s in shape)
+    n = int(np.prod(shape)) if shape else 1
+    leaf = key.rsplit(".", 1)[-1]
+    if leaf == "kernel":
+        return blur_kernel(2 if key.endswith(("conv.blur.kernel", "upsample.kernel")) else 1).reshape(shape)
+    if key.endswith("noise.weight"):
+        return np.full(shape, noise_weight, dtype=np.float32)
+    u = hash_uniform(key, n).reshape(shape)
+    if leaf == "bias":
+        v = 1.0 + 0.1 * u if key.endswith("modulation.bias") else 0.1 * u
+    elif _GPEN_STYLE_MLP.match(key):
+        v = u * np.sqrt(3.0) / lr_mlp
+    else:
+        v = u * np.sqrt(3.0)
+    return v.astype(np.float32)
+
+
+def synth_equal_state_dict(shapes: dict, noise_weight: float = 0.0) -> dict:
+    return {k: synth_equal_tensor(k, s, noise_weight) for k, s in shapes.items()}
 
 
 def synth_state_dict(shapes: dict, gain: float = 1.3, noise_weight: float = 0.0) -> dict:
@@ -99,12 +136,20 @@ def synth_state_dict(shapes: dict, gain: float = 1.3, noise_weight: float = 0.0)
     return out
 
 
-def synth_torch_state_dict(module, gain: float = 1.3, noise_weight: float = 0.0):
-    """Synthetic state_dict for any module whose keys follow the reference layout."""
+def synth_torch_state_dict(module, gain: float = 1.3, noise_weight: float = 0.0, equal: bool = False):
+    """Synthetic state_dict for any module whose keys follow the reference layout
+    (``equal``: the GPEN equalized-learning-rate scheme)."""
     import torch
     shapes = {k: tuple(v.shape) for k, v in module.state_dict().items()}
-    sd = synth_state_dict(shapes, gain, noise_weight)
+    sd = synth_equal_state_dict(shapes, noise_weight) if equal else synth_state_dict(shapes, gain, noise_weight)
     return {k: torch.from_numpy(v) for k, v in sd.items()}
+
+
+# Enhancer presets (shared by the golden generator, tests and benchmarks).  GFPGAN uses gain 1.0:
+# its SFT conditions multiply the decoder features level after level, and at 1.3 the synthetic
+# activations grow to ~1e14 by the 512 output; at 1.0 they stay O(1..10) like a trained model's.
+GFPGAN_SYNTH = dict(gain=1.0, noise_weight=0.1)
+GPEN_SYNTH = dict(noise_weight=0.1, equal=True)
 
 
 # ----------------------------------------------------------------------------- inputs
@@ -123,6 +168,11 @@ def lipsync_inputs(tag: str, batch: int, size: int):
     face[:, :3, size // 2:, :] = 0.0
     gt = face[:, 3:].copy()
     return mel, face, gt
+
+
+def face_inputs(tag: str, batch: int, size: int = 512):
+    """Enhancer input faces [B,3,S,S] in [-1,1) (gfpgan/utils.py:115-117 normalisation)."""
+    return hash_array(f"{tag}.face512", (batch, 3, size, size), -1.0, 1.0)
 
 
 def dnet_inputs(tag: str, batch: int, size: int):

@@ -184,6 +184,72 @@ def gen_ops():
     _save("ops", arrays)
 
 
+def _import_gfpgan():
+    """GFPGANv1Clean by file path: the gfpgan package __init__ needs basicsr/facexlib, so only
+    the two arch files are loaded, with ``basicsr.utils.registry.ARCH_REGISTRY`` stubbed as a
+    no-op decorator."""
+    reg = types.ModuleType("basicsr.utils.registry")
+
+    class _Registry:
+        def register(self, *a, **k):
+            return lambda c: c
+    reg.ARCH_REGISTRY = _Registry()
+    sys.modules.setdefault("basicsr.utils", types.ModuleType("basicsr.utils"))
+    sys.modules["basicsr.utils.registry"] = reg
+    base = os.path.join(REF, "third_part/GFPGAN/gfpgan/archs")
+    pkg = types.ModuleType("_ref_gfpgan_archs")
+    pkg.__path__ = [base]
+    sys.modules["_ref_gfpgan_archs"] = pkg
+    for m in ("stylegan2_clean_arch", "gfpganv1_clean_arch"):
+        spec = importlib.util.spec_from_file_location(f"_ref_gfpgan_archs.{m}", os.path.join(base, m + ".py"))
+        mod = importlib.util.module_from_spec(spec)
+        sys.modules[f"_ref_gfpgan_archs.{m}"] = mod
+        spec.loader.exec_module(mod)
+    return sys.modules["_ref_gfpgan_archs.gfpganv1_clean_arch"].GFPGANv1Clean
+
+
+GFPGAN_KW = dict(out_size=512, num_style_feat=512, channel_multiplier=2, decoder_load_path=None, fix_decoder=False,
+                 num_mlp=8, input_is_latent=True, different_w=True, narrow=1, sft_half=True)
+
+
+def gen_gfpgan():
+    from s2v_amd.models.enhancer_arch import GFPGANv1CleanParams
+    ref = _import_gfpgan()(**GFPGAN_KW).eval()
+    _check_keys("gfpgan", ref, GFPGANv1CleanParams(**GFPGAN_KW))
+    sd = synth.synth_torch_state_dict(ref, **synth.GFPGAN_SYNTH)
+    ref.load_state_dict(sd, strict=True)
+    acts = {}
+    ref.final_linear.register_forward_hook(lambda m, i, o: acts.__setitem__("style", o))
+    x = synth.face_inputs("golden.gfpgan", 1)
+    with torch.no_grad():
+        img, rgbs = ref(torch.from_numpy(x), return_rgb=True, randomize_noise=False)
+    arrays = {"style": acts["style"].numpy(), "rgb0": rgbs[0].numpy(), "rgb3": rgbs[3].numpy()}
+    for name, t in (("out", img), ("rgb6", rgbs[6])):
+        p = _probe(t, f"gfpgan.{name}")
+        arrays.update({f"{name}_idx": p["idx"], f"{name}_val": p["val"], f"{name}_stats": p["stats"]})
+    _save("gfpgan_b1_512", arrays)
+
+
+def gen_gpen():
+    sys.path.insert(0, os.path.join(REF, "third_part/GPEN/face_model"))
+    from gpen_model import FullGenerator
+    from s2v_amd.models.enhancer_arch import FullGeneratorParams
+    ref = FullGenerator(512, 512, 8, 2, narrow=1, device="cpu").eval()
+    _check_keys("gpen", ref, FullGeneratorParams(512, 512, 8, 2, narrow=1))
+    sd = synth.synth_torch_state_dict(ref, **synth.GPEN_SYNTH)
+    ref.load_state_dict(sd, strict=True)
+    acts = {}
+    ref.final_linear.register_forward_hook(lambda m, i, o: acts.__setitem__("code", o))
+    ref.generator.style.register_forward_hook(lambda m, i, o: acts.__setitem__("latent", o))
+    x = synth.face_inputs("golden.gpen", 1)
+    with torch.no_grad():
+        img, _ = ref(torch.from_numpy(x))
+    arrays = {"code": acts["code"].numpy(), "latent": acts["latent"].numpy()}
+    p = _probe(img, "gpen.out")
+    arrays.update({"out_idx": p["idx"], "out_val": p["val"], "out_stats": p["stats"]})
+    _save("gpen_b1_512", arrays)
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="lnet,enet,dnet,ops")

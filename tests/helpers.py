@@ -9,9 +9,19 @@ from s2v_amd import synth
 from s2v_amd.models import arch
 
 
+GFPGAN_KW = dict(out_size=512, num_style_feat=512, channel_multiplier=2, decoder_load_path=None, fix_decoder=False,
+                 num_mlp=8, input_is_latent=True, different_w=True, narrow=1, sft_half=True)   # gfpgan/utils.py:40-50
+
+
 @functools.lru_cache(maxsize=None)
 def synth_sd(net: str):
-    """Synthetic state_dict (CPU tensors) in the reference layout for 'lnet'|'enet'|'dnet'."""
+    """Synthetic state_dict (CPU tensors) in the reference layout for
+    'lnet'|'enet'|'dnet'|'gfpgan'|'gpen'."""
+    from s2v_amd.models import enhancer_arch as ea
+    if net == "gfpgan":
+        return synth.synth_torch_state_dict(ea.GFPGANv1CleanParams(**GFPGAN_KW), **synth.GFPGAN_SYNTH)
+    if net == "gpen":
+        return synth.synth_torch_state_dict(ea.FullGeneratorParams(512, 512, 8, 2), **synth.GPEN_SYNTH)
     mod = {"lnet": lambda: arch.LNetParams(), "enet": lambda: arch.ENetParams(lnet=arch.LNetParams()),
            "dnet": lambda: arch.DNetParams()}[net]()
     return synth.synth_torch_state_dict(mod)

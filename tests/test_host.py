@@ -14,10 +14,16 @@ import torch
 
 import s2v_import  # noqa: F401
 from conftest import GOLDEN, REPO
+from helpers import GFPGAN_KW
 from s2v_amd import _lib, synth
 from s2v_amd.models import arch
 
 HEADER = os.path.join(REPO, "include", "s2v.h")
+
+
+def _ea():
+    from s2v_amd.models import enhancer_arch
+    return enhancer_arch
 
 
 def header_functions():
@@ -61,7 +67,9 @@ def test_conv_params_struct_layout_matches_header(tmp_path):
 
 @pytest.mark.parametrize("name,ctor", [("lnet", lambda: arch.LNetParams()),
                                        ("enet", lambda: arch.ENetParams(lnet=arch.LNetParams())),
-                                       ("dnet", lambda: arch.DNetParams())])
+                                       ("dnet", lambda: arch.DNetParams()),
+                                       ("gfpgan", lambda: _ea().GFPGANv1CleanParams(**GFPGAN_KW)),
+                                       ("gpen", lambda: _ea().FullGeneratorParams(512, 512, 8, 2))])
 def test_state_dict_layout_matches_reference(name, ctor):
     ref = json.load(open(os.path.join(GOLDEN, f"{name}_keys.json")))
     mine = {k: list(v.shape) for k, v in ctor().state_dict().items()}
@@ -184,3 +192,14 @@ def test_mel_restatement_cross_checks():
     b = audio.mel_basis()
     assert b.shape == (80, 401) and b.dtype == np.float32
     assert np.array_equal(b, slaney_mel_basis())
+
+
+def test_gpen_synthetic_blur_kernels_are_the_fixed_buffers():
+    from helpers import synth_sd
+    sd = synth_sd("gpen")
+    k = torch.tensor([1.0, 3.0, 3.0, 1.0])
+    k = k[None, :] * k[:, None] / 64.0
+    assert torch.equal(sd["ecd1.0.0.kernel"], k)
+    assert torch.equal(sd["generator.convs.0.conv.blur.kernel"], 4 * k)
+    assert torch.equal(sd["generator.to_rgbs.0.upsample.kernel"], 4 * k)
+    assert float(sd["generator.conv1.noise.weight"]) == pytest.approx(0.1)

@@ -69,3 +69,40 @@ def test_flow_warp_oracle_matches_reference(golden):
     flow2 = torch.from_numpy(synth.hash_array("golden.flow2", (1, 2, 32, 32), -2.0, 2.0))
     src2 = torch.from_numpy(synth.hash_array("golden.flow2.src", (1, 3, 32, 32)))
     assert max_abs(nets.warp_image(src2, nets.flow_to_deformation(flow2)), g["warp_same"])[0] < 1e-5
+
+
+def test_gfpgan_oracle_matches_reference(golden):
+    from oracle import enhancers
+    g = golden("gfpgan_b1_512")
+    x = torch.from_numpy(synth.face_inputs("golden.gfpgan", 1))
+    with torch.no_grad():
+        img, rgbs, style = enhancers.gfpgan_forward(synth_sd("gfpgan"), x)
+    assert max_abs(style.reshape(1, -1), g["style"])[0] < 1e-4
+    assert max_abs(rgbs[0], g["rgb0"])[0] < 1e-3 and max_abs(rgbs[3], g["rgb3"])[0] < 1e-3
+    check_probe(rgbs[6], g, "rgb6", atol=1e-4, rtol=1e-4)
+    check_probe(img, g, "out", atol=1e-3, rtol=1e-4)
+
+
+def test_gpen_oracle_matches_reference(golden):
+    from oracle import enhancers
+    g = golden("gpen_b1_512")
+    x = torch.from_numpy(synth.face_inputs("golden.gpen", 1))
+    with torch.no_grad():
+        img, lat, code = enhancers.gpen_forward(synth_sd("gpen"), x)
+    assert max_abs(code, g["code"])[0] < 1e-5 and max_abs(lat, g["latent"])[0] < 1e-4
+    check_probe(img, g, "out", atol=1e-4, rtol=1e-4)
+
+
+def test_upfirdn2d_and_fused_act_oracle_match_reference_fallbacks(golden):
+    from oracle import enhancers
+    g = golden("ops")
+    x = torch.from_numpy(synth.hash_array("golden.fba.x", (2, 8, 5, 7)))
+    b = torch.from_numpy(synth.hash_array("golden.fba.b", (8,)))
+    assert max_abs(enhancers.fused_leaky_relu(x, b), g["fba_out"])[0] == 0.0
+    k = torch.tensor([1.0, 3.0, 3.0, 1.0])
+    k = k[None, :] * k[:, None] / 64.0
+    xi = torch.from_numpy(synth.hash_array("golden.ufd.x", (2, 3, 9, 11)))
+    for name, (up, down, pad) in {"up2": (2, 1, (2, 1)), "blur22": (1, 1, (2, 2)),
+                                  "blur11": (1, 1, (1, 1)), "down2": (1, 2, (1, 1))}.items():
+        got = enhancers.upfirdn2d(xi, k * (4 if up == 2 else 1), up=up, down=down, pad=pad)
+        assert max_abs(got, g[f"ufd_{name}"])[0] < 1e-6, name
