@@ -183,6 +183,16 @@ int s2v_upfirdn2d(const float *x, int major, int in_h, int in_w, int minor, cons
                   int up_x, int up_y, int down_x, int down_y, int pad_x0, int pad_x1, int pad_y0, int pad_y1,
                   float *y, int out_h, int out_w, s2v_stream_t stream);
 
+/* NHWC FIR resampling with fused epilogue (the engines' form of upfirdn2d, GPEN gpen_model.py:37-91
+ * Upsample / Blur and the blur after the transposed modulated conv, :270-276):
+ *   y[n,oy,ox,c] = post * act(gain * sum_{i,j} kflip[i][j] * xu[n, oy*down + i - pad_y0, ox*down + j - pad_x0, c]
+ *                             + bias[c])
+ * xu = x zero-inserted by `up`; positions outside it are zero (pad_y1 / pad_x1 are implied by oh / ow).
+ * x / y are channel-slice views (pitch xcs / ycs); kernel [kh][kw] (<= 64 taps) in device memory. */
+int s2v_fir2d(const float *x, int n, int ih, int iw, int c, int xcs, const float *k, int kh, int kw, int up,
+              int down, int pad_y0, int pad_x0, float *y, int oh, int ow, int ycs, float gain, const float *bias,
+              int act, float alpha, float post, s2v_stream_t stream);
+
 /* N(0,1) noise from a counter-based generator (StyleConv noise injection,
  * base_blocks.py:528-531): y[i] = BoxMuller(splitmix64(seed ^ splitmix64(offset + i))). */
 int s2v_gaussian_noise(float *y, long long n, unsigned long long seed, unsigned long long offset,

@@ -68,6 +68,8 @@ _SIGS = {
                                     _vp]),
     "s2v_upfirdn2d": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_int,
                                _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _vp]),
+    "s2v_fir2d": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_int,
+                           _c_int, _vp, _c_int, _c_int, _c_int, _c_float, _vp, _c_int, _c_float, _c_float, _vp]),
     "s2v_gaussian_noise": (_c_int, [_vp, _c_ll, ctypes.c_uint64, ctypes.c_uint64, _vp]),
     "s2v_lipsync_inputs": (_c_int, [_vp, _vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp]),
     "s2v_to_u8": (_c_int, [_vp, _c_ll, _c_float, _c_float, _c_float, _c_float, _vp, _vp]),

@@ -1,0 +1,91 @@
+// NHWC FIR resampling with a fused bias/activation epilogue (the StyleGAN2 / GPEN blur path).
+//
+// Semantics are upfirdn2d's (third_part/GPEN/face_model/op/upfirdn2d.py:160-193): zero-insert
+// `up`, pad, correlate with the flipped kernel, keep every `down`-th sample; here on NHWC views
+// with channel pitches so the result lands directly in a channel slice of a concat buffer, and
+// with y = post * act(gain * fir + bias[c]) fused (FusedLeakyReLU, op/fused_act.py:92-96).
+// HBM-bound: each thread produces 4 channels of one output pixel with 16-byte loads/stores.
+#include "common.hpp"
+
+namespace s2v {
+
+constexpr int FIR_MAX_TAPS = 64;
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void fir2d_kernel(const float *__restrict__ x, int ih, int iw, int c, int xcs,
+                                                    const float *__restrict__ k, int kh, int kw, int up, int down,
+                                                    int py0, int px0, float *__restrict__ y, int oh, int ow, int ycs,
+                                                    float gain, const float *__restrict__ bias, int act, float alpha,
+                                                    float post, long long total) {
+    __shared__ float ks[FIR_MAX_TAPS];
+    for (int i = threadIdx.x; i < kh * kw; i += 256) ks[i] = k[kh * kw - 1 - i];   // flipped
+    __syncthreads();
+    const int cv = VEC ? c / 4 : c;
+    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+        const int cc = (int)(e % cv);
+        long long t = e / cv;
+        const int ox = (int)(t % ow);
+        t /= ow;
+        const int oy = (int)(t % oh);
+        const int n = (int)(t / oh);
+        const float *xb = x + (long long)n * ih * iw * xcs + (VEC ? 4 * cc : cc);
+        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+        for (int i = 0; i < kh; ++i) {
+            const int uy = oy * down + i - py0;
+            if (uy < 0 || uy % up) continue;
+            const int iy = uy / up;
+            if (iy >= ih) continue;
+            for (int j = 0; j < kw; ++j) {
+                const int ux = ox * down + j - px0;
+                if (ux < 0 || ux % up) continue;
+                const int ix = ux / up;
+                if (ix >= iw) continue;
+                const float kv = ks[i * kw + j];
+                const float *src = xb + ((long long)iy * iw + ix) * xcs;
+                if (VEC) {
+                    const float4 v = *(const float4 *)src;
+                    a0 = fmaf(v.x, kv, a0); a1 = fmaf(v.y, kv, a1); a2 = fmaf(v.z, kv, a2); a3 = fmaf(v.w, kv, a3);
+                } else {
+                    a0 = fmaf(*src, kv, a0);
+                }
+            }
+        }
+        float *dst = y + (((long long)n * oh + oy) * ow + ox) * ycs + (VEC ? 4 * cc : cc);
+        if (VEC) {
+            float4 b = bias ? *(const float4 *)(bias + 4 * cc) : make_float4(0.f, 0.f, 0.f, 0.f);
+            float4 o;
+            o.x = post * apply_act(fmaf(gain, a0, b.x), act, alpha);
+            o.y = post * apply_act(fmaf(gain, a1, b.y), act, alpha);
+            o.z = post * apply_act(fmaf(gain, a2, b.z), act, alpha);
+            o.w = post * apply_act(fmaf(gain, a3, b.w), act, alpha);
+            *(float4 *)dst = o;
+        } else {
+            *dst = post * apply_act(fmaf(gain, a0, bias ? bias[cc] : 0.f), act, alpha);
+        }
+    }
+}
+
+}  // namespace s2v
+
+using namespace s2v;
+
+extern "C" int s2v_fir2d(const float *x, int n, int ih, int iw, int c, int xcs, const float *k, int kh, int kw,
+                         int up, int down, int pad_y0, int pad_x0, float *y, int oh, int ow, int ycs, float gain,
+                         const float *bias, int act, float alpha, float post, s2v_stream_t stream) {
+    S2V_REQUIRE(x && k && y && n > 0 && ih > 0 && iw > 0 && c > 0 && oh > 0 && ow > 0, "fir2d: bad args");
+    S2V_REQUIRE(xcs >= c && ycs >= c, "fir2d: channel pitch smaller than channel count");
+    S2V_REQUIRE(kh > 0 && kw > 0 && kh * kw <= FIR_MAX_TAPS, "fir2d: kernel must have 1..64 taps");
+    S2V_REQUIRE(up >= 1 && down >= 1, "fir2d: up/down must be >= 1");
+    const bool vec = (c % 4 == 0) && (xcs % 4 == 0) && (ycs % 4 == 0) && ((uintptr_t)x % 16 == 0) &&
+                     ((uintptr_t)y % 16 == 0) && (!bias || (uintptr_t)bias % 16 == 0);
+    const long long total = (long long)n * oh * ow * (vec ? c / 4 : c);
+    long long blocks = (total + 255) / 256;
+    if (blocks > 65535LL * 16) blocks = 65535LL * 16;
+    if (vec)
+        fir2d_kernel<true><<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(
+            x, ih, iw, c, xcs, k, kh, kw, up, down, pad_y0, pad_x0, y, oh, ow, ycs, gain, bias, act, alpha, post, total);
+    else
+        fir2d_kernel<false><<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(
+            x, ih, iw, c, xcs, k, kh, kw, up, down, pad_y0, pad_x0, y, oh, ow, ycs, gain, bias, act, alpha, post, total);
+    return check_launch("fir2d");
+}

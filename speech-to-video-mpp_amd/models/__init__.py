@@ -16,7 +16,7 @@ import torch
 
 from .. import ops
 from ..ops import NHWC
-from . import arch
+from . import arch, enhancer_arch
 
 
 def _fold5(x, dim):
@@ -126,6 +126,48 @@ class DNet(_EngineMixin, arch.DNetParams):
         return eng.forward(ctx, input_image.float(), driving_source.float(), stage=stage)
 
 
+# ----------------------------------------------------------------------------- enhancers
+class GFPGANv1Clean(_EngineMixin, enhancer_arch.GFPGANv1CleanParams):
+    """third_part/GFPGAN/gfpgan/archs/gfpganv1_clean_arch.py:154-324 (GFPGANer: out_size=512,
+    channel_multiplier=2, different_w=True, input_is_latent=True, sft_half=True)."""
+
+    def _build_engine(self, sd, device):
+        from ..engine.gfpgan import GFPGANEngine
+        return GFPGANEngine(sd, device, self.num_style_feat, self.sft_half, self.different_w, self.input_is_latent)
+
+    @torch.no_grad()
+    def forward(self, x, return_latents=False, return_rgb=True, randomize_noise=True):
+        """-> (image [B,3,S,S], list of U-Net RGB images) like the reference (:296-324)."""
+        _need_cuda(x)
+        eng, ctx = self._engine(x.device)
+        out = torch.empty_like(x, dtype=torch.float32)
+        return eng.forward(ctx, x.float(), out, return_rgb=return_rgb, randomize_noise=randomize_noise)
+
+
+class FullGenerator(_EngineMixin, enhancer_arch.FullGeneratorParams):
+    """third_part/GPEN/face_model/gpen_model.py:583-630 (GPEN-BFR-512: FullGenerator(512, 512, 8, 2))."""
+
+    def _build_engine(self, sd, device):
+        from ..engine.gpen import GPENEngine
+        return GPENEngine(sd, device, n_mlp=self.generator.n_mlp)
+
+    @torch.no_grad()
+    def forward(self, inputs, return_latents=False, inject_index=None, truncation=1, truncation_latent=None,
+                input_is_latent=False):
+        """-> (image, None) or (image, latent [B, n_latent, 512]) (Generator.forward, :450-512)."""
+        _need_cuda(inputs)
+        if truncation < 1:
+            raise NotImplementedError("FullGenerator: truncation < 1 is not on the GPEN inference path "
+                                      "(face_gan.py:40 calls model(img_t))")
+        eng, ctx = self._engine(inputs.device)
+        out = torch.empty_like(inputs, dtype=torch.float32)
+        lat = torch.empty((inputs.shape[0], self.style_dim), device=inputs.device) if return_latents else None
+        eng.forward(ctx, inputs.float(), out, input_is_latent=input_is_latent, latent_out=lat)
+        if return_latents:
+            return out, lat.unsqueeze(1).expand(-1, self.generator.n_latent, -1)
+        return out, None
+
+
 # ----------------------------------------------------------------------------- loaders
 def _load(path):
     return torch.load(path, map_location="cpu", weights_only=True)
@@ -160,4 +202,28 @@ def load_DNet(args):
     return dnet.eval()
 
 
-__all__ = ["LNet", "ENet", "DNet", "load_checkpoint", "load_network", "load_DNet"]
+def load_gfpgan(path, **kw):
+    """gfpgan/utils.py:40-50, :87-93: GFPGANv1Clean(arch='clean', channel_multiplier=2) with the
+    ``params_ema`` (else ``params``) weights, strict=True."""
+    cfg = dict(out_size=512, num_style_feat=512, channel_multiplier=2, decoder_load_path=None, fix_decoder=False,
+               num_mlp=8, input_is_latent=True, different_w=True, narrow=1, sft_half=True)
+    cfg.update(kw)
+    net = GFPGANv1Clean(**cfg)
+    ckpt = _load(path)
+    key = "params_ema" if "params_ema" in ckpt else "params"
+    net.load_state_dict(ckpt[key], strict=True)
+    return net.eval()
+
+
+def load_gpen(path, size=512, channel_multiplier=2, narrow=1, key=None):
+    """face_gan.py:26-36: FullGenerator(size, 512, 8, channel_multiplier, narrow) + state_dict."""
+    net = FullGenerator(size, 512, 8, channel_multiplier, narrow=narrow)
+    sd = _load(path)
+    if key is not None:
+        sd = sd[key]
+    net.load_state_dict(sd)
+    return net.eval()
+
+
+__all__ = ["LNet", "ENet", "DNet", "GFPGANv1Clean", "FullGenerator", "load_checkpoint", "load_network", "load_DNet",
+           "load_gfpgan", "load_gpen"]

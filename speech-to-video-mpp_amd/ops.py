@@ -405,3 +405,27 @@ def fourier_matrices(h: int, w: int, device):
         iv = iv.reshape(2 * F, P).t()                                                # [P, 2F]
         _DFT_CACHE[key] = (d2.float().contiguous().to(device), iv.float().contiguous().to(device))
     return _DFT_CACHE[key]
+
+
+# ----------------------------------------------------------------------------- FIR / elementwise
+def fir2d(ctx: Ctx, x: NHWC, kernel: torch.Tensor, y: NHWC, *, up=1, down=1, pad0=(0, 0), gain=1.0, bias=None,
+          act=ACT_NONE, alpha=0.0, post=1.0):
+    """upfirdn2d on NHWC views (pad0 = (pad_y0, pad_x0); the far pads follow from y's size)
+    with y = post * act(gain * fir + bias[c])."""
+    assert x.n == y.n and x.c == y.c, "fir2d: batch / channel mismatch"
+    kh, kw = kernel.shape
+    check(ctx.lib.s2v_fir2d(x.ptr, x.n, x.h, x.w, x.c, x.cs, kernel.data_ptr(), kh, kw, up, down, pad0[0], pad0[1],
+                            y.ptr, y.h, y.w, y.cs, gain, _ptr(bias), act, alpha, post, ctx.stream), "s2v_fir2d")
+    return y
+
+
+def eltwise(ctx: Ctx, x: NHWC, y: NHWC, *, a=1.0, mul: NHWC | None = None, add: NHWC | None = None, bias=None,
+            act=ACT_NONE, alpha=0.0, post=1.0):
+    """y = post * act(x * a * mul + add + bias[c]) over NHWC views of equal n/h/w/c (in place ok)."""
+    assert (x.n, x.h, x.w, x.c) == (y.n, y.h, y.w, y.c)
+    for v in (mul, add):
+        assert v is None or (v.n, v.h, v.w, v.c) == (x.n, x.h, x.w, x.c)
+    check(ctx.lib.s2v_eltwise(x.ptr, x.cs, None if mul is None else mul.ptr, 0 if mul is None else mul.cs,
+                              None if add is None else add.ptr, 0 if add is None else add.cs, _ptr(bias),
+                              x.n * x.h * x.w, x.c, a, act, alpha, post, y.ptr, y.cs, ctx.stream), "s2v_eltwise")
+    return y

@@ -1,0 +1,70 @@
+"""Dry run of every engine's host plan on CPU: the libs2v entry points are replaced by no-ops
+that only validate their argument counts, so the shape / view / slice bookkeeping of each
+forward (every NHWC assertion in ops.py) runs without a GPU.  Nothing is computed — numerics are
+the gpu-marked tests' job; this catches plumbing errors before a GPU box is spent on them."""
+import ctypes
+
+import pytest
+import torch
+
+import s2v_import  # noqa: F401
+from helpers import GFPGAN_KW, synth_sd
+from s2v_amd import _lib, ops, synth
+
+
+class _NoLib:
+    def __init__(self):
+        self.calls = {}
+
+    def __getattr__(self, name):
+        if name not in _lib.EXPORTS:
+            raise AttributeError(name)
+        nargs = len(_lib._SIGS[name][1])
+
+        def fn(*args):
+            assert len(args) == nargs, f"{name}: {len(args)} args, ABI has {nargs}"
+            self.calls[name] = self.calls.get(name, 0) + 1
+            return 0
+        return fn
+
+
+@pytest.fixture
+def dry(monkeypatch):
+    lib = _NoLib()
+    monkeypatch.setattr(ops, "_require_cuda", lambda t, what: None)
+    monkeypatch.setattr(ops.Ctx, "__init__", lambda self, device: (setattr(self, "device", torch.device(device)),
+                                                                   setattr(self, "ws", ops.Workspace(device)),
+                                                                   setattr(self, "lib", lib))[0])
+    monkeypatch.setattr(ops.Ctx, "stream", property(lambda self: ctypes.c_void_p(0)))
+    return lib
+
+
+def test_gfpgan_plan(dry):
+    from s2v_amd.engine.gfpgan import GFPGANEngine
+    eng = GFPGANEngine(synth_sd("gfpgan"), "cpu")
+    x = torch.zeros(2, 3, 512, 512)
+    out = torch.empty_like(x)
+    for rn in (True, False):
+        _, rgbs = eng.forward(ops.Ctx("cpu"), x, out, return_rgb=True, randomize_noise=rn)
+    assert [r.shape[-1] for r in rgbs] == [8, 16, 32, 64, 128, 256, 512]
+    assert dry.calls["s2v_conv2d"] > 120 and dry.calls["s2v_eltwise"] == 2 * 14
+
+
+def test_gpen_plan(dry):
+    from s2v_amd.engine.gpen import GPENEngine
+    eng = GPENEngine(synth_sd("gpen"), "cpu")
+    x = torch.zeros(2, 3, 512, 512)
+    eng.forward(ops.Ctx("cpu"), x, torch.empty_like(x))
+    assert dry.calls["s2v_fir2d"] == 7 + 7 + 7 and dry.calls["s2v_eltwise"] == 15
+
+
+def test_lipsync_engines_plan(dry):
+    from s2v_amd.engine.dnet import DNetEngine
+    from s2v_amd.engine.enet import ENetEngine
+    ctx = ops.Ctx("cpu")
+    e = ENetEngine(synth_sd("enet"), "cpu")
+    mel, face, gt = (torch.from_numpy(a) for a in synth.lipsync_inputs("dry", 2, 256))
+    e.forward(ctx, mel, face, gt, torch.empty(2, 3, 384, 384), torch.empty(2, 3, 96, 96))
+    d = DNetEngine(synth_sd("dnet"), "cpu")
+    src, coeff = (torch.from_numpy(a) for a in synth.dnet_inputs("dry", 1, 256))
+    d.forward(ctx, src, coeff)
