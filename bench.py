@@ -12,6 +12,12 @@ and synchronize on every rank and the max over ranks is reported.
 
 Prints ONE JSON line on rank 0 with the live roofline of the dominant kernel (HIP events on the
 stream the kernels run on) and, at N=1, the CPU baseline (oracle restatement on host cores).
+
+Other workloads (not the headline metric):
+  --workload pipeline   one step = 16 frames through DNet -> uint8 ref -> ENet(+LNet) -> uint8
+                        384x384 frames (s2v_amd.pipeline.LipSyncPipeline.run_batch), plus the
+                        host precompute of a 1000-frame clip timed once;
+  --workload enhance    one step = B 512x512 faces through GFPGANv1Clean and GPEN-512.
 """
 from __future__ import annotations
 
@@ -36,9 +42,10 @@ REF_GFLOP_PER_FRAME = 407.46       # ENet+LNet algorithmic GFLOP
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--workload", choices=("lipsync", "pipeline", "enhance"), default="lipsync")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--batch", type=int, default=0, help="0 = the workload's default (16, or 4 for enhance)")
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -58,9 +65,9 @@ def make_inputs(batch, size, device, seed):
     return mel, face, gt
 
 
-def live_roofline(model, inputs):
-    """One un-graphed forward with every conv/GEMM launch bracketed by HIP events on its stream;
-    per kernel symbol: sum of algorithmic FLOPs / sum of durations."""
+def live_roofline(forward, workload="lipsync"):
+    """One un-graphed ``forward()`` with every conv/GEMM launch bracketed by HIP events on its
+    stream; per kernel symbol: sum of algorithmic FLOPs / sum of durations."""
     from s2v_amd import ops
     recs = []
 
@@ -76,7 +83,7 @@ def live_roofline(model, inputs):
     ops.CONV_HOOK = hook
     try:
         with torch.no_grad():
-            model(*inputs)
+            forward()
         torch.cuda.synchronize()
     finally:
         ops.CONV_HOOK = None
@@ -98,7 +105,7 @@ def live_roofline(model, inputs):
     total_ms = sum(v["ms"] for v in per.values())
     total_flops = sum(v["flops"] for v in per.values())
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_r01.json")
+    pmc = os.path.join(ROOT, "profiles", f"pmc_r01_{workload}.json")
     if os.path.exists(pmc):
         with open(pmc) as f:
             traffic = json.load(f).get("per_launch_bytes", {}).get(dom)
@@ -112,22 +119,155 @@ def live_roofline(model, inputs):
     }
 
 
-def cpu_baseline(sd, batch, size, threads, seconds):
-    """Oracle (CPU restatement, oracle/nets.py) on the host cores, bounded sample."""
-    from oracle import nets
-    torch.set_num_threads(threads)
-    mel, face, gt = make_inputs(batch, size, "cpu", 1234)
-    frames, t0 = 0, time.perf_counter()
+def _timed_cpu(fn, units_per_call, seconds, max_calls):
+    n, t0 = 0, time.perf_counter()
     with torch.no_grad():
         while True:
-            nets.enet_forward(sd, mel, face, gt)
-            frames += batch
+            fn()
+            n += units_per_call
             el = time.perf_counter() - t0
-            if el >= seconds or frames >= 8 * batch:
-                break
-    return {"value": round(frames / el, 4), "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"{frames} frames ({batch}-frame batches) of the same ENet(+LNet) {size}x{size} workload "
-                      f"in {el:.1f}s, torch CPU fp32, {threads} threads"}
+            if el >= seconds or n >= max_calls * units_per_call:
+                return n, el
+
+
+# ----------------------------------------------------------------------------- workloads
+class Workload:
+    """name, metric, unit, per-step units, GFLOP per unit, graph-captured step, un-graphed forward
+    (for the roofline), CPU baseline."""
+    metric = METRIC
+    unit = "frames/s"
+    gflop_per_unit = REF_GFLOP_PER_FRAME
+
+
+class LipSync(Workload):
+    def __init__(self, args, dev, rank):
+        from s2v_amd import models, synth
+        from s2v_amd.models import arch
+        self.batch = args.batch or 16
+        self.sd = synth.synth_torch_state_dict(arch.ENetParams(lnet=arch.LNetParams()))
+        self.model = models.ENet()
+        self.model.load_state_dict(self.sd)
+        self.model.eval()
+        self.size = args.size
+        self.inputs = make_inputs(self.batch, args.size, dev, 1000 + rank)
+        self.fn = lambda m, f, g: self.model(m, f, g)  # noqa: E731
+        self.config = {"workload": f"ENet(+LNet) forward, B={self.batch} synthetic {args.size}x{args.size} crops "
+                                   f"+ [1,80,16] mel windows -> 384x384 (models/ENet.py:82-139)",
+                       "crop": args.size}
+
+    def forward(self):
+        return self.fn(*self.inputs)
+
+    def cpu(self, threads, seconds):
+        from oracle import nets
+        torch.set_num_threads(threads)
+        mel, face, gt = make_inputs(2, self.size, "cpu", 1234)
+        n, el = _timed_cpu(lambda: nets.enet_forward(self.sd, mel, face, gt), 2, seconds, 8)
+        return {"value": round(n / el, 4), "unit": "frames/s", "cores": threads, "kind": "port",
+                "sample": f"{n} frames (2-frame batches) of the same ENet(+LNet) {self.size}x{self.size} workload "
+                          f"in {el:.1f}s, torch CPU fp32, {threads} threads"}
+
+
+class Pipeline(Workload):
+    metric = "full DNet->LNet->ENet frames/sec/GPU (uint8 384x384 output)"
+    gflop_per_unit = 508.91            # SURVEY.md §8d config 3: ENet+LNet 407.46 + DNet 101.45 (live)
+
+    def __init__(self, args, dev, rank):
+        import numpy as np
+        from s2v_amd import audio, models, pipeline, synth
+        from s2v_amd.models import arch
+        self.batch = args.batch or 16
+        self.sd_d = synth.synth_torch_state_dict(arch.DNetParams())
+        self.sd_e = synth.synth_torch_state_dict(arch.ENetParams(lnet=arch.LNetParams()))
+        dnet, enet = models.DNet(), models.ENet()
+        dnet.load_state_dict(self.sd_d)
+        enet.load_state_dict(self.sd_e)
+        self.pipe = pipeline.LipSyncPipeline(dnet.eval(), enet.eval(), dev, batch=self.batch)
+        # host precompute of a 1000-frame clip (SURVEY.md §8d config 3 inputs), timed once
+        rng = np.random.default_rng(0)
+        t = np.arange(640000) / 16000.0
+        wav = (0.1 * rng.standard_normal(t.size) + 0.2 * (np.sin(2 * np.pi * 220 * t) + np.sin(2 * np.pi * 440 * t)
+                                                          + np.sin(2 * np.pi * 1000 * t))).astype(np.float32)
+        semantic = rng.standard_normal((1000, 262)).astype(np.float32)
+        semantic[:, -3] = 1.0 + 0.1 * rng.random(1000)
+        expression = rng.standard_normal(64).astype(np.float32)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        mel = audio.melspectrogram(torch.from_numpy(wav).to(dev))
+        chunks = audio.mel_chunks(mel)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        coeffs = pipeline.dnet_coefficients(semantic, expression)
+        t2 = time.perf_counter()
+        self.host = {"clip_frames": 1000, "mel_chunks": int(chunks.shape[0]), "mel_ms": round(1e3 * (t1 - t0), 2),
+                     "coeff_windows_ms": round(1e3 * (t2 - t1), 2)}
+        g = torch.Generator(device=dev)
+        g.manual_seed(2000 + rank)
+        b = self.batch
+        self.inputs = [chunks[:b].contiguous(), torch.rand((b, 3, 256, 256), generator=g, device=dev) * 2 - 1,
+                       torch.from_numpy(coeffs[:b]).to(dev)]
+        self.out = torch.empty((b, 3, 384, 384), dtype=torch.uint8, device=dev)
+        self.fn = lambda m, s, c: self.pipe.run_batch(m, s, c, self.out)  # noqa: E731
+        self.config = {"workload": f"DNet -> uint8 ref -> ENet(+LNet) -> uint8, B={b} frames per step "
+                                   "(inference.py:259-288, facing.py:176-191), 256x256 DNet/ENet crops",
+                       "host_precompute": self.host}
+
+    def forward(self):
+        return self.fn(*self.inputs)
+
+    def cpu(self, threads, seconds):
+        from oracle import pipeline as OP
+        torch.set_num_threads(threads)
+        m, s, c = (t[:2].cpu() for t in self.inputs)
+        n, el = _timed_cpu(lambda: OP.lipsync_frames(self.sd_d, self.sd_e, m, s, c), 2, seconds, 8)
+        return {"value": round(n / el, 4), "unit": "frames/s", "cores": threads, "kind": "port",
+                "sample": f"{n} frames (2-frame batches) DNet->ENet->uint8 in {el:.1f}s, torch CPU fp32, "
+                          f"{threads} threads"}
+
+
+class Enhance(Workload):
+    metric = "enhanced 512x512 faces/sec/GPU (GFPGANv1Clean + GPEN-512, both per face)"
+    unit = "faces/s"
+    gflop_per_unit = 395.5 + 276.2     # SURVEY.md §8d config 5
+
+    def __init__(self, args, dev, rank):
+        from s2v_amd import models, synth
+        from s2v_amd.models import enhancer_arch as ea
+        kw = dict(out_size=512, num_style_feat=512, channel_multiplier=2, decoder_load_path=None, fix_decoder=False,
+                  num_mlp=8, input_is_latent=True, different_w=True, narrow=1, sft_half=True)
+        self.batch = args.batch or 4
+        self.sd_g = synth.synth_torch_state_dict(ea.GFPGANv1CleanParams(**kw), **synth.GFPGAN_SYNTH)
+        self.sd_p = synth.synth_torch_state_dict(ea.FullGeneratorParams(512, 512, 8, 2), **synth.GPEN_SYNTH)
+        self.gfpgan = models.GFPGANv1Clean(**kw)
+        self.gfpgan.load_state_dict(self.sd_g)
+        self.gpen = models.FullGenerator(512, 512, 8, 2)
+        self.gpen.load_state_dict(self.sd_p)
+        g = torch.Generator(device=dev)
+        g.manual_seed(3000 + rank)
+        self.inputs = [torch.rand((self.batch, 3, 512, 512), generator=g, device=dev) * 2 - 1]
+        self.fn = lambda x: (self.gfpgan(x, return_rgb=False)[0], self.gpen(x)[0])  # noqa: E731
+        self.config = {"workload": f"GFPGANv1Clean(return_rgb=False, randomize_noise=True) + GPEN FullGenerator-512 "
+                                   f"on B={self.batch} synthetic 512x512 faces per step (gfpgan/utils.py:120, "
+                                   "face_gan.py:42)"}
+
+    def forward(self):
+        return self.fn(*self.inputs)
+
+    def cpu(self, threads, seconds):
+        from oracle import enhancers
+        torch.set_num_threads(threads)
+        x = self.inputs[0][:1].cpu()
+
+        def one():
+            enhancers.gfpgan_forward(self.sd_g, x, return_rgb=False)
+            enhancers.gpen_forward(self.sd_p, x)
+        n, el = _timed_cpu(one, 1, seconds, 8)
+        return {"value": round(n / el, 4), "unit": "faces/s", "cores": threads, "kind": "port",
+                "sample": f"{n} faces through GFPGAN + GPEN (oracle restatement) in {el:.1f}s, torch CPU fp32, "
+                          f"{threads} threads"}
+
+
+WORKLOADS = {"lipsync": LipSync, "pipeline": Pipeline, "enhance": Enhance}
 
 
 def main():
@@ -140,22 +280,15 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
-    from s2v_amd import models, synth
-    from s2v_amd.models import arch
     from s2v_amd.runtime import GraphRunner
 
-    sd = synth.synth_torch_state_dict(arch.ENetParams(lnet=arch.LNetParams()))
-    model = models.ENet()
-    model.load_state_dict(sd)
-    model.eval()
-    inputs = make_inputs(args.batch, args.size, dev, 1000 + rank)
-    fn = lambda m, f, g: model(m, f, g)  # noqa: E731
+    wl = WORKLOADS[args.workload](args, dev, rank)
     if args.no_graph:
-        step = lambda: fn(*inputs)  # noqa: E731
+        step = wl.forward
         for _ in range(max(1, args.warmup)):
             step()
     else:
-        runner = GraphRunner(fn, list(inputs), warmup=1)
+        runner = GraphRunner(wl.fn, list(wl.inputs), warmup=1)
         step = runner.replay
         for _ in range(args.warmup):
             step()
@@ -175,24 +308,23 @@ def main():
         t = torch.tensor([elapsed], device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
-    frames = world * args.batch * args.steps
-    value = frames / elapsed
+    units = world * wl.batch * args.steps
+    value = units / elapsed
+    config = dict(wl.config)
+    config.update({"global_batch": world * wl.batch, "batch_per_gpu": wl.batch,
+                   "parallelism": f"frame-shard x{world} (no data-path collective)", "graph": not args.no_graph,
+                   "achieved_tflops_algorithmic": round(value * wl.gflop_per_unit / 1e3, 2),
+                   "gflop_per_unit": wl.gflop_per_unit})
     result = {
-        "metric": METRIC, "value": round(value, 3), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+        "metric": wl.metric, "value": round(value, 3), "unit": wl.unit, "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": f"ENet(+LNet) forward, B={args.batch} synthetic {args.size}x{args.size} crops "
-                               f"+ [1,80,16] mel windows -> 384x384 (models/ENet.py:82-139)",
-                   "global_batch": world * args.batch, "batch_per_gpu": args.batch, "crop": args.size,
-                   "parallelism": f"frame-shard x{world} (no data-path collective)",
-                   "graph": not args.no_graph,
-                   "achieved_tflops_algorithmic": round(value * REF_GFLOP_PER_FRAME / 1e3, 2)},
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic", "config": config,
     }
     if rank == 0 and not args.no_roofline:
-        result["roofline"] = live_roofline(model, inputs)
+        result["roofline"] = live_roofline(wl.forward, args.workload)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        result["cpu_baseline"] = cpu_baseline(sd, 2, args.size, threads, args.cpu_seconds)
+        result["cpu_baseline"] = wl.cpu(threads, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -88,6 +88,10 @@ typedef struct s2v_conv_params {
     /* split-K workspace (see s2v_conv2d_ws_bytes) */
     float *ws; size_t ws_bytes;
     int force_tile; int force_splits;           /* 0 = heuristic (tests use these) */
+    /* strided output (0 = contiguous [n][oh][ow] rows of pitch ycs): output pixel (n, oy, ox)
+     * is written at y + ((n*out_full_h + oy*out_step)*out_full_w + ox*out_step)*ycs — one parity
+     * class of a polyphase transposed conv.  No pix_add; res only in place (res == y). */
+    int out_step; int out_full_h, out_full_w;
 } s2v_conv_params;
 
 /* Replaces the nn.Conv2d / ConvTranspose2d / Conv1d / Linear calls of models/LNet.py,

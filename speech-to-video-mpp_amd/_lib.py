@@ -37,6 +37,7 @@ class ConvParams(ctypes.Structure):
         ("batch", _c_int), ("x_bs", _c_ll), ("w_bs", _c_ll), ("y_bs", _c_ll), ("res_bs", _c_ll),
         ("ws", _vp), ("ws_bytes", _c_size),
         ("force_tile", _c_int), ("force_splits", _c_int),
+        ("out_step", _c_int), ("out_full_h", _c_int), ("out_full_w", _c_int),
     ]
 
 

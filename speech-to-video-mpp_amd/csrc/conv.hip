@@ -45,7 +45,18 @@ struct ConvArgs {
     long long x_bs, w_bs, y_bs, res_bs;
     int M, K, ktiles, splits, tps;
     float *ws;
+    int y_step, y_h, y_w;   // strided (polyphase) output, y_step > 1
 };
+
+// Element offset of output row m (flattened n, oy, ox) for channel 0.
+__device__ __forceinline__ long long out_row(const ConvArgs &a, long long m) {
+    if (a.y_step <= 1) return m * a.ycs;
+    const int hw = a.oh * a.ow;
+    const long long img = m / hw;
+    const int rem = (int)(m - img * hw);
+    const int oy = rem / a.ow, ox = rem - (rem / a.ow) * a.ow;
+    return ((img * a.y_h + (long long)oy * a.y_step) * a.y_w + (long long)ox * a.y_step) * a.ycs;
+}
 
 __device__ __forceinline__ void store_epilogue(const ConvArgs &a, int bidx, int m, int n, float v) {
     const Epi &e = a.epi;
@@ -63,7 +74,8 @@ __device__ __forceinline__ void store_epilogue(const ConvArgs &a, int bidx, int 
     if (e.pix_add) v += e.pix_w * e.pix_add[(long long)bidx * hw * a.n + m];
     float r = 0.f;
     if (e.res) {
-        long long off = e.res_simple
+        long long off = a.y_step > 1 ? out_row(a, m)     // in-place residual on a strided output
+            : e.res_simple
             ? (long long)m * e.res_cs
             : ((long long)(img * e.res_h + oy + e.res_oy) * e.res_w + ox + e.res_ox) * e.res_cs;
         r = e.res[(long long)bidx * a.res_bs + off + n];
@@ -71,7 +83,7 @@ __device__ __forceinline__ void store_epilogue(const ConvArgs &a, int bidx, int 
     }
     v = apply_act(v, e.act, e.alpha);
     if (e.res && e.res_after) v += r;
-    a.y[(long long)bidx * a.y_bs + (long long)m * a.ycs + n] = v;
+    a.y[(long long)bidx * a.y_bs + out_row(a, m) + n] = v;
 }
 
 // Map an output pixel + filter tap to an input pixel; false -> zero padding.
@@ -416,12 +428,12 @@ __global__ __launch_bounds__(256, 1) void conv_igemm(ConvArgs a) {
             float v = Cs[rr * LDC + cn] * sc + sh;
             float rv = 0.f;
             if (rsrc) {
-                rv = rsrc[m * e.res_cs];
+                rv = rsrc[a.y_step > 1 ? out_row(a, m) : m * e.res_cs];
                 if (!e.res_after) v += rv;
             }
             v = fast_act(v, e.act, slope);
             if (rsrc && e.res_after) v += rv;
-            yb[m * a.ycs] = v;
+            yb[out_row(a, m)] = v;
         }
     } else {
 #pragma unroll 1
@@ -669,6 +681,14 @@ static int validate(const s2v_conv_params *p, int &M, int &K) {
         S2V_REQUIRE(((uintptr_t)p->wt % 16) == 0, "conv2d: weights must be 16B aligned");
     }
     if (p->res) S2V_REQUIRE(p->res_cs >= p->cout, "conv2d: res_cs < cout");
+    if (p->out_step > 1) {
+        S2V_REQUIRE(!p->pix_add, "conv2d: strided output cannot take pix_add");
+        S2V_REQUIRE(!p->res || (p->res == p->y && p->res_cs == p->ycs && p->res_oy == 0 && p->res_ox == 0),
+                    "conv2d: strided output only takes an in-place residual (res == y)");
+        S2V_REQUIRE(p->cout > 4, "conv2d: strided output needs the implicit-GEMM path (cout > 4)");
+        S2V_REQUIRE(p->out_full_h >= (p->oh - 1) * p->out_step + 1 && p->out_full_w >= (p->ow - 1) * p->out_step + 1,
+                    "conv2d: strided output exceeds out_full_h/w");
+    }
     return 0;
 }
 
@@ -689,6 +709,7 @@ static ConvArgs make_args(const s2v_conv_params *p, int M, int K, const Plan &pl
     e.act = p->act; e.alpha = p->alpha;
     a.x_bs = p->x_bs; a.w_bs = p->w_bs; a.y_bs = p->y_bs; a.res_bs = p->res_bs;
     a.M = M; a.K = K; a.ktiles = pl.ktiles; a.splits = pl.splits; a.tps = pl.tps; a.ws = p->ws;
+    a.y_step = p->out_step > 1 ? p->out_step : 1; a.y_h = p->out_full_h; a.y_w = p->out_full_w;
     return a;
 }
 

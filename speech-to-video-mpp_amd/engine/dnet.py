@@ -41,8 +41,8 @@ class DNetEngine:
             d = f"{h}decoder.decoder{i}."
             tp = dict(transposed=True, stride=2, padding=1, output_padding=1)
             c0 = make_conv(sd, d + "conv_0.", dev, padding=1)
-            c1 = make_conv(sd, d + "conv_1.", dev, **tp)
-            cs = make_conv(sd, d + "conv_s.", dev, **tp)
+            c1 = make_conv(sd, d + "conv_1.", dev, **tp).make_polyphase(dev)
+            cs = make_conv(sd, d + "conv_s.", dev, **tp).make_polyphase(dev)
             self.dec.append(dict(c0=c0, c1=c1, cs=cs, n0=self._adain(sd, d + "norm_0.", c0.cin),
                                  n1=self._adain(sd, d + "norm_1.", c1.cin), ns=self._adain(sd, d + "norm_s.", cs.cin)))
         f = "warpping_net.flow_out."

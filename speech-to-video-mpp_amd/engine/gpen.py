@@ -36,7 +36,7 @@ class _StyledLayer:
         w = w / math.sqrt(i * k * k)                          # ModulatedConv2d.scale (:231-233)
         self.cin, self.cout, self.k, self.upsample, self.is_rgb = i, o, k, upsample, is_rgb
         if upsample:
-            self.conv = ConvW(w.transpose(0, 1), None, dev, transposed=True, stride=2, padding=0)
+            self.conv = ConvW(w.transpose(0, 1), None, dev, transposed=True, stride=2, padding=0).make_polyphase(dev)
             self.blur = sd[p + "conv.blur.kernel"].float().contiguous().to(dev)
         else:
             self.conv = ConvW(w, None, dev, padding=k // 2)

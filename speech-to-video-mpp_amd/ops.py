@@ -110,6 +110,8 @@ class ConvW:
             w = w.transpose(0, 1)
             in_mode = IN_TRANSPOSED
         self.cout, self.cin, self.kh, self.kw = (int(s) for s in w.shape)
+        self._w_oihw = w if in_mode == IN_TRANSPOSED else None
+        self.poly = None
         pair = lambda v: (v, v) if isinstance(v, int) else tuple(v)  # noqa: E731
         self.sh, self.sw = pair(stride)
         self.ph, self.pw = pair(padding)
@@ -140,6 +142,28 @@ class ConvW:
         self.scale = None if scale is None else scale.contiguous().to(device)
         self.shift = None if shift is None else shift.contiguous().to(device)
 
+    def make_polyphase(self, device):
+        """Polyphase plan of a stride-2 ConvTranspose2d: output parity class (ry, rx) is a stride-1
+        direct conv of the input with the taps ky = ry + p (mod 2), flipped, padded by T - 1 - c0
+        (c0 = (ry + p - ky_min) / 2), written with output step 2 at offset (ry, rx).  Work drops
+        from kh*kw taps per output pixel (3/4 of them zero) to the algorithmic count."""
+        assert self.in_mode == IN_TRANSPOSED and (self.sh, self.sw) == (2, 2) and (self.dh, self.dw) == (1, 1)
+        w = self._w_oihw
+        plans = []
+        for ry in range(2):
+            ty = [k for k in range(self.kh) if (ry + self.ph - k) % 2 == 0]
+            for rx in range(2):
+                tx = [k for k in range(self.kw) if (rx + self.pw - k) % 2 == 0]
+                if not ty or not tx:
+                    raise NotImplementedError("polyphase class without taps")
+                c0y, c0x = (ry + self.ph - ty[0]) // 2, (rx + self.pw - tx[0]) // 2
+                sub = w[:, :, ty[::-1]][:, :, :, tx[::-1]]
+                cw = ConvW(sub, None, device, padding=(len(ty) - 1 - c0y, len(tx) - 1 - c0x))
+                cw.scale, cw.shift = self.scale, self.shift
+                plans.append(((ry, rx), cw, (ry, rx)))
+        self.poly = plans
+        return self
+
     def out_hw(self, h, w):
         if self.in_mode == IN_TRANSPOSED:
             return ((h - 1) * self.sh - 2 * self.ph + self.dh * (self.kh - 1) + self.oph + 1,
@@ -157,10 +181,34 @@ def _ptr(t):
 def conv2d(ctx: Ctx, x: NHWC, cw: ConvW, y: NHWC, *, act=ACT_NONE, alpha=0.0, res: NHWC | None = None,
            res_after=False, res_offset=(0, 0), nc_scale=None, in_scale=None, pre_act=ACT_NONE, pre_alpha=0.0,
            pix_add=None, pix_w=0.0, scale=None, shift=None, force_tile=0, force_splits=0):
-    """Fused conv (see s2v_conv_params).  nc_scale / in_scale: [N, C] device tensors."""
+    """Fused conv (see s2v_conv_params).  nc_scale / in_scale: [N, C] device tensors.  A transposed
+    ConvW with a polyphase plan (``cw.poly``) runs as one stride-1 conv per output parity class."""
+    if getattr(cw, "poly", None) is not None:
+        assert pix_add is None, "polyphase transposed conv: no pix_add epilogue"
+        assert res is None or (res.t.data_ptr() == y.t.data_ptr() and res.coff == y.coff and not res_after), \
+            "polyphase transposed conv: only an in-place residual (res is the output view)"
+        oh, ow = cw.out_hw(x.h, x.w)
+        assert (y.n, y.h, y.w, y.c) == (x.n, oh, ow, cw.cout), "conv_transpose: output view mismatch"
+        for (ry, rx), sub, _ in cw.poly:
+            ch, cwid = (oh - ry + 1) // 2, (ow - rx + 1) // 2
+            if ch <= 0 or cwid <= 0:
+                continue
+            base = NHWC.__new__(NHWC)
+            base.t, base.n, base.h, base.w, base.cs, base.c = y.t, y.n, ch, cwid, y.cs, y.c
+            base.coff = y.coff + (ry * y.w + rx) * y.cs
+            _conv(ctx, x, sub, base, (ch, cwid), (2, y.h, y.w), act, alpha, None if res is None else base, False,
+                  (0, 0), nc_scale, in_scale, pre_act, pre_alpha, None, 0.0, scale, shift, force_tile, force_splits)
+        return y
     oh, ow = cw.out_hw(x.h, x.w)
     assert x.c == cw.cin, f"conv: input has {x.c} channels, weights expect {cw.cin}"
     assert (y.n, y.h, y.w, y.c) == (x.n, oh, ow, cw.cout), f"conv: output view {(y.n, y.h, y.w, y.c)} != {(x.n, oh, ow, cw.cout)}"
+    return _conv(ctx, x, cw, y, (oh, ow), None, act, alpha, res, res_after, res_offset, nc_scale, in_scale, pre_act,
+                 pre_alpha, pix_add, pix_w, scale, shift, force_tile, force_splits)
+
+
+def _conv(ctx, x, cw, y, ohw, out_view, act, alpha, res, res_after, res_offset, nc_scale, in_scale, pre_act,
+          pre_alpha, pix_add, pix_w, scale, shift, force_tile, force_splits):
+    oh, ow = ohw
     p = _lib.ConvParams()
     p.x, p.n, p.h, p.w, p.cin, p.xcs = x.ptr, x.n, x.h, x.w, x.c, x.cs
     p.in_mode, p.pad_mode, p.pre_act, p.pre_alpha = cw.in_mode, cw.pad_mode, pre_act, pre_alpha
@@ -183,6 +231,8 @@ def conv2d(ctx: Ctx, x: NHWC, cw: ConvW, y: NHWC, *, act=ACT_NONE, alpha=0.0, re
     p.act, p.alpha = act, alpha
     p.batch = 1
     p.force_tile, p.force_splits = force_tile, force_splits
+    if out_view is not None:
+        p.out_step, p.out_full_h, p.out_full_w = out_view
     need = ctx.lib.s2v_conv2d_ws_bytes(ctypes.byref(p))
     p.ws, p.ws_bytes = ctx.ws.get(need)
     if CONV_HOOK is not None:

@@ -135,6 +135,43 @@ def test_conv2d(ctx, case):
         assert (err <= lim).all(), f"variant {variant}: max err {err.max():.3e}, rel {(err / lim).max():.2f}"
 
 
+@pytest.mark.parametrize("cfg", [
+    dict(n=2, cin=64, h=7, w=9, cout=96, k=3, pad=0, op=0),      # GPEN upsampling modconv (:262-276)
+    dict(n=2, cin=32, h=6, w=6, cout=64, k=3, pad=1, op=1),      # DNet ADAINDecoderBlock (base_blocks.py:240-250)
+    dict(n=1, cin=64, h=5, w=8, cout=40, k=4, pad=1, op=0),
+    dict(n=2, cin=36, h=4, w=5, cout=33, k=3, pad=2, op=1),      # generic gather + negative class offsets
+])
+def test_conv_transpose_polyphase(ctx, cfg):
+    """Polyphase stride-2 ConvTranspose2d (one stride-1 conv per output parity class, strided
+    output) against F.conv_transpose2d, with the prologue / epilogue pieces the engines use."""
+    n, cin, h, w, cout, k, pad, op = (cfg[key] for key in ("n", "cin", "h", "w", "cout", "k", "pad", "op"))
+    wt = rnd(cin, cout, k, k, seed=11) / math.sqrt(cin * k * k)
+    bias = rnd(cout, seed=12)
+    x = rnd(n, cin, h, w, seed=13)
+    s = rnd(n, cin, seed=14, lo=0.5, hi=1.5)
+    d = rnd(n, cout, seed=15, lo=0.5, hi=1.5)
+    ref = F.conv_transpose2d(x * s[:, :, None, None], wt, None, 2, pad, output_padding=op)
+    bound = conv_bound(x * s[:, :, None, None], wt, 2, pad, 1, True, op)
+    cw = ConvW(wt.float(), bias.float(), DEV, transposed=True, stride=2, padding=pad, output_padding=op)
+    cw.make_polyphase(DEV)
+    oh, ow = ref.shape[-2:]
+    assert cw.out_hw(h, w) == (oh, ow)
+    exp = F.leaky_relu(ref * d[:, :, None, None] + bias[None, :, None, None], 0.2)
+    y = NHWC.empty(n, oh, ow, cout + 4, DEV).slice(4, cout)
+    ops.conv2d(ctx, nhwc(x.float()), cw, y, in_scale=s.float().to(DEV), nc_scale=d.float().to(DEV),
+               act=ops.ACT_LRELU, alpha=0.2)
+    err = (to_nchw(y) - exp).abs()
+    lim = 4e-6 * (bound * 1.5 + 1) + 1e-6
+    assert (err <= lim).all(), f"max err {err.max():.3e}"
+    # in-place residual (DNet x_s + dx): y += conv_transpose(x)
+    base = to_nchw(y)
+    cw2 = ConvW(wt.float(), None, DEV, transposed=True, stride=2, padding=pad, output_padding=op).make_polyphase(DEV)
+    ops.conv2d(ctx, nhwc(x.float()), cw2, y, res=y)
+    ref2 = F.conv_transpose2d(x, wt, None, 2, pad, output_padding=op)
+    err = (to_nchw(y) - (base + ref2)).abs()
+    assert (err <= lim + 4e-6 * base.abs()).all(), f"residual max err {err.max():.3e}"
+
+
 def test_conv2d_prologue(ctx):
     n, cin, h, w, cout = 2, 32, 10, 10, 64
     wt = rnd(cout, cin, 3, 3, seed=7) / math.sqrt(cin * 9)
