@@ -249,17 +249,39 @@ __global__ __launch_bounds__(256) void adain_heads(const float *__restrict__ hid
         if (b0 + i < batch) out[(long long)(b0 + i) * out_ns + o] = acc[i] + bb;
 }
 
+// One wave per output channel o; lanes stride over cin (coalesced rows of wsq), each lane keeps
+// the partial sums of up to 16 samples so a wsq row is read once for the whole batch chunk.
+constexpr int DEMOD_NB = 16;
 __global__ __launch_bounds__(256) void demod_kernel(const float *__restrict__ s, int batch, int s_ns, int cin,
                                                     const float *__restrict__ wsq, int cout, float eps, float post,
                                                     float *__restrict__ d, int d_ns) {
-    const int o = blockIdx.x * 256 + threadIdx.x;
-    const int b = blockIdx.y;
+    const int lane = threadIdx.x & 63;
+    const int o = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (o >= cout) return;
-    const float *sr = s + (long long)b * s_ns;
     const float *wr = wsq + (long long)o * cin;
-    float acc = 0.f;
-    for (int i = 0; i < cin; ++i) acc = fmaf(sr[i] * sr[i], wr[i], acc);
-    d[(long long)b * d_ns + o] = rsqrtf(acc + eps) * post;
+    for (int b0 = 0; b0 < batch; b0 += DEMOD_NB) {
+        const int nb = min(DEMOD_NB, batch - b0);
+        float acc[DEMOD_NB];
+#pragma unroll
+        for (int j = 0; j < DEMOD_NB; ++j) acc[j] = 0.f;
+        for (int i = lane; i < cin; i += 64) {
+            const float w = wr[i];
+#pragma unroll
+            for (int j = 0; j < DEMOD_NB; ++j) {
+                if (j < nb) {
+                    const float v = s[(long long)(b0 + j) * s_ns + i];
+                    acc[j] = fmaf(v * v, w, acc[j]);
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < DEMOD_NB; ++j) {
+            float v = acc[j];
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+            if (lane == 0 && j < nb) d[(long long)(b0 + j) * d_ns + o] = rsqrtf(v + eps) * post;
+        }
+    }
 }
 
 }  // namespace s2v
@@ -341,7 +363,7 @@ extern "C" int s2v_modconv_demod(const float *s, int batch, int s_ns, int cin, c
                                  float post, float *d, int d_ns, s2v_stream_t stream) {
     S2V_REQUIRE(s && wsq && d && batch > 0 && cin > 0 && cout > 0 && s_ns >= cin && d_ns >= cout,
                 "modconv_demod: bad args");
-    demod_kernel<<<dim3(cdiv(cout, 256), batch), 256, 0, (hipStream_t)stream>>>(s, batch, s_ns, cin, wsq, cout, eps,
-                                                                                post, d, d_ns);
+    demod_kernel<<<cdiv(cout, 4), 256, 0, (hipStream_t)stream>>>(s, batch, s_ns, cin, wsq, cout, eps, post, d,
+                                                                 d_ns);
     return check_launch("demod");
 }
