@@ -78,7 +78,8 @@ def live_roofline(forward, workload="lipsync"):
         s.record()
         launch()
         e.record()
-        recs.append((sym, flops, splits, s, e))
+        recs.append((sym, flops, splits, s, e, (p.n, p.h, p.w, p.cin, p.oh, p.ow, p.cout, p.kh, p.kw,
+                                                bool(p.in_scale), bool(p.nc_scale), bool(p.pix_add), bool(p.res))))
 
     ops.CONV_HOOK = hook
     try:
@@ -88,7 +89,12 @@ def live_roofline(forward, workload="lipsync"):
     finally:
         ops.CONV_HOOK = None
     per = {}
-    for sym, flops, splits, s, e in recs:
+    if os.environ.get("S2V_BENCH_VERBOSE") == "2":
+        for sym, flops, splits, s, e, shp in recs:
+            ms = s.elapsed_time(e)
+            print(f"  {ms * 1e3:9.1f} us {flops / max(ms, 1e-9) / 1e9:7.2f} TF/s splits={splits} "
+                  f"n,h,w,cin,oh,ow,cout,kh,kw,ins,ncs,pix,res={shp} {sym[11:40]}", file=sys.stderr)
+    for sym, flops, splits, s, e, _ in recs:
         d = per.setdefault(sym, {"flops": 0.0, "ms": 0.0, "launches": 0, "split_launches": 0})
         d["flops"] += flops
         d["ms"] += s.elapsed_time(e)

@@ -187,6 +187,20 @@ int s2v_upfirdn2d(const float *x, int major, int in_h, int in_w, int minor, cons
                   int up_x, int up_y, int down_x, int down_y, int pad_x0, int pad_x1, int pad_y0, int pad_y1,
                   float *y, int out_h, int out_w, s2v_stream_t stream);
 
+/* FourierUnit transforms (models/ffc.py:93-126): torch.fft.rfftn / irfftn over (H, W),
+ * norm='ortho', as separable 1-D passes staged in LDS (one block per sample x 4 channels).
+ *   s2v_rfft2:  x NHWC [n][h][w] (pitch xcs)  ->  spec[n][u*Wf + v][part*C + c] (pitch scs >= 2C),
+ *               Wf = w/2 + 1, part 0 = real, 1 = imaginary (the FourierUnit's [B, F, 2C] layout)
+ *   s2v_irfft2: spec (same layout)  ->  y NHWC = irfftn(spec, s=(h, w)) (+ res NHWC, may be NULL)
+ * tables: s2v_fft_tables_floats(h, w) floats = fw[2][Wf][w] | fh[2][h][h] | ih[2][h][h] |
+ * iw[2][w][Wf], the 1-D ortho transform matrices (host-built from torch.fft on basis vectors).
+ * C % 4 == 0, 16-byte aligned x / spec, h*w small enough for LDS (<= 48x48 fits). */
+size_t s2v_fft_tables_floats(int h, int w);
+int s2v_rfft2(const float *x, int n, int h, int w, int c, int xcs, const float *tables, float *spec, int scs,
+              s2v_stream_t stream);
+int s2v_irfft2(const float *spec, int n, int h, int w, int c, int scs, const float *tables, const float *res,
+               int rcs, float *y, int ycs, s2v_stream_t stream);
+
 /* NHWC FIR resampling with fused epilogue (the engines' form of upfirdn2d, GPEN gpen_model.py:37-91
  * Upsample / Blur and the blur after the transposed modulated conv, :270-276):
  *   y[n,oy,ox,c] = post * act(gain * sum_{i,j} kflip[i][j] * xu[n, oy*down + i - pad_y0, ox*down + j - pad_x0, c]

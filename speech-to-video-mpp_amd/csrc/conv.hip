@@ -324,13 +324,35 @@ __global__ __launch_bounds__(256, 1) void conv_igemm(ConvArgs a) {
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WAVES_N, wn = wave % WAVES_N;
-    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-    const int bz = blockIdx.z;
+    // XCD-aware tile order: the dispatcher deals workgroups round-robin over the 8 XCDs, so
+    // remap the linear id so that each XCD owns a contiguous run of tiles (neighbouring output
+    // rows share their 3x3 halo through that XCD's L2), N-tiles of one M-tile adjacent.
+    int mt, nt, bz;
+    {
+        const int gx = gridDim.x, gy = gridDim.y;
+        const int total = gx * gy * gridDim.z;
+        const int L = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+        const int per = total >> 3, rem = total & 7;
+        const int xcd = L & 7, idx = L >> 3;
+        const int Lp = xcd < rem ? xcd * (per + 1) + idx : rem * (per + 1) + (xcd - rem) * per + idx;
+        nt = Lp % gy;
+        const int t = Lp / gy;
+        mt = t % gx;
+        bz = t / gx;
+    }
+    const int m0 = mt * BM, n0 = nt * BN;
     const int bidx = bz / a.splits, split = bz - bidx * a.splits;
     const float *__restrict__ x = a.x + (long long)bidx * a.x_bs;
     const float *__restrict__ wt = a.wt + (long long)bidx * a.w_bs;
     const int kt0 = split * a.tps;
     const int kt1 = min(a.ktiles, kt0 + a.tps);
+    // AMODE 0/3: visit K-slices channel-slice-major (all taps of one 32-channel slice in a row),
+    // so the 3x3 neighbourhood of a slice is re-read from L2 right away instead of after the
+    // whole channel range; the weights are indexed by the same permuted slice, so the sum is
+    // unchanged apart from fp32 summation order.
+    const int taps = a.kh * a.kw, nsl = a.cin >> 5;
+    const bool kperm = (AMODE == 0 || AMODE == 3) && !BKN && taps > 1;
+    auto kmap = [&](int i) { return kperm ? (i % taps) * nsl + i / taps : i; };
     const int ar = tid >> 3, ak = (tid & 7) * 4;
 
     ARows<AR, AMODE> R;
@@ -347,8 +369,8 @@ __global__ __launch_bounds__(256, 1) void conv_igemm(ConvArgs a) {
 
     const int li = lane & 31, lh = lane >> 5;
     if (kt0 < kt1) {
-        load_a<AR, AMODE>(a, x, kt0, ak, R, ra);
-        load_b<BN, BR, BKN>(a, wt, kt0, n0, tid, rb);
+        load_a<AR, AMODE>(a, x, kmap(kt0), ak, R, ra);
+        load_b<BN, BR, BKN>(a, wt, kmap(kt0), n0, tid, rb);
         store_ab<BM, BN, AR, BR, BKN>(smem, smem + BM * LDK, tid, ra, rb);
         __syncthreads();
     }
@@ -356,7 +378,7 @@ __global__ __launch_bounds__(256, 1) void conv_igemm(ConvArgs a) {
     for (int kt = kt0; kt < kt1; ++kt) {
         // prefetch slice kt+1 into registers (the last iteration re-reads its own slice: no
         // control flow around the staging registers); it lands while the MFMAs below run
-        const int kn = min(kt + 1, kt1 - 1);
+        const int kn = kmap(min(kt + 1, kt1 - 1));
         load_a<AR, AMODE>(a, x, kn, ak, R, ra);
         load_b<BN, BR, BKN>(a, wt, kn, n0, tid, rb);
         __builtin_amdgcn_sched_barrier(0);   // keep the prefetch issue above the MFMA block

@@ -125,7 +125,7 @@ class FFCLama:
         self.fu = ConvW(wfu, None, device, bn=bn)
         self.st2 = ConvW(sd[st + "conv2.weight"], None, device)
         self.h, self.w = hw
-        self.d2, self.iv = ops.fourier_matrices(self.h, self.w, device)
+        self.fft = ops.fft_tables(self.h, self.w, device)
         self.F = self.h * (self.w // 2 + 1)
         self.gid = bank.add_group(sd, [(p + "bn_l.", self.cl), (p + "bn_g.", self.cg)])
         self.device = device
@@ -140,13 +140,12 @@ class FFCLama:
         ops.conv2d(ctx, x.slice(0, cl), self.conv_l2g, yg)
         t1 = NHWC.empty(b, self.h, self.w, cc, dev)
         ops.conv2d(ctx, x.slice(cl, cg), self.st1, t1, act=ops.ACT_RELU)
-        spec = torch.empty((b, 2 * self.F, cc), device=dev)
-        ops.gemm_kn(ctx, self.d2, t1.t, spec, batch=b, a_bs=0, b_bs=P * cc, out_bs=2 * self.F * cc)
+        spec = torch.empty((b, self.F, 2 * cc), device=dev)
+        ops.rfft2(ctx, t1, self.fft, spec)                             # rfftn ortho (ffc.py:99-104)
         spec2 = NHWC.empty(b, self.F, 1, 2 * cc, dev)
         ops.conv2d(ctx, NHWC(spec.view(b, self.F, 1, 2 * cc)), self.fu, spec2, act=ops.ACT_RELU)
         u = NHWC.empty(b, self.h, self.w, cc, dev)
-        ops.gemm_kn(ctx, self.iv, spec2.t.view(b, 2 * self.F, cc), u.t, batch=b, a_bs=0, b_bs=2 * self.F * cc, out_bs=P * cc,
-                    res=t1.t, res_bs=P * cc)
+        ops.irfft2(ctx, spec2.t.view(b, self.F, 2 * cc), self.fft, u, res=t1)   # irfftn + x (ffc.py:120-126, :158)
         ops.conv2d(ctx, u, self.st2, yg, res=yg)
 
     def norm(self, ctx, bank: AdainBank, y: NHWC, out: NHWC, res: NHWC | None = None):

@@ -479,3 +479,44 @@ def eltwise(ctx: Ctx, x: NHWC, y: NHWC, *, a=1.0, mul: NHWC | None = None, add: 
                               None if add is None else add.ptr, 0 if add is None else add.cs, _ptr(bias),
                               x.n * x.h * x.w, x.c, a, act, alpha, post, y.ptr, y.cs, ctx.stream), "s2v_eltwise")
     return y
+
+
+# ----------------------------------------------------------------------------- separable FFT
+_FFT_TABLES = {}
+
+
+def fft_tables(h: int, w: int, device):
+    """1-D ortho transform matrices for s2v_rfft2 / s2v_irfft2 (include/s2v.h), built by applying
+    torch.fft to basis vectors in float64: fw[2][Wf][w] | fh[2][h][h] | ih[2][h][h] | iw[2][w][Wf]."""
+    key = (h, w, str(device))
+    if key not in _FFT_TABLES:
+        wf = w // 2 + 1
+        rw = torch.fft.rfft(torch.eye(w, dtype=torch.float64), dim=1, norm="ortho")         # [w, Wf]
+        fw = torch.stack([rw.real.t(), rw.imag.t()])                                       # [2, Wf, w]
+        fhc = torch.fft.fft(torch.eye(h, dtype=torch.complex128), dim=1, norm="ortho")      # [h, u]
+        fh = torch.stack([fhc.real.t(), fhc.imag.t()])                                     # [2, u, h]
+        ihc = torch.fft.ifft(torch.eye(h, dtype=torch.complex128), dim=1, norm="ortho")     # [u, h]
+        ih = torch.stack([ihc.real.t(), ihc.imag.t()])                                     # [2, h, u]
+        eye = torch.eye(wf, dtype=torch.float64)
+        cre = torch.fft.irfft(torch.complex(eye, torch.zeros_like(eye)), n=w, dim=1, norm="ortho")   # [v, w]
+        cim = torch.fft.irfft(torch.complex(torch.zeros_like(eye), eye), n=w, dim=1, norm="ortho")
+        iw = torch.stack([cre.t(), cim.t()])                                               # [2, w, Wf]
+        t = torch.cat([fw.reshape(-1), fh.reshape(-1), ih.reshape(-1), iw.reshape(-1)]).float().contiguous()
+        assert t.numel() == 2 * wf * w + 4 * h * h + 2 * w * wf
+        _FFT_TABLES[key] = t.to(device)
+    return _FFT_TABLES[key]
+
+
+def rfft2(ctx: Ctx, x: NHWC, tables: torch.Tensor, spec: torch.Tensor):
+    """x NHWC [n,h,w,C] -> spec [n, h*(w//2+1), 2C] (channel = part*C + c), rfftn ortho."""
+    check(ctx.lib.s2v_rfft2(x.ptr, x.n, x.h, x.w, x.c, x.cs, tables.data_ptr(), spec.data_ptr(), spec.shape[-1],
+                            ctx.stream), "s2v_rfft2")
+    return spec
+
+
+def irfft2(ctx: Ctx, spec: torch.Tensor, tables: torch.Tensor, y: NHWC, res: NHWC | None = None):
+    """spec [n, F, >=2C] -> y NHWC = irfftn(spec, s=(h, w), ortho) (+ res)."""
+    check(ctx.lib.s2v_irfft2(spec.data_ptr(), y.n, y.h, y.w, y.c, spec.shape[-1], tables.data_ptr(),
+                             None if res is None else res.ptr, 0 if res is None else res.cs, y.ptr, y.cs, ctx.stream),
+          "s2v_irfft2")
+    return y

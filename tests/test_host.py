@@ -203,3 +203,28 @@ def test_gpen_synthetic_blur_kernels_are_the_fixed_buffers():
     assert torch.equal(sd["generator.convs.0.conv.blur.kernel"], 4 * k)
     assert torch.equal(sd["generator.to_rgbs.0.upsample.kernel"], 4 * k)
     assert float(sd["generator.conv1.noise.weight"]) == pytest.approx(0.1)
+
+
+def test_fft_tables_reproduce_torch_fft():
+    """The separable passes s2v_rfft2 / s2v_irfft2 run, emulated with the host-built tables."""
+    from s2v_amd.ops import fft_tables
+    for h, w in ((12, 12), (24, 24), (48, 48), (6, 10)):
+        wf = w // 2 + 1
+        t = fft_tables(h, w, "cpu").double()
+        o = 0
+        fw = t[o:o + 2 * wf * w].reshape(2, wf, w); o += 2 * wf * w
+        fh = t[o:o + 2 * h * h].reshape(2, h, h); o += 2 * h * h
+        ih = t[o:o + 2 * h * h].reshape(2, h, h); o += 2 * h * h
+        iw = t[o:].reshape(2, w, wf)
+        x = torch.randn(3, h, w, dtype=torch.float64)
+        yr, yi = x @ fw[0].t(), x @ fw[1].t()                              # W pass: [c, h, v]
+        zr = fh[0] @ yr - fh[1] @ yi                                       # H pass (complex)
+        zi = fh[1] @ yr + fh[0] @ yi
+        ref = torch.fft.rfftn(x, dim=(-2, -1), norm="ortho")
+        assert (zr - ref.real).abs().max() < 1e-5 and (zi - ref.imag).abs().max() < 1e-5
+        sr, si = torch.randn(3, h, wf, dtype=torch.float64), torch.randn(3, h, wf, dtype=torch.float64)
+        ar = ih[0] @ sr - ih[1] @ si                                       # inverse H pass
+        ai = ih[1] @ sr + ih[0] @ si
+        y = ar @ iw[0].t() + ai @ iw[1].t()                                # c2r W pass
+        ref = torch.fft.irfftn(torch.complex(sr, si), s=(h, w), dim=(-2, -1), norm="ortho")
+        assert (y - ref).abs().max() < 1e-5

@@ -172,6 +172,28 @@ def test_conv_transpose_polyphase(ctx, cfg):
     assert (err <= lim + 4e-6 * base.abs()).all(), f"residual max err {err.max():.3e}"
 
 
+@pytest.mark.parametrize("n,h,w,c", [(2, 12, 12, 384), (3, 24, 24, 96), (2, 48, 48, 48), (1, 6, 10, 8)])
+def test_rfft2_irfft2_match_torch_fft(ctx, n, h, w, c):
+    """Separable LDS transforms (s2v_rfft2 / s2v_irfft2) against torch.fft.rfftn / irfftn ortho
+    (ffc.py:99, :121), input a channel slice of a wider NHWC tensor, inverse with the residual."""
+    x = rnd(n, h, w, c + 4, seed=21)
+    wf = w // 2 + 1
+    tables = ops.fft_tables(h, w, DEV)
+    xin = NHWC(x.float().to(DEV)).slice(4, c)
+    spec = torch.empty((n, h * wf, 2 * c), device=DEV)
+    ops.rfft2(ctx, xin, tables, spec)
+    ref = torch.fft.rfftn(x[..., 4:], dim=(1, 2), norm="ortho")              # [n, h, wf, c]
+    got = spec.double().cpu().reshape(n, h, wf, 2, c)
+    assert (got[..., 0, :] - ref.real).abs().max() < 2e-5 and (got[..., 1, :] - ref.imag).abs().max() < 2e-5
+    sp = rnd(n, h * wf, 2 * c, seed=22)
+    res = rnd(n, h, w, c, seed=23)
+    y = NHWC.empty(n, h, w, c, DEV)
+    ops.irfft2(ctx, sp.float().to(DEV), tables, y, res=NHWC(res.float().to(DEV)))
+    z = sp.reshape(n, h, wf, 2, c)
+    ref = torch.fft.irfftn(torch.complex(z[..., 0, :], z[..., 1, :]), s=(h, w), dim=(1, 2), norm="ortho") + res
+    assert (y.t.double().cpu() - ref).abs().max() < 2e-5
+
+
 def test_conv2d_prologue(ctx):
     n, cin, h, w, cout = 2, 32, 10, 10, 64
     wt = rnd(cout, cin, 3, 3, seed=7) / math.sqrt(cin * 9)

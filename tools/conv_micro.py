@@ -1,0 +1,76 @@
+#!/usr/bin/env python3
+"""Micro-benchmark of one libs2v convolution shape (for kernel tuning and PMC passes).
+
+    python tools/conv_micro.py --n 16 --h 200 --w 200 --cin 256 --cout 128 --k 3 [--up2] [--iters 20]
+
+Prints the launch plan, the average time (HIP events on the launch stream) and the algorithmic
+TFLOP/s.  ``--sweep`` times every tile config the kernel offers for the shape.
+"""
+import argparse
+import math
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+import s2v_import  # noqa: E402,F401
+from s2v_amd import ops  # noqa: E402
+from s2v_amd.ops import NHWC, ConvW  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=16)
+    ap.add_argument("--h", type=int, default=200)
+    ap.add_argument("--w", type=int, default=200)
+    ap.add_argument("--cin", type=int, default=256)
+    ap.add_argument("--cout", type=int, default=128)
+    ap.add_argument("--k", type=int, default=3)
+    ap.add_argument("--stride", type=int, default=1)
+    ap.add_argument("--up2", action="store_true", help="nearest-x2 upsampled input (IN_NEAREST_UP2)")
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--sweep", action="store_true")
+    ap.add_argument("--splits", type=int, default=0)
+    a = ap.parse_args()
+    dev = torch.device("cuda")
+    ctx = ops.Ctx(dev)
+    w = torch.randn(a.cout, a.cin, a.k, a.k) / math.sqrt(a.cin * a.k * a.k)
+    cw = ConvW(w, torch.randn(a.cout), dev, stride=a.stride, padding=a.k // 2,
+               in_mode=ops.IN_NEAREST_UP2 if a.up2 else ops.IN_DIRECT)
+    x = NHWC(torch.randn(a.n, a.h, a.w, a.cin, device=dev))
+    oh, ow = cw.out_hw(a.h, a.w)
+    y = NHWC.empty(a.n, oh, ow, a.cout, dev)
+    flops = 2.0 * a.n * oh * ow * a.k * a.k * a.cin * a.cout
+    tiles = range(1, 7) if a.sweep else [0]
+    for t in tiles:
+        kw = dict(act=ops.ACT_LRELU, alpha=0.2, force_tile=t, force_splits=a.splits)
+        ops.conv2d(ctx, x, cw, y, **kw)
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(a.iters):
+            ops.conv2d(ctx, x, cw, y, **kw)
+        e.record()
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / a.iters
+        print(f"tile={t} {ops.conv_symbol(ctx, _params(ctx, x, cw, y, t, a.splits))}: {ms * 1e3:9.1f} us  "
+              f"{flops / ms / 1e9:7.2f} TFLOP/s", flush=True)
+
+
+def _params(ctx, x, cw, y, tile, splits):
+    captured = {}
+
+    def hook(c, p, flops, launch):
+        captured["p"] = p
+    ops.CONV_HOOK = hook
+    try:
+        ops.conv2d(ctx, x, cw, y, force_tile=tile, force_splits=splits)
+    finally:
+        ops.CONV_HOOK = None
+    return captured["p"]
+
+
+if __name__ == "__main__":
+    main()
