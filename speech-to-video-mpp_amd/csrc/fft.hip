@@ -142,6 +142,134 @@ __global__ __launch_bounds__(256) void irfft2_kernel(const float *__restrict__ s
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Register-blocked variants for the LNet sizes (12, 24, 48): each thread keeps a whole output
+// row / column of accumulators and the 1-D matrices are read with wave-uniform indices straight
+// from global memory (scalar loads into SGPRs), so LDS carries only the data (one read per
+// input element per pass) instead of one LDS read per multiply-add.
+constexpr int FCG = 4;   // channels per block
+
+template <int H, int W>
+__global__ __launch_bounds__(256) void rfft2_rb(const float *__restrict__ x, int C, int xcs,
+                                                const float *__restrict__ tables, float *__restrict__ spec,
+                                                int scs) {
+    constexpr int WF = W / 2 + 1;
+    constexpr int XS = W * FCG + 4;
+    constexpr int UC = H >= 24 ? H / 2 : H;          // u rows per H-pass item
+    __shared__ float X[H * XS];
+    __shared__ float Y[H * WF * 2 * FCG];
+    const int groups = C / FCG;
+    const int n = blockIdx.x / groups, c0 = (blockIdx.x - n * groups) * FCG;
+    const FftTables T = fft_tables(tables, H, W);
+    for (int p = threadIdx.x; p < H * W; p += 256) {
+        const int hh = p / W, ww = p - hh * W;
+        *(float4 *)&X[hh * XS + ww * FCG] = *(const float4 *)&x[((long long)n * H * W + p) * xcs + c0];
+    }
+    __syncthreads();
+    if (threadIdx.x < H * FCG) {                      // W pass: item (h, cg), all WF bins
+        const int h = threadIdx.x / FCG, cg = threadIdx.x % FCG;
+        float re[WF], im[WF];
+#pragma unroll
+        for (int v = 0; v < WF; ++v) re[v] = im[v] = 0.f;
+        for (int w = 0; w < W; ++w) {
+            const float xv = X[h * XS + w * FCG + cg];
+#pragma unroll
+            for (int v = 0; v < WF; ++v) {
+                re[v] = fmaf(T.fw[v * W + w], xv, re[v]);
+                im[v] = fmaf(T.fw[(WF + v) * W + w], xv, im[v]);
+            }
+        }
+#pragma unroll
+        for (int v = 0; v < WF; ++v) {
+            Y[((h * WF + v) * 2 + 0) * FCG + cg] = re[v];
+            Y[((h * WF + v) * 2 + 1) * FCG + cg] = im[v];
+        }
+    }
+    __syncthreads();
+    for (int it = threadIdx.x; it < WF * FCG * (H / UC); it += 256) {   // H pass: item (v, cg, u-chunk)
+        const int cg = it % FCG;
+        const int t = it / FCG;
+        const int v = t % WF, u0 = (t / WF) * UC;
+        float zr[UC], zi[UC];
+#pragma unroll
+        for (int u = 0; u < UC; ++u) zr[u] = zi[u] = 0.f;
+        for (int h = 0; h < H; ++h) {
+            const float yr = Y[((h * WF + v) * 2 + 0) * FCG + cg], yi = Y[((h * WF + v) * 2 + 1) * FCG + cg];
+#pragma unroll
+            for (int u = 0; u < UC; ++u) {
+                const float fr = T.fh[(u0 + u) * H + h], fi = T.fh[(H + u0 + u) * H + h];
+                zr[u] = fmaf(fr, yr, fmaf(-fi, yi, zr[u]));
+                zi[u] = fmaf(fi, yr, fmaf(fr, yi, zi[u]));
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < UC; ++u) {
+            float *o = spec + ((long long)n * H * WF + (u0 + u) * WF + v) * scs + c0 + cg;
+            o[0] = zr[u];
+            o[C] = zi[u];
+        }
+    }
+}
+
+template <int H, int W>
+__global__ __launch_bounds__(256) void irfft2_rb(const float *__restrict__ spec, int C, int scs,
+                                                 const float *__restrict__ tables, const float *__restrict__ res,
+                                                 int rcs, float *__restrict__ y, int ycs) {
+    constexpr int WF = W / 2 + 1;
+    constexpr int HC = H >= 24 ? H / 2 : H;          // h rows per inverse-H item
+    __shared__ float Z[H * WF * 2 * FCG];
+    __shared__ float Y[H * WF * 2 * FCG];
+    const int groups = C / FCG;
+    const int n = blockIdx.x / groups, c0 = (blockIdx.x - n * groups) * FCG;
+    const FftTables T = fft_tables(tables, H, W);
+    for (int i = threadIdx.x; i < H * WF * 2; i += 256) {
+        const int part = i & 1, f = i >> 1;
+        *(float4 *)&Z[(f * 2 + part) * FCG] = *(const float4 *)&spec[((long long)n * H * WF + f) * scs + part * C + c0];
+    }
+    __syncthreads();
+    for (int it = threadIdx.x; it < WF * FCG * (H / HC); it += 256) {   // inverse H: item (v, cg, h-chunk)
+        const int cg = it % FCG;
+        const int t = it / FCG;
+        const int v = t % WF, h0 = (t / WF) * HC;
+        float yr[HC], yi[HC];
+#pragma unroll
+        for (int h = 0; h < HC; ++h) yr[h] = yi[h] = 0.f;
+        for (int u = 0; u < H; ++u) {
+            const float zr = Z[((u * WF + v) * 2 + 0) * FCG + cg], zi = Z[((u * WF + v) * 2 + 1) * FCG + cg];
+#pragma unroll
+            for (int h = 0; h < HC; ++h) {
+                const float gr = T.ih[(h0 + h) * H + u], gi = T.ih[(H + h0 + h) * H + u];
+                yr[h] = fmaf(gr, zr, fmaf(-gi, zi, yr[h]));
+                yi[h] = fmaf(gi, zr, fmaf(gr, zi, yi[h]));
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < HC; ++h) {
+            Y[(((h0 + h) * WF + v) * 2 + 0) * FCG + cg] = yr[h];
+            Y[(((h0 + h) * WF + v) * 2 + 1) * FCG + cg] = yi[h];
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < H * FCG) {                      // c2r W pass: item (h, cg), all W outputs
+        const int h = threadIdx.x / FCG, cg = threadIdx.x % FCG;
+        float acc[W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) acc[w] = 0.f;
+        for (int v = 0; v < WF; ++v) {
+            const float a = Y[((h * WF + v) * 2 + 0) * FCG + cg], b = Y[((h * WF + v) * 2 + 1) * FCG + cg];
+#pragma unroll
+            for (int w = 0; w < W; ++w) acc[w] = fmaf(T.iw[w * WF + v], a, fmaf(T.iw[(W + w) * WF + v], b, acc[w]));
+        }
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            const long long p = (long long)n * H * W + h * W + w;
+            float o = acc[w];
+            if (res) o += res[p * rcs + c0 + cg];
+            y[p * ycs + c0 + cg] = o;
+        }
+    }
+}
+
 // 4 channels per block: the most blocks (the transforms are small, parallelism matters more
 // than table reuse), 16-byte channel vectors for the global loads / stores.
 static int pick_cg(int C, int H, int W, size_t per_cg_floats, size_t fixed_floats) {
@@ -167,6 +295,15 @@ extern "C" int s2v_rfft2(const float *x, int n, int h, int w, int c, int xcs, co
     const size_t per = (size_t)h * w + (size_t)h * wf * 2, fixed = (size_t)2 * wf * w + (size_t)2 * h * h + 4 * h;
     const int cg = pick_cg(c, h, w, per, fixed);
     S2V_REQUIRE(cg > 0, "rfft2: C %% 4 != 0 or the %dx%d tile does not fit in LDS", h, w);
+    const bool aligned = xcs % 4 == 0 && ((uintptr_t)x % 16) == 0;
+    hipStream_t st = (hipStream_t)stream;
+    if (c % FCG == 0 && aligned && h == w && (h == 12 || h == 24 || h == 48)) {
+        const unsigned grid = n * (c / FCG);
+        if (h == 12) rfft2_rb<12, 12><<<grid, 256, 0, st>>>(x, c, xcs, tables, spec, scs);
+        else if (h == 24) rfft2_rb<24, 24><<<grid, 256, 0, st>>>(x, c, xcs, tables, spec, scs);
+        else rfft2_rb<48, 48><<<grid, 256, 0, st>>>(x, c, xcs, tables, spec, scs);
+        return check_launch("rfft2");
+    }
     const size_t smem = (per * cg + fixed) * sizeof(float);
     static bool attr = false;
     if (!attr) {
@@ -186,6 +323,14 @@ extern "C" int s2v_irfft2(const float *spec, int n, int h, int w, int c, int scs
     const size_t per = (size_t)h * wf * 4, fixed = (size_t)2 * h * h + (size_t)2 * w * wf;
     const int cg = pick_cg(c, h, w, per, fixed);
     S2V_REQUIRE(cg > 0, "irfft2: C %% 4 != 0 or the %dx%d tile does not fit in LDS", h, w);
+    hipStream_t st = (hipStream_t)stream;
+    if (c % FCG == 0 && h == w && (h == 12 || h == 24 || h == 48)) {
+        const unsigned grid = n * (c / FCG);
+        if (h == 12) irfft2_rb<12, 12><<<grid, 256, 0, st>>>(spec, c, scs, tables, res, rcs, y, ycs);
+        else if (h == 24) irfft2_rb<24, 24><<<grid, 256, 0, st>>>(spec, c, scs, tables, res, rcs, y, ycs);
+        else irfft2_rb<48, 48><<<grid, 256, 0, st>>>(spec, c, scs, tables, res, rcs, y, ycs);
+        return check_launch("irfft2");
+    }
     const size_t smem = (per * cg + fixed) * sizeof(float);
     static bool attr = false;
     if (!attr) {
