@@ -192,8 +192,9 @@ int s2v_upfirdn2d(const float *x, int major, int in_h, int in_w, int minor, cons
  *   s2v_rfft2:  x NHWC [n][h][w] (pitch xcs)  ->  spec[n][u*Wf + v][part*C + c] (pitch scs >= 2C),
  *               Wf = w/2 + 1, part 0 = real, 1 = imaginary (the FourierUnit's [B, F, 2C] layout)
  *   s2v_irfft2: spec (same layout)  ->  y NHWC = irfftn(spec, s=(h, w)) (+ res NHWC, may be NULL)
- * tables: s2v_fft_tables_floats(h, w) floats = fw[2][Wf][w] | fh[2][h][h] | ih[2][h][h] |
- * iw[2][w][Wf], the 1-D ortho transform matrices (host-built from torch.fft on basis vectors).
+ * tables: s2v_fft_tables_floats(h, w) floats = fw[w][2][Wf] | fh[h][2][h(u)] | ih[h(u)][2][h] |
+ * iw[Wf][2][w], the 1-D ortho transform matrices (host-built from torch.fft on basis vectors),
+ * [.][0][.] real and [.][1][.] imaginary parts.
  * C % 4 == 0, 16-byte aligned x / spec, h*w small enough for LDS (<= 48x48 fits). */
 size_t s2v_fft_tables_floats(int h, int w);
 int s2v_rfft2(const float *x, int n, int h, int w, int c, int xcs, const float *tables, float *spec, int scs,

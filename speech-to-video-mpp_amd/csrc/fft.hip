@@ -9,7 +9,9 @@
 // multiply-adds per pixel-channel instead of the 2*F*H*W of a dense 2-D DFT matrix.  The 1-D
 // transform matrices come from the host (built by applying torch.fft to basis vectors, so the
 // ortho scaling and the c2r treatment of the DC / Nyquist imaginary parts are exactly torch's):
-//   tables = fw[2][Wf][W] | fh[2][H][H] | ih[2][H][H] | iw[2][W][Wf]
+//   tables = fw[W][2][Wf] | fh[H][2][H] | ih[H][2][H] | iw[Wf][2][W]
+// (each matrix stored loop-invariant-index major: the inner loops of the kernels walk the last,
+// contiguous index, so wave-uniform reads of a row batch into wide scalar loads).
 #include "common.hpp"
 
 namespace s2v {
@@ -56,12 +58,11 @@ __global__ __launch_bounds__(256) void rfft2_kernel(const float *__restrict__ x,
         const int h = it / CG, cg = it - h * CG;
         for (int v = 0; v < wf; ++v) {
             float re = 0.f, im = 0.f;
-            const float *tr = Tw + v * W, *ti = Tw + (wf + v) * W;
             const float *xr = X + h * XS + cg;
             for (int w = 0; w < W; ++w) {
                 const float xv = xr[w * CG];
-                re = fmaf(tr[w], xv, re);
-                im = fmaf(ti[w], xv, im);
+                re = fmaf(Tw[(w * 2 + 0) * wf + v], xv, re);
+                im = fmaf(Tw[(w * 2 + 1) * wf + v], xv, im);
             }
             Y[((h * wf + v) * 2 + 0) * CG + cg] = re;
             Y[((h * wf + v) * 2 + 1) * CG + cg] = im;
@@ -73,12 +74,12 @@ __global__ __launch_bounds__(256) void rfft2_kernel(const float *__restrict__ x,
         const int cg = it % CG;
         const int t = it / CG;
         const int v = t % wf, u = t / wf;
-        const float *fr = Th + u * H, *fi = Th + (H + u) * H;
         float zr = 0.f, zi = 0.f;
         for (int h = 0; h < H; ++h) {
             const float yr = Y[((h * wf + v) * 2 + 0) * CG + cg], yi = Y[((h * wf + v) * 2 + 1) * CG + cg];
-            zr = fmaf(fr[h], yr, fmaf(-fi[h], yi, zr));
-            zi = fmaf(fi[h], yr, fmaf(fr[h], yi, zi));
+            const float fr = Th[(h * 2 + 0) * H + u], fi = Th[(h * 2 + 1) * H + u];
+            zr = fmaf(fr, yr, fmaf(-fi, yi, zr));
+            zi = fmaf(fi, yr, fmaf(fr, yi, zi));
         }
         float *o = spec + ((long long)n * H * wf + u * wf + v) * scs + c0 + cg;
         o[0] = zr;
@@ -116,12 +117,12 @@ __global__ __launch_bounds__(256) void irfft2_kernel(const float *__restrict__ s
         const int cg = it % CG;
         const int t = it / CG;
         const int v = t % wf, h = t / wf;
-        const float *gr = Ti + h * H, *gi = Ti + (H + h) * H;
         float yr = 0.f, yi = 0.f;
         for (int u = 0; u < H; ++u) {
             const float zr = Z[((u * wf + v) * 2 + 0) * CG + cg], zi = Z[((u * wf + v) * 2 + 1) * CG + cg];
-            yr = fmaf(gr[u], zr, fmaf(-gi[u], zi, yr));
-            yi = fmaf(gi[u], zr, fmaf(gr[u], zi, yi));
+            const float gr = Ti[(u * 2 + 0) * H + h], gi = Ti[(u * 2 + 1) * H + h];
+            yr = fmaf(gr, zr, fmaf(-gi, zi, yr));
+            yi = fmaf(gi, zr, fmaf(gr, zi, yi));
         }
         Y[((h * wf + v) * 2 + 0) * CG + cg] = yr;
         Y[((h * wf + v) * 2 + 1) * CG + cg] = yi;
@@ -132,10 +133,10 @@ __global__ __launch_bounds__(256) void irfft2_kernel(const float *__restrict__ s
         const int cg = it % CG;
         const int t = it / CG;
         const int w = t % W, h = t / W;
-        const float *cr = Tw + w * wf, *ci = Tw + (W + w) * wf;
         float acc = 0.f;
         for (int v = 0; v < wf; ++v)
-            acc = fmaf(cr[v], Y[((h * wf + v) * 2 + 0) * CG + cg], fmaf(ci[v], Y[((h * wf + v) * 2 + 1) * CG + cg], acc));
+            acc = fmaf(Tw[(v * 2 + 0) * W + w], Y[((h * wf + v) * 2 + 0) * CG + cg],
+                       fmaf(Tw[(v * 2 + 1) * W + w], Y[((h * wf + v) * 2 + 1) * CG + cg], acc));
         const long long p = (long long)n * H * W + h * W + w;
         if (res) acc += res[p * rcs + c0 + cg];
         y[p * ycs + c0 + cg] = acc;
@@ -175,8 +176,8 @@ __global__ __launch_bounds__(256) void rfft2_rb(const float *__restrict__ x, int
             const float xv = X[h * XS + w * FCG + cg];
 #pragma unroll
             for (int v = 0; v < WF; ++v) {
-                re[v] = fmaf(T.fw[v * W + w], xv, re[v]);
-                im[v] = fmaf(T.fw[(WF + v) * W + w], xv, im[v]);
+                re[v] = fmaf(T.fw[(w * 2 + 0) * WF + v], xv, re[v]);
+                im[v] = fmaf(T.fw[(w * 2 + 1) * WF + v], xv, im[v]);
             }
         }
 #pragma unroll
@@ -197,7 +198,7 @@ __global__ __launch_bounds__(256) void rfft2_rb(const float *__restrict__ x, int
             const float yr = Y[((h * WF + v) * 2 + 0) * FCG + cg], yi = Y[((h * WF + v) * 2 + 1) * FCG + cg];
 #pragma unroll
             for (int u = 0; u < UC; ++u) {
-                const float fr = T.fh[(u0 + u) * H + h], fi = T.fh[(H + u0 + u) * H + h];
+                const float fr = T.fh[(h * 2 + 0) * H + u0 + u], fi = T.fh[(h * 2 + 1) * H + u0 + u];
                 zr[u] = fmaf(fr, yr, fmaf(-fi, yi, zr[u]));
                 zi[u] = fmaf(fi, yr, fmaf(fr, yi, zi[u]));
             }
@@ -238,7 +239,7 @@ __global__ __launch_bounds__(256) void irfft2_rb(const float *__restrict__ spec,
             const float zr = Z[((u * WF + v) * 2 + 0) * FCG + cg], zi = Z[((u * WF + v) * 2 + 1) * FCG + cg];
 #pragma unroll
             for (int h = 0; h < HC; ++h) {
-                const float gr = T.ih[(h0 + h) * H + u], gi = T.ih[(H + h0 + h) * H + u];
+                const float gr = T.ih[(u * 2 + 0) * H + h0 + h], gi = T.ih[(u * 2 + 1) * H + h0 + h];
                 yr[h] = fmaf(gr, zr, fmaf(-gi, zi, yr[h]));
                 yi[h] = fmaf(gi, zr, fmaf(gr, zi, yi[h]));
             }
@@ -258,7 +259,7 @@ __global__ __launch_bounds__(256) void irfft2_rb(const float *__restrict__ spec,
         for (int v = 0; v < WF; ++v) {
             const float a = Y[((h * WF + v) * 2 + 0) * FCG + cg], b = Y[((h * WF + v) * 2 + 1) * FCG + cg];
 #pragma unroll
-            for (int w = 0; w < W; ++w) acc[w] = fmaf(T.iw[w * WF + v], a, fmaf(T.iw[(W + w) * WF + v], b, acc[w]));
+            for (int w = 0; w < W; ++w) acc[w] = fmaf(T.iw[(v * 2 + 0) * W + w], a, fmaf(T.iw[(v * 2 + 1) * W + w], b, acc[w]));
         }
 #pragma unroll
         for (int w = 0; w < W; ++w) {

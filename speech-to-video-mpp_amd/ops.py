@@ -487,20 +487,20 @@ _FFT_TABLES = {}
 
 def fft_tables(h: int, w: int, device):
     """1-D ortho transform matrices for s2v_rfft2 / s2v_irfft2 (include/s2v.h), built by applying
-    torch.fft to basis vectors in float64: fw[2][Wf][w] | fh[2][h][h] | ih[2][h][h] | iw[2][w][Wf]."""
+    torch.fft to basis vectors in float64: fw[w][2][Wf] | fh[h][2][u] | ih[u][2][h] | iw[Wf][2][w]."""
     key = (h, w, str(device))
     if key not in _FFT_TABLES:
         wf = w // 2 + 1
         rw = torch.fft.rfft(torch.eye(w, dtype=torch.float64), dim=1, norm="ortho")         # [w, Wf]
-        fw = torch.stack([rw.real.t(), rw.imag.t()])                                       # [2, Wf, w]
+        fw = torch.stack([rw.real, rw.imag], 1)                                           # [w, 2, Wf]
         fhc = torch.fft.fft(torch.eye(h, dtype=torch.complex128), dim=1, norm="ortho")      # [h, u]
-        fh = torch.stack([fhc.real.t(), fhc.imag.t()])                                     # [2, u, h]
+        fh = torch.stack([fhc.real, fhc.imag], 1)                                         # [h, 2, u]
         ihc = torch.fft.ifft(torch.eye(h, dtype=torch.complex128), dim=1, norm="ortho")     # [u, h]
-        ih = torch.stack([ihc.real.t(), ihc.imag.t()])                                     # [2, h, u]
+        ih = torch.stack([ihc.real, ihc.imag], 1)                                         # [u, 2, h]
         eye = torch.eye(wf, dtype=torch.float64)
         cre = torch.fft.irfft(torch.complex(eye, torch.zeros_like(eye)), n=w, dim=1, norm="ortho")   # [v, w]
         cim = torch.fft.irfft(torch.complex(torch.zeros_like(eye), eye), n=w, dim=1, norm="ortho")
-        iw = torch.stack([cre.t(), cim.t()])                                               # [2, w, Wf]
+        iw = torch.stack([cre, cim], 1)                                                   # [Wf, 2, w]
         t = torch.cat([fw.reshape(-1), fh.reshape(-1), ih.reshape(-1), iw.reshape(-1)]).float().contiguous()
         assert t.numel() == 2 * wf * w + 4 * h * h + 2 * w * wf
         _FFT_TABLES[key] = t.to(device)

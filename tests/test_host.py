@@ -212,10 +212,10 @@ def test_fft_tables_reproduce_torch_fft():
         wf = w // 2 + 1
         t = fft_tables(h, w, "cpu").double()
         o = 0
-        fw = t[o:o + 2 * wf * w].reshape(2, wf, w); o += 2 * wf * w
-        fh = t[o:o + 2 * h * h].reshape(2, h, h); o += 2 * h * h
-        ih = t[o:o + 2 * h * h].reshape(2, h, h); o += 2 * h * h
-        iw = t[o:].reshape(2, w, wf)
+        fw = t[o:o + 2 * wf * w].reshape(w, 2, wf).permute(1, 2, 0); o += 2 * wf * w     # -> [2, v, w]
+        fh = t[o:o + 2 * h * h].reshape(h, 2, h).permute(1, 2, 0); o += 2 * h * h        # -> [2, u, h]
+        ih = t[o:o + 2 * h * h].reshape(h, 2, h).permute(1, 2, 0); o += 2 * h * h        # -> [2, h, u]
+        iw = t[o:].reshape(wf, 2, w).permute(1, 2, 0)                                     # -> [2, w, v]
         x = torch.randn(3, h, w, dtype=torch.float64)
         yr, yi = x @ fw[0].t(), x @ fw[1].t()                              # W pass: [c, h, v]
         zr = fh[0] @ yr - fh[1] @ yi                                       # H pass (complex)
