@@ -202,6 +202,13 @@ int s2v_rfft2(const float *x, int n, int h, int w, int c, int xcs, const float *
 int s2v_irfft2(const float *spec, int n, int h, int w, int c, int scs, const float *tables, const float *res,
                int rcs, float *y, int ycs, s2v_stream_t stream);
 
+/* Per-sample modulated conv weights (StyleGAN2 ModulatedConv2d, base_blocks.py:487-495,
+ * stylegan2_clean_arch.py:66-80, gpen_model.py:245-256) from packed [npad][kpad] weights:
+ *   out[b][o][k] = wt[o][k] * s[b][k % cin] * (d ? d[b][o] : 1)   (k < K; padding stays 0)
+ * out is [batch][npad][kpad]; run the conv with batch = B, n = 1 and w_bs = npad * kpad. */
+int s2v_modulate_weights(const float *wt, int npad, int kpad, int K, int cin, int cout, const float *s, int s_ns,
+                         const float *d, int d_ns, int batch, float *out, s2v_stream_t stream);
+
 /* NHWC FIR resampling with fused epilogue (the engines' form of upfirdn2d, GPEN gpen_model.py:37-91
  * Upsample / Blur and the blur after the transposed modulated conv, :270-276):
  *   y[n,oy,ox,c] = post * act(gain * sum_{i,j} kflip[i][j] * xu[n, oy*down + i - pad_y0, ox*down + j - pad_x0, c]

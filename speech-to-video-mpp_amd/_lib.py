@@ -74,6 +74,8 @@ _SIGS = {
     "s2v_fft_tables_floats": (_c_size, [_c_int, _c_int]),
     "s2v_rfft2": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_int, _vp]),
     "s2v_irfft2": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_int, _vp, _c_int, _vp]),
+    "s2v_modulate_weights": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp, _c_int, _c_int,
+                                      _vp, _vp]),
     "s2v_gaussian_noise": (_c_int, [_vp, _c_ll, ctypes.c_uint64, ctypes.c_uint64, _vp]),
     "s2v_lipsync_inputs": (_c_int, [_vp, _vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp]),
     "s2v_to_u8": (_c_int, [_vp, _c_ll, _c_float, _c_float, _c_float, _c_float, _vp, _vp]),

@@ -808,6 +808,8 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
         const bool cpar = (p->cin % 4 == 0) && (p->xcs % 4 == 0) && (((uintptr_t)p->x % 16) == 0) &&
                           (p->x_bs % 4 == 0) && (!p->in_scale || (p->in_scale_ns % 4 == 0 &&
                                                                   ((uintptr_t)p->in_scale % 16) == 0));
+        S2V_REQUIRE(cpar || p->w_bs == 0 || batch == 1 || M % 256 == 0,
+                    "conv2d: per-batch weights on the LDS-staged small-Cout path need M %% 256 == 0");
         switch (p->cout) {
             case 1: launch_small<1>(a, batch, cpar, s); break;
             case 2: launch_small<2>(a, batch, cpar, s); break;

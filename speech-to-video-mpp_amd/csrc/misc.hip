@@ -389,6 +389,30 @@ __global__ __launch_bounds__(256) void fill_kernel(float *__restrict__ y, long l
     for (long long e = blockIdx.x * 256LL + threadIdx.x; e < n; e += (long long)gridDim.x * 256) y[e] = v;
 }
 
+// Per-sample StyleGAN2 weights (base_blocks.py:487-495 / stylegan2_clean_arch.py:66-80 /
+// gpen_model.py:245-256): out[b][o][k] = wt[o][k] * s[b][k % cin] * d[b][o] for packed
+// [npad][kpad] weights (k = tap * cin + c); padding rows / columns stay zero.  The conv then runs
+// in batch mode with these weights, free of prologue / epilogue scaling.
+__global__ __launch_bounds__(256) void modulate_weights_kernel(const float *__restrict__ wt, int npad, int kpad,
+                                                               int K, int cin, int cout, const float *__restrict__ s,
+                                                               int s_ns, const float *__restrict__ d, int d_ns,
+                                                               int batch, float *__restrict__ out) {
+    const long long per = (long long)npad * kpad;
+    const long long total = per * batch;
+    for (long long e = (blockIdx.x * 256LL + threadIdx.x) * 4; e < total; e += (long long)gridDim.x * 256 * 4) {
+        const int b = (int)(e / per);
+        const long long r = e - b * per;
+        const int o = (int)(r / kpad), k = (int)(r - (long long)o * kpad);
+        float4 w = *(const float4 *)(wt + r);
+        const float dd = (d && o < cout) ? d[(long long)b * d_ns + o] : 1.f;
+        float f[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) f[j] = (k + j < K) ? s[(long long)b * s_ns + (k + j) % cin] * dd : 0.f;
+        w.x *= f[0]; w.y *= f[1]; w.z *= f[2]; w.w *= f[3];
+        *(float4 *)(out + e) = w;
+    }
+}
+
 static unsigned grid_for(long long total) {
     long long b = (total + 255) / 256;
     if (b > 65535LL * 16) b = 65535LL * 16;
@@ -531,4 +555,15 @@ extern "C" int s2v_fill(float *y, long long n, float value, s2v_stream_t stream)
     if (n == 0) return 0;
     fill_kernel<<<grid_for(n), 256, 0, (hipStream_t)stream>>>(y, n, value);
     return check_launch("fill");
+}
+
+extern "C" int s2v_modulate_weights(const float *wt, int npad, int kpad, int K, int cin, int cout, const float *s,
+                                    int s_ns, const float *d, int d_ns, int batch, float *out, s2v_stream_t stream) {
+    S2V_REQUIRE(wt && s && out && npad > 0 && kpad > 0 && K > 0 && K <= kpad && cin > 0 && cout > 0 && cout <= npad &&
+                batch > 0 && s_ns >= cin && (!d || d_ns >= cout), "modulate_weights: bad args");
+    S2V_REQUIRE(kpad % 4 == 0 && ((uintptr_t)wt % 16) == 0 && ((uintptr_t)out % 16) == 0,
+                "modulate_weights: kpad %% 4 and 16-byte aligned weights required");
+    modulate_weights_kernel<<<grid_for((long long)npad * kpad * batch / 4), 256, 0, (hipStream_t)stream>>>(
+        wt, npad, kpad, K, cin, cout, s, s_ns, d, d_ns, batch, out);
+    return check_launch("modulate_weights");
 }

@@ -1,11 +1,11 @@
 """ENet engine (reference models/ENet.py:82-139): style encoder + LNet + two StyleGAN2 stages.
 
-Modulated convolutions (base_blocks.py:460-554) are computed without per-sample weights:
-    conv(x, W * s[b,i]) * demod[b,o]  ==  (conv(x * s[b,:], W)) * demod[b,o]
-so the input modulation is a prologue scale on the gathered activations (``in_scale``), the
-demodulation rsqrt(sum_i s_i^2 sum_k W_oik^2 + eps) a per-(b,o) epilogue scale (``nc_scale``),
-and all convolutions share one set of packed weights across the batch (the reference builds a
-grouped conv with B distinct weight sets).
+Modulated convolutions (base_blocks.py:460-554): the per-sample weights W * s[b, i] * demod[b, o]
+(demod = rsqrt(sum_i s_i^2 sum_k W_oik^2 + eps), times sqrt(2)) are materialised by one small
+kernel (s2v_modulate_weights, a few MB per layer) and the conv runs in batch mode with them, so
+the implicit GEMM carries no prologue / epilogue scaling; noise and bias stay in the epilogue.
+(The engine can also run them as conv(x * s, W) * demod with shared weights: ops.conv2d's
+in_scale / nc_scale, used where per-sample weights do not apply.)
 """
 from __future__ import annotations
 
@@ -149,14 +149,14 @@ class ENetEngine:
                     else:
                         noise = torch.empty((b, x.h, x.w), device=dev)
                         ops.gaussian_noise(ctx, noise, self.noise_seed, (self.calls << 40) + ((2 * st + li) << 36))
-                ops.conv2d(ctx, x, L.conv, y, in_scale=s2[:, off: off + L.cin], nc_scale=d, act=ops.ACT_LRELU,
-                           alpha=LRELU, pix_add=noise, pix_w=L.noise_w or 0.0)
+                ops.modulated_conv2d(ctx, x, L.conv, y, s2[:, off: off + L.cin], d, act=ops.ACT_LRELU, alpha=LRELU,
+                                     pix_add=noise, pix_w=L.noise_w or 0.0)
                 cur = y
             R = self.layers[3 * st + 2]
             off = self.mod_offs[3 * st + 2]
             rgb = NHWC.empty(b, cur.h, cur.w, 3, dev)
             ops.resize_nhwc(ctx, skip, rgb, scale_factor=2)          # skip upsample (base_blocks.py:552)
-            ops.conv2d(ctx, cur, R.conv, rgb, in_scale=s2[:, off: off + R.cin], res=rgb)
+            ops.modulated_conv2d(ctx, cur, R.conv, rgb, s2[:, off: off + R.cin], res=rgb)
             skip = rgb
         ops.nhwc_to_nchw(ctx, skip, out, crop=(8, 8))                # [:, :, 8:-8, 8:-8]
         return out, low

@@ -207,7 +207,7 @@ def conv2d(ctx: Ctx, x: NHWC, cw: ConvW, y: NHWC, *, act=ACT_NONE, alpha=0.0, re
 
 
 def _conv(ctx, x, cw, y, ohw, out_view, act, alpha, res, res_after, res_offset, nc_scale, in_scale, pre_act,
-          pre_alpha, pix_add, pix_w, scale, shift, force_tile, force_splits):
+          pre_alpha, pix_add, pix_w, scale, shift, force_tile, force_splits, per_sample_wt=None):
     oh, ow = ohw
     p = _lib.ConvParams()
     p.x, p.n, p.h, p.w, p.cin, p.xcs = x.ptr, x.n, x.h, x.w, x.c, x.cs
@@ -233,6 +233,13 @@ def _conv(ctx, x, cw, y, ohw, out_view, act, alpha, res, res_after, res_offset, 
     p.force_tile, p.force_splits = force_tile, force_splits
     if out_view is not None:
         p.out_step, p.out_full_h, p.out_full_w = out_view
+    if per_sample_wt is not None:        # batch mode: one image per batch entry, its own weights
+        assert in_scale is None and nc_scale is None and out_view is None
+        p.n, p.batch = 1, x.n
+        p.wt, p.w_bs = per_sample_wt.data_ptr(), cw.npad * cw.kpad
+        p.x_bs, p.y_bs = x.h * x.w * x.cs, oh * ow * y.cs
+        if res is not None:
+            p.res_bs = res.h * res.w * res.cs
     need = ctx.lib.s2v_conv2d_ws_bytes(ctypes.byref(p))
     p.ws, p.ws_bytes = ctx.ws.get(need)
     if CONV_HOOK is not None:
@@ -244,6 +251,25 @@ def _conv(ctx, x, cw, y, ohw, out_view, act, alpha, res, res_after, res_offset, 
         return y
     check(ctx.lib.s2v_conv2d(ctypes.byref(p), ctx.stream), "s2v_conv2d")
     return y
+
+
+def modulated_conv2d(ctx: Ctx, x: NHWC, cw: ConvW, y: NHWC, s: torch.Tensor, d: torch.Tensor | None = None, *,
+                     act=ACT_NONE, alpha=0.0, res: NHWC | None = None, res_after=False, pix_add=None, pix_w=0.0,
+                     shift=None):
+    """StyleGAN2 modulated conv with per-sample weights W * s[b, c] (* d[b, o]) built by
+    s2v_modulate_weights, then one batched conv (no prologue / epilogue scaling in the GEMM).
+    s: [B, cin] (row stride s.stride(0)); d: [B, cout] demodulation or None."""
+    oh, ow = cw.out_hw(x.h, x.w)
+    assert cw.in_mode != IN_TRANSPOSED and cw.poly is None, "modulated_conv2d: direct / up2 convs only"
+    assert x.c == cw.cin and (y.n, y.h, y.w, y.c) == (x.n, oh, ow, cw.cout)
+    b = x.n
+    wb = torch.empty((b, cw.npad, cw.kpad), device=cw.wt.device)
+    check(ctx.lib.s2v_modulate_weights(cw.wt.data_ptr(), cw.npad, cw.kpad, cw.K, cw.cin, cw.cout, s.data_ptr(),
+                                       s.stride(0), None if d is None else d.data_ptr(),
+                                       0 if d is None else d.stride(0), b, wb.data_ptr(), ctx.stream),
+          "s2v_modulate_weights")
+    return _conv(ctx, x, cw, y, (oh, ow), None, act, alpha, res, res_after, (0, 0), None, None, ACT_NONE, 0.0,
+                 pix_add, pix_w, None, shift, 0, 0, per_sample_wt=wb)
 
 
 def gemm_kn(ctx: Ctx, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, batch: int, a_bs: int, b_bs: int,

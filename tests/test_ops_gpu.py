@@ -194,6 +194,32 @@ def test_rfft2_irfft2_match_torch_fft(ctx, n, h, w, c):
     assert (y.t.double().cpu() - ref).abs().max() < 2e-5
 
 
+@pytest.mark.parametrize("n,cin,h,w,cout,k,mode", [(3, 64, 10, 12, 96, 3, "direct"), (2, 4, 9, 9, 64, 3, "direct"),
+                                                   (2, 32, 6, 6, 48, 3, "up2"), (2, 128, 7, 7, 3, 1, "direct")])
+def test_modulated_conv_per_sample_weights(ctx, n, cin, h, w, cout, k, mode):
+    """s2v_modulate_weights + batched conv == the shared-weight form conv(x * s, W) * d (and the
+    grouped per-sample conv of the reference, base_blocks.py:487-508)."""
+    wt = rnd(cout, cin, k, k, seed=31) / math.sqrt(cin * k * k)
+    bias = rnd(cout, seed=32)
+    x = rnd(n, cin, h, w, seed=33)
+    s = rnd(n, cin, seed=34, lo=0.5, hi=1.5)
+    d = rnd(n, cout, seed=35, lo=0.5, hi=1.5)
+    noise = rnd(n, 2 * h if mode == "up2" else h, 2 * w if mode == "up2" else w, seed=36)
+    cw = ConvW(wt.float(), bias.float(), DEV, padding=k // 2,
+               in_mode=ops.IN_NEAREST_UP2 if mode == "up2" else ops.IN_DIRECT)
+    xin = F.interpolate(x, scale_factor=2, mode="nearest") if mode == "up2" else x
+    wb = wt[None] * s[:, None, :, None, None] * d[:, :, None, None, None]
+    ref = torch.stack([F.conv2d(xin[i:i + 1], wb[i], None, 1, k // 2)[0] for i in range(n)])
+    ref = F.leaky_relu(ref + 0.3 * noise[:, None] + bias[None, :, None, None], 0.2)
+    bound = conv_bound(xin * s[:, :, None, None], wt, 1, k // 2, 1) * 1.5 + 1
+    oh, ow = ref.shape[-2:]
+    y = NHWC.empty(n, oh, ow, cout + 4, DEV).slice(2, cout)
+    ops.modulated_conv2d(ctx, nhwc(x.float()), cw, y, s.float().to(DEV), d.float().to(DEV), act=ops.ACT_LRELU,
+                         alpha=0.2, pix_add=noise.float().to(DEV).contiguous(), pix_w=0.3)
+    err = (to_nchw(y) - ref).abs()
+    assert (err <= 4e-6 * bound + 1e-6).all(), f"max err {err.max():.3e}"
+
+
 def test_conv2d_prologue(ctx):
     n, cin, h, w, cout = 2, 32, 10, 10, 64
     wt = rnd(cout, cin, 3, 3, seed=7) / math.sqrt(cin * 9)
