@@ -187,10 +187,14 @@ __global__ __launch_bounds__(256) void rfft2_rb(const float *__restrict__ x, int
         }
     }
     __syncthreads();
-    for (int it = threadIdx.x; it < WF * FCG * (H / UC); it += 256) {   // H pass: item (v, cg, u-chunk)
-        const int cg = it % FCG;
-        const int t = it / FCG;
-        const int v = t % WF, u0 = (t / WF) * UC;
+    // H pass: item (v, cg) of u-chunk q; each chunk padded to whole waves so that u0 (and with it
+    // every table index) is wave-uniform
+    constexpr int IPC = (WF * FCG + 63) / 64 * 64;
+    for (int it = threadIdx.x; it < IPC * (H / UC); it += 256) {
+        const int q = it / IPC, r = it - q * IPC;
+        if (r >= WF * FCG) continue;
+        const int cg = r % FCG;
+        const int v = r / FCG, u0 = q * UC;
         float zr[UC], zi[UC];
 #pragma unroll
         for (int u = 0; u < UC; ++u) zr[u] = zi[u] = 0.f;
@@ -228,10 +232,12 @@ __global__ __launch_bounds__(256) void irfft2_rb(const float *__restrict__ spec,
         *(float4 *)&Z[(f * 2 + part) * FCG] = *(const float4 *)&spec[((long long)n * H * WF + f) * scs + part * C + c0];
     }
     __syncthreads();
-    for (int it = threadIdx.x; it < WF * FCG * (H / HC); it += 256) {   // inverse H: item (v, cg, h-chunk)
-        const int cg = it % FCG;
-        const int t = it / FCG;
-        const int v = t % WF, h0 = (t / WF) * HC;
+    constexpr int IPC = (WF * FCG + 63) / 64 * 64;   // inverse H: item (v, cg) of h-chunk q (wave-uniform h0)
+    for (int it = threadIdx.x; it < IPC * (H / HC); it += 256) {
+        const int q = it / IPC, r = it - q * IPC;
+        if (r >= WF * FCG) continue;
+        const int cg = r % FCG;
+        const int v = r / FCG, h0 = q * HC;
         float yr[HC], yi[HC];
 #pragma unroll
         for (int h = 0; h < HC; ++h) yr[h] = yi[h] = 0.f;
