@@ -203,6 +203,111 @@ __global__ __launch_bounds__(256) void in_apply(const float *__restrict__ x, int
     }
 }
 
+// Vectorised InstanceNorm/ADAIN (c % 4 == 0, 16-byte aligned views): a thread owns 4 channels
+// (one float4) and a pixel phase; 4 independent loads in flight per thread; fp64 partial sums.
+// grid (chunks, ceil(c / 256), n)
+__global__ __launch_bounds__(256) void in_stats_v(const float *__restrict__ x, int hw, int c, int xcs, int chunks,
+                                                  double *__restrict__ part) {
+    const int q4 = threadIdx.x & 63, ph = threadIdx.x >> 6;
+    const int cc = blockIdx.y * 256 + 4 * q4;
+    const int n = blockIdx.z, ch = blockIdx.x;
+    const int per = (hw + chunks - 1) / chunks;
+    const int p0 = ch * per, p1 = min(hw, p0 + per);
+    double s[4] = {0.0, 0.0, 0.0, 0.0}, q[4] = {0.0, 0.0, 0.0, 0.0};
+    if (cc < c) {
+        const float *xb = x + (long long)n * hw * xcs + cc;
+        int p = p0 + ph;
+        for (; p + 12 < p1; p += 16) {
+            float4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = *(const float4 *)(xb + (long long)(p + 4 * u) * xcs);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const double a = v[u].x, b = v[u].y, d = v[u].z, e = v[u].w;
+                s[0] += a; s[1] += b; s[2] += d; s[3] += e;
+                q[0] += a * a; q[1] += b * b; q[2] += d * d; q[3] += e * e;
+            }
+        }
+        for (; p < p1; p += 4) {
+            const float4 v = *(const float4 *)(xb + (long long)p * xcs);
+            const double a = v.x, b = v.y, d = v.z, e = v.w;
+            s[0] += a; s[1] += b; s[2] += d; s[3] += e;
+            q[0] += a * a; q[1] += b * b; q[2] += d * d; q[3] += e * e;
+        }
+    }
+    __shared__ double red[4][64][8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        red[ph][q4][j] = s[j];
+        red[ph][q4][4 + j] = q[j];
+    }
+    __syncthreads();
+    if (ph == 0 && cc < c) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const double ss = red[0][q4][j] + red[1][q4][j] + red[2][q4][j] + red[3][q4][j];
+            const double qq = red[0][q4][4 + j] + red[1][q4][4 + j] + red[2][q4][4 + j] + red[3][q4][4 + j];
+            const long long o = (((long long)n * c + cc + j) * chunks + ch) * 2;
+            part[o] = ss;
+            part[o + 1] = qq;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void in_apply_v(const float *__restrict__ x, int hw, int c, int xcs,
+                                                  const float *__restrict__ gamma, const float *__restrict__ beta,
+                                                  int gb_ns, float eps, int act, float alpha, const float *res,
+                                                  int res_cs, float *y, int ycs, const double *__restrict__ part,
+                                                  int chunks, int achunks) {
+    const int q4 = threadIdx.x & 63, ph = threadIdx.x >> 6;
+    const int cc = blockIdx.y * 256 + 4 * q4;
+    const int n = blockIdx.z;
+    if (cc >= c) return;
+    float mul[4], add[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        double s = 0.0, q = 0.0;
+        const long long o = ((long long)n * c + cc + j) * chunks * 2;
+        for (int i = 0; i < chunks; ++i) {
+            s += part[o + 2 * i];
+            q += part[o + 2 * i + 1];
+        }
+        const double mean = s / hw;
+        double var = q / hw - mean * mean;
+        if (var < 0.0) var = 0.0;
+        const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+        const float g = gamma ? 1.f + gamma[(long long)n * gb_ns + cc + j] : 1.f;
+        const float b = beta ? beta[(long long)n * gb_ns + cc + j] : 0.f;
+        mul[j] = rstd * g;                                   // (x - mean) * rstd * g + b
+        add[j] = b - (float)mean * rstd * g;
+    }
+    const int per = (hw + achunks - 1) / achunks;
+    const int p0 = blockIdx.x * per, p1 = min(hw, p0 + per);
+    const float *xb = x + (long long)n * hw * xcs + cc;
+    float *yb = y + (long long)n * hw * ycs + cc;
+    const float *rb = res ? res + (long long)n * hw * res_cs + cc : nullptr;
+    for (int p = p0 + ph; p < p1; p += 4) {
+        const float4 v = *(const float4 *)(xb + (long long)p * xcs);
+        float4 o;
+        o.x = apply_act(fmaf(v.x, mul[0], add[0]), act, alpha);
+        o.y = apply_act(fmaf(v.y, mul[1], add[1]), act, alpha);
+        o.z = apply_act(fmaf(v.z, mul[2], add[2]), act, alpha);
+        o.w = apply_act(fmaf(v.w, mul[3], add[3]), act, alpha);
+        if (rb) {
+            const float4 r = *(const float4 *)(rb + (long long)p * res_cs);
+            o.x += r.x; o.y += r.y; o.z += r.z; o.w += r.w;
+        }
+        *(float4 *)(yb + (long long)p * ycs) = o;
+    }
+}
+
+static int in_chunks_v(int n, long long hw, int c) {
+    const long long cq = (c + 255) / 256;
+    long long k = 1;
+    while ((long long)n * cq * k < 512 && k * 64 < hw && k < 64) k *= 2;
+    return (int)k;
+}
+
 // ------------------------------------------------------------------ token LayerNorm
 __global__ __launch_bounds__(256) void row_ln(const float *__restrict__ x, int rows, int dim, int xld,
                                               const float *__restrict__ w, const float *__restrict__ b, float eps,
@@ -317,7 +422,9 @@ extern "C" int s2v_layernorm2d(const float *x, int n, int h, int w, int c, int x
 }
 
 extern "C" size_t s2v_instnorm_ws_bytes(int n, int h, int w, int c) {
-    return (size_t)n * c * in_chunks((long long)h * w) * 2 * sizeof(double);
+    const long long hw = (long long)h * w;
+    const int k = in_chunks(hw) > in_chunks_v(n, hw, c) ? in_chunks(hw) : in_chunks_v(n, hw, c);
+    return (size_t)n * c * k * 2 * sizeof(double);
 }
 
 extern "C" int s2v_instnorm_adain(const float *x, int n, int h, int w, int c, int xcs, const float *gamma,
@@ -333,6 +440,23 @@ extern "C" int s2v_instnorm_adain(const float *x, int n, int h, int w, int c, in
         return S2V_E_WORKSPACE;
     }
     hipStream_t s = (hipStream_t)stream;
+    const bool vec = c % 4 == 0 && xcs % 4 == 0 && ycs % 4 == 0 && (!res || res_cs % 4 == 0) &&
+                     ((uintptr_t)x % 16) == 0 && ((uintptr_t)y % 16) == 0 && (!res || ((uintptr_t)res % 16) == 0);
+    if (vec) {
+        const int kv = in_chunks_v(n, hw, c);
+        const size_t needv = (size_t)n * c * kv * 2 * sizeof(double);
+        if (ws_bytes < needv) {
+            set_error("instnorm: workspace of %zu bytes required", needv);
+            return S2V_E_WORKSPACE;
+        }
+        const unsigned cq = cdiv(c, 256);
+        in_stats_v<<<dim3(kv, cq, n), 256, 0, s>>>(x, hw, c, xcs, kv, (double *)ws);
+        int rc = check_launch("in_stats");
+        if (rc) return rc;
+        in_apply_v<<<dim3(kv, cq, n), 256, 0, s>>>(x, hw, c, xcs, gamma, beta, gb_ns, eps, act, alpha, res, res_cs,
+                                                    y, ycs, (const double *)ws, kv, kv);
+        return check_launch("in_apply");
+    }
     const unsigned cg = cdiv(c, 64);
     in_stats<<<dim3(chunks, cg, n), 256, 0, s>>>(x, hw, c, xcs, chunks, (double *)ws);
     int rc = check_launch("in_stats");

@@ -261,14 +261,15 @@ def test_layernorm2d(ctx):
         assert (to_nchw(y) - ref).abs().max() < 2e-5
 
 
-def test_instnorm_adain(ctx):
+@pytest.mark.parametrize("c", [70, 72, 300])          # scalar path, float4 path, two 256-channel blocks
+def test_instnorm_adain(ctx, c):
     for (h, w) in ((12, 12), (70, 40)):
-        x = rnd(2, 70, h, w, seed=17) * 2 - 0.5
-        g, bt = rnd(2, 70, seed=18), rnd(2, 70, seed=19)
+        x = rnd(2, c, h, w, seed=17) * 2 - 0.5
+        g, bt = rnd(2, c, seed=18), rnd(2, c, seed=19)
         gb = torch.cat([g, bt], 1).float().to(DEV)
-        res = rnd(2, 70, h, w, seed=20)
-        y = NHWC.empty(2, h, w, 70, DEV)
-        ops.instnorm(ctx, nhwc(x.float()), y, gb.data_ptr(), gb.data_ptr() + 4 * 70, 140, act=ops.ACT_LRELU,
+        res = rnd(2, c, h, w, seed=20)
+        y = NHWC.empty(2, h, w, c, DEV)
+        ops.instnorm(ctx, nhwc(x.float()), y, gb.data_ptr(), gb.data_ptr() + 4 * c, 2 * c, act=ops.ACT_LRELU,
                      alpha=0.01, res=nhwc(res.float()))
         ref = F.leaky_relu(F.instance_norm(x, eps=1e-5) * (1 + g[:, :, None, None]) + bt[:, :, None, None], 0.01) + res
         assert (to_nchw(y) - ref).abs().max() < 2e-5
