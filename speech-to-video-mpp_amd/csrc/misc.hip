@@ -46,6 +46,41 @@ __global__ __launch_bounds__(256) void resize_kernel(const float *__restrict__ x
     }
 }
 
+// NHWC fast path: channel-contiguous views (xsc == ysc == 1), c % 4 == 0, 16-byte aligned:
+// one float4 of channels per thread, 32-bit index math.
+__global__ __launch_bounds__(256) void resize_nhwc4_kernel(const float *__restrict__ x, int n, int c4, int ih,
+                                                           int iw, long long xsn, int xsy, int xsx,
+                                                           float *__restrict__ y, int oh, int ow, long long ysn,
+                                                           int ysy, int ysx, float sh, float sw, int mode) {
+    const long long total = (long long)n * oh * ow * c4;
+    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+        const int cq = (int)(e % c4);
+        const long long t = e / c4;
+        const int pix = (int)(t % ((long long)oh * ow));
+        const int nn = (int)(t / ((long long)oh * ow));
+        const int oy = pix / ow, ox = pix - (pix / ow) * ow;
+        const float *xb = x + nn * xsn + 4 * cq;
+        float4 v;
+        if (mode == 0) {
+            int y0, y1, x0, x1;
+            float ly0, ly1, lx0, lx1;
+            bilin_index(sh, oy, ih, y0, y1, ly0, ly1);
+            bilin_index(sw, ox, iw, x0, x1, lx0, lx1);
+            const float4 a = *(const float4 *)(xb + y0 * xsy + x0 * xsx), b = *(const float4 *)(xb + y0 * xsy + x1 * xsx);
+            const float4 cc = *(const float4 *)(xb + y1 * xsy + x0 * xsx), d = *(const float4 *)(xb + y1 * xsy + x1 * xsx);
+            v.x = ly0 * (lx0 * a.x + lx1 * b.x) + ly1 * (lx0 * cc.x + lx1 * d.x);
+            v.y = ly0 * (lx0 * a.y + lx1 * b.y) + ly1 * (lx0 * cc.y + lx1 * d.y);
+            v.z = ly0 * (lx0 * a.z + lx1 * b.z) + ly1 * (lx0 * cc.z + lx1 * d.z);
+            v.w = ly0 * (lx0 * a.w + lx1 * b.w) + ly1 * (lx0 * cc.w + lx1 * d.w);
+        } else {
+            const int sy = min((int)floorf((float)oy * sh), ih - 1);
+            const int sx = min((int)floorf((float)ox * sw), iw - 1);
+            v = *(const float4 *)(xb + sy * xsy + sx * xsx);
+        }
+        *(float4 *)(y + nn * ysn + oy * ysy + ox * ysx + 4 * cq) = v;
+    }
+}
+
 __global__ __launch_bounds__(256) void pad_reflect_kernel(const float *__restrict__ x, int n, int h, int w, int c,
                                                           int xcs, int pt, int pl, int oh, int ow,
                                                           float *__restrict__ y, int ycs) {
@@ -428,6 +463,14 @@ extern "C" int s2v_resize(const float *x, int n, int c, int ih, int iw, long lon
                           long long ysx, float scale_h, float scale_w, int mode, s2v_stream_t stream) {
     S2V_REQUIRE(x && y && n > 0 && c > 0 && ih > 0 && iw > 0 && oh > 0 && ow > 0, "resize: bad args");
     S2V_REQUIRE(mode == 0 || mode == 1, "resize: bad mode");
+    const bool v4 = xsc == 1 && ysc == 1 && c % 4 == 0 && xsx % 4 == 0 && ysx % 4 == 0 && xsy % 4 == 0 &&
+                    ysy % 4 == 0 && xsn % 4 == 0 && ysn % 4 == 0 && ((uintptr_t)x % 16) == 0 &&
+                    ((uintptr_t)y % 16) == 0 && xsy < (1LL << 31) && ysy < (1LL << 31);
+    if (v4) {
+        resize_nhwc4_kernel<<<grid_for((long long)n * oh * ow * (c / 4)), 256, 0, (hipStream_t)stream>>>(
+            x, n, c / 4, ih, iw, xsn, (int)xsy, (int)xsx, y, oh, ow, ysn, (int)ysy, (int)ysx, scale_h, scale_w, mode);
+        return check_launch("resize");
+    }
     resize_kernel<<<grid_for((long long)n * oh * ow * c), 256, 0, (hipStream_t)stream>>>(
         x, n, c, ih, iw, xsn, xsc, xsy, xsx, y, oh, ow, ysn, ysc, ysy, ysx, scale_h, scale_w, mode);
     return check_launch("resize");

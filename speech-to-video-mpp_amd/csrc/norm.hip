@@ -286,6 +286,7 @@ __global__ __launch_bounds__(256) void in_apply_v(const float *__restrict__ x, i
     const float *xb = x + (long long)n * hw * xcs + cc;
     float *yb = y + (long long)n * hw * ycs + cc;
     const float *rb = res ? res + (long long)n * hw * res_cs + cc : nullptr;
+#pragma unroll 4
     for (int p = p0 + ph; p < p1; p += 4) {
         const float4 v = *(const float4 *)(xb + (long long)p * xcs);
         float4 o;

@@ -316,7 +316,8 @@ def test_adain_params_and_demod(ctx):
 
 @pytest.mark.parametrize("shape", [((2, 3, 384, 384), (96, 96), None), ((2, 5, 64, 64), None, 0.5),
                                    ((1, 4, 50, 50), None, 2), ((1, 3, 256, 256), (256, 256), None),
-                                   ((2, 6, 100, 90), (37, 53), None)])
+                                   ((2, 6, 100, 90), (37, 53), None), ((2, 8, 40, 36), None, 0.5),
+                                   ((1, 16, 20, 20), None, 2)])
 def test_resize_bilinear(ctx, shape):
     ishape, size, sf = shape
     x = rnd(*ishape, seed=31).float()
