@@ -275,7 +275,7 @@ __global__ __launch_bounds__(256) void in_apply_v(const float *__restrict__ x, i
         const double mean = s / hw;
         double var = q / hw - mean * mean;
         if (var < 0.0) var = 0.0;
-        const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+        const float rstd = 1.f / sqrtf((float)(var + (double)eps));   // fp64 moments, fp32 root
         const float g = gamma ? 1.f + gamma[(long long)n * gb_ns + cc + j] : 1.f;
         const float b = beta ? beta[(long long)n * gb_ns + cc + j] : 0.f;
         mul[j] = rstd * g;                                   // (x - mean) * rstd * g + b
