@@ -92,15 +92,30 @@ typedef struct s2v_conv_params {
      * is written at y + ((n*out_full_h + oy*out_step)*out_full_w + ox*out_step)*ycs — one parity
      * class of a polyphase transposed conv.  No pix_add; res only in place (res == y). */
     int out_step; int out_full_h, out_full_w;
+    /* arithmetic of the implicit-GEMM kernels (the Cout <= 4 VALU kernels are always fp32):
+     *   S2V_PREC_F32     v_mfma_f32_32x32x2_f32, exact fp32 products (reads ``wt``);
+     *   S2V_PREC_BF16X3  split-fp32 on v_mfma_f32_32x32x16_bf16: a*b ~ ah*bh + ah*bl + al*bh with
+     *                    ah = bf16(a), al = bf16(a - ah); <= 3*2^-16 relative error per product.  Packed
+     *                    weights are read from ``wt_x3`` (s2v_split_weights_x3 layout); a b_kn
+     *                    matrix is split on the fly. */
+    int prec;
+    const void *wt_x3;
 } s2v_conv_params;
+
+enum { S2V_PREC_F32 = 0, S2V_PREC_BF16X3 = 1 };
 
 /* Replaces the nn.Conv2d / ConvTranspose2d / Conv1d / Linear calls of models/LNet.py,
  * ENet.py, DNet.py, base_blocks.py, ffc.py, transformer.py (inventory: SURVEY.md App. A). */
 int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream);
 size_t s2v_conv2d_ws_bytes(const s2v_conv_params *p);
-/* The launch plan s2v_conv2d would use: out6 = {BM, BN, WAVES_M, AVEC, B_KN, splits} of the
- * conv_igemm<BM,BN,WAVES_M,AVEC,B_KN> instance, or {0, CO, 0, 0, 0, 1} for conv_direct_small<CO>. */
-int s2v_conv2d_plan(const s2v_conv_params *p, int *out6);
+/* The launch plan s2v_conv2d would use: out7 = {BM, BN, WAVES_M, AVEC, B_KN, splits, prec} of the
+ * conv_igemm<BM,BN,WAVES_M,AVEC,B_KN> (prec 0) / conv_igemm_x3<...> (prec 1) instance, or
+ * {0, CO, TPP, 0, 0, 1, 0} for conv_small_cpar<CO,TPP> (conv_direct_small<CO> when TPP == 0). */
+int s2v_conv2d_plan(const s2v_conv_params *p, int *out7);
+
+/* Split packed fp32 weights [rows][kpad] (kpad % 32 == 0) into the S2V_PREC_BF16X3 layout
+ * [rows][kpad/32][hi 32 | lo 32] bf16 (same byte size), hi = bf16_rne(w), lo = bf16_rne(w - hi). */
+int s2v_split_weights_x3(const float *w, int rows, int kpad, void *out, s2v_stream_t stream);
 
 /* LayerNorm2d (base_blocks.py:52-69) over (H,W,C) per sample, fused affine + act
  * (+ 2x2 average pool: DownBlock2d base_blocks.py:95-109) (+ residual after act: Jump + out,
@@ -208,6 +223,9 @@ int s2v_irfft2(const float *spec, int n, int h, int w, int c, int scs, const flo
  * out is [batch][npad][kpad]; run the conv with batch = B, n = 1 and w_bs = npad * kpad. */
 int s2v_modulate_weights(const float *wt, int npad, int kpad, int K, int cin, int cout, const float *s, int s_ns,
                          const float *d, int d_ns, int batch, float *out, s2v_stream_t stream);
+/* Same, written in the S2V_PREC_BF16X3 split layout (kpad % 32 == 0): pass ``out`` as wt_x3. */
+int s2v_modulate_weights_x3(const float *wt, int npad, int kpad, int K, int cin, int cout, const float *s, int s_ns,
+                            const float *d, int d_ns, int batch, void *out, s2v_stream_t stream);
 
 /* NHWC FIR resampling with fused epilogue (the engines' form of upfirdn2d, GPEN gpen_model.py:37-91
  * Upsample / Blur and the blur after the transposed modulated conv, :270-276):

@@ -15,274 +15,11 @@
 // ``splitk_reduce`` folds with the same epilogue.
 #include "common.hpp"
 
+#include "conv_impl.hpp"
+
 namespace s2v {
 
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-typedef float f4 __attribute__((ext_vector_type(4)));   // register-native 16-byte vector
-
-struct Epi {
-    const float *scale, *shift, *nc_scale, *pix_add, *res;
-    int nc_ns;
-    float pix_w;
-    int res_cs, res_h, res_w, res_oy, res_ox, res_after, res_simple;
-    int act;
-    float alpha;
-};
-
-struct ConvArgs {
-    const float *x;
-    int n, h, w, cin, xcs;
-    int in_mode, pad_mode, pre_act;
-    float pre_alpha;
-    const float *in_scale;
-    int in_scale_ns;
-    int kh, kw, sh, sw, ph, pw, dh, dw;
-    const float *wt;
-    int kpad, cout, ldb;
-    float *y;
-    int oh, ow, ycs;
-    Epi epi;
-    long long x_bs, w_bs, y_bs, res_bs;
-    int M, K, ktiles, splits, tps;
-    float *ws;
-    int y_step, y_h, y_w;   // strided (polyphase) output, y_step > 1
-};
-
-// Element offset of output row m (flattened n, oy, ox) for channel 0.
-__device__ __forceinline__ long long out_row(const ConvArgs &a, long long m) {
-    if (a.y_step <= 1) return m * a.ycs;
-    const int hw = a.oh * a.ow;
-    const long long img = m / hw;
-    const int rem = (int)(m - img * hw);
-    const int oy = rem / a.ow, ox = rem - (rem / a.ow) * a.ow;
-    return ((img * a.y_h + (long long)oy * a.y_step) * a.y_w + (long long)ox * a.y_step) * a.ycs;
-}
-
-__device__ __forceinline__ void store_epilogue(const ConvArgs &a, int bidx, int m, int n, float v) {
-    const Epi &e = a.epi;
-    const int hw = a.oh * a.ow;
-    int img = 0, oy = 0, ox = 0;
-    if (e.nc_scale || (e.res && !e.res_simple)) {
-        img = m / hw;
-        int rem = m - img * hw;
-        oy = rem / a.ow;
-        ox = rem - oy * a.ow;
-    }
-    if (e.scale) v *= e.scale[n];
-    if (e.nc_scale) v *= e.nc_scale[(long long)img * e.nc_ns + n];
-    if (e.shift) v += e.shift[n];
-    if (e.pix_add) v += e.pix_w * e.pix_add[(long long)bidx * hw * a.n + m];
-    float r = 0.f;
-    if (e.res) {
-        long long off = a.y_step > 1 ? out_row(a, m)     // in-place residual on a strided output
-            : e.res_simple
-            ? (long long)m * e.res_cs
-            : ((long long)(img * e.res_h + oy + e.res_oy) * e.res_w + ox + e.res_ox) * e.res_cs;
-        r = e.res[(long long)bidx * a.res_bs + off + n];
-        if (!e.res_after) v += r;
-    }
-    v = apply_act(v, e.act, e.alpha);
-    if (e.res && e.res_after) v += r;
-    a.y[(long long)bidx * a.y_bs + out_row(a, m) + n] = v;
-}
-
-// Map an output pixel + filter tap to an input pixel; false -> zero padding.
-__device__ __forceinline__ bool map_tap(const ConvArgs &a, int oy, int ox, int ky, int kx, int &iy, int &ix) {
-    if (a.in_mode == S2V_IN_DIRECT) {
-        iy = oy * a.sh - a.ph + ky * a.dh;
-        ix = ox * a.sw - a.pw + kx * a.dw;
-        if (a.pad_mode == S2V_PAD_REFLECT) {
-            iy = reflect_idx(iy, a.h);
-            ix = reflect_idx(ix, a.w);
-            return true;
-        }
-        return (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
-    } else if (a.in_mode == S2V_IN_NEAREST_UP2) {
-        int uy = oy * a.sh - a.ph + ky * a.dh;
-        int ux = ox * a.sw - a.pw + kx * a.dw;
-        if ((unsigned)uy >= (unsigned)(2 * a.h) || (unsigned)ux >= (unsigned)(2 * a.w)) return false;
-        iy = uy >> 1;
-        ix = ux >> 1;
-        return true;
-    } else {  // transposed
-        int ty = oy + a.ph - ky * a.dh;
-        int tx = ox + a.pw - kx * a.dw;
-        if (ty < 0 || tx < 0) return false;
-        iy = ty / a.sh;
-        ix = tx / a.sw;
-        return iy * a.sh == ty && ix * a.sw == tx && iy < a.h && ix < a.w;
-    }
-}
-
-__device__ __forceinline__ float prologue(const ConvArgs &a, float v, int img, int c) {
-    if (a.in_scale) v *= a.in_scale[(long long)img * a.in_scale_ns + c];
-    if (a.pre_act) v = apply_act(v, a.pre_act, a.pre_alpha);
-    return v;
-}
-
-// Branch-light activation for the epilogue hot path: NONE / RELU / LRELU are one select; the
-// transcendental ones go through an out-of-line call so 64 unrolled copies stay small.
-__device__ __noinline__ float act_complex(float v, int act) { return apply_act(v, act, 0.f); }
-
-__device__ __forceinline__ float fast_act(float v, int act, float slope) {
-    if (act > S2V_ACT_LRELU) return act_complex(v, act);
-    return v >= 0.f ? v : v * slope;
-}
-
-// A operand loaders.  AMODE 0: direct conv, zero padding, no prologue, cin % 32 == 0 (a whole
-// K-slice lies in one filter tap: the tap offset is tile-uniform).  AMODE 1: any input mode,
-// cin % 4 == 0 (one tap per float4).  AMODE 2: anything (scalar gather).
-template <int AR, int AMODE>
-struct ARows {
-    long long base[AR];  // AMODE 0: element offset of (img, iy0, ix0) (may point outside the image)
-    int iy0[AR], ix0[AR];
-    int img[AR], oy[AR], ox[AR];
-    bool ok[AR];
-};
-
-template <int AR, int AMODE>
-__device__ __forceinline__ void a_rows_init(const ConvArgs &a, int m0, int ar, ARows<AR, AMODE> &R) {
-    const int hw = a.oh * a.ow;
-#pragma unroll
-    for (int j = 0; j < AR; ++j) {
-        const int m = m0 + ar + 32 * j;
-        R.ok[j] = m < a.M;
-        const int mm = R.ok[j] ? m : 0;
-        const int img = mm / hw;
-        const int rem = mm - img * hw;
-        const int oy = rem / a.ow;
-        const int ox = rem - oy * a.ow;
-        R.img[j] = img;
-        R.oy[j] = oy;
-        R.ox[j] = ox;
-        R.iy0[j] = oy * a.sh - a.ph;
-        R.ix0[j] = ox * a.sw - a.pw;
-        R.base[j] = AMODE == 3 ? (long long)img * a.h * a.w * a.xcs
-                               : ((long long)(img * a.h + R.iy0[j]) * a.w + R.ix0[j]) * a.xcs;
-    }
-}
-
-template <int AR, int AMODE>
-__device__ __forceinline__ void load_a(const ConvArgs &a, const float *__restrict__ x, int kt, int ak,
-                                       const ARows<AR, AMODE> &R, f4 (&ra)[AR]) {
-    const int kbase = kt * 32;
-    if (AMODE == 0 || AMODE == 3) {
-        // tile-uniform tap (scalar math); AMODE 3 reflects out-of-range rows/cols (FFC, ffc.py:196-204)
-        const int tap = kbase / a.cin;
-        const int c = kbase - tap * a.cin + ak;
-        const int ky = tap / a.kw, kx = tap - (tap / a.kw) * a.kw;
-        const int dy = ky * a.dh, dx = kx * a.dw;
-        const long long toff = ((long long)dy * a.w + dx) * a.xcs + c;
-        if (AMODE == 0) {
-#pragma unroll
-            for (int j = 0; j < AR; ++j) {
-                const bool ok = R.ok[j] && (unsigned)(R.iy0[j] + dy) < (unsigned)a.h &&
-                                (unsigned)(R.ix0[j] + dx) < (unsigned)a.w;
-                f4 v = {0.f, 0.f, 0.f, 0.f};
-                if (ok) v = *(const f4 *)(x + R.base[j] + toff);
-                ra[j] = v;
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < AR; ++j) {
-                const int iy = reflect_idx(R.iy0[j] + dy, a.h), ix = reflect_idx(R.ix0[j] + dx, a.w);
-                f4 v = {0.f, 0.f, 0.f, 0.f};
-                if (R.ok[j]) v = *(const f4 *)(x + R.base[j] + ((long long)iy * a.w + ix) * a.xcs + c);
-                ra[j] = v;
-            }
-        }
-        if (a.in_scale) {   // StyleGAN2 input modulation s[n, c] (zero padding stays zero)
-#pragma unroll
-            for (int j = 0; j < AR; ++j)
-                ra[j] *= *(const f4 *)(a.in_scale + (long long)R.img[j] * a.in_scale_ns + c);
-        }
-        if (a.pre_act) {
-            const float sl = a.pre_act == S2V_ACT_RELU ? 0.f : a.pre_alpha;
-#pragma unroll
-            for (int j = 0; j < AR; ++j) {
-                ra[j].x = ra[j].x >= 0.f ? ra[j].x : ra[j].x * sl;
-                ra[j].y = ra[j].y >= 0.f ? ra[j].y : ra[j].y * sl;
-                ra[j].z = ra[j].z >= 0.f ? ra[j].z : ra[j].z * sl;
-                ra[j].w = ra[j].w >= 0.f ? ra[j].w : ra[j].w * sl;
-            }
-        }
-    } else if (AMODE == 1) {
-        const int k = kbase + ak;
-        const bool kok = k < a.K;
-        const int tap = k / a.cin;
-        const int c = k - tap * a.cin;
-        const int ky = tap / a.kw, kx = tap - (tap / a.kw) * a.kw;
-#pragma unroll
-        for (int j = 0; j < AR; ++j) {
-            f4 v = {0.f, 0.f, 0.f, 0.f};
-            int iy, ix;
-            if (R.ok[j] && kok && map_tap(a, R.oy[j], R.ox[j], ky, kx, iy, ix)) {
-                v = *(const f4 *)(x + ((long long)(R.img[j] * a.h + iy) * a.w + ix) * a.xcs + c);
-                if (a.in_scale || a.pre_act) {
-                    v.x = prologue(a, v.x, R.img[j], c);
-                    v.y = prologue(a, v.y, R.img[j], c + 1);
-                    v.z = prologue(a, v.z, R.img[j], c + 2);
-                    v.w = prologue(a, v.w, R.img[j], c + 3);
-                }
-            }
-            ra[j] = v;
-        }
-    } else {
-#pragma unroll
-        for (int j = 0; j < AR; ++j) {
-            float vv[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int k = kbase + ak + e;
-                float v = 0.f;
-                if (R.ok[j] && k < a.K) {
-                    const int tap = k / a.cin;
-                    const int c = k - tap * a.cin;
-                    const int ky = tap / a.kw, kx = tap - (tap / a.kw) * a.kw;
-                    int iy, ix;
-                    if (map_tap(a, R.oy[j], R.ox[j], ky, kx, iy, ix)) {
-                        v = x[((long long)(R.img[j] * a.h + iy) * a.w + ix) * a.xcs + c];
-                        v = prologue(a, v, R.img[j], c);
-                    }
-                }
-                vv[e] = v;
-            }
-            ra[j] = f4{vv[0], vv[1], vv[2], vv[3]};
-        }
-    }
-}
-
-template <int BN, int BR, int BKN>
-__device__ __forceinline__ void load_b(const ConvArgs &a, const float *__restrict__ wt, int kt, int n0, int tid,
-                                       f4 (&rb)[BR]) {
-    const int kbase = kt * 32;
-    if (!BKN) {
-        const int ar = tid >> 3, ak = (tid & 7) * 4;
-        const float *p = wt + (long long)(n0 + ar) * a.kpad + kbase + ak;
-#pragma unroll
-        for (int j = 0; j < BR; ++j) rb[j] = *(const f4 *)(p + (long long)32 * j * a.kpad);
-    } else {
-        constexpr int NV = BN / 4, RPP = 256 / NV;
-        const int kr = tid / NV, nn = (tid - (tid / NV) * NV) * 4;
-#pragma unroll
-        for (int j = 0; j < BR; ++j) {
-            const int k = kbase + kr + RPP * j;
-            const int n = n0 + nn;
-            f4 v = {0.f, 0.f, 0.f, 0.f};
-            if (k < a.K) {
-                const float *src = wt + (long long)k * a.ldb + n;
-                if (n + 3 < a.cout) {
-                    v = *(const f4 *)src;
-                } else {
-                    if (n < a.cout) v.x = src[0];
-                    if (n + 1 < a.cout) v.y = src[1];
-                    if (n + 2 < a.cout) v.z = src[2];
-                }
-            }
-            rb[j] = v;
-        }
-    }
-}
+void launch_conv_x3(int tile, const ConvArgs &a, int amode, bool bkn, dim3 grid, hipStream_t s);   // conv_x3.hip
 
 template <int BM, int BN, int AR, int BR, int BKN>
 __device__ __forceinline__ void store_ab(float *As, float *Bs, int tid, const f4 (&ra)[AR],
@@ -410,57 +147,9 @@ __global__ __launch_bounds__(256, 1) void conv_igemm(ConvArgs a) {
         buf ^= 1;
     }
 
-    // ---- epilogue.  The lane owns column li of each 32x32 tile, rows (r&3) + 8(r>>2) + 4 lh:
-    // stage the tile through LDS with static indices, then every thread walks the tile row by
-    // row (consecutive threads -> consecutive output channels: coalesced stores).
-    constexpr int LDC = BN + 4;
-    static_assert(BM * LDC <= 2 * STAGE, "C tile must fit in the staging LDS");
-    float *Cs = smem;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-                Cs[(wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * LDC + wn * WTN + j * 32 + li] = acc[i][j][r];
-    __syncthreads();
-    const Epi &e = a.epi;
-    constexpr int TPR = BN < 256 ? BN : 256;   // threads per tile row
-    constexpr int RSTEP = 256 / TPR;
-    const int cn = tid % TPR;
-    const int n = n0 + cn;
-    if (n >= a.cout) return;
-    const int mlim = min(BM, a.M - m0);
-    if (a.splits > 1) {
-        float *w = a.ws + (long long)bz * a.M * a.cout;
-#pragma unroll 1
-        for (int rr = tid / TPR; rr < mlim; rr += RSTEP) w[(long long)(m0 + rr) * a.cout + n] = Cs[rr * LDC + cn];
-        return;
-    }
-    const bool simple = !e.nc_scale && !e.pix_add && (!e.res || e.res_simple);
-    if (simple) {
-        const float sc = e.scale ? e.scale[n] : 1.f;
-        const float sh = e.shift ? e.shift[n] : 0.f;
-        const float slope = e.act == S2V_ACT_RELU ? 0.f : (e.act == S2V_ACT_LRELU ? e.alpha : 1.f);
-        float *__restrict__ yb = a.y + (long long)bidx * a.y_bs + n;
-        const float *rsrc = e.res ? e.res + (long long)bidx * a.res_bs + n : nullptr;
-#pragma unroll 1
-        for (int rr = tid / TPR; rr < mlim; rr += RSTEP) {
-            const long long m = m0 + rr;
-            float v = Cs[rr * LDC + cn] * sc + sh;
-            float rv = 0.f;
-            if (rsrc) {
-                rv = rsrc[a.y_step > 1 ? out_row(a, m) : m * e.res_cs];
-                if (!e.res_after) v += rv;
-            }
-            v = fast_act(v, e.act, slope);
-            if (rsrc && e.res_after) v += rv;
-            yb[out_row(a, m)] = v;
-        }
-    } else {
-#pragma unroll 1
-        for (int rr = tid / TPR; rr < mlim; rr += RSTEP) store_epilogue(a, bidx, m0 + rr, n, Cs[rr * LDC + cn]);
-    }
+    // ---- epilogue (shared with the split-bf16 kernel, conv_impl.hpp)
+    static_assert(BM * (BN + 4) <= 2 * STAGE, "C tile must fit in the staging LDS");
+    epilogue_tile<BM, BN, WAVES_M, TM, TN>(a, acc, smem, tid, m0, n0, bz, bidx);
 }
 
 __global__ void splitk_reduce(ConvArgs a, int batch) {
@@ -628,6 +317,14 @@ struct Plan {
 
 static bool use_direct(const s2v_conv_params *p) { return p->cout <= 4 && !p->b_kn; }
 
+// the split-bf16 kernel reads the pre-split packed weights; b_kn matrices are split on the fly
+static bool uses_x3(const s2v_conv_params *p) {
+    return p->prec == S2V_PREC_BF16X3 && !(use_direct(p) && !p->force_tile) && !p->b_kn;
+}
+static bool tiled_x3(const s2v_conv_params *p) {
+    return p->prec == S2V_PREC_BF16X3 && !(use_direct(p) && !p->force_tile);
+}
+
 static Plan make_plan(const s2v_conv_params *p, int M, int K) {
     Plan pl{};
     pl.ktiles = (K + 31) / 32;
@@ -678,7 +375,12 @@ static Plan make_plan(const s2v_conv_params *p, int M, int K) {
 }
 
 static int validate(const s2v_conv_params *p, int &M, int &K) {
-    S2V_REQUIRE(p && p->x && p->wt && p->y, "conv2d: null pointer");
+    S2V_REQUIRE(p && p->x && p->y, "conv2d: null pointer");
+    S2V_REQUIRE(p->prec == S2V_PREC_F32 || p->prec == S2V_PREC_BF16X3, "conv2d: bad prec %d", p->prec);
+    if (uses_x3(p))
+        S2V_REQUIRE(p->wt_x3 && ((uintptr_t)p->wt_x3 % 16) == 0, "conv2d: prec BF16X3 needs 16B-aligned wt_x3");
+    else
+        S2V_REQUIRE(p->wt != nullptr, "conv2d: null weights");
     S2V_REQUIRE(p->n > 0 && p->h > 0 && p->w > 0 && p->cin > 0 && p->cout > 0 && p->oh > 0 && p->ow > 0,
                 "conv2d: bad shape n=%d h=%d w=%d cin=%d cout=%d oh=%d ow=%d", p->n, p->h, p->w, p->cin,
                 p->cout, p->oh, p->ow);
@@ -700,7 +402,7 @@ static int validate(const s2v_conv_params *p, int &M, int &K) {
     } else {
         S2V_REQUIRE(p->kpad >= k && p->kpad % 32 == 0, "conv2d: kpad=%d must be >= K=%lld and %%32", p->kpad, k);
         S2V_REQUIRE(p->npad >= p->cout && p->npad % 128 == 0, "conv2d: npad=%d must be >= cout and %%128", p->npad);
-        S2V_REQUIRE(((uintptr_t)p->wt % 16) == 0, "conv2d: weights must be 16B aligned");
+        S2V_REQUIRE(uses_x3(p) || ((uintptr_t)p->wt % 16) == 0, "conv2d: weights must be 16B aligned");
     }
     if (p->res) S2V_REQUIRE(p->res_cs >= p->cout, "conv2d: res_cs < cout");
     if (p->out_step > 1) {
@@ -774,6 +476,7 @@ extern "C" size_t s2v_conv2d_ws_bytes(const s2v_conv_params *p) {
 }
 
 extern "C" int s2v_conv2d_plan(const s2v_conv_params *p, int *out6) {
+    out6[6] = 0;
     int M, K;
     int rc = validate(p, M, K);
     if (rc) return rc;
@@ -793,6 +496,7 @@ extern "C" int s2v_conv2d_plan(const s2v_conv_params *p, int *out6) {
     out6[3] = a_mode(p);
     out6[4] = p->b_kn != 0;
     out6[5] = pl.splits;
+    out6[6] = tiled_x3(p) ? 1 : 0;
     return 0;
 }
 
@@ -829,7 +533,10 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
     const bool bkn = p->b_kn != 0;
     const TileCfg &t = kTiles[pl.tile];
     dim3 grid(cdiv(M, t.bm), cdiv(p->cout, t.bn), batch * pl.splits);
-    switch (pl.tile) {
+    if (tiled_x3(p)) {
+        if (!bkn) a.wt = (const float *)p->wt_x3;
+        launch_conv_x3(pl.tile, a, amode, bkn, grid, s);
+    } else switch (pl.tile) {
         case 0: launch_tile<128, 128, 2>(a, amode, bkn, grid, s); break;
         case 1: launch_tile<128, 64, 2>(a, amode, bkn, grid, s); break;
         case 2: launch_tile<64, 128, 2>(a, amode, bkn, grid, s); break;

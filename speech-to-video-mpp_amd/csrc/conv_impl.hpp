@@ -1,0 +1,337 @@
+// Device-side pieces shared by the fp32 (conv.hip) and split-bf16 (conv_x3.hip) implicit-GEMM
+// convolutions: argument block, epilogue, tap mapping and the A/B operand gather loaders.
+#pragma once
+#include "common.hpp"
+
+namespace s2v {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float f4 __attribute__((ext_vector_type(4)));   // register-native 16-byte vector
+
+struct Epi {
+    const float *scale, *shift, *nc_scale, *pix_add, *res;
+    int nc_ns;
+    float pix_w;
+    int res_cs, res_h, res_w, res_oy, res_ox, res_after, res_simple;
+    int act;
+    float alpha;
+};
+
+struct ConvArgs {
+    const float *x;
+    int n, h, w, cin, xcs;
+    int in_mode, pad_mode, pre_act;
+    float pre_alpha;
+    const float *in_scale;
+    int in_scale_ns;
+    int kh, kw, sh, sw, ph, pw, dh, dw;
+    const float *wt;
+    int kpad, cout, ldb;
+    float *y;
+    int oh, ow, ycs;
+    Epi epi;
+    long long x_bs, w_bs, y_bs, res_bs;
+    int M, K, ktiles, splits, tps;
+    float *ws;
+    int y_step, y_h, y_w;   // strided (polyphase) output, y_step > 1
+};
+
+// Element offset of output row m (flattened n, oy, ox) for channel 0.
+__device__ __forceinline__ long long out_row(const ConvArgs &a, long long m) {
+    if (a.y_step <= 1) return m * a.ycs;
+    const int hw = a.oh * a.ow;
+    const long long img = m / hw;
+    const int rem = (int)(m - img * hw);
+    const int oy = rem / a.ow, ox = rem - (rem / a.ow) * a.ow;
+    return ((img * a.y_h + (long long)oy * a.y_step) * a.y_w + (long long)ox * a.y_step) * a.ycs;
+}
+
+__device__ __forceinline__ void store_epilogue(const ConvArgs &a, int bidx, int m, int n, float v) {
+    const Epi &e = a.epi;
+    const int hw = a.oh * a.ow;
+    int img = 0, oy = 0, ox = 0;
+    if (e.nc_scale || (e.res && !e.res_simple)) {
+        img = m / hw;
+        int rem = m - img * hw;
+        oy = rem / a.ow;
+        ox = rem - oy * a.ow;
+    }
+    if (e.scale) v *= e.scale[n];
+    if (e.nc_scale) v *= e.nc_scale[(long long)img * e.nc_ns + n];
+    if (e.shift) v += e.shift[n];
+    if (e.pix_add) v += e.pix_w * e.pix_add[(long long)bidx * hw * a.n + m];
+    float r = 0.f;
+    if (e.res) {
+        long long off = a.y_step > 1 ? out_row(a, m)     // in-place residual on a strided output
+            : e.res_simple
+            ? (long long)m * e.res_cs
+            : ((long long)(img * e.res_h + oy + e.res_oy) * e.res_w + ox + e.res_ox) * e.res_cs;
+        r = e.res[(long long)bidx * a.res_bs + off + n];
+        if (!e.res_after) v += r;
+    }
+    v = apply_act(v, e.act, e.alpha);
+    if (e.res && e.res_after) v += r;
+    a.y[(long long)bidx * a.y_bs + out_row(a, m) + n] = v;
+}
+
+// Map an output pixel + filter tap to an input pixel; false -> zero padding.
+__device__ __forceinline__ bool map_tap(const ConvArgs &a, int oy, int ox, int ky, int kx, int &iy, int &ix) {
+    if (a.in_mode == S2V_IN_DIRECT) {
+        iy = oy * a.sh - a.ph + ky * a.dh;
+        ix = ox * a.sw - a.pw + kx * a.dw;
+        if (a.pad_mode == S2V_PAD_REFLECT) {
+            iy = reflect_idx(iy, a.h);
+            ix = reflect_idx(ix, a.w);
+            return true;
+        }
+        return (unsigned)iy < (unsigned)a.h && (unsigned)ix < (unsigned)a.w;
+    } else if (a.in_mode == S2V_IN_NEAREST_UP2) {
+        int uy = oy * a.sh - a.ph + ky * a.dh;
+        int ux = ox * a.sw - a.pw + kx * a.dw;
+        if ((unsigned)uy >= (unsigned)(2 * a.h) || (unsigned)ux >= (unsigned)(2 * a.w)) return false;
+        iy = uy >> 1;
+        ix = ux >> 1;
+        return true;
+    } else {  // transposed
+        int ty = oy + a.ph - ky * a.dh;
+        int tx = ox + a.pw - kx * a.dw;
+        if (ty < 0 || tx < 0) return false;
+        iy = ty / a.sh;
+        ix = tx / a.sw;
+        return iy * a.sh == ty && ix * a.sw == tx && iy < a.h && ix < a.w;
+    }
+}
+
+__device__ __forceinline__ float prologue(const ConvArgs &a, float v, int img, int c) {
+    if (a.in_scale) v *= a.in_scale[(long long)img * a.in_scale_ns + c];
+    if (a.pre_act) v = apply_act(v, a.pre_act, a.pre_alpha);
+    return v;
+}
+
+// Branch-light activation for the epilogue hot path: NONE / RELU / LRELU are one select; the
+// transcendental ones go through an out-of-line call so 64 unrolled copies stay small.
+static __device__ __noinline__ float act_complex(float v, int act) { return apply_act(v, act, 0.f); }
+
+__device__ __forceinline__ float fast_act(float v, int act, float slope) {
+    if (act > S2V_ACT_LRELU) return act_complex(v, act);
+    return v >= 0.f ? v : v * slope;
+}
+
+// A operand loaders.  AMODE 0: direct conv, zero padding, no prologue, cin % 32 == 0 (a whole
+// K-slice lies in one filter tap: the tap offset is tile-uniform).  AMODE 1: any input mode,
+// cin % 4 == 0 (one tap per float4).  AMODE 2: anything (scalar gather).
+template <int AR, int AMODE>
+struct ARows {
+    long long base[AR];  // AMODE 0: element offset of (img, iy0, ix0) (may point outside the image)
+    int iy0[AR], ix0[AR];
+    int img[AR], oy[AR], ox[AR];
+    bool ok[AR];
+};
+
+template <int AR, int AMODE>
+__device__ __forceinline__ void a_rows_init(const ConvArgs &a, int m0, int ar, ARows<AR, AMODE> &R) {
+    const int hw = a.oh * a.ow;
+#pragma unroll
+    for (int j = 0; j < AR; ++j) {
+        const int m = m0 + ar + 32 * j;
+        R.ok[j] = m < a.M;
+        const int mm = R.ok[j] ? m : 0;
+        const int img = mm / hw;
+        const int rem = mm - img * hw;
+        const int oy = rem / a.ow;
+        const int ox = rem - oy * a.ow;
+        R.img[j] = img;
+        R.oy[j] = oy;
+        R.ox[j] = ox;
+        R.iy0[j] = oy * a.sh - a.ph;
+        R.ix0[j] = ox * a.sw - a.pw;
+        R.base[j] = AMODE == 3 ? (long long)img * a.h * a.w * a.xcs
+                               : ((long long)(img * a.h + R.iy0[j]) * a.w + R.ix0[j]) * a.xcs;
+    }
+}
+
+template <int AR, int AMODE>
+__device__ __forceinline__ void load_a(const ConvArgs &a, const float *__restrict__ x, int kt, int ak,
+                                       const ARows<AR, AMODE> &R, f4 (&ra)[AR]) {
+    const int kbase = kt * 32;
+    if (AMODE == 0 || AMODE == 3) {
+        // tile-uniform tap (scalar math); AMODE 3 reflects out-of-range rows/cols (FFC, ffc.py:196-204)
+        const int tap = kbase / a.cin;
+        const int c = kbase - tap * a.cin + ak;
+        const int ky = tap / a.kw, kx = tap - (tap / a.kw) * a.kw;
+        const int dy = ky * a.dh, dx = kx * a.dw;
+        const long long toff = ((long long)dy * a.w + dx) * a.xcs + c;
+        if (AMODE == 0) {
+#pragma unroll
+            for (int j = 0; j < AR; ++j) {
+                const bool ok = R.ok[j] && (unsigned)(R.iy0[j] + dy) < (unsigned)a.h &&
+                                (unsigned)(R.ix0[j] + dx) < (unsigned)a.w;
+                f4 v = {0.f, 0.f, 0.f, 0.f};
+                if (ok) v = *(const f4 *)(x + R.base[j] + toff);
+                ra[j] = v;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < AR; ++j) {
+                const int iy = reflect_idx(R.iy0[j] + dy, a.h), ix = reflect_idx(R.ix0[j] + dx, a.w);
+                f4 v = {0.f, 0.f, 0.f, 0.f};
+                if (R.ok[j]) v = *(const f4 *)(x + R.base[j] + ((long long)iy * a.w + ix) * a.xcs + c);
+                ra[j] = v;
+            }
+        }
+        if (a.in_scale) {   // StyleGAN2 input modulation s[n, c] (zero padding stays zero)
+#pragma unroll
+            for (int j = 0; j < AR; ++j)
+                ra[j] *= *(const f4 *)(a.in_scale + (long long)R.img[j] * a.in_scale_ns + c);
+        }
+        if (a.pre_act) {
+            const float sl = a.pre_act == S2V_ACT_RELU ? 0.f : a.pre_alpha;
+#pragma unroll
+            for (int j = 0; j < AR; ++j) {
+                ra[j].x = ra[j].x >= 0.f ? ra[j].x : ra[j].x * sl;
+                ra[j].y = ra[j].y >= 0.f ? ra[j].y : ra[j].y * sl;
+                ra[j].z = ra[j].z >= 0.f ? ra[j].z : ra[j].z * sl;
+                ra[j].w = ra[j].w >= 0.f ? ra[j].w : ra[j].w * sl;
+            }
+        }
+    } else if (AMODE == 1) {
+        const int k = kbase + ak;
+        const bool kok = k < a.K;
+        const int tap = k / a.cin;
+        const int c = k - tap * a.cin;
+        const int ky = tap / a.kw, kx = tap - (tap / a.kw) * a.kw;
+#pragma unroll
+        for (int j = 0; j < AR; ++j) {
+            f4 v = {0.f, 0.f, 0.f, 0.f};
+            int iy, ix;
+            if (R.ok[j] && kok && map_tap(a, R.oy[j], R.ox[j], ky, kx, iy, ix)) {
+                v = *(const f4 *)(x + ((long long)(R.img[j] * a.h + iy) * a.w + ix) * a.xcs + c);
+                if (a.in_scale || a.pre_act) {
+                    v.x = prologue(a, v.x, R.img[j], c);
+                    v.y = prologue(a, v.y, R.img[j], c + 1);
+                    v.z = prologue(a, v.z, R.img[j], c + 2);
+                    v.w = prologue(a, v.w, R.img[j], c + 3);
+                }
+            }
+            ra[j] = v;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < AR; ++j) {
+            float vv[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int k = kbase + ak + e;
+                float v = 0.f;
+                if (R.ok[j] && k < a.K) {
+                    const int tap = k / a.cin;
+                    const int c = k - tap * a.cin;
+                    const int ky = tap / a.kw, kx = tap - (tap / a.kw) * a.kw;
+                    int iy, ix;
+                    if (map_tap(a, R.oy[j], R.ox[j], ky, kx, iy, ix)) {
+                        v = x[((long long)(R.img[j] * a.h + iy) * a.w + ix) * a.xcs + c];
+                        v = prologue(a, v, R.img[j], c);
+                    }
+                }
+                vv[e] = v;
+            }
+            ra[j] = f4{vv[0], vv[1], vv[2], vv[3]};
+        }
+    }
+}
+
+template <int BN, int BR, int BKN>
+__device__ __forceinline__ void load_b(const ConvArgs &a, const float *__restrict__ wt, int kt, int n0, int tid,
+                                       f4 (&rb)[BR]) {
+    const int kbase = kt * 32;
+    if (!BKN) {
+        const int ar = tid >> 3, ak = (tid & 7) * 4;
+        const float *p = wt + (long long)(n0 + ar) * a.kpad + kbase + ak;
+#pragma unroll
+        for (int j = 0; j < BR; ++j) rb[j] = *(const f4 *)(p + (long long)32 * j * a.kpad);
+    } else {
+        constexpr int NV = BN / 4, RPP = 256 / NV;
+        const int kr = tid / NV, nn = (tid - (tid / NV) * NV) * 4;
+#pragma unroll
+        for (int j = 0; j < BR; ++j) {
+            const int k = kbase + kr + RPP * j;
+            const int n = n0 + nn;
+            f4 v = {0.f, 0.f, 0.f, 0.f};
+            if (k < a.K) {
+                const float *src = wt + (long long)k * a.ldb + n;
+                if (n + 3 < a.cout) {
+                    v = *(const f4 *)src;
+                } else {
+                    if (n < a.cout) v.x = src[0];
+                    if (n + 1 < a.cout) v.y = src[1];
+                    if (n + 2 < a.cout) v.z = src[2];
+                }
+            }
+            rb[j] = v;
+        }
+    }
+}
+
+// Epilogue of one BM x BN output tile held as 32x32 MFMA accumulators (C/D map: lane owns column
+// li of each tile, rows (r&3) + 8(r>>2) + 4 lh).  The tile is staged through LDS (``Cs``, at least
+// BM*(BN+4) floats) with static indices, then every thread walks it row by row (consecutive
+// threads -> consecutive output channels: coalesced stores).  Split-K launches write raw partial
+// sums to the workspace instead.
+template <int BM, int BN, int WAVES_M, int TM, int TN>
+__device__ __forceinline__ void epilogue_tile(const ConvArgs &a, const floatx16 (&acc)[TM][TN], float *Cs, int tid,
+                                              int m0, int n0, int bz, int bidx) {
+    constexpr int WAVES_N = 4 / WAVES_M;
+    constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
+    constexpr int LDC = BN + 4;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+    const int li = lane & 31, lh = lane >> 5;
+    __syncthreads();   // every wave is done reading the operand stages that Cs overlays
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                Cs[(wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * LDC + wn * WTN + j * 32 + li] = acc[i][j][r];
+    __syncthreads();
+    const Epi &e = a.epi;
+    constexpr int TPR = BN < 256 ? BN : 256;   // threads per tile row
+    constexpr int RSTEP = 256 / TPR;
+    const int cn = tid % TPR;
+    const int n = n0 + cn;
+    if (n >= a.cout) return;
+    const int mlim = min(BM, a.M - m0);
+    if (a.splits > 1) {
+        float *w = a.ws + (long long)bz * a.M * a.cout;
+#pragma unroll 1
+        for (int rr = tid / TPR; rr < mlim; rr += RSTEP) w[(long long)(m0 + rr) * a.cout + n] = Cs[rr * LDC + cn];
+        return;
+    }
+    const bool simple = !e.nc_scale && !e.pix_add && (!e.res || e.res_simple);
+    if (simple) {
+        const float sc = e.scale ? e.scale[n] : 1.f;
+        const float sh = e.shift ? e.shift[n] : 0.f;
+        const float slope = e.act == S2V_ACT_RELU ? 0.f : (e.act == S2V_ACT_LRELU ? e.alpha : 1.f);
+        float *__restrict__ yb = a.y + (long long)bidx * a.y_bs + n;
+        const float *rsrc = e.res ? e.res + (long long)bidx * a.res_bs + n : nullptr;
+#pragma unroll 1
+        for (int rr = tid / TPR; rr < mlim; rr += RSTEP) {
+            const long long m = m0 + rr;
+            float v = Cs[rr * LDC + cn] * sc + sh;
+            float rv = 0.f;
+            if (rsrc) {
+                rv = rsrc[a.y_step > 1 ? out_row(a, m) : m * e.res_cs];
+                if (!e.res_after) v += rv;
+            }
+            v = fast_act(v, e.act, slope);
+            if (rsrc && e.res_after) v += rv;
+            yb[out_row(a, m)] = v;
+        }
+    } else {
+#pragma unroll 1
+        for (int rr = tid / TPR; rr < mlim; rr += RSTEP) store_epilogue(a, bidx, m0 + rr, n, Cs[rr * LDC + cn]);
+    }
+}
+
+}  // namespace s2v

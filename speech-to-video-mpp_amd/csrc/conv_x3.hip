@@ -1,0 +1,308 @@
+// Implicit-GEMM convolution on gfx950 bf16 MFMA with split-fp32 operands ("bf16x3").
+//
+// Every fp32 operand v is carried as two bf16 halves, hi = bf16(v) and lo = bf16(v - hi) (RNE both:
+// |v - hi - lo| <= 2^-16 |v|, i.e. 16 significant bits), and a product as hi*hi + hi*lo + lo*hi
+// (the dropped lo*lo term is <= 2^-16 |a*b|), accumulated in fp32 by v_mfma_f32_32x32x16_bf16
+// (bf16 x bf16 products are exact in fp32).  Worst case 3 * 2^-16 relative per product, typically
+// ~1e-5: 32x tighter per operand than TF32 (10 explicit mantissa bits), the arithmetic cuDNN uses
+// for these fp32 convolutions by default on the reference's own GPU path.  Measured model-level
+// error vs the reference CPU goldens: DESIGN.md §3.  Three bf16 MFMAs cost 96 cycles per 32x32x16
+// block against 512 for eight v_mfma_f32_32x32x2_f32.
+//
+// Same GEMM view, gather loaders, K-slice order, XCD-aware tile order and epilogue as the fp32
+// kernel (conv.hip / conv_impl.hpp).  Differences:
+//   * B (packed weights) is pre-split on the host side into [npad][kpad/32][hi 32 | lo 32] bf16
+//     (s2v_split_weights_x3 / s2v_modulate_weights_x3: same bytes as fp32), so a 128-byte weight
+//     row slice lands in LDS unchanged;
+//   * A is split in registers after its global load, while the MFMAs of the previous slice run;
+//   * LDS rows are 128 B (eight 16-byte slots: hi k0-7, k8-15, k16-23, k24-31, then lo), slot s of
+//     row r stored at s ^ ((r >> 1) & 7): the 16 rows of each ds_read_b128 lane group hit 16
+//     distinct slots of the 256-byte bank row (conflict-free operand reads).
+#include "conv_impl.hpp"
+
+namespace s2v {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ unsigned pack_bf16(float a, float b) {
+    bf16x2 v = {(__bf16)a, (__bf16)b};   // v_cvt_pk_bf16_f32 (round to nearest even)
+    return __builtin_bit_cast(unsigned, v);
+}
+
+// 4 fp32 -> 4 bf16 hi (8 bytes) + 4 bf16 lo (8 bytes)
+__device__ __forceinline__ void split4(const f4 &v, u32x2 &hi, u32x2 &lo) {
+    hi.x = pack_bf16(v.x, v.y);
+    hi.y = pack_bf16(v.z, v.w);
+    const float h0 = __uint_as_float(hi.x << 16), h1 = __uint_as_float(hi.x & 0xffff0000u);
+    const float h2 = __uint_as_float(hi.y << 16), h3 = __uint_as_float(hi.y & 0xffff0000u);
+    lo.x = pack_bf16(v.x - h0, v.y - h1);
+    lo.y = pack_bf16(v.z - h2, v.w - h3);
+}
+
+__device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
+
+// byte offset of 16-byte slot ``slot`` (0..7) of LDS row ``row``
+__device__ __forceinline__ int slot_off(int row, int slot) { return row * 128 + ((slot ^ swz(row)) << 4); }
+
+template <int BM, int AR>
+__device__ __forceinline__ void store_a_x3(char *As, int tid, const f4 (&ra)[AR]) {
+    const int ar = tid >> 3, q = tid & 7;          // 4 k-values: slot q>>1, bytes (q&1)*8
+#pragma unroll
+    for (int j = 0; j < AR; ++j) {
+        const int row = ar + 32 * j;
+        u32x2 hi, lo;
+        split4(ra[j], hi, lo);
+        const int off = slot_off(row, q >> 1) + (q & 1) * 8;
+        *(u32x2 *)(As + off) = hi;
+        *(u32x2 *)(As + (off ^ 64)) = lo;          // slot ^ 4 == the lo slot (slot < 4)
+    }
+}
+
+// pre-split packed weights: thread loads 16 bytes (one slot) of rows br + 32 j
+template <int BR>
+__device__ __forceinline__ void load_b_x3(const ConvArgs &a, const char *__restrict__ wt, int kt, int n0, int tid,
+                                          u32x4 (&rb)[BR]) {
+    const int br = tid >> 3, sl = tid & 7;
+    const char *p = wt + ((long long)(n0 + br) * a.kpad + kt * 32) * 4 + sl * 16;
+#pragma unroll
+    for (int j = 0; j < BR; ++j) rb[j] = *(const u32x4 *)(p + (long long)32 * j * a.kpad * 4);
+}
+
+template <int BR>
+__device__ __forceinline__ void store_b_x3(char *Bs, int tid, const u32x4 (&rb)[BR]) {
+    const int br = tid >> 3, sl = tid & 7;
+#pragma unroll
+    for (int j = 0; j < BR; ++j) *(u32x4 *)(Bs + slot_off(br + 32 * j, sl)) = rb[j];
+}
+
+// activation B ([K][ldb] fp32, b_kn): split on the fly, scattered 2-byte stores (small GEMMs only)
+template <int BN, int BR>
+__device__ __forceinline__ void store_b_kn_x3(char *Bs, int tid, const f4 (&rb)[BR]) {
+    constexpr int NV = BN / 4, RPP = 256 / NV;
+    const int kr = tid / NV, nn = (tid - (tid / NV) * NV) * 4;
+#pragma unroll
+    for (int j = 0; j < BR; ++j) {
+        const int k = kr + RPP * j;
+        const float v[4] = {rb[j].x, rb[j].y, rb[j].z, rb[j].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const __bf16 h = (__bf16)v[e];
+            const __bf16 l = (__bf16)(v[e] - (float)h);
+            const int off = slot_off(nn + e, k >> 3) + (k & 7) * 2;
+            *(__bf16 *)(Bs + off) = h;
+            *(__bf16 *)(Bs + (off ^ 64)) = l;
+        }
+    }
+}
+
+template <int BM, int BN, int WAVES_M, int AMODE, int BKN>
+__global__ __launch_bounds__(256, 1) void conv_igemm_x3(ConvArgs a) {
+    constexpr int WAVES_N = 4 / WAVES_M;
+    constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
+    constexpr int TM = WTM / 32, TN = WTN / 32;
+    constexpr int AR = BM / 32;
+    constexpr int BR = BN / 32;
+    constexpr int STAGE = (BM + BN) * 128;                    // bytes
+    constexpr int CBYTES = BM * (BN + 4) * 4;                 // epilogue C staging
+    constexpr int SMEM = 2 * STAGE > CBYTES ? 2 * STAGE : CBYTES;
+    static_assert(TM >= 1 && TN >= 1 && WTM % 32 == 0 && WTN % 32 == 0, "tile");
+
+    __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+    int mt, nt, bz;
+    {   // XCD-aware tile order (see conv.hip)
+        const int gx = gridDim.x, gy = gridDim.y;
+        const int total = gx * gy * gridDim.z;
+        const int L = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+        const int per = total >> 3, rem = total & 7;
+        const int xcd = L & 7, idx = L >> 3;
+        const int Lp = xcd < rem ? xcd * (per + 1) + idx : rem * (per + 1) + (xcd - rem) * per + idx;
+        nt = Lp % gy;
+        const int t = Lp / gy;
+        mt = t % gx;
+        bz = t / gx;
+    }
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int bidx = bz / a.splits, split = bz - bidx * a.splits;
+    const float *__restrict__ x = a.x + (long long)bidx * a.x_bs;
+    const float *__restrict__ wtf = a.wt + (long long)bidx * a.w_bs;      // fp32 view (b_kn)
+    const char *__restrict__ wtb = (const char *)wtf;                      // split-bf16 view (packed)
+    const int kt0 = split * a.tps;
+    const int kt1 = min(a.ktiles, kt0 + a.tps);
+    const int taps = a.kh * a.kw, nsl = a.cin >> 5;
+    const bool kperm = (AMODE == 0 || AMODE == 3) && !BKN && taps > 1;
+    auto kmap = [&](int i) { return kperm ? (i % taps) * nsl + i / taps : i; };
+    const int ak = (tid & 7) * 4;
+
+    ARows<AR, AMODE> R;
+    a_rows_init<AR, AMODE>(a, m0, tid >> 3, R);
+
+    f4 ra[AR];
+    u32x4 rbp[BKN ? 1 : BR];
+    f4 rbk[BKN ? BR : 1];
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    auto load = [&](int kt) {
+        load_a<AR, AMODE>(a, x, kt, ak, R, ra);
+        if constexpr (BKN) load_b<BN, BR, 1>(a, wtf, kt, n0, tid, rbk);
+        else load_b_x3<BR>(a, wtb, kt, n0, tid, rbp);
+    };
+    auto store = [&](char *st) {
+        store_a_x3<BM, AR>(st, tid, ra);
+        if constexpr (BKN) store_b_kn_x3<BN, BR>(st + BM * 128, tid, rbk);
+        else store_b_x3<BR>(st + BM * 128, tid, rbp);
+    };
+
+    const int li = lane & 31, lh = lane >> 5;
+    const int rsw = swz(li);     // rows wm*WTM + i*32 + li share li's swizzle (tile bases are multiples of 32)
+    if (kt0 < kt1) {
+        load(kmap(kt0));
+        store(smem);
+        __syncthreads();
+    }
+    int buf = 0;
+    for (int kt = kt0; kt < kt1; ++kt) {
+        load(kmap(min(kt + 1, kt1 - 1)));
+        __builtin_amdgcn_sched_barrier(0);   // keep the prefetch issue above the MFMA block
+        const char *As = smem + buf * STAGE;
+        const char *Bs = As + BM * 128;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int hs = ((2 * s + lh) ^ rsw) << 4, ls = hs ^ 64;
+            bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const char *p = As + (wm * WTM + i * 32 + li) * 128;
+                ah[i] = *(const bf16x8 *)(p + hs);
+                al[i] = *(const bf16x8 *)(p + ls);
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const char *p = Bs + (wn * WTN + j * 32 + li) * 128;
+                bh[j] = *(const bf16x8 *)(p + hs);
+                bl[j] = *(const bf16x8 *)(p + ls);
+            }
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+                }
+        }
+        store(smem + (buf ^ 1) * STAGE);     // the other buffer was last read before the previous barrier
+        __syncthreads();
+        buf ^= 1;
+    }
+    epilogue_tile<BM, BN, WAVES_M, TM, TN>(a, acc, (float *)smem, tid, m0, n0, bz, bidx);
+}
+
+template <int BM, int BN, int WM>
+static void launch_tile_x3(const ConvArgs &a, int amode, bool bkn, dim3 grid, hipStream_t s) {
+    switch (amode * 2 + (bkn ? 1 : 0)) {
+        case 0: conv_igemm_x3<BM, BN, WM, 0, 0><<<grid, 256, 0, s>>>(a); break;
+        case 1: conv_igemm_x3<BM, BN, WM, 0, 1><<<grid, 256, 0, s>>>(a); break;
+        case 2: conv_igemm_x3<BM, BN, WM, 1, 0><<<grid, 256, 0, s>>>(a); break;
+        case 3: conv_igemm_x3<BM, BN, WM, 1, 1><<<grid, 256, 0, s>>>(a); break;
+        case 4: conv_igemm_x3<BM, BN, WM, 2, 0><<<grid, 256, 0, s>>>(a); break;
+        case 5: conv_igemm_x3<BM, BN, WM, 2, 1><<<grid, 256, 0, s>>>(a); break;
+        default: conv_igemm_x3<BM, BN, WM, 3, 0><<<grid, 256, 0, s>>>(a); break;
+    }
+}
+
+void launch_conv_x3(int tile, const ConvArgs &a, int amode, bool bkn, dim3 grid, hipStream_t s) {
+    switch (tile) {
+        case 0: launch_tile_x3<128, 128, 2>(a, amode, bkn, grid, s); break;
+        case 1: launch_tile_x3<128, 64, 2>(a, amode, bkn, grid, s); break;
+        case 2: launch_tile_x3<64, 128, 2>(a, amode, bkn, grid, s); break;
+        case 3: launch_tile_x3<64, 64, 2>(a, amode, bkn, grid, s); break;
+        case 4: launch_tile_x3<256, 32, 4>(a, amode, bkn, grid, s); break;
+        default: launch_tile_x3<128, 32, 4>(a, amode, bkn, grid, s); break;
+    }
+}
+
+// ---------------------------------------------------------------- weight splitting kernels
+// [rows][kpad] fp32 -> [rows][kpad/32][hi 32 | lo 32] bf16 (kpad % 32 == 0)
+__global__ __launch_bounds__(256) void split_weights_kernel(const float *__restrict__ w, long long slices,
+                                                            char *__restrict__ out) {
+    // one thread per 4 consecutive k of one 32-k slice
+    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < slices * 8; e += (long long)gridDim.x * 256) {
+        const long long sl = e >> 3;
+        const int q = (int)(e & 7);
+        const f4 v = *(const f4 *)(w + sl * 32 + q * 4);
+        u32x2 hi, lo;
+        split4(v, hi, lo);
+        char *o = out + sl * 128 + q * 8;
+        *(u32x2 *)o = hi;
+        *(u32x2 *)(o + 64) = lo;
+    }
+}
+
+// StyleGAN2 per-sample weights (s2v_modulate_weights) written directly in the split layout
+__global__ __launch_bounds__(256) void modulate_weights_x3_kernel(const float *__restrict__ wt, int npad, int kpad,
+                                                                  int K, int cin, int cout,
+                                                                  const float *__restrict__ s, int s_ns,
+                                                                  const float *__restrict__ d, int d_ns, int batch,
+                                                                  char *__restrict__ out) {
+    const long long per = (long long)npad * kpad;
+    const long long total = per * batch;
+    for (long long e = (blockIdx.x * 256LL + threadIdx.x) * 4; e < total; e += (long long)gridDim.x * 256 * 4) {
+        const int b = (int)(e / per);
+        const long long r = e - b * per;
+        const int o = (int)(r / kpad), k = (int)(r - (long long)o * kpad);
+        f4 w = *(const f4 *)(wt + r);
+        const float dd = (d && o < cout) ? d[(long long)b * d_ns + o] : 1.f;
+        float f[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) f[j] = (k + j < K) ? s[(long long)b * s_ns + (k + j) % cin] * dd : 0.f;
+        w.x *= f[0]; w.y *= f[1]; w.z *= f[2]; w.w *= f[3];
+        u32x2 hi, lo;
+        split4(w, hi, lo);
+        char *ob = out + (e >> 5) * 128 + (k & 31) * 2;    // slice e/32, k-offset within it
+        *(u32x2 *)ob = hi;
+        *(u32x2 *)(ob + 64) = lo;
+    }
+}
+
+static unsigned grid_x3(long long total) {
+    long long b = (total + 255) / 256;
+    if (b > 65535LL * 16) b = 65535LL * 16;
+    return (unsigned)(b < 1 ? 1 : b);
+}
+
+}  // namespace s2v
+
+using namespace s2v;
+
+extern "C" int s2v_split_weights_x3(const float *w, int rows, int kpad, void *out, s2v_stream_t stream) {
+    S2V_REQUIRE(w && out && rows > 0 && kpad > 0 && kpad % 32 == 0, "split_weights_x3: bad args");
+    S2V_REQUIRE(((uintptr_t)w % 16) == 0 && ((uintptr_t)out % 16) == 0, "split_weights_x3: 16-byte alignment");
+    const long long slices = (long long)rows * (kpad / 32);
+    split_weights_kernel<<<grid_x3(slices * 8), 256, 0, (hipStream_t)stream>>>(w, slices, (char *)out);
+    return check_launch("split_weights_x3");
+}
+
+extern "C" int s2v_modulate_weights_x3(const float *wt, int npad, int kpad, int K, int cin, int cout, const float *s,
+                                       int s_ns, const float *d, int d_ns, int batch, void *out,
+                                       s2v_stream_t stream) {
+    S2V_REQUIRE(wt && s && out && npad > 0 && kpad > 0 && K > 0 && K <= kpad && cin > 0 && cout > 0 && cout <= npad &&
+                batch > 0 && s_ns >= cin && (!d || d_ns >= cout), "modulate_weights_x3: bad args");
+    S2V_REQUIRE(kpad % 32 == 0 && ((uintptr_t)wt % 16) == 0 && ((uintptr_t)out % 16) == 0,
+                "modulate_weights_x3: kpad %% 32 and 16-byte aligned buffers required");
+    modulate_weights_x3_kernel<<<grid_x3((long long)npad * kpad * batch / 4), 256, 0, (hipStream_t)stream>>>(
+        wt, npad, kpad, K, cin, cout, s, s_ns, d, d_ns, batch, (char *)out);
+    return check_launch("modulate_weights_x3");
+}

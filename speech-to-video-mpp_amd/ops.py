@@ -11,14 +11,38 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import torch
 
 from . import _lib
 from ._lib import (ACT_GELU_TANH, ACT_LRELU, ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_TANH,  # noqa: F401
-                   IN_DIRECT, IN_NEAREST_UP2, IN_TRANSPOSED, PAD_REFLECT, PAD_ZERO, check)
+                   IN_DIRECT, IN_NEAREST_UP2, IN_TRANSPOSED, PAD_REFLECT, PAD_ZERO, PREC_BF16X3, PREC_F32, check)
 
 F32 = 4
+
+# Arithmetic of the implicit-GEMM convolutions (s2v_conv_params.prec): "bf16x3" = split-fp32 on the
+# bf16 MFMA (16 significant bits per operand, <= 3*2^-16 relative error per product, the default),
+# "f32" = exact fp32 MFMA.  The
+# S2V_PRECISION environment variable sets the process default; set_precision() changes it.
+_PRECISIONS = {"bf16x3": PREC_BF16X3, "f32": PREC_F32}
+PRECISION = os.environ.get("S2V_PRECISION", "bf16x3")
+if PRECISION not in _PRECISIONS:
+    raise ValueError(f"S2V_PRECISION must be one of {sorted(_PRECISIONS)}, got {PRECISION!r}")
+
+
+def set_precision(name: str) -> str:
+    """Select the conv arithmetic ("bf16x3" or "f32") for launches issued from now on; returns the
+    previous setting.  A captured HIP graph keeps the precision it was captured with."""
+    global PRECISION
+    if name not in _PRECISIONS:
+        raise ValueError(f"precision must be one of {sorted(_PRECISIONS)}, got {name!r}")
+    prev, PRECISION = PRECISION, name
+    return prev
+
+
+def prec_code() -> int:
+    return _PRECISIONS[PRECISION]
 
 # Optional per-launch observer (bench.py's live roofline): called as hook(ctx, params, flops, launch)
 # where launch() performs the conv; the hook may bracket it with events.
@@ -142,6 +166,19 @@ class ConvW:
         self.scale = None if scale is None else scale.contiguous().to(device)
         self.shift = None if shift is None else shift.contiguous().to(device)
 
+    _wt_x3 = None
+
+    def wt_x3(self, ctx: "Ctx") -> torch.Tensor:
+        """The packed weights in the S2V_PREC_BF16X3 split layout (built once, on first use)."""
+        if self._wt_x3 is None:
+            if self.wt.is_cuda and torch.cuda.is_current_stream_capturing():
+                raise _lib.S2VError("split weights must be built by an eager run before graph capture")
+            out = torch.empty(self.wt.shape, dtype=torch.float32, device=self.wt.device)
+            check(ctx.lib.s2v_split_weights_x3(self.wt.data_ptr(), self.npad, self.kpad, out.data_ptr(), ctx.stream),
+                  "s2v_split_weights_x3")
+            self._wt_x3 = out
+        return self._wt_x3
+
     def make_polyphase(self, device):
         """Polyphase plan of a stride-2 ConvTranspose2d: output parity class (ry, rx) is a stride-1
         direct conv of the input with the taps ky = ry + p (mod 2), flipped, padded by T - 1 - c0
@@ -216,6 +253,7 @@ def _conv(ctx, x, cw, y, ohw, out_view, act, alpha, res, res_after, res_offset, 
         p.in_scale, p.in_scale_ns = in_scale.data_ptr(), in_scale.stride(0)
     p.kh, p.kw, p.sh, p.sw, p.ph, p.pw, p.dh, p.dw = cw.kh, cw.kw, cw.sh, cw.sw, cw.ph, cw.pw, cw.dh, cw.dw
     p.wt, p.kpad, p.npad, p.cout = cw.wt.data_ptr(), cw.kpad, cw.npad, cw.cout
+    p.prec = prec_code()
     p.y, p.oh, p.ow, p.ycs = y.ptr, oh, ow, y.cs
     sc = cw.scale if scale is None else scale
     sh = cw.shift if shift is None else shift
@@ -236,10 +274,13 @@ def _conv(ctx, x, cw, y, ohw, out_view, act, alpha, res, res_after, res_offset, 
     if per_sample_wt is not None:        # batch mode: one image per batch entry, its own weights
         assert in_scale is None and nc_scale is None and out_view is None
         p.n, p.batch = 1, x.n
-        p.wt, p.w_bs = per_sample_wt.data_ptr(), cw.npad * cw.kpad
+        wfp, wx3 = per_sample_wt
+        p.wt, p.wt_x3, p.w_bs = _ptr(wfp), _ptr(wx3), cw.npad * cw.kpad
         p.x_bs, p.y_bs = x.h * x.w * x.cs, oh * ow * y.cs
         if res is not None:
             p.res_bs = res.h * res.w * res.cs
+    elif p.prec == PREC_BF16X3 and (cw.cout > 4 or force_tile):   # implicit-GEMM path (not Cout <= 4 VALU)
+        p.wt_x3 = cw.wt_x3(ctx).data_ptr()
     need = ctx.lib.s2v_conv2d_ws_bytes(ctypes.byref(p))
     p.ws, p.ws_bytes = ctx.ws.get(need)
     if CONV_HOOK is not None:
@@ -264,12 +305,14 @@ def modulated_conv2d(ctx: Ctx, x: NHWC, cw: ConvW, y: NHWC, s: torch.Tensor, d: 
     assert x.c == cw.cin and (y.n, y.h, y.w, y.c) == (x.n, oh, ow, cw.cout)
     b = x.n
     wb = torch.empty((b, cw.npad, cw.kpad), device=cw.wt.device)
-    check(ctx.lib.s2v_modulate_weights(cw.wt.data_ptr(), cw.npad, cw.kpad, cw.K, cw.cin, cw.cout, s.data_ptr(),
-                                       s.stride(0), None if d is None else d.data_ptr(),
-                                       0 if d is None else d.stride(0), b, wb.data_ptr(), ctx.stream),
+    # the implicit-GEMM kernel in bf16x3 mode reads split weights; the small-Cout kernel fp32
+    x3 = prec_code() == PREC_BF16X3 and cw.cout > 4
+    fn = ctx.lib.s2v_modulate_weights_x3 if x3 else ctx.lib.s2v_modulate_weights
+    check(fn(cw.wt.data_ptr(), cw.npad, cw.kpad, cw.K, cw.cin, cw.cout, s.data_ptr(), s.stride(0),
+             None if d is None else d.data_ptr(), 0 if d is None else d.stride(0), b, wb.data_ptr(), ctx.stream),
           "s2v_modulate_weights")
     return _conv(ctx, x, cw, y, (oh, ow), None, act, alpha, res, res_after, (0, 0), None, None, ACT_NONE, 0.0,
-                 pix_add, pix_w, None, shift, 0, 0, per_sample_wt=wb)
+                 pix_add, pix_w, None, shift, 0, 0, per_sample_wt=(None, wb) if x3 else (wb, None))
 
 
 def gemm_kn(ctx: Ctx, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, batch: int, a_bs: int, b_bs: int,
@@ -283,6 +326,7 @@ def gemm_kn(ctx: Ctx, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, ba
     p.x, p.n, p.h, p.w, p.cin, p.xcs = a.data_ptr(), 1, 1, M, K, K
     p.kh = p.kw = p.sh = p.sw = p.dh = p.dw = 1
     p.wt, p.cout, p.b_kn, p.ldb = b.data_ptr(), N, 1, N
+    p.prec = prec_code()
     p.y, p.oh, p.ow, p.ycs = out.data_ptr(), 1, M, N
     if res is not None:
         p.res, p.res_cs, p.res_h, p.res_w = res.data_ptr(), N, 1, M
@@ -299,22 +343,25 @@ def gemm_kn(ctx: Ctx, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, ba
     return out
 
 
+def _plan(ctx: Ctx, p):
+    out = (ctypes.c_int * 7)()
+    check(ctx.lib.s2v_conv2d_plan(ctypes.byref(p), out), "s2v_conv2d_plan")
+    return list(out)
+
+
 def conv_symbol(ctx: Ctx, p) -> str:
     """Kernel symbol (as rocprofv3 reports it, demangled) the launch of ``p`` runs."""
-    out = (ctypes.c_int * 6)()
-    check(ctx.lib.s2v_conv2d_plan(ctypes.byref(p), out), "s2v_conv2d_plan")
-    bm, bn, wm, avec, bkn, splits = list(out)
+    bm, bn, wm, avec, bkn, splits, x3 = _plan(ctx, p)
     if bm == 0:
         if wm:
             return f"void s2v::conv_small_cpar<{bn}, {wm}>(s2v::ConvArgs, int)"
         return f"void s2v::conv_direct_small<{bn}>(s2v::ConvArgs, int)"
-    return f"void s2v::conv_igemm<{bm}, {bn}, {wm}, {avec}, {bkn}>(s2v::ConvArgs)"
+    name = "conv_igemm_x3" if x3 else "conv_igemm"
+    return f"void s2v::{name}<{bm}, {bn}, {wm}, {avec}, {bkn}>(s2v::ConvArgs)"
 
 
 def conv_splits(ctx: Ctx, p) -> int:
-    out = (ctypes.c_int * 6)()
-    check(ctx.lib.s2v_conv2d_plan(ctypes.byref(p), out), "s2v_conv2d_plan")
-    return out[5]
+    return _plan(ctx, p)[5]
 
 
 def layernorm2d(ctx: Ctx, x: NHWC, weight, bias, y: NHWC, *, act=ACT_LRELU, alpha=0.1, pool=False,

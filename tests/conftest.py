@@ -23,3 +23,13 @@ def golden():
     def load(name):
         return np.load(os.path.join(GOLDEN, f"{name}.npz"))
     return load
+
+
+@pytest.fixture(params=["f32", "bf16x3"])
+def prec(request):
+    """Run a test once per conv arithmetic mode (s2v_amd.ops.set_precision): exact fp32 MFMA and
+    the split-fp32 bf16 MFMA default."""
+    from s2v_amd import ops
+    prev = ops.set_precision(request.param)
+    yield request.param
+    ops.set_precision(prev)

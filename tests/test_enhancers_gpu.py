@@ -62,7 +62,7 @@ def test_fir2d_matches_upfirdn2d(cfg):
         assert max_abs(got, ref_act if fused else ref)[0] < 1e-5
 
 
-def test_gfpgan_matches_reference(gfpgan, golden):
+def test_gfpgan_matches_reference(prec, gfpgan, golden):
     g = golden("gfpgan_b1_512")
     x = torch.from_numpy(synth.face_inputs("golden.gfpgan", 1)).to(DEV)
     img, rgbs = gfpgan(x, return_rgb=True, randomize_noise=False)
@@ -85,7 +85,7 @@ def test_gfpgan_batch_vs_oracle_and_noise(gfpgan):
     assert torch.isfinite(a).all() and (a - b).abs().max() > 0       # fresh N(0,1) noise per call
 
 
-def test_gpen_matches_reference(gpen, golden):
+def test_gpen_matches_reference(prec, gpen, golden):
     g = golden("gpen_b1_512")
     x = torch.from_numpy(synth.face_inputs("golden.gpen", 1)).to(DEV)
     img, lat = gpen(x, return_latents=True)

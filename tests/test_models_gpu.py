@@ -1,7 +1,8 @@
 """End-to-end parity of the HIP models (s2v_amd.models, drop-in for reference models/) against
 the reference outputs stored in tests/golden/ (and the CPU oracle for larger batches).
 
-Tolerances (fp32 everywhere; reference fp32-vs-fp64 spread 5e-4..7e-4):
+Tolerances (fp32 everywhere; reference fp32-vs-fp64 spread 5e-4..7e-4), the same for
+both conv arithmetic modes (``prec``: exact fp32 MFMA and split-fp32 bf16x3):
   LNet  [0,1] output  max|d| <= 2e-3, mean|d| <= 1e-4;  pre-sigmoid logits max|d| <= 5e-3
   ENet  output (unclamped, |x| <= ~9)  max|d| <= 1e-2, mean|d| <= 5e-4;  low as LNet
   DNet  fake/warp  max|d| <= 2e-3 (tanh-saturated regions amplify nothing);  flow max|d| <= 1e-3
@@ -40,7 +41,7 @@ def dnet():
     return _model("dnet")
 
 
-def test_lnet_matches_reference(lnet, golden):
+def test_lnet_matches_reference(prec, lnet, golden):
     g = golden("lnet_b2_96")
     mel, face, _ = synth.lipsync_inputs("golden.lnet", 2, 96)
     out = lnet(torch.from_numpy(mel).to(DEV), torch.from_numpy(face).to(DEV))
@@ -48,7 +49,7 @@ def test_lnet_matches_reference(lnet, golden):
     assert m <= 2e-3 and mean <= 1e-4, (m, mean)
 
 
-def test_lnet_intermediates(lnet, golden):
+def test_lnet_intermediates(prec, lnet, golden):
     """Audio feature and pre-sigmoid logits through the engine directly."""
     from s2v_amd import ops
     from s2v_amd.ops import NHWC
@@ -80,7 +81,7 @@ def test_lnet_5d_input_fold(lnet):
     assert (out5[:, :, 0] - flat[:2]).abs().max() < 1e-6 and (out5[:, :, 1] - flat[2:]).abs().max() < 1e-6
 
 
-def test_enet_matches_reference(enet, golden):
+def test_enet_matches_reference(prec, enet, golden):
     for size in (256, 384):
         g = golden(f"enet_b1_{size}")
         mel, face, gt = synth.lipsync_inputs(f"golden.enet{size}", 1, size)
@@ -94,7 +95,7 @@ def test_enet_matches_reference(enet, golden):
             check_probe(out, g, "out", atol=1e-2)
 
 
-def test_enet_batch16_vs_oracle(enet):
+def test_enet_batch16_vs_oracle(prec, enet):
     """Full-size bench workload batch (B=16, 256x256 crops) against the CPU oracle on 2 frames of
     it, and batch-invariance (frames are independent) on the rest."""
     from oracle import nets
@@ -112,7 +113,7 @@ def test_enet_batch16_vs_oracle(enet):
     assert (out2 - out[8:10]).abs().max() < 2e-3
 
 
-def test_dnet_matches_reference(dnet, golden):
+def test_dnet_matches_reference(prec, dnet, golden):
     for size, batch in ((128, 2), (256, 1)):
         g = golden(f"dnet_b{batch}_{size}")
         src, coeff = synth.dnet_inputs(f"golden.dnet{size}", batch, size)

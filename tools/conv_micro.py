@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--sweep", action="store_true")
     ap.add_argument("--splits", type=int, default=0)
+    ap.add_argument("--prec", default="both", choices=("f32", "bf16x3", "both"))
     a = ap.parse_args()
     dev = torch.device("cuda")
     ctx = ops.Ctx(dev)
@@ -44,7 +45,8 @@ def main():
     y = NHWC.empty(a.n, oh, ow, a.cout, dev)
     flops = 2.0 * a.n * oh * ow * a.k * a.k * a.cin * a.cout
     tiles = range(1, 7) if a.sweep else [0]
-    for t in tiles:
+    for prec, t in [(p, t) for p in (("f32", "bf16x3") if a.prec == "both" else (a.prec,)) for t in tiles]:
+        ops.set_precision(prec)
         kw = dict(act=ops.ACT_LRELU, alpha=0.2, force_tile=t, force_splits=a.splits)
         ops.conv2d(ctx, x, cw, y, **kw)
         torch.cuda.synchronize()
