@@ -36,7 +36,15 @@ import s2v_import  # noqa: E402,F401
 
 METRIC = "synthesized 256×256 frames/sec/GPU (LNet+ENet path); 1/2/4/8-GPU scaling"
 FP32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 matrix 157.3 TF (spec)
+# bf16x3 kernels issue 3 dense bf16 MFMAs (2.5 PF/s dense, MI355X_MICROARCH.md) per fp32 MAC, so
+# their ceiling in algorithmic (fp32-equivalent) FLOP/s is a third of the bf16 peak
+BF16X3_PEAK_TFLOPS = 2500.0 / 3
 REF_GFLOP_PER_FRAME = 407.46       # ENet+LNet algorithmic GFLOP/frame (2*MAC)
+
+
+ARITH = {"bf16x3": "bf16x3: fp32 tensors, conv products as split-fp32 hi*hi+hi*lo+lo*hi on bf16 MFMA "
+                    "(16 significant bits per operand), fp32 accumulate; all other ops fp32",
+         "f32": "f32: exact fp32 MFMA (v_mfma_f32_32x32x2_f32) convs; all other ops fp32"}
 
 
 def parse():
@@ -52,6 +60,9 @@ def parse():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--precision", choices=("bf16x3", "f32"), default="bf16x3",
+                    help="conv arithmetic (s2v_amd.ops.set_precision)")
+    ap.add_argument("--no-alt", action="store_true", help="skip the timing of the other conv arithmetic")
     return ap.parse_args()
 
 
@@ -108,6 +119,7 @@ def live_roofline(forward, workload="lipsync"):
             print(f"  {v['ms']:9.3f} ms  {v['launches']:4d} launches  {tf:7.2f} TF/s  {k}", file=sys.stderr)
     d = per[dom]
     achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12
+    peak = BF16X3_PEAK_TFLOPS if "conv_igemm_x3" in dom else FP32_MFMA_PEAK_TFLOPS
     total_ms = sum(v["ms"] for v in per.values())
     total_flops = sum(v["flops"] for v in per.values())
     traffic = None
@@ -116,8 +128,8 @@ def live_roofline(forward, workload="lipsync"):
         with open(pmc) as f:
             traffic = json.load(f).get("per_launch_bytes", {}).get(dom)
     return {
-        "bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-        "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+        "bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
+        "frac": round(achieved / peak, 4), "traffic": traffic,
         "kernel": dom, "launches": d["launches"], "avg_launch_us": round(1e3 * d["ms"] / d["launches"], 2),
         "flops_per_launch": d["flops"] / d["launches"],
         "conv_family": {"achieved": round(total_flops / (total_ms * 1e-3) / 1e12, 2),
@@ -288,32 +300,40 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
     from s2v_amd.runtime import GraphRunner
 
+    from s2v_amd import ops
     wl = WORKLOADS[args.workload](args, dev, rank)
-    if args.no_graph:
-        step = wl.forward
-        for _ in range(max(1, args.warmup)):
-            step()
-    else:
-        runner = GraphRunner(wl.fn, list(wl.inputs), warmup=1)
-        step = runner.replay
-        for _ in range(args.warmup):
-            step()
 
     def barrier():
         if world > 1:
             torch.distributed.barrier()
         torch.cuda.synchronize()
 
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
+    def timed(prec):
+        """Capture (or not) the step in conv arithmetic ``prec``, warm up, time args.steps steps
+        between barriers; returns the max over ranks of the elapsed seconds."""
+        ops.set_precision(prec)
+        if args.no_graph:
+            step = wl.forward
+            for _ in range(max(1, args.warmup)):
+                step()
+        else:
+            runner = GraphRunner(wl.fn, list(wl.inputs), warmup=1)
+            step = runner.replay
+            for _ in range(args.warmup):
+                step()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], device=dev)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            el = float(t.item())
+        return el
+
+    elapsed = timed(args.precision)
     units = world * wl.batch * args.steps
     value = units / elapsed
     config = dict(wl.config)
@@ -326,6 +346,13 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic", "config": config,
     }
+    config["conv_arith"] = ARITH[args.precision]
+    if world == 1 and not args.no_alt:
+        other = "f32" if args.precision == "bf16x3" else "bf16x3"
+        el = timed(other)
+        result["alt_precision"] = {"conv_arith": ARITH[other], "value": round(units / el, 3),
+                                   "ms_per_step": round(1e3 * el / args.steps, 3)}
+        ops.set_precision(args.precision)
     if rank == 0 and not args.no_roofline:
         result["roofline"] = live_roofline(wl.forward, args.workload)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -108,10 +108,12 @@ enum { S2V_PREC_F32 = 0, S2V_PREC_BF16X3 = 1 };
  * ENet.py, DNet.py, base_blocks.py, ffc.py, transformer.py (inventory: SURVEY.md App. A). */
 int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream);
 size_t s2v_conv2d_ws_bytes(const s2v_conv_params *p);
-/* The launch plan s2v_conv2d would use: out7 = {BM, BN, WAVES_M, AVEC, B_KN, splits, prec} of the
- * conv_igemm<BM,BN,WAVES_M,AVEC,B_KN> (prec 0) / conv_igemm_x3<...> (prec 1) instance, or
- * {0, CO, TPP, 0, 0, 1, 0} for conv_small_cpar<CO,TPP> (conv_direct_small<CO> when TPP == 0). */
-int s2v_conv2d_plan(const s2v_conv_params *p, int *out7);
+/* The launch plan s2v_conv2d would use: out10 = {BM, BN, WAVES_M, AVEC, B_KN, splits, prec, NW, KS, PF}
+ * of the conv_igemm<BM,BN,WAVES_M,AVEC,B_KN> (prec 0) or
+ * conv_igemm_x3<BM,BN,WAVES_M,NW,KS,PF,AVEC,B_KN> (prec 1) instance, or {0, CO, TPP, 0, 0, 1, 0, 0, 0, 0}
+ * for conv_small_cpar<CO,TPP> (conv_direct_small<CO> when TPP == 0).  force_tile: 0 = planner,
+ * 1..6 a fixed tile of the selected precision's table (tests / tuning). */
+int s2v_conv2d_plan(const s2v_conv_params *p, int *out10);
 
 /* Split packed fp32 weights [rows][kpad] (kpad % 32 == 0) into the S2V_PREC_BF16X3 layout
  * [rows][kpad/32][hi 32 | lo 32] bf16 (same byte size), hi = bf16_rne(w), lo = bf16_rne(w - hi). */

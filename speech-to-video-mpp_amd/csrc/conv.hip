@@ -17,6 +17,8 @@
 
 #include "conv_impl.hpp"
 
+#include <cmath>
+
 namespace s2v {
 
 void launch_conv_x3(int tile, const ConvArgs &a, int amode, bool bkn, dim3 grid, hipStream_t s);   // conv_x3.hip
@@ -304,10 +306,25 @@ static void launch_small(const ConvArgs &a, int batch, bool cpar, hipStream_t s)
 
 // ------------------------------------------------------------------ host side
 struct TileCfg {
-    int bm, bn, wm;
+    int bm, bn, wm, nw, ks, pf;   // nw / ks / pf: waves, K-slices per stage, prefetch sets (x3 kernel)
 };
 static const TileCfg kTiles[] = {
-    {128, 128, 2}, {128, 64, 2}, {64, 128, 2}, {64, 64, 2}, {256, 32, 4}, {128, 32, 4}};
+    {128, 128, 2, 4, 1, 2}, {128, 64, 2, 4, 1, 2}, {64, 128, 2, 4, 1, 2}, {64, 64, 2, 4, 1, 2}, {256, 32, 4, 4, 1, 2},
+    {128, 32, 4, 4, 1, 2}};
+// split-bf16 (S2V_PREC_BF16X3) configurations, conv_x3.hip launch_conv_x3, with the sustained
+// throughput each reaches on a full chip (TFLOP/s fp32-equivalent, MI355X, tools/conv_micro.py r01)
+// and resident blocks per CU (LDS / waves) for the planner's cost model
+struct X3Cfg {
+    TileCfg t;
+    float tflops;
+    int bpc;
+};
+static const X3Cfg kX3Tiles[] = {
+    {{256, 256, 2, 8, 1, 1}, 365.f, 1}, {{128, 128, 2, 8, 1, 1}, 295.f, 2}, {{64, 128, 2, 8, 1, 1}, 255.f, 3},
+    {{128, 64, 2, 4, 1, 1}, 230.f, 3},  {{64, 64, 2, 4, 1, 1}, 200.f, 4},   {{128, 32, 4, 4, 1, 1}, 150.f, 4}};
+constexpr int kNumX3 = sizeof(kX3Tiles) / sizeof(kX3Tiles[0]);
+
+static const TileCfg &tile_cfg(const s2v_conv_params *p, int tile);
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
 struct Plan {
@@ -325,6 +342,67 @@ static bool tiled_x3(const s2v_conv_params *p) {
     return p->prec == S2V_PREC_BF16X3 && !(use_direct(p) && !p->force_tile);
 }
 
+static int a_mode(const s2v_conv_params *p);
+
+static const TileCfg &tile_cfg(const s2v_conv_params *p, int tile) {
+    return tiled_x3(p) ? kX3Tiles[tile].t : kTiles[tile];
+}
+
+static void finish_plan(Plan &pl, int splits) {
+    if (splits > pl.ktiles) splits = pl.ktiles;
+    if (splits < 1) splits = 1;
+    pl.tps = (pl.ktiles + splits - 1) / splits;
+    pl.splits = (pl.ktiles + pl.tps - 1) / pl.tps;
+}
+
+// Split-bf16 planner: minimise a simple time model over (tile, split-K):
+//   T = ceil(blocks / (CUs * bpc)) * t_block + splitk_reduce
+// with t_block = one block's share of the tile's sustained full-chip rate (kX3Tiles).
+static Plan make_plan_x3(const s2v_conv_params *p, int M, Plan pl) {
+    const int batch = p->batch > 0 ? p->batch : 1;
+    const int cus = device_cus() > 0 ? device_cus() : 256;
+    if (p->force_tile > 0) {
+        pl.tile = p->force_tile - 1;
+        const TileCfg &t = kX3Tiles[pl.tile].t;
+        const long long blocks = (long long)cdiv(M, t.bm) * cdiv(p->cout, t.bn) * batch;
+        int splits = p->force_splits;
+        if (splits <= 0) {
+            splits = 1;
+            if (blocks < 2LL * cus) splits = (int)((2LL * cus + blocks - 1) / blocks);
+            if (splits > pl.ktiles / 8) splits = pl.ktiles / 8;
+        }
+        finish_plan(pl, splits);
+        return pl;
+    }
+    double best = 1e30;
+    int bt = kNumX3 - 1, bs = 1;
+    const int am = a_mode(p);
+    for (int i = 0; i < kNumX3; ++i) {
+        const X3Cfg &c = kX3Tiles[i];
+        if (p->b_kn && c.t.nw != 4) continue;
+        if (c.t.bm == 256 && c.t.bn == 256 && am != 0 && am != 3) continue;   // generic gathers spill there
+        const long long tiles = (long long)cdiv(M, c.t.bm) * cdiv(p->cout, c.t.bn) * batch;
+        const double slots = (double)cus * c.bpc;
+        for (int s = 1; s <= 16; s *= 2) {
+            if (s > 1 && (p->force_splits > 0 || s > pl.ktiles / 4)) break;
+            if (p->force_splits > 0) s = p->force_splits;
+            const int tps = (pl.ktiles + s - 1) / s;
+            const double t_block = 2.0 * c.t.bm * c.t.bn * 32.0 * tps / (c.tflops * 1e12 / slots);
+            double t = std::ceil((double)(tiles * s) / slots) * t_block;
+            if (s > 1) t += 4e-6 + (double)batch * M * p->cout * 4.0 * (s + 1) / 4e12;
+            if (t < best * 0.97) {   // prefer the earlier (larger) tile / fewer splits on near ties
+                best = t;
+                bt = i;
+                bs = s;
+            }
+            if (p->force_splits > 0) break;
+        }
+    }
+    pl.tile = bt;
+    finish_plan(pl, bs);
+    return pl;
+}
+
 static Plan make_plan(const s2v_conv_params *p, int M, int K) {
     Plan pl{};
     pl.ktiles = (K + 31) / 32;
@@ -334,6 +412,7 @@ static Plan make_plan(const s2v_conv_params *p, int M, int K) {
         pl.tps = pl.ktiles;
         return pl;
     }
+    if (tiled_x3(p)) return make_plan_x3(p, M, pl);
     const int batch = p->batch > 0 ? p->batch : 1;
     const long long target = 2LL * (device_cus() > 0 ? device_cus() : 256);
     int cands[kNumTiles];
@@ -368,15 +447,17 @@ static Plan make_plan(const s2v_conv_params *p, int M, int K) {
         if (splits > maxs) splits = maxs;
         if (splits < 1) splits = 1;
     }
-    if (splits > pl.ktiles) splits = pl.ktiles;
-    pl.tps = (pl.ktiles + splits - 1) / splits;
-    pl.splits = (pl.ktiles + pl.tps - 1) / pl.tps;
+    finish_plan(pl, splits);
     return pl;
 }
 
 static int validate(const s2v_conv_params *p, int &M, int &K) {
     S2V_REQUIRE(p && p->x && p->y, "conv2d: null pointer");
     S2V_REQUIRE(p->prec == S2V_PREC_F32 || p->prec == S2V_PREC_BF16X3, "conv2d: bad prec %d", p->prec);
+    S2V_REQUIRE(p->force_tile >= 0 && p->force_tile <= (tiled_x3(p) ? kNumX3 : kNumTiles),
+                "conv2d: bad force_tile %d", p->force_tile);
+    S2V_REQUIRE(!(tiled_x3(p) && p->b_kn && p->force_tile > 0 && kX3Tiles[p->force_tile - 1].t.nw != 4),
+                "conv2d: b_kn operands need a 4-wave split-bf16 tile (force_tile 4..6)");
     if (uses_x3(p))
         S2V_REQUIRE(p->wt_x3 && ((uintptr_t)p->wt_x3 % 16) == 0, "conv2d: prec BF16X3 needs 16B-aligned wt_x3");
     else
@@ -476,7 +557,7 @@ extern "C" size_t s2v_conv2d_ws_bytes(const s2v_conv_params *p) {
 }
 
 extern "C" int s2v_conv2d_plan(const s2v_conv_params *p, int *out6) {
-    out6[6] = 0;
+    for (int i = 6; i < 10; ++i) out6[i] = 0;
     int M, K;
     int rc = validate(p, M, K);
     if (rc) return rc;
@@ -491,12 +572,13 @@ extern "C" int s2v_conv2d_plan(const s2v_conv_params *p, int *out6) {
         out6[3] = 0; out6[4] = 0; out6[5] = 1;
         return 0;
     }
-    const TileCfg &t = kTiles[pl.tile];
+    const TileCfg &t = tile_cfg(p, pl.tile);
     out6[0] = t.bm; out6[1] = t.bn; out6[2] = t.wm;
     out6[3] = a_mode(p);
     out6[4] = p->b_kn != 0;
     out6[5] = pl.splits;
     out6[6] = tiled_x3(p) ? 1 : 0;
+    out6[7] = t.nw; out6[8] = t.ks; out6[9] = t.pf;
     return 0;
 }
 
@@ -531,7 +613,7 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
     }
     const int amode = a_mode(p);
     const bool bkn = p->b_kn != 0;
-    const TileCfg &t = kTiles[pl.tile];
+    const TileCfg &t = tile_cfg(p, pl.tile);
     dim3 grid(cdiv(M, t.bm), cdiv(p->cout, t.bn), batch * pl.splits);
     if (tiled_x3(p)) {
         if (!bkn) a.wt = (const float *)p->wt_x3;

@@ -128,12 +128,13 @@ struct ARows {
     bool ok[AR];
 };
 
-template <int AR, int AMODE>
+// rows m0 + ar + RS * j of the tile (RS = rows covered by one load pass of the block)
+template <int AR, int AMODE, int RS = 32>
 __device__ __forceinline__ void a_rows_init(const ConvArgs &a, int m0, int ar, ARows<AR, AMODE> &R) {
     const int hw = a.oh * a.ow;
 #pragma unroll
     for (int j = 0; j < AR; ++j) {
-        const int m = m0 + ar + 32 * j;
+        const int m = m0 + ar + RS * j;
         R.ok[j] = m < a.M;
         const int mm = R.ok[j] ? m : 0;
         const int img = mm / hw;
@@ -150,50 +151,56 @@ __device__ __forceinline__ void a_rows_init(const ConvArgs &a, int m0, int ar, A
     }
 }
 
+// AMODE 0 / 3 gather of one K-slice: filter tap (ky, kx), channels [c, c + 4) per row (the tap is
+// tile-uniform: scalar math); AMODE 3 reflects out-of-range rows/cols (FFC, ffc.py:196-204).
+template <int AR, int AMODE>
+__device__ __forceinline__ void load_a_tap(const ConvArgs &a, const float *__restrict__ x, int ky, int kx, int c,
+                                           const ARows<AR, AMODE> &R, f4 (&ra)[AR]) {
+    const int dy = ky * a.dh, dx = kx * a.dw;
+    if (AMODE == 0) {
+        const long long toff = ((long long)dy * a.w + dx) * a.xcs + c;
+#pragma unroll
+        for (int j = 0; j < AR; ++j) {
+            const bool ok = R.ok[j] && (unsigned)(R.iy0[j] + dy) < (unsigned)a.h &&
+                            (unsigned)(R.ix0[j] + dx) < (unsigned)a.w;
+            f4 v = {0.f, 0.f, 0.f, 0.f};
+            if (ok) v = *(const f4 *)(x + R.base[j] + toff);
+            ra[j] = v;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < AR; ++j) {
+            const int iy = reflect_idx(R.iy0[j] + dy, a.h), ix = reflect_idx(R.ix0[j] + dx, a.w);
+            f4 v = {0.f, 0.f, 0.f, 0.f};
+            if (R.ok[j]) v = *(const f4 *)(x + R.base[j] + ((long long)iy * a.w + ix) * a.xcs + c);
+            ra[j] = v;
+        }
+    }
+    if (a.in_scale) {   // StyleGAN2 input modulation s[n, c] (zero padding stays zero)
+#pragma unroll
+        for (int j = 0; j < AR; ++j)
+            ra[j] *= *(const f4 *)(a.in_scale + (long long)R.img[j] * a.in_scale_ns + c);
+    }
+    if (a.pre_act) {
+        const float sl = a.pre_act == S2V_ACT_RELU ? 0.f : a.pre_alpha;
+#pragma unroll
+        for (int j = 0; j < AR; ++j) {
+            ra[j].x = ra[j].x >= 0.f ? ra[j].x : ra[j].x * sl;
+            ra[j].y = ra[j].y >= 0.f ? ra[j].y : ra[j].y * sl;
+            ra[j].z = ra[j].z >= 0.f ? ra[j].z : ra[j].z * sl;
+            ra[j].w = ra[j].w >= 0.f ? ra[j].w : ra[j].w * sl;
+        }
+    }
+}
+
 template <int AR, int AMODE>
 __device__ __forceinline__ void load_a(const ConvArgs &a, const float *__restrict__ x, int kt, int ak,
                                        const ARows<AR, AMODE> &R, f4 (&ra)[AR]) {
     const int kbase = kt * 32;
     if (AMODE == 0 || AMODE == 3) {
-        // tile-uniform tap (scalar math); AMODE 3 reflects out-of-range rows/cols (FFC, ffc.py:196-204)
         const int tap = kbase / a.cin;
-        const int c = kbase - tap * a.cin + ak;
         const int ky = tap / a.kw, kx = tap - (tap / a.kw) * a.kw;
-        const int dy = ky * a.dh, dx = kx * a.dw;
-        const long long toff = ((long long)dy * a.w + dx) * a.xcs + c;
-        if (AMODE == 0) {
-#pragma unroll
-            for (int j = 0; j < AR; ++j) {
-                const bool ok = R.ok[j] && (unsigned)(R.iy0[j] + dy) < (unsigned)a.h &&
-                                (unsigned)(R.ix0[j] + dx) < (unsigned)a.w;
-                f4 v = {0.f, 0.f, 0.f, 0.f};
-                if (ok) v = *(const f4 *)(x + R.base[j] + toff);
-                ra[j] = v;
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < AR; ++j) {
-                const int iy = reflect_idx(R.iy0[j] + dy, a.h), ix = reflect_idx(R.ix0[j] + dx, a.w);
-                f4 v = {0.f, 0.f, 0.f, 0.f};
-                if (R.ok[j]) v = *(const f4 *)(x + R.base[j] + ((long long)iy * a.w + ix) * a.xcs + c);
-                ra[j] = v;
-            }
-        }
-        if (a.in_scale) {   // StyleGAN2 input modulation s[n, c] (zero padding stays zero)
-#pragma unroll
-            for (int j = 0; j < AR; ++j)
-                ra[j] *= *(const f4 *)(a.in_scale + (long long)R.img[j] * a.in_scale_ns + c);
-        }
-        if (a.pre_act) {
-            const float sl = a.pre_act == S2V_ACT_RELU ? 0.f : a.pre_alpha;
-#pragma unroll
-            for (int j = 0; j < AR; ++j) {
-                ra[j].x = ra[j].x >= 0.f ? ra[j].x : ra[j].x * sl;
-                ra[j].y = ra[j].y >= 0.f ? ra[j].y : ra[j].y * sl;
-                ra[j].z = ra[j].z >= 0.f ? ra[j].z : ra[j].z * sl;
-                ra[j].w = ra[j].w >= 0.f ? ra[j].w : ra[j].w * sl;
-            }
-        }
+        load_a_tap<AR, AMODE>(a, x, ky, kx, kbase - tap * a.cin + ak, R, ra);
     } else if (AMODE == 1) {
         const int k = kbase + ak;
         const bool kok = k < a.K;
@@ -273,64 +280,73 @@ __device__ __forceinline__ void load_b(const ConvArgs &a, const float *__restric
 }
 
 // Epilogue of one BM x BN output tile held as 32x32 MFMA accumulators (C/D map: lane owns column
-// li of each tile, rows (r&3) + 8(r>>2) + 4 lh).  The tile is staged through LDS (``Cs``, at least
-// BM*(BN+4) floats) with static indices, then every thread walks it row by row (consecutive
-// threads -> consecutive output channels: coalesced stores).  Split-K launches write raw partial
-// sums to the workspace instead.
-template <int BM, int BN, int WAVES_M, int TM, int TN>
+// li of each tile, rows (r&3) + 8(r>>2) + 4 lh) by NW waves.  The tile is staged through LDS
+// (``Cs``, at least CH*(BN+4) floats) CH rows at a time with static indices, then every thread walks
+// the chunk row by row (consecutive threads -> consecutive output channels: coalesced stores).
+// Split-K launches write raw partial sums to the workspace instead.
+template <int BM, int BN, int WAVES_M, int TM, int TN, int NW = 4, int CH = BM>
 __device__ __forceinline__ void epilogue_tile(const ConvArgs &a, const floatx16 (&acc)[TM][TN], float *Cs, int tid,
                                               int m0, int n0, int bz, int bidx) {
-    constexpr int WAVES_N = 4 / WAVES_M;
+    constexpr int NT = 64 * NW;
+    constexpr int WAVES_N = NW / WAVES_M;
     constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
     constexpr int LDC = BN + 4;
+    static_assert(CH % 32 == 0 && BM % CH == 0, "epilogue chunk");
     const int lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WAVES_N, wn = wave % WAVES_N;
     const int li = lane & 31, lh = lane >> 5;
-    __syncthreads();   // every wave is done reading the operand stages that Cs overlays
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-                Cs[(wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * LDC + wn * WTN + j * 32 + li] = acc[i][j][r];
-    __syncthreads();
     const Epi &e = a.epi;
-    constexpr int TPR = BN < 256 ? BN : 256;   // threads per tile row
-    constexpr int RSTEP = 256 / TPR;
+    constexpr int TPR = BN < NT ? BN : NT;   // threads per tile row
+    constexpr int RSTEP = NT / TPR;
     const int cn = tid % TPR;
     const int n = n0 + cn;
-    if (n >= a.cout) return;
+    const bool live = n < a.cout;
     const int mlim = min(BM, a.M - m0);
-    if (a.splits > 1) {
-        float *w = a.ws + (long long)bz * a.M * a.cout;
-#pragma unroll 1
-        for (int rr = tid / TPR; rr < mlim; rr += RSTEP) w[(long long)(m0 + rr) * a.cout + n] = Cs[rr * LDC + cn];
-        return;
-    }
     const bool simple = !e.nc_scale && !e.pix_add && (!e.res || e.res_simple);
-    if (simple) {
-        const float sc = e.scale ? e.scale[n] : 1.f;
-        const float sh = e.shift ? e.shift[n] : 0.f;
-        const float slope = e.act == S2V_ACT_RELU ? 0.f : (e.act == S2V_ACT_LRELU ? e.alpha : 1.f);
-        float *__restrict__ yb = a.y + (long long)bidx * a.y_bs + n;
-        const float *rsrc = e.res ? e.res + (long long)bidx * a.res_bs + n : nullptr;
+    const float sc = (live && e.scale) ? e.scale[n] : 1.f;
+    const float sh = (live && e.shift) ? e.shift[n] : 0.f;
+    const float slope = e.act == S2V_ACT_RELU ? 0.f : (e.act == S2V_ACT_LRELU ? e.alpha : 1.f);
 #pragma unroll 1
-        for (int rr = tid / TPR; rr < mlim; rr += RSTEP) {
-            const long long m = m0 + rr;
-            float v = Cs[rr * LDC + cn] * sc + sh;
-            float rv = 0.f;
-            if (rsrc) {
-                rv = rsrc[a.y_step > 1 ? out_row(a, m) : m * e.res_cs];
-                if (!e.res_after) v += rv;
-            }
-            v = fast_act(v, e.act, slope);
-            if (rsrc && e.res_after) v += rv;
-            yb[out_row(a, m)] = v;
+    for (int c0 = 0; c0 < BM; c0 += CH) {
+        __syncthreads();   // operand stages (first chunk) / the previous chunk are no longer read
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int r0 = wm * WTM + i * 32 - c0;
+            if (r0 < 0 || r0 >= CH) continue;
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    Cs[(r0 + (r & 3) + 8 * (r >> 2) + 4 * lh) * LDC + wn * WTN + j * 32 + li] = acc[i][j][r];
         }
-    } else {
+        __syncthreads();
+        const int clim = min(CH, mlim - c0);
+        if (!live || clim <= 0) continue;
+        if (a.splits > 1) {
+            float *w = a.ws + (long long)bz * a.M * a.cout;
 #pragma unroll 1
-        for (int rr = tid / TPR; rr < mlim; rr += RSTEP) store_epilogue(a, bidx, m0 + rr, n, Cs[rr * LDC + cn]);
+            for (int rr = tid / TPR; rr < clim; rr += RSTEP)
+                w[(long long)(m0 + c0 + rr) * a.cout + n] = Cs[rr * LDC + cn];
+        } else if (simple) {
+            float *__restrict__ yb = a.y + (long long)bidx * a.y_bs + n;
+            const float *rsrc = e.res ? e.res + (long long)bidx * a.res_bs + n : nullptr;
+#pragma unroll 1
+            for (int rr = tid / TPR; rr < clim; rr += RSTEP) {
+                const long long m = m0 + c0 + rr;
+                float v = Cs[rr * LDC + cn] * sc + sh;
+                float rv = 0.f;
+                if (rsrc) {
+                    rv = rsrc[a.y_step > 1 ? out_row(a, m) : m * e.res_cs];
+                    if (!e.res_after) v += rv;
+                }
+                v = fast_act(v, e.act, slope);
+                if (rsrc && e.res_after) v += rv;
+                yb[out_row(a, m)] = v;
+            }
+        } else {
+#pragma unroll 1
+            for (int rr = tid / TPR; rr < clim; rr += RSTEP) store_epilogue(a, bidx, m0 + c0 + rr, n, Cs[rr * LDC + cn]);
+        }
     }
 }
 

@@ -47,12 +47,13 @@ __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 // byte offset of 16-byte slot ``slot`` (0..7) of LDS row ``row``
 __device__ __forceinline__ int slot_off(int row, int slot) { return row * 128 + ((slot ^ swz(row)) << 4); }
 
-template <int BM, int AR>
+// A rows ar + RS*j of the tile: 4 k-values per thread (slot q>>1, bytes (q&1)*8)
+template <int AR, int RS>
 __device__ __forceinline__ void store_a_x3(char *As, int tid, const f4 (&ra)[AR]) {
-    const int ar = tid >> 3, q = tid & 7;          // 4 k-values: slot q>>1, bytes (q&1)*8
+    const int ar = tid >> 3, q = tid & 7;
 #pragma unroll
     for (int j = 0; j < AR; ++j) {
-        const int row = ar + 32 * j;
+        const int row = ar + RS * j;
         u32x2 hi, lo;
         split4(ra[j], hi, lo);
         const int off = slot_off(row, q >> 1) + (q & 1) * 8;
@@ -61,24 +62,25 @@ __device__ __forceinline__ void store_a_x3(char *As, int tid, const f4 (&ra)[AR]
     }
 }
 
-// pre-split packed weights: thread loads 16 bytes (one slot) of rows br + 32 j
-template <int BR>
+// pre-split packed weights: thread loads 16 bytes (one slot) of rows br + RS j
+template <int BR, int RS>
 __device__ __forceinline__ void load_b_x3(const ConvArgs &a, const char *__restrict__ wt, int kt, int n0, int tid,
                                           u32x4 (&rb)[BR]) {
     const int br = tid >> 3, sl = tid & 7;
     const char *p = wt + ((long long)(n0 + br) * a.kpad + kt * 32) * 4 + sl * 16;
 #pragma unroll
-    for (int j = 0; j < BR; ++j) rb[j] = *(const u32x4 *)(p + (long long)32 * j * a.kpad * 4);
+    for (int j = 0; j < BR; ++j) rb[j] = *(const u32x4 *)(p + (long long)RS * j * a.kpad * 4);
 }
 
-template <int BR>
+template <int BR, int RS>
 __device__ __forceinline__ void store_b_x3(char *Bs, int tid, const u32x4 (&rb)[BR]) {
     const int br = tid >> 3, sl = tid & 7;
 #pragma unroll
-    for (int j = 0; j < BR; ++j) *(u32x4 *)(Bs + slot_off(br + 32 * j, sl)) = rb[j];
+    for (int j = 0; j < BR; ++j) *(u32x4 *)(Bs + slot_off(br + RS * j, sl)) = rb[j];
 }
 
-// activation B ([K][ldb] fp32, b_kn): split on the fly, scattered 2-byte stores (small GEMMs only)
+// activation B ([K][ldb] fp32, b_kn, 256 threads): split on the fly, scattered 2-byte stores
+// (small GEMMs only)
 template <int BN, int BR>
 __device__ __forceinline__ void store_b_kn_x3(char *Bs, int tid, const f4 (&rb)[BR]) {
     constexpr int NV = BN / 4, RPP = 256 / NV;
@@ -98,17 +100,64 @@ __device__ __forceinline__ void store_b_kn_x3(char *Bs, int tid, const f4 (&rb)[
     }
 }
 
-template <int BM, int BN, int WAVES_M, int AMODE, int BKN>
-__global__ __launch_bounds__(256, 1) void conv_igemm_x3(ConvArgs a) {
-    constexpr int WAVES_N = 4 / WAVES_M;
+// K-slice cursor.  Slice kt = tap * nsl + cs covers channels [32 cs, 32 cs + 32) of filter tap
+// ``tap`` = ky * kw + kx.  With ``kperm`` (AMODE 0/3 multi-tap convs) slices are visited
+// channel-slice-major — all taps of one 32-channel slice in a row, so a 3x3 neighbourhood is
+// re-read from L2 right away; the weights are indexed by the same kt, so the sum is the same up
+// to fp32 summation order.  Otherwise in natural k order.  Advancing needs no division.
+struct SliceIt {
+    int i, tap, cs, ky, kx;
+    __device__ __forceinline__ void init(int i0, bool kperm, int taps, int nsl, int kw) {
+        i = i0;
+        if (kperm) { tap = i0 % taps; cs = i0 / taps; }
+        else if (nsl > 0) { tap = i0 / nsl; cs = i0 - tap * nsl; }
+        else { tap = 0; cs = 0; }                 // generic gathers only use i
+        ky = tap / kw;
+        kx = tap - ky * kw;
+    }
+    __device__ __forceinline__ void next(bool kperm, int taps, int nsl, int kw) {
+        ++i;
+        if (kperm) {
+            ++tap; ++kx;
+            if (kx == kw) { kx = 0; ++ky; }
+            if (tap == taps) { tap = 0; ky = 0; kx = 0; ++cs; }
+        } else {
+            ++cs;
+            if (cs == nsl) { cs = 0; ++tap; ++kx; if (kx == kw) { kx = 0; ++ky; } }
+        }
+    }
+    __device__ __forceinline__ int kt(int nsl) const { return tap * nsl + cs; }
+};
+
+constexpr int x3_chunk(int bm, int bn, int smem) {
+    int ch = bm;
+    while (ch > 32 && ch * (bn + 4) * 4 > smem) ch /= 2;
+    return ch;
+}
+
+// BM x BN tile, NW waves (WAVES_M x NW/WAVES_M), KS 32-deep K-slices per LDS stage (two stages),
+// PF register stages of prefetch (1: slice group t+1 in flight during group t; 2: t+2).
+// Measured on MI355X (tools/conv_micro.py, r01): KS = 1, PF = 1 with 8 waves (two or more waves
+// per SIMD hide each other's load waits) beats deeper register prefetch (PF = 2 costs ~64 VGPRs and
+// drops to one wave per SIMD: -40 %) and BK = 64 stages (KS = 2: LDS for one block per CU: -40 %).
+template <int BM, int BN, int WAVES_M, int NW, int KS, int PF, int AMODE, int BKN>
+__global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3(ConvArgs a) {
+    constexpr int NT = 64 * NW, RS = NT / 8;
+    constexpr int WAVES_N = NW / WAVES_M;
     constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
     constexpr int TM = WTM / 32, TN = WTN / 32;
-    constexpr int AR = BM / 32;
-    constexpr int BR = BN / 32;
-    constexpr int STAGE = (BM + BN) * 128;                    // bytes
-    constexpr int CBYTES = BM * (BN + 4) * 4;                 // epilogue C staging
-    constexpr int SMEM = 2 * STAGE > CBYTES ? 2 * STAGE : CBYTES;
-    static_assert(TM >= 1 && TN >= 1 && WTM % 32 == 0 && WTN % 32 == 0, "tile");
+    constexpr int AR = BM / RS;
+    constexpr int BR = BN / RS;
+    constexpr int SUB = (BM + BN) * 128;                      // one K-slice of A and B (bytes)
+    constexpr int STAGE = KS * SUB;
+    constexpr int OPS = 2 * STAGE;
+    constexpr int CH = x3_chunk(BM, BN, OPS > 65536 ? OPS : 65536);
+    constexpr int CBYTES = CH * (BN + 4) * 4;                 // epilogue C staging
+    constexpr int SMEM = OPS > CBYTES ? OPS : CBYTES;
+    static_assert(TM >= 1 && TN >= 1 && WTM % 32 == 0 && WTN % 32 == 0 && AR >= 1 && BR >= 1, "tile");
+    static_assert(!BKN || NW == 4, "b_kn operands only with 4 waves");
+    static_assert(SMEM <= 160 * 1024, "LDS");
+    constexpr int BKR = BKN ? BN / 32 : 1;                    // b_kn loader rows (256 threads)
 
     __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
@@ -137,15 +186,14 @@ __global__ __launch_bounds__(256, 1) void conv_igemm_x3(ConvArgs a) {
     const int kt1 = min(a.ktiles, kt0 + a.tps);
     const int taps = a.kh * a.kw, nsl = a.cin >> 5;
     const bool kperm = (AMODE == 0 || AMODE == 3) && !BKN && taps > 1;
-    auto kmap = [&](int i) { return kperm ? (i % taps) * nsl + i / taps : i; };
     const int ak = (tid & 7) * 4;
 
     ARows<AR, AMODE> R;
-    a_rows_init<AR, AMODE>(a, m0, tid >> 3, R);
+    a_rows_init<AR, AMODE, RS>(a, m0, tid >> 3, R);
 
-    f4 ra[AR];
-    u32x4 rbp[BKN ? 1 : BR];
-    f4 rbk[BKN ? BR : 1];
+    f4 ra[PF][KS][AR];
+    u32x4 rbp[PF][KS][BKN ? 1 : BR];
+    f4 rbk[PF][KS][BKN ? BKR : 1];
     floatx16 acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -154,83 +202,135 @@ __global__ __launch_bounds__(256, 1) void conv_igemm_x3(ConvArgs a) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    auto load = [&](int kt) {
-        load_a<AR, AMODE>(a, x, kt, ak, R, ra);
-        if constexpr (BKN) load_b<BN, BR, 1>(a, wtf, kt, n0, tid, rbk);
-        else load_b_x3<BR>(a, wtb, kt, n0, tid, rbp);
+    SliceIt ld;                      // the next K-slice to load
+    ld.init(kt0, kperm, taps, nsl, a.kw);
+    // load one group of KS slices into register set p (slices past the end re-load the last one;
+    // their products are never formed)
+    auto issue = [&](int p) {
+#pragma unroll
+        for (int u = 0; u < KS; ++u) {
+            const int kt = (AMODE == 0 || AMODE == 3) ? ld.kt(nsl) : ld.i;
+            if constexpr (AMODE == 0 || AMODE == 3)
+                load_a_tap<AR, AMODE>(a, x, ld.ky, ld.kx, ld.cs * 32 + ak, R, ra[p][u]);
+            else
+                load_a<AR, AMODE>(a, x, kt, ak, R, ra[p][u]);
+            if constexpr (BKN) load_b<BN, BKR, 1>(a, wtf, kt, n0, tid, rbk[p][u]);
+            else load_b_x3<BR, RS>(a, wtb, kt, n0, tid, rbp[p][u]);
+            if (ld.i < kt1 - 1) ld.next(kperm, taps, nsl, a.kw);
+        }
     };
-    auto store = [&](char *st) {
-        store_a_x3<BM, AR>(st, tid, ra);
-        if constexpr (BKN) store_b_kn_x3<BN, BR>(st + BM * 128, tid, rbk);
-        else store_b_x3<BR>(st + BM * 128, tid, rbp);
+    auto store = [&](char *st, int p) {
+#pragma unroll
+        for (int u = 0; u < KS; ++u) {
+            char *sb = st + u * SUB;
+            store_a_x3<AR, RS>(sb, tid, ra[p][u]);
+            if constexpr (BKN) store_b_kn_x3<BN, BKR>(sb + BM * 128, tid, rbk[p][u]);
+            else store_b_x3<BR, RS>(sb + BM * 128, tid, rbp[p][u]);
+        }
     };
 
     const int li = lane & 31, lh = lane >> 5;
     const int rsw = swz(li);     // rows wm*WTM + i*32 + li share li's swizzle (tile bases are multiples of 32)
-    if (kt0 < kt1) {
-        load(kmap(kt0));
-        store(smem);
-        __syncthreads();
-    }
-    int buf = 0;
-    for (int kt = kt0; kt < kt1; ++kt) {
-        load(kmap(min(kt + 1, kt1 - 1)));
-        __builtin_amdgcn_sched_barrier(0);   // keep the prefetch issue above the MFMA block
-        const char *As = smem + buf * STAGE;
-        const char *Bs = As + BM * 128;
+    // multiply ``nv`` (<= KS) slices of one stage
+    auto compute = [&](const char *st, int nv) {
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const int hs = ((2 * s + lh) ^ rsw) << 4, ls = hs ^ 64;
-            bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
+        for (int u = 0; u < KS; ++u) {
+            if (u >= nv) break;
+            const char *As = st + u * SUB;
+            const char *Bs = As + BM * 128;
 #pragma unroll
-            for (int i = 0; i < TM; ++i) {
-                const char *p = As + (wm * WTM + i * 32 + li) * 128;
-                ah[i] = *(const bf16x8 *)(p + hs);
-                al[i] = *(const bf16x8 *)(p + ls);
-            }
+            for (int s = 0; s < 2; ++s) {
+                const int hs = ((2 * s + lh) ^ rsw) << 4, ls = hs ^ 64;
+                bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
 #pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                const char *p = Bs + (wn * WTN + j * 32 + li) * 128;
-                bh[j] = *(const bf16x8 *)(p + hs);
-                bl[j] = *(const bf16x8 *)(p + ls);
-            }
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
+                for (int i = 0; i < TM; ++i) {
+                    const char *p = As + (wm * WTM + i * 32 + li) * 128;
+                    ah[i] = *(const bf16x8 *)(p + hs);
+                    al[i] = *(const bf16x8 *)(p + ls);
+                }
 #pragma unroll
                 for (int j = 0; j < TN; ++j) {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+                    const char *p = Bs + (wn * WTN + j * 32 + li) * 128;
+                    bh[j] = *(const bf16x8 *)(p + hs);
+                    bl[j] = *(const bf16x8 *)(p + ls);
                 }
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) {
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+                    }
+            }
         }
-        store(smem + (buf ^ 1) * STAGE);     // the other buffer was last read before the previous barrier
+    };
+
+    const int n = kt1 - kt0;
+    const int ng = (n + KS - 1) / KS;            // stage groups
+    if (ng > 0) {
+        issue(0);
+        store(smem, 0);
         __syncthreads();
-        buf ^= 1;
+        if (PF == 1) {
+            // group g: load g+1 into the registers, multiply stage g%2, store g+1 into the other
+            // stage (last read before the previous barrier)
+            for (int g = 0; g < ng; ++g) {
+                issue(0);
+                __builtin_amdgcn_sched_barrier(0);
+                compute(smem + (g & 1) * STAGE, min(KS, n - g * KS));
+                store(smem + ((g + 1) & 1) * STAGE, 0);
+                __syncthreads();
+            }
+        } else {
+            issue(PF - 1);
+            // group g: load g+2 into set g%2, multiply stage g%2, store set (g+1)%2 (group g+1)
+            for (int g = 0; g < ng; g += 2) {
+                issue(0);
+                __builtin_amdgcn_sched_barrier(0);
+                compute(smem, min(KS, n - g * KS));
+                store(smem + STAGE, PF - 1);
+                __syncthreads();
+                if (g + 1 >= ng) break;
+                issue(PF - 1);
+                __builtin_amdgcn_sched_barrier(0);
+                compute(smem + STAGE, min(KS, n - (g + 1) * KS));
+                store(smem, 0);
+                __syncthreads();
+            }
+        }
     }
-    epilogue_tile<BM, BN, WAVES_M, TM, TN>(a, acc, (float *)smem, tid, m0, n0, bz, bidx);
+    epilogue_tile<BM, BN, WAVES_M, TM, TN, NW, CH>(a, acc, (float *)smem, tid, m0, n0, bz, bidx);
 }
 
-template <int BM, int BN, int WM>
-static void launch_tile_x3(const ConvArgs &a, int amode, bool bkn, dim3 grid, hipStream_t s) {
-    switch (amode * 2 + (bkn ? 1 : 0)) {
-        case 0: conv_igemm_x3<BM, BN, WM, 0, 0><<<grid, 256, 0, s>>>(a); break;
-        case 1: conv_igemm_x3<BM, BN, WM, 0, 1><<<grid, 256, 0, s>>>(a); break;
-        case 2: conv_igemm_x3<BM, BN, WM, 1, 0><<<grid, 256, 0, s>>>(a); break;
-        case 3: conv_igemm_x3<BM, BN, WM, 1, 1><<<grid, 256, 0, s>>>(a); break;
-        case 4: conv_igemm_x3<BM, BN, WM, 2, 0><<<grid, 256, 0, s>>>(a); break;
-        case 5: conv_igemm_x3<BM, BN, WM, 2, 1><<<grid, 256, 0, s>>>(a); break;
-        default: conv_igemm_x3<BM, BN, WM, 3, 0><<<grid, 256, 0, s>>>(a); break;
+template <int BM, int BN, int WM, int NW, int KS, int PF>
+static void launch_x3(const ConvArgs &a, int amode, bool bkn, dim3 grid, hipStream_t s) {
+    constexpr int NT = 64 * NW;
+    if (bkn) {
+        if constexpr (NW == 4) {
+            if (amode == 0) conv_igemm_x3<BM, BN, WM, NW, KS, PF, 0, 1><<<grid, NT, 0, s>>>(a);
+            else if (amode == 1) conv_igemm_x3<BM, BN, WM, NW, KS, PF, 1, 1><<<grid, NT, 0, s>>>(a);
+            else conv_igemm_x3<BM, BN, WM, NW, KS, PF, 2, 1><<<grid, NT, 0, s>>>(a);
+        }
+        return;
+    }
+    switch (amode) {
+        case 0: conv_igemm_x3<BM, BN, WM, NW, KS, PF, 0, 0><<<grid, NT, 0, s>>>(a); break;
+        case 1: conv_igemm_x3<BM, BN, WM, NW, KS, PF, 1, 0><<<grid, NT, 0, s>>>(a); break;
+        case 2: conv_igemm_x3<BM, BN, WM, NW, KS, PF, 2, 0><<<grid, NT, 0, s>>>(a); break;
+        default: conv_igemm_x3<BM, BN, WM, NW, KS, PF, 3, 0><<<grid, NT, 0, s>>>(a); break;
     }
 }
 
-void launch_conv_x3(int tile, const ConvArgs &a, int amode, bool bkn, dim3 grid, hipStream_t s) {
-    switch (tile) {
-        case 0: launch_tile_x3<128, 128, 2>(a, amode, bkn, grid, s); break;
-        case 1: launch_tile_x3<128, 64, 2>(a, amode, bkn, grid, s); break;
-        case 2: launch_tile_x3<64, 128, 2>(a, amode, bkn, grid, s); break;
-        case 3: launch_tile_x3<64, 64, 2>(a, amode, bkn, grid, s); break;
-        case 4: launch_tile_x3<256, 32, 4>(a, amode, bkn, grid, s); break;
-        default: launch_tile_x3<128, 32, 4>(a, amode, bkn, grid, s); break;
+// x3 kernel configurations (index = the host planner's tile id, conv.hip kX3Tiles)
+void launch_conv_x3(int cfg, const ConvArgs &a, int amode, bool bkn, dim3 grid, hipStream_t s) {
+    switch (cfg) {
+        case 0: launch_x3<256, 256, 2, 8, 1, 1>(a, amode, bkn, grid, s); break;
+        case 1: launch_x3<128, 128, 2, 8, 1, 1>(a, amode, bkn, grid, s); break;
+        case 2: launch_x3<64, 128, 2, 8, 1, 1>(a, amode, bkn, grid, s); break;
+        case 3: launch_x3<128, 64, 2, 4, 1, 1>(a, amode, bkn, grid, s); break;
+        case 4: launch_x3<64, 64, 2, 4, 1, 1>(a, amode, bkn, grid, s); break;
+        default: launch_x3<128, 32, 4, 4, 1, 1>(a, amode, bkn, grid, s); break;   // 5
     }
 }
 

@@ -344,20 +344,21 @@ def gemm_kn(ctx: Ctx, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, ba
 
 
 def _plan(ctx: Ctx, p):
-    out = (ctypes.c_int * 7)()
+    out = (ctypes.c_int * 10)()
     check(ctx.lib.s2v_conv2d_plan(ctypes.byref(p), out), "s2v_conv2d_plan")
     return list(out)
 
 
 def conv_symbol(ctx: Ctx, p) -> str:
     """Kernel symbol (as rocprofv3 reports it, demangled) the launch of ``p`` runs."""
-    bm, bn, wm, avec, bkn, splits, x3 = _plan(ctx, p)
+    bm, bn, wm, avec, bkn, splits, x3, nw, ks, pf = _plan(ctx, p)
     if bm == 0:
         if wm:
             return f"void s2v::conv_small_cpar<{bn}, {wm}>(s2v::ConvArgs, int)"
         return f"void s2v::conv_direct_small<{bn}>(s2v::ConvArgs, int)"
-    name = "conv_igemm_x3" if x3 else "conv_igemm"
-    return f"void s2v::{name}<{bm}, {bn}, {wm}, {avec}, {bkn}>(s2v::ConvArgs)"
+    if x3:
+        return f"void s2v::conv_igemm_x3<{bm}, {bn}, {wm}, {nw}, {ks}, {pf}, {avec}, {bkn}>(s2v::ConvArgs)"
+    return f"void s2v::conv_igemm<{bm}, {bn}, {wm}, {avec}, {bkn}>(s2v::ConvArgs)"
 
 
 def conv_splits(ctx: Ctx, p) -> int:
