@@ -154,18 +154,32 @@ __global__ __launch_bounds__(256, 1) void conv_igemm(ConvArgs a) {
     epilogue_tile<BM, BN, WAVES_M, TM, TN>(a, acc, smem, tid, m0, n0, bz, bidx);
 }
 
+// Split-K fold: one thread per 4 consecutive output channels (16-byte partial-sum loads) when
+// cout % 4 == 0, else per channel; the epilogue is the kernels' own.
 __global__ void splitk_reduce(ConvArgs a, int batch) {
-    const long long total = (long long)batch * a.M * a.cout;
+    const int cv = (a.cout & 3) == 0 ? 4 : 1;
+    const int nq = a.cout / cv;
+    const long long total = (long long)batch * a.M * nq;
+    const long long slab = (long long)a.M * a.cout;
     for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
          idx += (long long)gridDim.x * blockDim.x) {
-        const int n = (int)(idx % a.cout);
-        const long long bm = idx / a.cout;
+        const int q = (int)(idx % nq);
+        const long long bm = idx / nq;
         const int m = (int)(bm % a.M);
         const int bidx = (int)(bm / a.M);
-        float s = 0.f;
-        for (int sp = 0; sp < a.splits; ++sp)
-            s += a.ws[(((long long)bidx * a.splits + sp) * a.M + m) * a.cout + n];
-        store_epilogue(a, bidx, m, n, s);
+        const float *src = a.ws + (long long)bidx * a.splits * slab + (long long)m * a.cout + q * cv;
+        if (cv == 4) {
+            f4 s = *(const f4 *)src;
+            for (int sp = 1; sp < a.splits; ++sp) s += *(const f4 *)(src + sp * slab);
+            store_epilogue(a, bidx, m, 4 * q + 0, s.x);
+            store_epilogue(a, bidx, m, 4 * q + 1, s.y);
+            store_epilogue(a, bidx, m, 4 * q + 2, s.z);
+            store_epilogue(a, bidx, m, 4 * q + 3, s.w);
+        } else {
+            float s = src[0];
+            for (int sp = 1; sp < a.splits; ++sp) s += src[sp * slab];
+            store_epilogue(a, bidx, m, q, s);
+        }
     }
 }
 
@@ -238,8 +252,11 @@ __global__ __launch_bounds__(256) void conv_direct_small(ConvArgs a, int batch) 
 // channels (16-byte loads; consecutive lanes read consecutive bytes of the pixel row, so a wave
 // reads 64/TPP neighbouring pixels contiguously), partial dot products are combined with
 // shuffles.  Requires cin % 4 == 0 and 16-byte aligned rows.
-template <int CO, int TPP>
+// LW: the block's filter (CO x K floats of one batch entry) is staged in LDS first, so the per-tap
+// weight reads are LDS broadcasts instead of CO global loads per input float4.
+template <int CO, int TPP, bool LW>
 __global__ __launch_bounds__(256) void conv_small_cpar(ConvArgs a, int batch) {
+    extern __shared__ __attribute__((aligned(16))) float wsm_dyn[];
     const long long total = (long long)batch * a.M;
     const long long gid = (blockIdx.x * 256LL + threadIdx.x) / TPP;
     const int sub = threadIdx.x % TPP;
@@ -252,6 +269,21 @@ __global__ __launch_bounds__(256) void conv_small_cpar(ConvArgs a, int batch) {
     const int oy = rem / a.ow, ox = rem - (rem / a.ow) * a.ow;
     const float *x = a.x + (long long)bidx * a.x_bs;
     const float *wt = a.wt + (long long)bidx * a.w_bs;
+    int wstride = a.kpad;
+    if (LW) {
+        // every pixel of the block belongs to the batch entry of its first pixel (the host
+        // guarantees M % (256 / TPP) == 0 when the weights are per batch entry)
+        const long long g0 = blockIdx.x * (256LL / TPP);
+        const int b0 = (int)((g0 < total ? g0 : 0) / a.M);
+        const float *w0 = a.wt + (long long)b0 * a.w_bs;
+        for (int e = threadIdx.x; e < CO * a.K; e += 256) {
+            const int o = e / a.K, k = e - (e / a.K) * a.K;
+            wsm_dyn[e] = o < a.cout ? w0[(long long)o * a.kpad + k] : 0.f;
+        }
+        __syncthreads();
+        wt = wsm_dyn;
+        wstride = a.K;
+    }
     float acc[CO];
 #pragma unroll
     for (int o = 0; o < CO; ++o) acc[o] = 0.f;
@@ -273,7 +305,7 @@ __global__ __launch_bounds__(256) void conv_small_cpar(ConvArgs a, int batch) {
                     }
 #pragma unroll
                     for (int o = 0; o < CO; ++o) {
-                        const f4 wv = *(const f4 *)(wt + (long long)o * a.kpad + kb + c);
+                        const f4 wv = *(const f4 *)(wt + (long long)o * wstride + kb + c);
                         acc[o] = fmaf(v.x, wv.x, fmaf(v.y, wv.y, fmaf(v.z, wv.z, fmaf(v.w, wv.w, acc[o]))));
                     }
                 }
@@ -289,6 +321,18 @@ __global__ __launch_bounds__(256) void conv_small_cpar(ConvArgs a, int batch) {
         if (o < a.cout) store_epilogue(a, bidx, m, o, acc[o]);
 }
 
+// LDS weights when the filter is small next to the block's input (<= 16 KB: ToRGB 1x1s); the 7x7
+// heads keep global (L1-resident) weight reads
+template <int CO, int TPP>
+static void launch_cpar(const ConvArgs &a, int batch, hipStream_t s) {
+    const long long total = (long long)batch * a.M;
+    const unsigned grid = cdiv(total * TPP, 256);
+    const size_t wbytes = (size_t)CO * a.K * sizeof(float);
+    const bool lw = wbytes <= 16 * 1024 && (a.w_bs == 0 || batch == 1 || a.M % (256 / TPP) == 0);
+    if (lw) conv_small_cpar<CO, TPP, true><<<grid, 256, wbytes, s>>>(a, batch);
+    else conv_small_cpar<CO, TPP, false><<<grid, 256, 0, s>>>(a, batch);
+}
+
 template <int CO>
 static void launch_small(const ConvArgs &a, int batch, bool cpar, hipStream_t s) {
     const long long total = (long long)batch * a.M;
@@ -296,12 +340,10 @@ static void launch_small(const ConvArgs &a, int batch, bool cpar, hipStream_t s)
         conv_direct_small<CO><<<cdiv(total, 256), 256, 0, s>>>(a, batch);
         return;
     }
-    const int c4 = a.cin / 4;
-    if (c4 >= 64) conv_small_cpar<CO, 64><<<cdiv(total * 64, 256), 256, 0, s>>>(a, batch);
-    else if (c4 >= 32) conv_small_cpar<CO, 32><<<cdiv(total * 32, 256), 256, 0, s>>>(a, batch);
-    else if (c4 >= 16) conv_small_cpar<CO, 16><<<cdiv(total * 16, 256), 256, 0, s>>>(a, batch);
-    else if (c4 >= 8) conv_small_cpar<CO, 8><<<cdiv(total * 8, 256), 256, 0, s>>>(a, batch);
-    else conv_small_cpar<CO, 4><<<cdiv(total * 4, 256), 256, 0, s>>>(a, batch);
+    // 8 lanes per pixel (each lane walks cin/32 float4s): 3 shuffle levels per output instead of
+    // 5-6 with one float4 per lane, 128-byte contiguous row pieces per load instruction
+    if (a.cin / 4 >= 8) launch_cpar<CO, 8>(a, batch, s);
+    else launch_cpar<CO, 4>(a, batch, s);
 }
 
 // ------------------------------------------------------------------ host side
@@ -568,7 +610,7 @@ extern "C" int s2v_conv2d_plan(const s2v_conv_params *p, int *out6) {
                                                                   ((uintptr_t)p->in_scale % 16) == 0));
         const int c4 = p->cin / 4;
         out6[0] = 0; out6[1] = p->cout < 4 ? p->cout : 4;
-        out6[2] = !cpar ? 0 : (c4 >= 64 ? 64 : c4 >= 32 ? 32 : c4 >= 16 ? 16 : c4 >= 8 ? 8 : 4);
+        out6[2] = !cpar ? 0 : (c4 >= 8 ? 8 : 4);
         out6[3] = 0; out6[4] = 0; out6[5] = 1;
         return 0;
     }
@@ -628,7 +670,7 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
     }
     rc = check_launch("conv_igemm");
     if (rc || pl.splits <= 1) return rc;
-    const long long total = (long long)batch * M * p->cout;
+    const long long total = (long long)batch * M * (p->cout % 4 == 0 ? p->cout / 4 : p->cout);
     unsigned blocks = cdiv(total, 256);
     if (blocks > 65535u * 4u) blocks = 65535u * 4u;
     splitk_reduce<<<blocks, 256, 0, s>>>(a, batch);

@@ -274,13 +274,31 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3(ConvArgs a) {
         __syncthreads();
         if (PF == 1) {
             // group g: load g+1 into the registers, multiply stage g%2, store g+1 into the other
-            // stage (last read before the previous barrier)
-            for (int g = 0; g < ng; ++g) {
-                issue(0);
-                __builtin_amdgcn_sched_barrier(0);
-                compute(smem + (g & 1) * STAGE, min(KS, n - g * KS));
-                store(smem + ((g + 1) & 1) * STAGE, 0);
-                __syncthreads();
+            // stage (last read before the previous barrier).  In 8-wave blocks the two waves that
+            // share a SIMD run each step in opposite phase orders (the upper half: store the group
+            // loaded one step earlier, load the next, multiply), so one wave's split + LDS-store
+            // phase overlaps its partner's MFMAs instead of both leaving the matrix pipe idle at
+            // the same time (MI355X_MICROARCH.md, two waves per SIMD, item 9).  Either order stores
+            // into the buffer last read before the previous barrier and multiplies the one
+            // completed before it.
+            const bool late = NW == 8 && __builtin_amdgcn_readfirstlane(wave) >= NW / 2;
+            if (late) {
+                issue(0);                                        // group 1
+                for (int g = 0; g < ng; ++g) {
+                    store(smem + ((g + 1) & 1) * STAGE, 0);       // group g+1
+                    issue(0);                                    // group g+2
+                    __builtin_amdgcn_sched_barrier(0);
+                    compute(smem + (g & 1) * STAGE, min(KS, n - g * KS));
+                    __syncthreads();
+                }
+            } else {
+                for (int g = 0; g < ng; ++g) {
+                    issue(0);
+                    __builtin_amdgcn_sched_barrier(0);
+                    compute(smem + (g & 1) * STAGE, min(KS, n - g * KS));
+                    store(smem + ((g + 1) & 1) * STAGE, 0);
+                    __syncthreads();
+                }
             }
         } else {
             issue(PF - 1);

@@ -144,135 +144,174 @@ __global__ __launch_bounds__(256) void irfft2_kernel(const float *__restrict__ s
 }
 
 // ---------------------------------------------------------------------------------------------
-// Register-blocked variants for the LNet sizes (12, 24, 48): each thread keeps a whole output
-// row / column of accumulators and the 1-D matrices are read with wave-uniform indices straight
-// from global memory (scalar loads into SGPRs), so LDS carries only the data (one read per
-// input element per pass) instead of one LDS read per multiply-add.
+// MFMA variants for the LNet sizes (H == W in {12, 24, 48}): one block per (image, 4-channel
+// group); both 1-D passes of the tile run as small GEMMs out of LDS on v_mfma_f32_32x32x2_f32
+// (exact fp32 products and sums, the k-ordered fma chains of the generic kernels):
+//   rfft2   W pass  Y[(p,h)][(v,c)] = sum_w fw[w][p][v] X[h][w][c]        rows (p,v), K = w
+//           H pass  Z[q][u][(v,c)]  = sum_h fh[h][u] * Y[h][(v,c)]       complex, rows u, K = h
+//   irfft2  H pass  Y[p][h][(v,c)]  = sum_u ih[u][h] * Z[u][(v,c)]       complex, rows h, K = u
+//           W pass  y[h][w][c]      = sum_(v,p) iw[v][p][w] Y[(p,h)][(v,c)]   rows w, K = 2v + p
+// 32x32x2 f32 operand maps: lane l holds A[l & 31][k0 + (l >> 5)] and B[k0 + (l >> 5)][l & 31];
+// the accumulator holds column l & 31, rows (r & 3) + 8 (r >> 2) + 4 (l >> 5).  Against the
+// VALU register-blocked form this replaces (one thread per output row, 1.4M serial fmas per
+// block), the 4 waves of a block now share every pass.
+typedef float mf16 __attribute__((ext_vector_type(16)));
 constexpr int FCG = 4;   // channels per block
 
-template <int H, int W>
-__global__ __launch_bounds__(256) void rfft2_rb(const float *__restrict__ x, int C, int xcs,
+__device__ __forceinline__ int mf_row(int r, int lh) { return (r & 3) + 8 * (r >> 2) + 4 * lh; }
+
+__device__ __forceinline__ mf16 mfma32(float a, float b, mf16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+template <int H>
+__global__ __launch_bounds__(256) void rfft2_mf(const float *__restrict__ x, int C, int xcs,
                                                 const float *__restrict__ tables, float *__restrict__ spec,
                                                 int scs) {
-    constexpr int WF = W / 2 + 1;
-    constexpr int XS = W * FCG + 4;
-    constexpr int UC = H >= 24 ? H / 2 : H;          // u rows per H-pass item
+    constexpr int W = H, WF = W / 2 + 1;
+    constexpr int XS = W * FCG + 4;                  // X row pitch: the B reads of 8 rows hit distinct banks
+    constexpr int N1 = H * FCG, N2 = WF * FCG;       // W-pass columns (h, c), H-pass columns (v, c)
+    constexpr int T1M = (2 * WF + 31) / 32, T1N = (N1 + 31) / 32;
+    constexpr int T2M = (H + 31) / 32, T2N = (N2 + 31) / 32;
     __shared__ float X[H * XS];
-    __shared__ float Y[H * WF * 2 * FCG];
+    __shared__ float Y[2 * H * N2];                  // [(p, h)][(v, c)]
+    __shared__ float Tw[W * 2 * WF];                 // fw[w][p][v]
+    __shared__ float Th[H * 2 * H];                  // fh[h][p][u]
     const int groups = C / FCG;
     const int n = blockIdx.x / groups, c0 = (blockIdx.x - n * groups) * FCG;
+    const int tid = threadIdx.x, wave = tid >> 6, li = tid & 31, lh = (tid >> 5) & 1;
     const FftTables T = fft_tables(tables, H, W);
-    for (int p = threadIdx.x; p < H * W; p += 256) {
+    for (int i = tid; i < W * 2 * WF; i += 256) Tw[i] = T.fw[i];
+    for (int i = tid; i < H * 2 * H; i += 256) Th[i] = T.fh[i];
+    for (int p = tid; p < H * W; p += 256) {
         const int hh = p / W, ww = p - hh * W;
         *(float4 *)&X[hh * XS + ww * FCG] = *(const float4 *)&x[((long long)n * H * W + p) * xcs + c0];
     }
     __syncthreads();
-    if (threadIdx.x < H * FCG) {                      // W pass: item (h, cg), all WF bins
-        const int h = threadIdx.x / FCG, cg = threadIdx.x % FCG;
-        float re[WF], im[WF];
-#pragma unroll
-        for (int v = 0; v < WF; ++v) re[v] = im[v] = 0.f;
-        for (int w = 0; w < W; ++w) {
-            const float xv = X[h * XS + w * FCG + cg];
-#pragma unroll
-            for (int v = 0; v < WF; ++v) {
-                re[v] = fmaf(T.fw[(w * 2 + 0) * WF + v], xv, re[v]);
-                im[v] = fmaf(T.fw[(w * 2 + 1) * WF + v], xv, im[v]);
-            }
+    for (int t = wave; t < T1M * T1N; t += 4) {      // W pass (real -> half spectrum)
+        const int tm = t / T1N, tn = t - tm * T1N;
+        const int i = tm * 32 + li, j = tn * 32 + li;
+        const bool iok = i < 2 * WF, jok = j < N1;
+        const float *xb = X + (j / FCG) * XS + (j % FCG);
+        mf16 acc = {};
+        for (int k0 = 0; k0 < W; k0 += 2) {
+            const int k = k0 + lh;
+            acc = mfma32(iok ? Tw[k * 2 * WF + i] : 0.f, jok ? xb[k * FCG] : 0.f, acc);
         }
+        if (jok) {
+            const int hh = j / FCG, cc = j % FCG;
 #pragma unroll
-        for (int v = 0; v < WF; ++v) {
-            Y[((h * WF + v) * 2 + 0) * FCG + cg] = re[v];
-            Y[((h * WF + v) * 2 + 1) * FCG + cg] = im[v];
+            for (int r = 0; r < 16; ++r) {
+                const int row = tm * 32 + mf_row(r, lh);
+                if (row < 2 * WF) {
+                    const int p = row >= WF ? 1 : 0, v = row - p * WF;
+                    Y[(p * H + hh) * N2 + v * FCG + cc] = acc[r];
+                }
+            }
         }
     }
     __syncthreads();
-    // H pass: item (v, cg) of u-chunk q; each chunk padded to whole waves so that u0 (and with it
-    // every table index) is wave-uniform
-    constexpr int IPC = (WF * FCG + 63) / 64 * 64;
-    for (int it = threadIdx.x; it < IPC * (H / UC); it += 256) {
-        const int q = it / IPC, r = it - q * IPC;
-        if (r >= WF * FCG) continue;
-        const int cg = r % FCG;
-        const int v = r / FCG, u0 = q * UC;
-        float zr[UC], zi[UC];
-#pragma unroll
-        for (int u = 0; u < UC; ++u) zr[u] = zi[u] = 0.f;
-        for (int h = 0; h < H; ++h) {
-            const float yr = Y[((h * WF + v) * 2 + 0) * FCG + cg], yi = Y[((h * WF + v) * 2 + 1) * FCG + cg];
-#pragma unroll
-            for (int u = 0; u < UC; ++u) {
-                const float fr = T.fh[(h * 2 + 0) * H + u0 + u], fi = T.fh[(h * 2 + 1) * H + u0 + u];
-                zr[u] = fmaf(fr, yr, fmaf(-fi, yi, zr[u]));
-                zi[u] = fmaf(fi, yr, fmaf(fr, yi, zi[u]));
-            }
+    for (int t = wave; t < T2M * T2N; t += 4) {      // H pass (complex)
+        const int tm = t / T2N, tn = t - tm * T2N;
+        const int u = tm * 32 + li, j = tn * 32 + li;
+        const bool uok = u < H, jok = j < N2;
+        mf16 zr = {}, zi = {};
+        for (int k0 = 0; k0 < H; k0 += 2) {
+            const int h = k0 + lh;
+            const float fr = uok ? Th[(h * 2 + 0) * H + u] : 0.f, fi = uok ? Th[(h * 2 + 1) * H + u] : 0.f;
+            const float yr = jok ? Y[h * N2 + j] : 0.f, yi = jok ? Y[(H + h) * N2 + j] : 0.f;
+            zr = mfma32(-fi, yi, zr);
+            zr = mfma32(fr, yr, zr);
+            zi = mfma32(fr, yi, zi);
+            zi = mfma32(fi, yr, zi);
         }
+        if (jok) {
+            const int v = j / FCG, cc = j % FCG;
 #pragma unroll
-        for (int u = 0; u < UC; ++u) {
-            float *o = spec + ((long long)n * H * WF + (u0 + u) * WF + v) * scs + c0 + cg;
-            o[0] = zr[u];
-            o[C] = zi[u];
+            for (int r = 0; r < 16; ++r) {
+                const int uu = tm * 32 + mf_row(r, lh);
+                if (uu < H) {
+                    float *o = spec + ((long long)n * H * WF + uu * WF + v) * scs + c0 + cc;
+                    o[0] = zr[r];
+                    o[C] = zi[r];
+                }
+            }
         }
     }
 }
 
-template <int H, int W>
-__global__ __launch_bounds__(256) void irfft2_rb(const float *__restrict__ spec, int C, int scs,
+template <int H>
+__global__ __launch_bounds__(256) void irfft2_mf(const float *__restrict__ spec, int C, int scs,
                                                  const float *__restrict__ tables, const float *__restrict__ res,
                                                  int rcs, float *__restrict__ y, int ycs) {
-    constexpr int WF = W / 2 + 1;
-    constexpr int HC = H >= 24 ? H / 2 : H;          // h rows per inverse-H item
-    __shared__ float Z[H * WF * 2 * FCG];
-    __shared__ float Y[H * WF * 2 * FCG];
+    constexpr int W = H, WF = W / 2 + 1;
+    constexpr int N1 = WF * FCG, N2 = H * FCG;       // H-pass columns (v, c), W-pass columns (h, c)
+    constexpr int T1M = (H + 31) / 32, T1N = (N1 + 31) / 32;
+    constexpr int T2M = (W + 31) / 32, T2N = (N2 + 31) / 32;
+    __shared__ float Z[2 * H * N1];                  // [(q, u)][(v, c)]
+    __shared__ float Y[2 * H * N1];                  // [(p, h)][(v, c)]
+    __shared__ float Ti[H * 2 * H];                  // ih[u][p][h]
+    __shared__ float Tw[WF * 2 * W];                 // iw[v][p][w]
     const int groups = C / FCG;
     const int n = blockIdx.x / groups, c0 = (blockIdx.x - n * groups) * FCG;
+    const int tid = threadIdx.x, wave = tid >> 6, li = tid & 31, lh = (tid >> 5) & 1;
     const FftTables T = fft_tables(tables, H, W);
-    for (int i = threadIdx.x; i < H * WF * 2; i += 256) {
-        const int part = i & 1, f = i >> 1;
-        *(float4 *)&Z[(f * 2 + part) * FCG] = *(const float4 *)&spec[((long long)n * H * WF + f) * scs + part * C + c0];
+    for (int i = tid; i < H * 2 * H; i += 256) Ti[i] = T.ih[i];
+    for (int i = tid; i < WF * 2 * W; i += 256) Tw[i] = T.iw[i];
+    for (int i = tid; i < H * WF * 2; i += 256) {
+        const int q = i & 1, f = i >> 1;
+        const int u = f / WF, v = f - u * WF;
+        *(float4 *)&Z[(q * H + u) * N1 + v * FCG] =
+            *(const float4 *)&spec[((long long)n * H * WF + f) * scs + q * C + c0];
     }
     __syncthreads();
-    constexpr int IPC = (WF * FCG + 63) / 64 * 64;   // inverse H: item (v, cg) of h-chunk q (wave-uniform h0)
-    for (int it = threadIdx.x; it < IPC * (H / HC); it += 256) {
-        const int q = it / IPC, r = it - q * IPC;
-        if (r >= WF * FCG) continue;
-        const int cg = r % FCG;
-        const int v = r / FCG, h0 = q * HC;
-        float yr[HC], yi[HC];
+    for (int t = wave; t < T1M * T1N; t += 4) {      // inverse H pass (complex)
+        const int tm = t / T1N, tn = t - tm * T1N;
+        const int h = tm * 32 + li, j = tn * 32 + li;
+        const bool hok = h < H, jok = j < N1;
+        mf16 yr = {}, yi = {};
+        for (int k0 = 0; k0 < H; k0 += 2) {
+            const int u = k0 + lh;
+            const float gr = hok ? Ti[(u * 2 + 0) * H + h] : 0.f, gi = hok ? Ti[(u * 2 + 1) * H + h] : 0.f;
+            const float zr = jok ? Z[u * N1 + j] : 0.f, zi = jok ? Z[(H + u) * N1 + j] : 0.f;
+            yr = mfma32(-gi, zi, yr);
+            yr = mfma32(gr, zr, yr);
+            yi = mfma32(gr, zi, yi);
+            yi = mfma32(gi, zr, yi);
+        }
+        if (jok) {
 #pragma unroll
-        for (int h = 0; h < HC; ++h) yr[h] = yi[h] = 0.f;
-        for (int u = 0; u < H; ++u) {
-            const float zr = Z[((u * WF + v) * 2 + 0) * FCG + cg], zi = Z[((u * WF + v) * 2 + 1) * FCG + cg];
-#pragma unroll
-            for (int h = 0; h < HC; ++h) {
-                const float gr = T.ih[(u * 2 + 0) * H + h0 + h], gi = T.ih[(u * 2 + 1) * H + h0 + h];
-                yr[h] = fmaf(gr, zr, fmaf(-gi, zi, yr[h]));
-                yi[h] = fmaf(gi, zr, fmaf(gr, zi, yi[h]));
+            for (int r = 0; r < 16; ++r) {
+                const int hh = tm * 32 + mf_row(r, lh);
+                if (hh < H) {
+                    Y[hh * N1 + j] = yr[r];
+                    Y[(H + hh) * N1 + j] = yi[r];
+                }
             }
         }
-#pragma unroll
-        for (int h = 0; h < HC; ++h) {
-            Y[(((h0 + h) * WF + v) * 2 + 0) * FCG + cg] = yr[h];
-            Y[(((h0 + h) * WF + v) * 2 + 1) * FCG + cg] = yi[h];
-        }
     }
     __syncthreads();
-    if (threadIdx.x < H * FCG) {                      // c2r W pass: item (h, cg), all W outputs
-        const int h = threadIdx.x / FCG, cg = threadIdx.x % FCG;
-        float acc[W];
-#pragma unroll
-        for (int w = 0; w < W; ++w) acc[w] = 0.f;
-        for (int v = 0; v < WF; ++v) {
-            const float a = Y[((h * WF + v) * 2 + 0) * FCG + cg], b = Y[((h * WF + v) * 2 + 1) * FCG + cg];
-#pragma unroll
-            for (int w = 0; w < W; ++w) acc[w] = fmaf(T.iw[(v * 2 + 0) * W + w], a, fmaf(T.iw[(v * 2 + 1) * W + w], b, acc[w]));
+    for (int t = wave; t < T2M * T2N; t += 4) {      // c2r W pass
+        const int tm = t / T2N, tn = t - tm * T2N;
+        const int w = tm * 32 + li, j = tn * 32 + li;
+        const bool wok = w < W, jok = j < N2;
+        const int hh = j / FCG, cc = j % FCG;
+        mf16 acc = {};
+        for (int k0 = 0; k0 < 2 * WF; k0 += 2) {
+            const int k = k0 + lh, v = k >> 1, p = k & 1;     // k = 2 v + p
+            acc = mfma32(wok ? Tw[k * W + w] : 0.f, jok ? Y[(p * H + hh) * N1 + v * FCG + cc] : 0.f, acc);
         }
+        if (jok) {
 #pragma unroll
-        for (int w = 0; w < W; ++w) {
-            const long long p = (long long)n * H * W + h * W + w;
-            float o = acc[w];
-            if (res) o += res[p * rcs + c0 + cg];
-            y[p * ycs + c0 + cg] = o;
+            for (int r = 0; r < 16; ++r) {
+                const int ww = tm * 32 + mf_row(r, lh);
+                if (ww < W) {
+                    const long long pix = ((long long)n * H + hh) * W + ww;
+                    float o = acc[r];
+                    if (res) o += res[pix * rcs + c0 + cc];
+                    y[pix * ycs + c0 + cc] = o;
+                }
+            }
         }
     }
 }
@@ -306,9 +345,9 @@ extern "C" int s2v_rfft2(const float *x, int n, int h, int w, int c, int xcs, co
     hipStream_t st = (hipStream_t)stream;
     if (c % FCG == 0 && aligned && h == w && (h == 12 || h == 24 || h == 48)) {
         const unsigned grid = n * (c / FCG);
-        if (h == 12) rfft2_rb<12, 12><<<grid, 256, 0, st>>>(x, c, xcs, tables, spec, scs);
-        else if (h == 24) rfft2_rb<24, 24><<<grid, 256, 0, st>>>(x, c, xcs, tables, spec, scs);
-        else rfft2_rb<48, 48><<<grid, 256, 0, st>>>(x, c, xcs, tables, spec, scs);
+        if (h == 12) rfft2_mf<12><<<grid, 256, 0, st>>>(x, c, xcs, tables, spec, scs);
+        else if (h == 24) rfft2_mf<24><<<grid, 256, 0, st>>>(x, c, xcs, tables, spec, scs);
+        else rfft2_mf<48><<<grid, 256, 0, st>>>(x, c, xcs, tables, spec, scs);
         return check_launch("rfft2");
     }
     const size_t smem = (per * cg + fixed) * sizeof(float);
@@ -333,9 +372,9 @@ extern "C" int s2v_irfft2(const float *spec, int n, int h, int w, int c, int scs
     hipStream_t st = (hipStream_t)stream;
     if (c % FCG == 0 && h == w && (h == 12 || h == 24 || h == 48)) {
         const unsigned grid = n * (c / FCG);
-        if (h == 12) irfft2_rb<12, 12><<<grid, 256, 0, st>>>(spec, c, scs, tables, res, rcs, y, ycs);
-        else if (h == 24) irfft2_rb<24, 24><<<grid, 256, 0, st>>>(spec, c, scs, tables, res, rcs, y, ycs);
-        else irfft2_rb<48, 48><<<grid, 256, 0, st>>>(spec, c, scs, tables, res, rcs, y, ycs);
+        if (h == 12) irfft2_mf<12><<<grid, 256, 0, st>>>(spec, c, scs, tables, res, rcs, y, ycs);
+        else if (h == 24) irfft2_mf<24><<<grid, 256, 0, st>>>(spec, c, scs, tables, res, rcs, y, ycs);
+        else irfft2_mf<48><<<grid, 256, 0, st>>>(spec, c, scs, tables, res, rcs, y, ycs);
         return check_launch("irfft2");
     }
     const size_t smem = (per * cg + fixed) * sizeof(float);
