@@ -183,6 +183,102 @@ __global__ void splitk_reduce(ConvArgs a, int batch) {
     }
 }
 
+// Epilogue of 4 consecutive output channels [n, n + 4) of row m as one 16-byte store (host
+// guarantees 16-byte aligned rows: ycs, res_cs % 4 == 0; n % 4 == 0); per-element otherwise.
+__device__ __forceinline__ void store_epilogue4(const ConvArgs &a, int bidx, int m, int n, f4 v, bool vec) {
+    const Epi &e = a.epi;
+    if (!vec || e.nc_scale || (e.res && !e.res_simple) || a.y_step > 1) {
+        store_epilogue(a, bidx, m, n + 0, v.x);
+        store_epilogue(a, bidx, m, n + 1, v.y);
+        store_epilogue(a, bidx, m, n + 2, v.z);
+        store_epilogue(a, bidx, m, n + 3, v.w);
+        return;
+    }
+    if (e.scale) v *= *(const f4 *)(e.scale + n);
+    if (e.shift) v += *(const f4 *)(e.shift + n);
+    if (e.pix_add) v += e.pix_w * e.pix_add[(long long)bidx * a.oh * a.ow * a.n + m];
+    f4 r = {0.f, 0.f, 0.f, 0.f};
+    if (e.res) {
+        r = *(const f4 *)(e.res + (long long)bidx * a.res_bs + (long long)m * e.res_cs + n);
+        if (!e.res_after) v += r;
+    }
+    v.x = apply_act(v.x, e.act, e.alpha);
+    v.y = apply_act(v.y, e.act, e.alpha);
+    v.z = apply_act(v.z, e.act, e.alpha);
+    v.w = apply_act(v.w, e.act, e.alpha);
+    if (e.res && e.res_after) v += r;
+    *(f4 *)(a.y + (long long)bidx * a.y_bs + (long long)m * a.ycs + n) = v;
+}
+
+// Small-K direct convolution (K = kh*kw*cin <= 64: the 4-channel image-input layers and the
+// 4-channel StyleConv input): tppx threads per pixel, each QPT x 4 output channels; a block walks
+// iters x (256 / tppx) pixels of one batch entry with that entry's filter [K][cout] staged in LDS
+// once; one float4 of input per tap and channel group; fp32 VALU; 16-byte output stores.  These
+// layers are bound by their output write; the implicit GEMM pads K to 32 per slice and stages
+// every output tile through LDS (3-27 TFLOP/s measured on them).
+template <int QPT>
+__global__ __launch_bounds__(256) void conv_smallk(ConvArgs a, int batch, int tppx, int iters, int vec) {
+    extern __shared__ __attribute__((aligned(16))) float wk[];   // [K][cout]
+    const int ppi = 256 / tppx;
+    const long long total = (long long)batch * a.M;
+    const long long g0 = (long long)blockIdx.x * ppi * iters;
+    {
+        const int b0 = (int)((g0 < total ? g0 : 0) / a.M);
+        const float *w0 = a.wt + (long long)b0 * a.w_bs;
+        for (int e = threadIdx.x; e < a.K * a.cout; e += 256) {
+            const int k = e / a.cout, o = e - k * a.cout;
+            wk[e] = w0[(long long)o * a.kpad + k];
+        }
+    }
+    __syncthreads();
+    const int tq = threadIdx.x % tppx;
+    const int hw = a.oh * a.ow;
+    for (int it = 0; it < iters; ++it) {
+        const long long gid = g0 + (long long)it * ppi + threadIdx.x / tppx;
+        if (gid >= total) break;
+        const int bidx = (int)(gid / a.M);
+        const int m = (int)(gid - (long long)bidx * a.M);
+        const int img = m / hw, rem = m - img * hw;
+        const int oy = rem / a.ow, ox = rem - oy * a.ow;
+        const float *x = a.x + (long long)bidx * a.x_bs;
+        f4 acc[QPT];
+#pragma unroll
+        for (int q = 0; q < QPT; ++q) acc[q] = f4{0.f, 0.f, 0.f, 0.f};
+        for (int ky = 0; ky < a.kh; ++ky)
+            for (int kx = 0; kx < a.kw; ++kx) {
+                int iy, ix;
+                if (!map_tap(a, oy, ox, ky, kx, iy, ix)) continue;
+                const float *px = x + ((long long)(img * a.h + iy) * a.w + ix) * a.xcs;
+                const int kb = (ky * a.kw + kx) * a.cin;
+                for (int c = 0; c < a.cin; c += 4) {
+                    f4 v = *(const f4 *)(px + c);
+                    if (a.in_scale) v *= *(const f4 *)(a.in_scale + (long long)img * a.in_scale_ns + c);
+                    if (a.pre_act) {
+                        v.x = apply_act(v.x, a.pre_act, a.pre_alpha);
+                        v.y = apply_act(v.y, a.pre_act, a.pre_alpha);
+                        v.z = apply_act(v.z, a.pre_act, a.pre_alpha);
+                        v.w = apply_act(v.w, a.pre_act, a.pre_alpha);
+                    }
+                    const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const float *wr = wk + (kb + c + e) * a.cout + 4 * tq;
+#pragma unroll
+                        for (int q = 0; q < QPT; ++q) {
+                            const f4 w4 = *(const f4 *)(wr + 4 * tppx * q);
+                            acc[q].x = fmaf(vv[e], w4.x, acc[q].x);
+                            acc[q].y = fmaf(vv[e], w4.y, acc[q].y);
+                            acc[q].z = fmaf(vv[e], w4.z, acc[q].z);
+                            acc[q].w = fmaf(vv[e], w4.w, acc[q].w);
+                        }
+                    }
+                }
+            }
+#pragma unroll
+        for (int q = 0; q < QPT; ++q) store_epilogue4(a, bidx, m, 4 * (tq + tppx * q), acc[q], vec != 0);
+    }
+}
+
 // Direct VALU convolution for tiny Cout (final RGB / flow heads, ToRGB): one thread per output
 // pixel, all CO outputs per thread.  Per filter tap the block stages W[:, tap, c0:c0+CCH] in LDS,
 // so every weight read is an LDS broadcast (all lanes read the same address).
@@ -376,13 +472,45 @@ struct Plan {
 
 static bool use_direct(const s2v_conv_params *p) { return p->cout <= 4 && !p->b_kn; }
 
+static bool vec4_input(const s2v_conv_params *p) {
+    return (p->cin % 4 == 0) && (p->xcs % 4 == 0) && (((uintptr_t)p->x % 16) == 0) && (p->x_bs % 4 == 0) &&
+           (!p->in_scale || (p->in_scale_ns % 4 == 0 && ((uintptr_t)p->in_scale % 16) == 0));
+}
+
+// conv_smallk geometry: threads per pixel (cout / 4 channel quads, at most 64) and quads per thread
+static bool smallk_cfg(const s2v_conv_params *p, int M, int K, int &tppx, int &qpt) {
+    if (p->b_kn || p->force_tile || p->cout < 8 || (p->cout & 3) || K > 64 || !vec4_input(p)) return false;
+    const int quads = p->cout / 4;
+    if (quads & (quads - 1)) return false;                       // power of two
+    tppx = quads < 64 ? quads : 64;
+    qpt = quads / tppx;
+    if (qpt > 2 || (size_t)K * p->cout * sizeof(float) > 64 * 1024) return false;
+    const int batch = p->batch > 0 ? p->batch : 1;
+    return p->w_bs == 0 || batch == 1 || M % (256 / tppx) == 0;
+}
+
+// pixels per block = iters x (256 / tppx): up to 16 iterations, and a divisor of M when each
+// batch entry has its own weights (a block never straddles two entries)
+static int smallk_iters(const s2v_conv_params *p, int M, int tppx) {
+    const int batch = p->batch > 0 ? p->batch : 1;
+    const bool per_entry = p->w_bs != 0 && batch > 1;
+    int it = 16;
+    while (it > 1 && per_entry && M % (it * (256 / tppx)) != 0) it /= 2;
+    return it;
+}
+
 // the split-bf16 kernel reads the pre-split packed weights; b_kn matrices are split on the fly
-static bool uses_x3(const s2v_conv_params *p) {
-    return p->prec == S2V_PREC_BF16X3 && !(use_direct(p) && !p->force_tile) && !p->b_kn;
+static bool smallk_cfg(const s2v_conv_params *p, int M, int K, int &tppx, int &qpt);
+
+static bool is_smallk(const s2v_conv_params *p) {
+    const long long m = (long long)p->n * p->oh * p->ow, k = (long long)p->kh * p->kw * p->cin;
+    int tppx, qpt;
+    return m < (1LL << 31) && k <= 64 && smallk_cfg(p, (int)m, (int)k, tppx, qpt);
 }
 static bool tiled_x3(const s2v_conv_params *p) {
-    return p->prec == S2V_PREC_BF16X3 && !(use_direct(p) && !p->force_tile);
+    return p->prec == S2V_PREC_BF16X3 && !(use_direct(p) && !p->force_tile) && !is_smallk(p);
 }
+static bool uses_x3(const s2v_conv_params *p) { return tiled_x3(p) && !p->b_kn; }
 
 static int a_mode(const s2v_conv_params *p);
 
@@ -450,6 +578,13 @@ static Plan make_plan(const s2v_conv_params *p, int M, int K) {
     pl.ktiles = (K + 31) / 32;
     if (use_direct(p) && !p->force_tile) {
         pl.tile = -1;
+        pl.splits = 1;
+        pl.tps = pl.ktiles;
+        return pl;
+    }
+    int tppx, qpt;
+    if (smallk_cfg(p, M, K, tppx, qpt)) {
+        pl.tile = -2;
         pl.splits = 1;
         pl.tps = pl.ktiles;
         return pl;
@@ -604,6 +739,13 @@ extern "C" int s2v_conv2d_plan(const s2v_conv_params *p, int *out6) {
     int rc = validate(p, M, K);
     if (rc) return rc;
     Plan pl = make_plan(p, M, K);
+    if (pl.tile == -2) {
+        int tppx, qpt;
+        smallk_cfg(p, M, K, tppx, qpt);
+        out6[0] = 0; out6[1] = p->cout; out6[2] = -qpt;
+        out6[3] = 0; out6[4] = 0; out6[5] = 1;
+        return 0;
+    }
     if (pl.tile < 0) {
         const bool cpar = (p->cin % 4 == 0) && (p->xcs % 4 == 0) && (((uintptr_t)p->x % 16) == 0) &&
                           (p->x_bs % 4 == 0) && (!p->in_scale || (p->in_scale_ns % 4 == 0 &&
@@ -632,6 +774,20 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
     const int batch = p->batch > 0 ? p->batch : 1;
     Plan pl = make_plan(p, M, K);
     ConvArgs a = make_args(p, M, K, pl);
+    if (pl.tile == -2) {
+        int tppx, qpt;
+        smallk_cfg(p, M, K, tppx, qpt);
+        const int iters = smallk_iters(p, M, tppx);
+        const long long total = (long long)batch * M;
+        const unsigned grid = cdiv(total, (256 / tppx) * iters);
+        const size_t lds = (size_t)K * p->cout * sizeof(float);
+        const int vec = p->ycs % 4 == 0 && ((uintptr_t)p->y % 16) == 0 && p->y_bs % 4 == 0 &&
+                        (!p->res || (p->res_cs % 4 == 0 && ((uintptr_t)p->res % 16) == 0 && p->res_bs % 4 == 0)) &&
+                        (!p->scale || ((uintptr_t)p->scale % 16) == 0) && (!p->shift || ((uintptr_t)p->shift % 16) == 0);
+        if (qpt == 1) conv_smallk<1><<<grid, 256, lds, s>>>(a, batch, tppx, iters, vec);
+        else conv_smallk<2><<<grid, 256, lds, s>>>(a, batch, tppx, iters, vec);
+        return check_launch("conv_smallk");
+    }
     if (pl.tile < 0) {
         const bool cpar = (p->cin % 4 == 0) && (p->xcs % 4 == 0) && (((uintptr_t)p->x % 16) == 0) &&
                           (p->x_bs % 4 == 0) && (!p->in_scale || (p->in_scale_ns % 4 == 0 &&

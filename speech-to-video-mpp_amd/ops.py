@@ -274,12 +274,22 @@ def _conv(ctx, x, cw, y, ohw, out_view, act, alpha, res, res_after, res_offset, 
     if per_sample_wt is not None:        # batch mode: one image per batch entry, its own weights
         assert in_scale is None and nc_scale is None and out_view is None
         p.n, p.batch = 1, x.n
-        wfp, wx3 = per_sample_wt
-        p.wt, p.wt_x3, p.w_bs = _ptr(wfp), _ptr(wx3), cw.npad * cw.kpad
+        p.w_bs = cw.npad * cw.kpad
         p.x_bs, p.y_bs = x.h * x.w * x.cs, oh * ow * y.cs
         if res is not None:
             p.res_bs = res.h * res.w * res.cs
-    elif p.prec == PREC_BF16X3 and (cw.cout > 4 or force_tile):   # implicit-GEMM path (not Cout <= 4 VALU)
+    use_x3 = False
+    if p.prec == PREC_BF16X3:
+        p.wt_x3 = p.wt                   # placeholder: the plan query only checks it is set
+        use_x3 = bool(_plan(ctx, p)[6]) and not p.b_kn
+        p.wt_x3 = None
+    if per_sample_wt is not None:
+        wb = per_sample_wt(use_x3)       # split or fp32 per-sample weights, as the kernel reads them
+        if use_x3:
+            p.wt, p.wt_x3 = None, wb.data_ptr()
+        else:
+            p.wt = wb.data_ptr()
+    elif use_x3:                         # implicit-GEMM path: pre-split packed weights
         p.wt_x3 = cw.wt_x3(ctx).data_ptr()
     need = ctx.lib.s2v_conv2d_ws_bytes(ctypes.byref(p))
     p.ws, p.ws_bytes = ctx.ws.get(need)
@@ -304,15 +314,17 @@ def modulated_conv2d(ctx: Ctx, x: NHWC, cw: ConvW, y: NHWC, s: torch.Tensor, d: 
     assert cw.in_mode != IN_TRANSPOSED and cw.poly is None, "modulated_conv2d: direct / up2 convs only"
     assert x.c == cw.cin and (y.n, y.h, y.w, y.c) == (x.n, oh, ow, cw.cout)
     b = x.n
-    wb = torch.empty((b, cw.npad, cw.kpad), device=cw.wt.device)
-    # the implicit-GEMM kernel in bf16x3 mode reads split weights; the small-Cout kernel fp32
-    x3 = prec_code() == PREC_BF16X3 and cw.cout > 4
-    fn = ctx.lib.s2v_modulate_weights_x3 if x3 else ctx.lib.s2v_modulate_weights
-    check(fn(cw.wt.data_ptr(), cw.npad, cw.kpad, cw.K, cw.cin, cw.cout, s.data_ptr(), s.stride(0),
-             None if d is None else d.data_ptr(), 0 if d is None else d.stride(0), b, wb.data_ptr(), ctx.stream),
-          "s2v_modulate_weights")
+
+    def weights(x3):
+        # the split-bf16 implicit GEMM reads split weights; the VALU kernels (small K / Cout) fp32
+        wb = torch.empty((b, cw.npad, cw.kpad), device=cw.wt.device)
+        fn = ctx.lib.s2v_modulate_weights_x3 if x3 else ctx.lib.s2v_modulate_weights
+        check(fn(cw.wt.data_ptr(), cw.npad, cw.kpad, cw.K, cw.cin, cw.cout, s.data_ptr(), s.stride(0),
+                 None if d is None else d.data_ptr(), 0 if d is None else d.stride(0), b, wb.data_ptr(), ctx.stream),
+              "s2v_modulate_weights")
+        return wb
     return _conv(ctx, x, cw, y, (oh, ow), None, act, alpha, res, res_after, (0, 0), None, None, ACT_NONE, 0.0,
-                 pix_add, pix_w, None, shift, 0, 0, per_sample_wt=(None, wb) if x3 else (wb, None))
+                 pix_add, pix_w, None, shift, 0, 0, per_sample_wt=weights)
 
 
 def gemm_kn(ctx: Ctx, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, batch: int, a_bs: int, b_bs: int,
@@ -353,6 +365,8 @@ def conv_symbol(ctx: Ctx, p) -> str:
     """Kernel symbol (as rocprofv3 reports it, demangled) the launch of ``p`` runs."""
     bm, bn, wm, avec, bkn, splits, x3, nw, ks, pf = _plan(ctx, p)
     if bm == 0:
+        if wm < 0:
+            return f"void s2v::conv_smallk<{-wm}>(s2v::ConvArgs, int, int, int, int)"
         if wm:
             return f"void s2v::conv_small_cpar<{bn}, {wm}>(s2v::ConvArgs, int)"
         return f"void s2v::conv_direct_small<{bn}>(s2v::ConvArgs, int)"

@@ -88,6 +88,13 @@ CONV_CASES = [
     (2, 64, 9, 9, 3, 7, 1, 3, 1, "direct", "zero", 0, 0),     # direct small-N kernel
     (3, 1, 20, 16, 32, 3, (3, 1), 1, 1, "direct", "zero", 0, 0),
     (2, 128, 3, 3, 256, 3, (3, 2), 1, 1, "direct", "zero", 0, 0),
+    # small-K direct kernel (K = kh*kw*cin <= 64, cin % 4 == 0): image-input / 4-channel layers
+    (2, 4, 17, 19, 64, 3, 1, 1, 1, "direct", "zero", 0, 0),
+    (2, 4, 16, 16, 256, 1, 1, 0, 1, "direct", "zero", 0, 0),
+    (1, 4, 9, 9, 512, 1, 1, 0, 1, "direct", "zero", 0, 0),
+    (2, 4, 10, 12, 32, 3, 1, 1, 1, "direct", "reflect", 0, 0),
+    (2, 4, 8, 8, 64, 3, 1, 1, 1, "up2", "zero", 0, 0),
+    (2, 4, 14, 14, 128, 3, 2, 1, 1, "direct", "zero", 0, 0),
 ]
 
 

@@ -6,5 +6,5 @@ run() { echo "== $1"; timeout -k 10 120 python tools/conv_micro.py $1 --iters 10
 run "--n 16 --h 200 --w 200 --cin 256 --cout 256 --k 3" 1
 
 
-S2V_BENCH_VERBOSE=2 timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1 || exit 1
+S2V_BENCH_VERBOSE=1 timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1 || exit 1
 tail -1 gpurun_out/bench.log
