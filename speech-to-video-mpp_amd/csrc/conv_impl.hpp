@@ -128,13 +128,13 @@ struct ARows {
     bool ok[AR];
 };
 
-// rows m0 + ar + RS * j of the tile (RS = rows covered by one load pass of the block)
-template <int AR, int AMODE, int RS = 32>
-__device__ __forceinline__ void a_rows_init(const ConvArgs &a, int m0, int ar, ARows<AR, AMODE> &R) {
+// tile rows rows[j] (j < AR): output pixel m0 + rows[j]
+template <int AR, int AMODE>
+__device__ __forceinline__ void a_rows_init_at(const ConvArgs &a, int m0, const int (&rows)[AR], ARows<AR, AMODE> &R) {
     const int hw = a.oh * a.ow;
 #pragma unroll
     for (int j = 0; j < AR; ++j) {
-        const int m = m0 + ar + RS * j;
+        const int m = m0 + rows[j];
         R.ok[j] = m < a.M;
         const int mm = R.ok[j] ? m : 0;
         const int img = mm / hw;
@@ -149,6 +149,15 @@ __device__ __forceinline__ void a_rows_init(const ConvArgs &a, int m0, int ar, A
         R.base[j] = AMODE == 3 ? (long long)img * a.h * a.w * a.xcs
                                : ((long long)(img * a.h + R.iy0[j]) * a.w + R.ix0[j]) * a.xcs;
     }
+}
+
+// rows m0 + ar + RS * j of the tile (RS = rows covered by one load pass of the block)
+template <int AR, int AMODE, int RS = 32>
+__device__ __forceinline__ void a_rows_init(const ConvArgs &a, int m0, int ar, ARows<AR, AMODE> &R) {
+    int rows[AR];
+#pragma unroll
+    for (int j = 0; j < AR; ++j) rows[j] = ar + RS * j;
+    a_rows_init_at<AR, AMODE>(a, m0, rows, R);
 }
 
 // AMODE 0 / 3 gather of one K-slice: filter tap (ky, kx), channels [c, c + 4) per row (the tap is

@@ -62,6 +62,31 @@ __device__ __forceinline__ void store_a_x3(char *As, int tid, const f4 (&ra)[AR]
     }
 }
 
+// Wide A staging (AMODE 0/3): a thread owns 8 consecutive k (two float4 loads) of AR8 rows and
+// writes each as one 16-byte hi slot + one 16-byte lo slot (ds_write_b128).  Lane t of a pass
+// takes row 16 (t >> 6) + ((t >> 3) & 7) + 8 ((t >> 2) & 1): the two rows of every 8-lane store
+// group are r and r + 8, whose swizzles differ in bit 2, so their four slots land in disjoint
+// halves of the 128-byte bank window (no write conflicts); 4 lanes cover a 128-byte row piece.
+template <int NT>
+__device__ __forceinline__ int a_row8(int t, int j) {
+    return j * (NT / 4) + ((t >> 6) << 4) + ((t >> 3) & 7) + 8 * ((t >> 2) & 1);
+}
+
+template <int AR8, int NT>
+__device__ __forceinline__ void store_a8_x3(char *As, int tid, const f4 (&ra)[2 * AR8]) {
+    const int q = tid & 3;
+#pragma unroll
+    for (int j = 0; j < AR8; ++j) {
+        u32x2 h0, l0, h1, l1;
+        split4(ra[2 * j], h0, l0);
+        split4(ra[2 * j + 1], h1, l1);
+        const u32x4 hi = {h0.x, h0.y, h1.x, h1.y}, lo = {l0.x, l0.y, l1.x, l1.y};
+        const int off = slot_off(a_row8<NT>(tid, j), q);
+        *(u32x4 *)(As + off) = hi;
+        *(u32x4 *)(As + (off ^ 64)) = lo;
+    }
+}
+
 // pre-split packed weights: thread loads 16 bytes (one slot) of rows br + RS j
 template <int BR, int RS>
 __device__ __forceinline__ void load_b_x3(const ConvArgs &a, const char *__restrict__ wt, int kt, int n0, int tid,
@@ -188,8 +213,18 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3(ConvArgs a) {
     const bool kperm = (AMODE == 0 || AMODE == 3) && !BKN && taps > 1;
     const int ak = (tid & 7) * 4;
 
-    ARows<AR, AMODE> R;
-    a_rows_init<AR, AMODE, RS>(a, m0, tid >> 3, R);
+    constexpr bool A8 = (AMODE == 0 || AMODE == 3) && !BKN && BM % (NT / 4) == 0;
+    constexpr int AR8 = A8 ? BM / (NT / 4) : 1;
+    ARows<A8 ? AR8 : AR, AMODE> R;
+    if constexpr (A8) {
+        int rows[AR8];
+#pragma unroll
+        for (int j = 0; j < AR8; ++j) rows[j] = a_row8<NT>(tid, j);
+        a_rows_init_at<AR8, AMODE>(a, m0, rows, R);
+    } else {
+        a_rows_init<AR, AMODE, RS>(a, m0, tid >> 3, R);
+    }
+    static_assert(!A8 || 2 * AR8 == AR, "wide A staging: same float4 count");
 
     f4 ra[PF][KS][AR];
     u32x4 rbp[PF][KS][BKN ? 1 : BR];
@@ -210,10 +245,21 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3(ConvArgs a) {
 #pragma unroll
         for (int u = 0; u < KS; ++u) {
             const int kt = (AMODE == 0 || AMODE == 3) ? ld.kt(nsl) : ld.i;
-            if constexpr (AMODE == 0 || AMODE == 3)
+            if constexpr (A8) {
+                f4 t0[AR8], t1[AR8];
+                const int c8 = ld.cs * 32 + 8 * (tid & 3);
+                load_a_tap<AR8, AMODE>(a, x, ld.ky, ld.kx, c8, R, t0);
+                load_a_tap<AR8, AMODE>(a, x, ld.ky, ld.kx, c8 + 4, R, t1);
+#pragma unroll
+                for (int j = 0; j < AR8; ++j) {
+                    ra[p][u][2 * j] = t0[j];
+                    ra[p][u][2 * j + 1] = t1[j];
+                }
+            } else if constexpr (AMODE == 0 || AMODE == 3) {
                 load_a_tap<AR, AMODE>(a, x, ld.ky, ld.kx, ld.cs * 32 + ak, R, ra[p][u]);
-            else
+            } else {
                 load_a<AR, AMODE>(a, x, kt, ak, R, ra[p][u]);
+            }
             if constexpr (BKN) load_b<BN, BKR, 1>(a, wtf, kt, n0, tid, rbk[p][u]);
             else load_b_x3<BR, RS>(a, wtb, kt, n0, tid, rbp[p][u]);
             if (ld.i < kt1 - 1) ld.next(kperm, taps, nsl, a.kw);
@@ -223,7 +269,8 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3(ConvArgs a) {
 #pragma unroll
         for (int u = 0; u < KS; ++u) {
             char *sb = st + u * SUB;
-            store_a_x3<AR, RS>(sb, tid, ra[p][u]);
+            if constexpr (A8) store_a8_x3<AR8, NT>(sb, tid, ra[p][u]);
+            else store_a_x3<AR, RS>(sb, tid, ra[p][u]);
             if constexpr (BKN) store_b_kn_x3<BN, BKR>(sb + BM * 128, tid, rbk[p][u]);
             else store_b_x3<BR, RS>(sb + BM * 128, tid, rbp[p][u]);
         }
