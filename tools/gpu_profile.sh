@@ -12,14 +12,14 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 for w in $STATS_WORKLOADS; do
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/stats_$w" -o run -- \
-    python3 bench.py --workload "$w" --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/stats_$w.log" 2>&1
+    python3 bench.py --workload "$w" --steps 5 --warmup 2 --no-cpu-baseline --no-alt > "$OUT/stats_$w.log" 2>&1
   python3 tools/rocprof_summary.py "$OUT/stats_$w/run_results.db" "$OUT/stats_$w.csv"
   echo "stats $w done"
 done
 for w in $PMC_WORKLOADS; do
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 500 rocprofv3 --pmc "$c" --output-format csv -d "$OUT/pmc_${w}_$c" -o run -- \
-      python3 bench.py --workload "$w" --no-graph --steps 1 --warmup 1 --no-roofline --no-cpu-baseline \
+      python3 bench.py --workload "$w" --no-graph --steps 1 --warmup 1 --no-roofline --no-cpu-baseline --no-alt \
       > "$OUT/pmc_${w}_$c.log" 2>&1
     echo "pmc $w $c done"
   done
