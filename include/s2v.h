@@ -68,7 +68,7 @@ enum { S2V_PAD_ZERO = 0, S2V_PAD_REFLECT = 1 };
 typedef struct s2v_conv_params {
     /* input */
     const float *x; int n, h, w, cin, xcs;
-    int in_mode; int pad_mode;
+    int in_mode; int pad_mode;                  /* PAD_REFLECT: direct or nearest-x2 input (reflected in the upsampled frame) */
     int pre_act; float pre_alpha;
     const float *in_scale; int in_scale_ns;     /* [n][in_scale_ns], may be NULL */
     /* filter */
@@ -112,7 +112,7 @@ size_t s2v_conv2d_ws_bytes(const s2v_conv_params *p);
  * of the conv_igemm<BM,BN,WAVES_M,AVEC,B_KN> (prec 0) or
  * conv_igemm_x3<BM,BN,WAVES_M,NW,KS,PF,AVEC,B_KN> (prec 1) instance, or {0, CO, TPP, 0, 0, 1, 0, 0, 0, 0}
  * for conv_small_cpar<CO,TPP> (conv_direct_small<CO> when TPP == 0).  force_tile: 0 = planner,
- * 1..6 a fixed tile of the selected precision's table (tests / tuning). */
+ * 1..6 (f32) / 1..7 (bf16x3) a fixed tile of the selected precision's table (tests / tuning). */
 int s2v_conv2d_plan(const s2v_conv_params *p, int *out10);
 
 /* Split packed fp32 weights [rows][kpad] (kpad % 32 == 0) into the S2V_PREC_BF16X3 layout

@@ -459,7 +459,8 @@ struct X3Cfg {
 };
 static const X3Cfg kX3Tiles[] = {
     {{256, 256, 2, 8, 1, 1}, 365.f, 1}, {{128, 128, 2, 8, 1, 1}, 295.f, 2}, {{64, 128, 2, 8, 1, 1}, 255.f, 3},
-    {{128, 64, 2, 4, 1, 1}, 230.f, 3},  {{64, 64, 2, 4, 1, 1}, 200.f, 4},   {{128, 32, 4, 4, 1, 1}, 150.f, 4}};
+    {{128, 64, 2, 4, 1, 1}, 230.f, 3},  {{64, 64, 2, 4, 1, 1}, 200.f, 4},   {{128, 32, 4, 4, 1, 1}, 150.f, 4},
+    {{256, 128, 4, 8, 1, 1}, 285.f, 1}};
 constexpr int kNumX3 = sizeof(kX3Tiles) / sizeof(kX3Tiles[0]);
 
 static const TileCfg &tile_cfg(const s2v_conv_params *p, int tile);
@@ -645,10 +646,13 @@ static int validate(const s2v_conv_params *p, int &M, int &K) {
     S2V_REQUIRE(p->kh > 0 && p->kw > 0 && p->sh > 0 && p->sw > 0 && p->dh > 0 && p->dw > 0, "conv2d: bad kernel");
     S2V_REQUIRE(p->xcs >= p->cin && p->ycs >= p->cout, "conv2d: channel stride smaller than channels");
     S2V_REQUIRE(p->in_mode >= 0 && p->in_mode <= 2, "conv2d: bad in_mode %d", p->in_mode);
-    S2V_REQUIRE(!(p->pad_mode == S2V_PAD_REFLECT && p->in_mode != S2V_IN_DIRECT),
-                "conv2d: reflect padding only with direct input");
-    S2V_REQUIRE(!(p->pad_mode == S2V_PAD_REFLECT && (p->ph >= p->h || p->pw >= p->w)),
-                "conv2d: reflect pad must be smaller than the input");
+    S2V_REQUIRE(!(p->pad_mode == S2V_PAD_REFLECT && p->in_mode == S2V_IN_TRANSPOSED),
+                "conv2d: reflect padding only with direct or nearest-x2 input");
+    {
+        const int up = p->in_mode == S2V_IN_NEAREST_UP2 ? 2 : 1;   // reflection happens in the upsampled frame
+        S2V_REQUIRE(!(p->pad_mode == S2V_PAD_REFLECT && (p->ph >= up * p->h || p->pw >= up * p->w)),
+                    "conv2d: reflect pad must be smaller than the input");
+    }
     const long long m = (long long)p->n * p->oh * p->ow;
     const long long k = (long long)p->kh * p->kw * p->cin;
     S2V_REQUIRE(m < (1LL << 31) && k < (1LL << 31), "conv2d: problem too large");
@@ -714,8 +718,8 @@ static int a_mode(const s2v_conv_params *p) {
     if (!vec) return 2;
     const bool simple_pre = (p->pre_act == S2V_ACT_NONE || p->pre_act == S2V_ACT_RELU || p->pre_act == S2V_ACT_LRELU) &&
                             (!p->in_scale || (p->in_scale_ns % 4 == 0 && ((uintptr_t)p->in_scale % 16) == 0));
-    if (p->cin % 32 == 0 && p->in_mode == S2V_IN_DIRECT && simple_pre && !p->b_kn)
-        return p->pad_mode == S2V_PAD_ZERO ? 0 : 3;
+    if (p->cin % 32 == 0 && p->in_mode != S2V_IN_TRANSPOSED && simple_pre && !p->b_kn)
+        return (p->pad_mode == S2V_PAD_ZERO && p->in_mode == S2V_IN_DIRECT) ? 0 : 3;
     if (p->cin % 32 == 0 && p->in_mode == S2V_IN_DIRECT && p->pad_mode == S2V_PAD_ZERO && simple_pre) return 0;
     return 1;
 }

@@ -88,6 +88,10 @@ __device__ __forceinline__ bool map_tap(const ConvArgs &a, int oy, int ox, int k
     } else if (a.in_mode == S2V_IN_NEAREST_UP2) {
         int uy = oy * a.sh - a.ph + ky * a.dh;
         int ux = ox * a.sw - a.pw + kx * a.dw;
+        if (a.pad_mode == S2V_PAD_REFLECT) {   // reflected in the upsampled frame (ParseNet, blocks.py:92-96)
+            uy = reflect_idx(uy, 2 * a.h);
+            ux = reflect_idx(ux, 2 * a.w);
+        }
         if ((unsigned)uy >= (unsigned)(2 * a.h) || (unsigned)ux >= (unsigned)(2 * a.w)) return false;
         iy = uy >> 1;
         ix = ux >> 1;
@@ -177,11 +181,23 @@ __device__ __forceinline__ void load_a_tap(const ConvArgs &a, const float *__res
             ra[j] = v;
         }
     } else {
+        // AMODE 3: per-row index math — reflect padding and / or a nearest-x2 upsampled input
+        // (tap coordinates in the upsampled frame, source pixel = coordinate >> 1); the mode
+        // branches are tile-uniform
+        const bool up = a.in_mode == S2V_IN_NEAREST_UP2, refl = a.pad_mode == S2V_PAD_REFLECT;
+        const int uh = up ? 2 * a.h : a.h, uw = up ? 2 * a.w : a.w, sh = up ? 1 : 0;
 #pragma unroll
         for (int j = 0; j < AR; ++j) {
-            const int iy = reflect_idx(R.iy0[j] + dy, a.h), ix = reflect_idx(R.ix0[j] + dx, a.w);
+            int uy = R.iy0[j] + dy, ux = R.ix0[j] + dx;
+            bool ok = R.ok[j];
+            if (refl) {
+                uy = reflect_idx(uy, uh);
+                ux = reflect_idx(ux, uw);
+            } else {
+                ok = ok && (unsigned)uy < (unsigned)uh && (unsigned)ux < (unsigned)uw;
+            }
             f4 v = {0.f, 0.f, 0.f, 0.f};
-            if (R.ok[j]) v = *(const f4 *)(x + R.base[j] + ((long long)iy * a.w + ix) * a.xcs + c);
+            if (ok) v = *(const f4 *)(x + R.base[j] + ((long long)(uy >> sh) * a.w + (ux >> sh)) * a.xcs + c);
             ra[j] = v;
         }
     }

@@ -154,7 +154,7 @@ __global__ __launch_bounds__(256) void irfft2_kernel(const float *__restrict__ s
 // 32x32x2 f32 operand maps: lane l holds A[l & 31][k0 + (l >> 5)] and B[k0 + (l >> 5)][l & 31];
 // the accumulator holds column l & 31, rows (r & 3) + 8 (r >> 2) + 4 (l >> 5).  Against the
 // VALU register-blocked form this replaces (one thread per output row, 1.4M serial fmas per
-// block), the 4 waves of a block now share every pass.
+// block), the waves of a block (4, or 8 at 48x48) share every pass.
 typedef float mf16 __attribute__((ext_vector_type(16)));
 constexpr int FCG = 4;   // channels per block
 
@@ -164,8 +164,8 @@ __device__ __forceinline__ mf16 mfma32(float a, float b, mf16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
-template <int H>
-__global__ __launch_bounds__(256) void rfft2_mf(const float *__restrict__ x, int C, int xcs,
+template <int H, int NWV>
+__global__ __launch_bounds__(64 * NWV) void rfft2_mf(const float *__restrict__ x, int C, int xcs,
                                                 const float *__restrict__ tables, float *__restrict__ spec,
                                                 int scs) {
     constexpr int W = H, WF = W / 2 + 1;
@@ -181,14 +181,14 @@ __global__ __launch_bounds__(256) void rfft2_mf(const float *__restrict__ x, int
     const int n = blockIdx.x / groups, c0 = (blockIdx.x - n * groups) * FCG;
     const int tid = threadIdx.x, wave = tid >> 6, li = tid & 31, lh = (tid >> 5) & 1;
     const FftTables T = fft_tables(tables, H, W);
-    for (int i = tid; i < W * 2 * WF; i += 256) Tw[i] = T.fw[i];
-    for (int i = tid; i < H * 2 * H; i += 256) Th[i] = T.fh[i];
-    for (int p = tid; p < H * W; p += 256) {
+    for (int i = tid; i < W * 2 * WF; i += 64 * NWV) Tw[i] = T.fw[i];
+    for (int i = tid; i < H * 2 * H; i += 64 * NWV) Th[i] = T.fh[i];
+    for (int p = tid; p < H * W; p += 64 * NWV) {
         const int hh = p / W, ww = p - hh * W;
         *(float4 *)&X[hh * XS + ww * FCG] = *(const float4 *)&x[((long long)n * H * W + p) * xcs + c0];
     }
     __syncthreads();
-    for (int t = wave; t < T1M * T1N; t += 4) {      // W pass (real -> half spectrum)
+    for (int t = wave; t < T1M * T1N; t += NWV) {      // W pass (real -> half spectrum)
         const int tm = t / T1N, tn = t - tm * T1N;
         const int i = tm * 32 + li, j = tn * 32 + li;
         const bool iok = i < 2 * WF, jok = j < N1;
@@ -211,7 +211,7 @@ __global__ __launch_bounds__(256) void rfft2_mf(const float *__restrict__ x, int
         }
     }
     __syncthreads();
-    for (int t = wave; t < T2M * T2N; t += 4) {      // H pass (complex)
+    for (int t = wave; t < T2M * T2N; t += NWV) {      // H pass (complex)
         const int tm = t / T2N, tn = t - tm * T2N;
         const int u = tm * 32 + li, j = tn * 32 + li;
         const bool uok = u < H, jok = j < N2;
@@ -240,8 +240,8 @@ __global__ __launch_bounds__(256) void rfft2_mf(const float *__restrict__ x, int
     }
 }
 
-template <int H>
-__global__ __launch_bounds__(256) void irfft2_mf(const float *__restrict__ spec, int C, int scs,
+template <int H, int NWV>
+__global__ __launch_bounds__(64 * NWV) void irfft2_mf(const float *__restrict__ spec, int C, int scs,
                                                  const float *__restrict__ tables, const float *__restrict__ res,
                                                  int rcs, float *__restrict__ y, int ycs) {
     constexpr int W = H, WF = W / 2 + 1;
@@ -256,16 +256,16 @@ __global__ __launch_bounds__(256) void irfft2_mf(const float *__restrict__ spec,
     const int n = blockIdx.x / groups, c0 = (blockIdx.x - n * groups) * FCG;
     const int tid = threadIdx.x, wave = tid >> 6, li = tid & 31, lh = (tid >> 5) & 1;
     const FftTables T = fft_tables(tables, H, W);
-    for (int i = tid; i < H * 2 * H; i += 256) Ti[i] = T.ih[i];
-    for (int i = tid; i < WF * 2 * W; i += 256) Tw[i] = T.iw[i];
-    for (int i = tid; i < H * WF * 2; i += 256) {
+    for (int i = tid; i < H * 2 * H; i += 64 * NWV) Ti[i] = T.ih[i];
+    for (int i = tid; i < WF * 2 * W; i += 64 * NWV) Tw[i] = T.iw[i];
+    for (int i = tid; i < H * WF * 2; i += 64 * NWV) {
         const int q = i & 1, f = i >> 1;
         const int u = f / WF, v = f - u * WF;
         *(float4 *)&Z[(q * H + u) * N1 + v * FCG] =
             *(const float4 *)&spec[((long long)n * H * WF + f) * scs + q * C + c0];
     }
     __syncthreads();
-    for (int t = wave; t < T1M * T1N; t += 4) {      // inverse H pass (complex)
+    for (int t = wave; t < T1M * T1N; t += NWV) {      // inverse H pass (complex)
         const int tm = t / T1N, tn = t - tm * T1N;
         const int h = tm * 32 + li, j = tn * 32 + li;
         const bool hok = h < H, jok = j < N1;
@@ -291,7 +291,7 @@ __global__ __launch_bounds__(256) void irfft2_mf(const float *__restrict__ spec,
         }
     }
     __syncthreads();
-    for (int t = wave; t < T2M * T2N; t += 4) {      // c2r W pass
+    for (int t = wave; t < T2M * T2N; t += NWV) {      // c2r W pass
         const int tm = t / T2N, tn = t - tm * T2N;
         const int w = tm * 32 + li, j = tn * 32 + li;
         const bool wok = w < W, jok = j < N2;
@@ -345,9 +345,10 @@ extern "C" int s2v_rfft2(const float *x, int n, int h, int w, int c, int xcs, co
     hipStream_t st = (hipStream_t)stream;
     if (c % FCG == 0 && aligned && h == w && (h == 12 || h == 24 || h == 48)) {
         const unsigned grid = n * (c / FCG);
-        if (h == 12) rfft2_mf<12><<<grid, 256, 0, st>>>(x, c, xcs, tables, spec, scs);
-        else if (h == 24) rfft2_mf<24><<<grid, 256, 0, st>>>(x, c, xcs, tables, spec, scs);
-        else rfft2_mf<48><<<grid, 256, 0, st>>>(x, c, xcs, tables, spec, scs);
+        // 48x48: 8 waves per block (one block per CU by LDS; the blocks barely cover the chip)
+        if (h == 12) rfft2_mf<12, 4><<<grid, 256, 0, st>>>(x, c, xcs, tables, spec, scs);
+        else if (h == 24) rfft2_mf<24, 4><<<grid, 256, 0, st>>>(x, c, xcs, tables, spec, scs);
+        else rfft2_mf<48, 8><<<grid, 512, 0, st>>>(x, c, xcs, tables, spec, scs);
         return check_launch("rfft2");
     }
     const size_t smem = (per * cg + fixed) * sizeof(float);
@@ -372,9 +373,9 @@ extern "C" int s2v_irfft2(const float *spec, int n, int h, int w, int c, int scs
     hipStream_t st = (hipStream_t)stream;
     if (c % FCG == 0 && h == w && (h == 12 || h == 24 || h == 48)) {
         const unsigned grid = n * (c / FCG);
-        if (h == 12) irfft2_mf<12><<<grid, 256, 0, st>>>(spec, c, scs, tables, res, rcs, y, ycs);
-        else if (h == 24) irfft2_mf<24><<<grid, 256, 0, st>>>(spec, c, scs, tables, res, rcs, y, ycs);
-        else irfft2_mf<48><<<grid, 256, 0, st>>>(spec, c, scs, tables, res, rcs, y, ycs);
+        if (h == 12) irfft2_mf<12, 4><<<grid, 256, 0, st>>>(spec, c, scs, tables, res, rcs, y, ycs);
+        else if (h == 24) irfft2_mf<24, 4><<<grid, 256, 0, st>>>(spec, c, scs, tables, res, rcs, y, ycs);
+        else irfft2_mf<48, 8><<<grid, 512, 0, st>>>(spec, c, scs, tables, res, rcs, y, ycs);
         return check_launch("irfft2");
     }
     const size_t smem = (per * cg + fixed) * sizeof(float);

@@ -95,12 +95,24 @@ CONV_CASES = [
     (2, 4, 10, 12, 32, 3, 1, 1, 1, "direct", "reflect", 0, 0),
     (2, 4, 8, 8, 64, 3, 1, 1, 1, "up2", "zero", 0, 0),
     (2, 4, 14, 14, 128, 3, 2, 1, 1, "direct", "zero", 0, 0),
+    # nearest-x2 input with reflect padding (ParseNet 'up' ConvLayers, blocks.py:92-96): per-row
+    # index path (cin % 32), float4 gather, small-K and small-Cout kernels
+    (2, 64, 9, 7, 64, 3, 1, 1, 1, "up2", "reflect", 0, 0),
+    (2, 36, 5, 6, 40, 3, 1, 1, 1, "up2", "reflect", 0, 0),
+    (2, 4, 8, 8, 64, 3, 1, 1, 1, "up2", "reflect", 0, 0),
+    (2, 64, 6, 6, 3, 3, 1, 1, 1, "up2", "reflect", 0, 0),
+    (2, 64, 12, 12, 48, 3, 1, 1, 1, "up2", "zero", 4, 2),
+    # bf16x3 256x128 8-wave tile (force_tile 7; the f32 table has 6 tiles)
+    (2, 64, 18, 16, 128, 3, 1, 1, 1, "direct", "zero", 7, 0),
+    (2, 96, 10, 11, 72, 3, 1, 1, 1, "up2", "reflect", 7, 2),
 ]
 
 
 @pytest.mark.parametrize("case", CONV_CASES, ids=[str(i) for i in range(len(CONV_CASES))])
 def test_conv2d(ctx, prec, case):
     n, cin, h, w, cout, k, stride, pad, dil, mode, pad_mode, tile, splits = case
+    if tile > 6 and prec == "f32":
+        pytest.skip("tile 7 exists in the bf16x3 table only")
     kh, kw = (k, k) if isinstance(k, int) else k
     transposed = mode == "transposed"
     wshape = (cin, cout, kh, kw) if transposed else (cout, cin, kh, kw)
