@@ -262,6 +262,35 @@ int s2v_eltwise(const float *x, int xcs, const float *mul, int mcs, const float 
 /* y[0:n) = value (channel padding of 3-channel images to the vectorised 4-channel layout). */
 int s2v_fill(float *y, long long n, float value, s2v_stream_t stream);
 
+/* ---- Mouth-region post-process (inference.py:302-313) ----------------------- */
+
+/* cv2.resize(src, (ow, oh)) with INTER_LINEAR (OpenCV imgproc resize.cpp) on HWC images:
+ * element (b, y, x, ch) at x + b*xis + y*xrs + x*c + ch (pitches in elements; ROIs of larger frames
+ * are plain pointer offsets).  mode 0: uint8 -> uint8 (11-bit fixed-point weights), 1: fp32 -> fp32,
+ * 2: fp32 -> uint8 truncated (np.uint8 of the float result, inference.py:313), 3: uint8 -> fp32
+ * (v == 255 ? 1 : 0: the mask paste of inference.py:305-308, resized / 255. stored into uint8). */
+int s2v_resize_linear(const void *x, int n, int h, int w, int c, long long xrs, long long xis, void *y, int oh,
+                      int ow, long long yrs, long long yis, int mode, s2v_stream_t stream);
+
+/* Laplacian_Pyramid_Blending_with_mask (futils/inference_utils.py:181-222): A, B uint8 [n][h][w][c],
+ * m fp32 [n][h][w] -> out fp32 [n][h][w][c]; cv2.pyrDown / pyrUp semantics (reflect-101 borders,
+ * uint8 Gaussian pyramids of A and B, fp32 of m); ``clip`` applies np.clip(out, 0, 255) (:313).
+ * h and w must be divisible by 2^(levels-1) (the reference's np.subtract fails otherwise).
+ * ws: >= s2v_laplacian_blend_ws_bytes(n, h, w, c, levels) bytes (0 for levels == 1). */
+size_t s2v_laplacian_blend_ws_bytes(int n, int h, int w, int c, int levels);
+int s2v_laplacian_blend(const unsigned char *a, const unsigned char *b, const float *m, int n, int h, int w, int c,
+                        int levels, int clip, float *out, void *ws, size_t ws_bytes, s2v_stream_t stream);
+
+/* FaceParse mask (face_parsing.py:47-57, :65-81): per pixel the first argmax over c parsing logits
+ * at x + b*xbs + p*ps + k*cs (NCHW: ps = 1, cs = h*w; NHWC: ps = c, cs = 1) -> out[b*h*w + p] =
+ * cmap[argmax] (uint8, may be NULL) and / or cls[...] = argmax (may be NULL). */
+int s2v_parse_mask(const float *x, int n, int h, int w, int c, long long xbs, long long ps, long long cs,
+                   const unsigned char *cmap, unsigned char *out, int *cls, s2v_stream_t stream);
+
+/* FaceParse.img2tensor (face_parsing.py:59-63): uint8 HWC pixels (3 bytes, BGR if ``flip``) ->
+ * fp32 RGB (img / 255. * 2 - 1, in float64 then rounded) at pixel pitch ycs (>= 3; channel 3 = 0). */
+int s2v_img_u8_to_m11(const unsigned char *x, long long pixels, int flip, float *y, int ycs, s2v_stream_t stream);
+
 const char *s2v_last_error(void);
 /* number of compute units of the current device (0 if no device) */
 int s2v_device_cus(void);

@@ -87,6 +87,13 @@ _SIGS = {
     "s2v_eltwise": (_c_int, [_vp, _c_int, _vp, _c_int, _vp, _c_int, _vp, _c_ll, _c_int, _c_float, _c_int, _c_float,
                              _c_float, _vp, _c_int, _vp]),
     "s2v_fill": (_c_int, [_vp, _c_ll, _c_float, _vp]),
+    "s2v_resize_linear": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_ll, _c_ll, _vp, _c_int, _c_int, _c_ll,
+                                   _c_ll, _c_int, _vp]),
+    "s2v_laplacian_blend_ws_bytes": (_c_size, [_c_int, _c_int, _c_int, _c_int, _c_int]),
+    "s2v_laplacian_blend": (_c_int, [_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_size,
+                                     _vp]),
+    "s2v_parse_mask": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_ll, _c_ll, _c_ll, _vp, _vp, _vp, _vp]),
+    "s2v_img_u8_to_m11": (_c_int, [_vp, _c_ll, _c_int, _vp, _c_int, _vp]),
     "s2v_last_error": (ctypes.c_char_p, []),
     "s2v_device_cus": (_c_int, []),
     "s2v_version": (ctypes.c_char_p, []),

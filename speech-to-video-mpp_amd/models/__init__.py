@@ -16,7 +16,7 @@ import torch
 
 from .. import ops
 from ..ops import NHWC
-from . import arch, enhancer_arch
+from . import arch, enhancer_arch, parse_arch
 
 
 def _fold5(x, dim):
@@ -168,6 +168,25 @@ class FullGenerator(_EngineMixin, enhancer_arch.FullGeneratorParams):
         return out, None
 
 
+class ParseNet(_EngineMixin, parse_arch.ParseNetParams):
+    """third_part/GPEN/face_parse/parse_model.py:21-75 (FaceParse: ParseNet(512, 512, 32, 64, 19,
+    norm_type='bn', relu_type='LeakyReLU', ch_range=[32, 256]), eval mode)."""
+
+    def _build_engine(self, sd, device):
+        from ..engine.parsenet import ParseNetEngine
+        return ParseNetEngine(sd, device, self.describe())
+
+    @torch.no_grad()
+    def forward(self, x):
+        """x [B,3,H,W] in [-1,1] -> (out_mask [B,parsing_ch,H,W], out_img [B,3,H,W]) (:69-75)."""
+        _need_cuda(x)
+        eng, ctx = self._engine(x.device)
+        b, _, h, w = x.shape
+        mask = torch.empty((b, self.parsing_ch, h, w), device=x.device)
+        img = torch.empty((b, 3, h, w), device=x.device)
+        return eng.forward(ctx, x.float(), mask, img)
+
+
 # ----------------------------------------------------------------------------- loaders
 def _load(path):
     return torch.load(path, map_location="cpu", weights_only=True)
@@ -225,5 +244,12 @@ def load_gpen(path, size=512, channel_multiplier=2, narrow=1, key=None):
     return net.eval()
 
 
-__all__ = ["LNet", "ENet", "DNet", "GFPGANv1Clean", "FullGenerator", "load_checkpoint", "load_network", "load_DNet",
-           "load_gfpgan", "load_gpen"]
+def load_parsenet(path, size=512):
+    """face_parsing.py:33-37: ParseNet(size, size, 32, 64, 19, 'bn', 'LeakyReLU', [32, 256]) + state_dict."""
+    net = ParseNet(**parse_arch.face_parse_net(size))
+    net.load_state_dict(_load(path))
+    return net.eval()
+
+
+__all__ = ["LNet", "ENet", "DNet", "GFPGANv1Clean", "FullGenerator", "ParseNet", "load_checkpoint", "load_network",
+           "load_DNet", "load_gfpgan", "load_gpen", "load_parsenet"]

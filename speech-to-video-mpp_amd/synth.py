@@ -150,6 +150,9 @@ def synth_torch_state_dict(module, gain: float = 1.3, noise_weight: float = 0.0,
 # activations grow to ~1e14 by the 512 output; at 1.0 they stay O(1..10) like a trained model's.
 GFPGAN_SYNTH = dict(gain=1.0, noise_weight=0.1)
 GPEN_SYNTH = dict(noise_weight=0.1, equal=True)
+# ParseNet: 18 residual blocks add their branch to the identity level after level; gain 1.0 keeps
+# the synthetic logits O(1..10) so the argmax is not decided by fp32 rounding
+PARSENET_SYNTH = dict(gain=1.0)
 
 
 # ----------------------------------------------------------------------------- inputs

@@ -10,7 +10,7 @@ Import shims (neither touches arithmetic; both documented in SURVEY.md §8c):
     own vendored copy third_part/GPEN/sr_model/arch_util.py (only used for init, which the
     synthetic state_dict overwrites).
 
-Usage:  python tests/golden/make_golden.py [--only lnet,enet,dnet,ops]
+Usage:  python tests/golden/make_golden.py [--only lnet,enet,dnet,ops,gfpgan,gpen,parsenet]
 """
 import argparse
 import importlib.util
@@ -248,6 +248,32 @@ def gen_gpen():
     p = _probe(img, "gpen.out")
     arrays.update({"out_idx": p["idx"], "out_val": p["val"], "out_stats": p["stats"]})
     _save("gpen_b1_512", arrays)
+
+
+def gen_parsenet():
+    """GPEN ParseNet (face_parse/parse_model.py) at the FaceParse configuration (512, with the
+    synthetic weights) and at a small one (128), outputs as full tensors / probes."""
+    sys.path.insert(0, os.path.join(REF, "third_part/GPEN/face_parse"))
+    from parse_model import ParseNet
+    from s2v_amd.models.parse_arch import ParseNetParams, face_parse_net
+    cfg = face_parse_net(512)
+    ref = ParseNet(512, 512, 32, 64, 19, norm_type="bn", relu_type="LeakyReLU", ch_range=[32, 256]).eval()
+    _check_keys("parsenet", ref, ParseNetParams(**cfg))
+    for size, batch in ((128, 2), (512, 1)):
+        net = ParseNet(size, size, 32, 64, 19, norm_type="bn", relu_type="LeakyReLU", ch_range=[32, 256]).eval()
+        sd = synth.synth_torch_state_dict(net, **synth.PARSENET_SYNTH)
+        net.load_state_dict(sd, strict=True)
+        x = synth.face_inputs(f"golden.parsenet{size}", batch, size)
+        with torch.no_grad():
+            mask, img = net(torch.from_numpy(x))
+        arrays = {"argmax": mask.argmax(1).numpy().astype(np.int8)}
+        if size == 128:
+            arrays.update({"mask": mask.numpy(), "img": img.numpy()})
+        else:
+            for name, t in (("mask", mask), ("img", img)):
+                pr = _probe(t, f"parsenet.{name}")
+                arrays.update({f"{name}_idx": pr["idx"], f"{name}_val": pr["val"], f"{name}_stats": pr["stats"]})
+        _save(f"parsenet_b{batch}_{size}", arrays)
 
 
 if __name__ == "__main__":

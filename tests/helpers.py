@@ -27,6 +27,13 @@ def synth_sd(net: str):
     return synth.synth_torch_state_dict(mod)
 
 
+@functools.lru_cache(maxsize=None)
+def parsenet_sd(size: int = 512):
+    """Synthetic ParseNet state_dict at the FaceParse configuration for ``size`` (face_parsing.py:34)."""
+    from s2v_amd.models.parse_arch import ParseNetParams, face_parse_net
+    return synth.synth_torch_state_dict(ParseNetParams(**face_parse_net(size)), **synth.PARSENET_SYNTH)
+
+
 def max_abs(a, b):
     a = a.detach().cpu().double().numpy() if isinstance(a, torch.Tensor) else np.asarray(a, np.float64)
     b = b.detach().cpu().double().numpy() if isinstance(b, torch.Tensor) else np.asarray(b, np.float64)

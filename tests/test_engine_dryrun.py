@@ -68,3 +68,15 @@ def test_lipsync_engines_plan(dry):
     d = DNetEngine(synth_sd("dnet"), "cpu")
     src, coeff = (torch.from_numpy(a) for a in synth.dnet_inputs("dry", 1, 256))
     d.forward(ctx, src, coeff)
+
+
+def test_parsenet_plan(dry):
+    from helpers import parsenet_sd
+    from s2v_amd.engine.parsenet import ParseNetEngine
+    from s2v_amd.models.parse_arch import ParseNetParams, face_parse_net
+    desc = ParseNetParams(**face_parse_net(512)).describe()
+    eng = ParseNetEngine(parsenet_sd(512), "cpu", desc)
+    x = torch.zeros(2, 3, 512, 512)
+    eng.forward(ops.Ctx("cpu"), x, torch.empty(2, 19, 512, 512), torch.empty(2, 3, 512, 512))
+    # encoder conv + 4 down blocks (3 convs) + 10 body blocks (2) + 4 up blocks (3) + 2 heads
+    assert dry.calls["s2v_conv2d"] == 1 + 12 + 20 + 12 + 2 and dry.calls["s2v_eltwise"] == 1

@@ -106,3 +106,21 @@ def test_upfirdn2d_and_fused_act_oracle_match_reference_fallbacks(golden):
                                   "blur11": (1, 1, (1, 1)), "down2": (1, 2, (1, 1))}.items():
         got = enhancers.upfirdn2d(xi, k * (4 if up == 2 else 1), up=up, down=down, pad=pad)
         assert max_abs(got, g[f"ufd_{name}"])[0] < 1e-6, name
+
+
+def test_parsenet_oracle_matches_reference(golden):
+    from oracle import parse
+    from helpers import parsenet_sd
+    for size, batch in ((128, 2), (512, 1)):
+        g = golden(f"parsenet_b{batch}_{size}")
+        x = torch.from_numpy(synth.face_inputs(f"golden.parsenet{size}", batch, size))
+        with torch.no_grad():
+            mask, img = parse.parsenet_forward(parsenet_sd(size), x)
+        if size == 128:
+            scale = float(np.abs(g["mask"]).max())
+            assert max_abs(mask, g["mask"])[0] < 1e-4 * scale and max_abs(img, g["img"])[0] < 1e-4 * scale
+        else:
+            check_probe(mask, g, "mask", atol=1e-4 * float(g["mask_stats"][2]))
+            check_probe(img, g, "img", atol=1e-4 * float(g["img_stats"][2]))
+        agree = (mask.argmax(1).numpy() == g["argmax"]).mean()
+        assert agree > 0.9999, agree

@@ -1,9 +1,4 @@
 set -o pipefail
 mkdir -p gpurun_out
-run() { echo "== $1"; timeout -k 10 120 python tools/conv_micro.py $1 --iters 20 --prec bf16x3 --tiles $2 2>&1 | grep tile= || exit 1; }
-run "--n 16 --h 12 --w 7 --cin 768 --cout 768 --k 1" 0,5,8,9,10
-run "--n 16 --h 12 --w 12 --cin 768 --cout 384 --k 1" 0,5,8,9,10
-run "--n 16 --h 24 --w 13 --cin 192 --cout 192 --k 1" 0,5,8,9,10
-run "--n 16 --h 48 --w 25 --cin 96 --cout 96 --k 1" 0,5,8,9,10
-run "--n 16 --h 12 --w 12 --cin 256 --cout 256 --k 3" 0,5,8,9,10
-run "--n 16 --h 12 --w 12 --cin 768 --cout 256 --k 3" 0,5,8,9,10
+timeout -k 10 600 python -u -m pytest tests/test_post_gpu.py tests/test_ops_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { echo TESTS_FAIL; grep -E "FAIL|Error|assert" gpurun_out/gpu_tests.log | head -30; tail -25 gpurun_out/gpu_tests.log; exit 1; }
+tail -1 gpurun_out/gpu_tests.log
