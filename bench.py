@@ -17,7 +17,10 @@ Other workloads (not the headline metric):
   --workload pipeline   one step = 16 frames through DNet -> uint8 ref -> ENet(+LNet) -> uint8
                         384x384 frames (s2v_amd.pipeline.LipSyncPipeline.run_batch), plus the
                         host precompute of a 1000-frame clip timed once;
-  --workload enhance    one step = B 512x512 faces through GFPGANv1Clean and GPEN-512.
+  --workload enhance    one step = B 512x512 faces through GFPGANv1Clean and GPEN-512;
+  --workload mouth      one step = B 720x720 frames through the mouth-region post-process
+                        (FaceParse-512 mask of the face box + 10-level Laplacian blend,
+                        inference.py:302-313, s2v_amd.post.MouthBlend).
 """
 from __future__ import annotations
 
@@ -50,7 +53,7 @@ ARITH = {"bf16x3": "bf16x3: fp32 tensors, conv products as split-fp32 hi*hi+hi*l
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--workload", choices=("lipsync", "pipeline", "enhance"), default="lipsync")
+    ap.add_argument("--workload", choices=("lipsync", "pipeline", "enhance", "mouth"), default="lipsync")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=0, help="0 = the workload's default (16, or 4 for enhance)")
@@ -285,7 +288,55 @@ class Enhance(Workload):
                           f"{threads} threads"}
 
 
-WORKLOADS = {"lipsync": LipSync, "pipeline": Pipeline, "enhance": Enhance}
+class Mouth(Workload):
+    metric = "mouth-region post-process frames/sec/GPU (FaceParse-512 mouth mask + 10-level Laplacian blend)"
+    gflop_per_unit = 468.08            # ParseNet-512 mask path, 2*MAC (469 GF/face)
+    FRAME = 720
+
+    def __init__(self, args, dev, rank):
+        from s2v_amd import models, post, synth
+        from s2v_amd.models import parse_arch
+        self.batch = args.batch or 8
+        cfg = parse_arch.face_parse_net(512)
+        self.sd = synth.synth_torch_state_dict(parse_arch.ParseNetParams(**cfg), **synth.PARSENET_SYNTH)
+        net = models.ParseNet(**cfg)
+        net.load_state_dict(self.sd)
+        self.mb = post.MouthBlend(post.FaceParse(device=dev, net=net.eval()))
+        b, S = self.batch, self.FRAME
+        g = torch.Generator(device=dev)
+        g.manual_seed(4000 + rank)
+        self.inputs = [torch.randint(0, 256, (b, S, S, 3), generator=g, device=dev, dtype=torch.uint8)
+                       for _ in range(2)]
+        self.coords = [(190 + 4 * i, 510 + 4 * i, 170 + 2 * i, 530 + 2 * i) for i in range(b)]   # face boxes
+        self.out = torch.empty((b, S, S, 3), dtype=torch.uint8, device=dev)
+        self.fn = lambda r, f: self.mb.run_batch(r, f, self.coords, self.out)  # noqa: E731
+        self.config = {"workload": f"MouthBlend.run_batch on B={b} synthetic {S}x{S} uint8 frames (GFPGAN-restored + "
+                                   "original) with ~320x360 face boxes: box resize to 512, FaceParse ParseNet-512 "
+                                   "mask, mask paste, three 512 resizes, 10-level Laplacian blend, clip, resize back "
+                                   "(inference.py:302-313)"}
+
+    def forward(self):
+        return self.fn(*self.inputs)
+
+    def cpu(self, threads, seconds):
+        import numpy as np
+        from oracle import parse as OPARSE
+        from oracle import post as OP
+        torch.set_num_threads(threads)
+        r, f = (t[:1].cpu().numpy() for t in self.inputs)
+        y1, y2, x1, x2 = self.coords[0]
+
+        def one():
+            im = OP.resize_linear(np.ascontiguousarray(r[0, y1:y2, x1:x2]), (512, 512))
+            tmp = OP.tenor2mask(OPARSE.mask_logits(self.sd, im).numpy(), OP.MOUTH_MM)[0]
+            OP.blend_frame(r[0], f[0], OP.mouth_mask_full(tmp, r.shape[1:3], self.coords[0]))
+        n, el = _timed_cpu(one, 1, seconds, 4)
+        return {"value": round(n / el, 4), "unit": "frames/s", "cores": threads, "kind": "port",
+                "sample": f"{n} frames through the oracle restatement (torch CPU ParseNet + NumPy blend) in "
+                          f"{el:.1f}s, {threads} threads"}
+
+
+WORKLOADS = {"lipsync": LipSync, "pipeline": Pipeline, "enhance": Enhance, "mouth": Mouth}
 
 
 def main():

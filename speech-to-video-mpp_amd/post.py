@@ -106,10 +106,21 @@ def laplacian_pyramid_blending_with_mask(A, B, m, num_levels=6, clip=False):
     return out
 
 
+_CMAPS = {}
+
+
+def _cmap(colormap, device) -> torch.Tensor:
+    """Device copy of a colormap, made once (not inside a graph capture)."""
+    key = (tuple(int(v) for v in colormap), str(device))
+    if key not in _CMAPS:
+        _CMAPS[key] = torch.tensor(key[0], dtype=torch.uint8).to(device)
+    return _CMAPS[key]
+
+
 def parse_mask(logits: NHWC, colormap, out: torch.Tensor | None = None) -> torch.Tensor:
     """argmax over the parsing channels of NHWC logits -> colormap value, uint8 [N,H,W]."""
     ctx = _ctx(logits.t.device)
-    cmap = torch.tensor(list(colormap), dtype=torch.uint8).to(logits.t.device)
+    cmap = _cmap(colormap, logits.t.device)
     if out is None:
         out = torch.empty((logits.n, logits.h, logits.w), dtype=torch.uint8, device=logits.t.device)
     check(ctx.lib.s2v_parse_mask(logits.ptr, logits.n, logits.h, logits.w, logits.c, logits.h * logits.w * logits.cs,
@@ -203,7 +214,8 @@ class MouthBlend:
         dev = R.device
         n, H, W, _ = R.shape
         S = self.parser.size
-        full = torch.zeros((n, H, W), dtype=torch.float32, device=dev)
+        full = torch.empty((n, H, W), dtype=torch.float32, device=dev)
+        ops.fill(_ctx(dev), full)
         for i, (y1, y2, x1, x2) in enumerate(coords):
             resize_linear(tmp[i], (x2 - x1, y2 - y1), out=full[i, y1:y2, x1:x2], mode=RS_U8_EQ255)
         A, B = resize_linear(R, (S, S)), resize_linear(Fr, (S, S))
