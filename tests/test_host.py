@@ -26,6 +26,11 @@ def _ea():
     return enhancer_arch
 
 
+def _pa():
+    from s2v_amd.models import parse_arch
+    return parse_arch
+
+
 def header_functions():
     text = open(HEADER).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
@@ -69,7 +74,8 @@ def test_conv_params_struct_layout_matches_header(tmp_path):
                                        ("enet", lambda: arch.ENetParams(lnet=arch.LNetParams())),
                                        ("dnet", lambda: arch.DNetParams()),
                                        ("gfpgan", lambda: _ea().GFPGANv1CleanParams(**GFPGAN_KW)),
-                                       ("gpen", lambda: _ea().FullGeneratorParams(512, 512, 8, 2))])
+                                       ("gpen", lambda: _ea().FullGeneratorParams(512, 512, 8, 2)),
+                                       ("parsenet", lambda: _pa().ParseNetParams(**_pa().face_parse_net(512)))])
 def test_state_dict_layout_matches_reference(name, ctor):
     ref = json.load(open(os.path.join(GOLDEN, f"{name}_keys.json")))
     mine = {k: list(v.shape) for k, v in ctor().state_dict().items()}
