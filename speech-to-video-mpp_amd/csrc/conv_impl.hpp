@@ -164,9 +164,25 @@ __device__ __forceinline__ void a_rows_init(const ConvArgs &a, int m0, int ar, A
     a_rows_init_at<AR, AMODE>(a, m0, rows, R);
 }
 
-// AMODE 0 / 3 gather of one K-slice: filter tap (ky, kx), channels [c, c + 4) per row (the tap is
-// tile-uniform: scalar math); AMODE 3 reflects out-of-range rows/cols (FFC, ffc.py:196-204).
+// prologue of 4 gathered channels [c, c + 4) of tile row j: StyleGAN2 input modulation s[n, c]
+// (zero padding stays zero), then the pre-activation (NONE / RELU / LRELU only on these paths)
 template <int AR, int AMODE>
+__device__ __forceinline__ void prologue4(const ConvArgs &a, const ARows<AR, AMODE> &R, int j, int c, f4 &v) {
+    if (a.in_scale) v *= *(const f4 *)(a.in_scale + (long long)R.img[j] * a.in_scale_ns + c);
+    if (a.pre_act) {
+        const float sl = a.pre_act == S2V_ACT_RELU ? 0.f : a.pre_alpha;
+        v.x = v.x >= 0.f ? v.x : v.x * sl;
+        v.y = v.y >= 0.f ? v.y : v.y * sl;
+        v.z = v.z >= 0.f ? v.z : v.z * sl;
+        v.w = v.w >= 0.f ? v.w : v.w * sl;
+    }
+}
+
+// AMODE 0 / 3 gather of one K-slice: filter tap (ky, kx), channels [c, c + 4) per row (the tap is
+// tile-uniform: scalar math).  PRO = false leaves the prologue to the caller (the bf16x3 kernel applies it when it stores the
+// slice to LDS, so the global loads stay in flight under the MFMAs instead of being waited for
+// right after issue)
+template <int AR, int AMODE, bool PRO = true>
 __device__ __forceinline__ void load_a_tap(const ConvArgs &a, const float *__restrict__ x, int ky, int kx, int c,
                                            const ARows<AR, AMODE> &R, f4 (&ra)[AR]) {
     const int dy = ky * a.dh, dx = kx * a.dw;
@@ -201,20 +217,9 @@ __device__ __forceinline__ void load_a_tap(const ConvArgs &a, const float *__res
             ra[j] = v;
         }
     }
-    if (a.in_scale) {   // StyleGAN2 input modulation s[n, c] (zero padding stays zero)
+    if (PRO && (a.in_scale || a.pre_act)) {
 #pragma unroll
-        for (int j = 0; j < AR; ++j)
-            ra[j] *= *(const f4 *)(a.in_scale + (long long)R.img[j] * a.in_scale_ns + c);
-    }
-    if (a.pre_act) {
-        const float sl = a.pre_act == S2V_ACT_RELU ? 0.f : a.pre_alpha;
-#pragma unroll
-        for (int j = 0; j < AR; ++j) {
-            ra[j].x = ra[j].x >= 0.f ? ra[j].x : ra[j].x * sl;
-            ra[j].y = ra[j].y >= 0.f ? ra[j].y : ra[j].y * sl;
-            ra[j].z = ra[j].z >= 0.f ? ra[j].z : ra[j].z * sl;
-            ra[j].w = ra[j].w >= 0.f ? ra[j].w : ra[j].w * sl;
-        }
+        for (int j = 0; j < AR; ++j) prologue4<AR, AMODE>(a, R, j, c, ra[j]);
     }
 }
 

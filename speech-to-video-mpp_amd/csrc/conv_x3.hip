@@ -227,6 +227,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3(ConvArgs a) {
     static_assert(!A8 || 2 * AR8 == AR, "wide A staging: same float4 count");
 
     f4 ra[PF][KS][AR];
+    int rc[PF][KS];                  // A8: channel base of the staged slice (for the deferred prologue)
     u32x4 rbp[PF][KS][BKN ? 1 : BR];
     f4 rbk[PF][KS][BKN ? BKR : 1];
     floatx16 acc[TM][TN];
@@ -248,8 +249,9 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3(ConvArgs a) {
             if constexpr (A8) {
                 f4 t0[AR8], t1[AR8];
                 const int c8 = ld.cs * 32 + 8 * (tid & 3);
-                load_a_tap<AR8, AMODE>(a, x, ld.ky, ld.kx, c8, R, t0);
-                load_a_tap<AR8, AMODE>(a, x, ld.ky, ld.kx, c8 + 4, R, t1);
+                rc[p][u] = c8;
+                load_a_tap<AR8, AMODE, false>(a, x, ld.ky, ld.kx, c8, R, t0);
+                load_a_tap<AR8, AMODE, false>(a, x, ld.ky, ld.kx, c8 + 4, R, t1);
 #pragma unroll
                 for (int j = 0; j < AR8; ++j) {
                     ra[p][u][2 * j] = t0[j];
@@ -269,7 +271,16 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3(ConvArgs a) {
 #pragma unroll
         for (int u = 0; u < KS; ++u) {
             char *sb = st + u * SUB;
-            if constexpr (A8) store_a8_x3<AR8, NT>(sb, tid, ra[p][u]);
+            if constexpr (A8) {
+                if (a.in_scale || a.pre_act) {
+#pragma unroll
+                    for (int j = 0; j < AR8; ++j) {
+                        prologue4<AR8, AMODE>(a, R, j, rc[p][u], ra[p][u][2 * j]);
+                        prologue4<AR8, AMODE>(a, R, j, rc[p][u] + 4, ra[p][u][2 * j + 1]);
+                    }
+                }
+                store_a8_x3<AR8, NT>(sb, tid, ra[p][u]);
+            }
             else store_a_x3<AR, RS>(sb, tid, ra[p][u]);
             if constexpr (BKN) store_b_kn_x3<BN, BKR>(sb + BM * 128, tid, rbk[p][u]);
             else store_b_x3<BR, RS>(sb + BM * 128, tid, rbp[p][u]);
