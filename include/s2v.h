@@ -112,7 +112,7 @@ size_t s2v_conv2d_ws_bytes(const s2v_conv_params *p);
  * of the conv_igemm<BM,BN,WAVES_M,AVEC,B_KN> (prec 0) or
  * conv_igemm_x3<BM,BN,WAVES_M,NW,KS,PF,AVEC,B_KN> (prec 1) instance, or {0, CO, TPP, 0, 0, 1, 0, 0, 0, 0}
  * for conv_small_cpar<CO,TPP> (conv_direct_small<CO> when TPP == 0).  force_tile: 0 = planner,
- * 1..6 (f32) / 1..7 (bf16x3) a fixed tile of the selected precision's table (tests / tuning). */
+ * 1..6 (f32) / 1..8 (bf16x3) a fixed tile of the selected precision's table (tests / tuning). */
 int s2v_conv2d_plan(const s2v_conv_params *p, int *out10);
 
 /* Split packed fp32 weights [rows][kpad] (kpad % 32 == 0) into the S2V_PREC_BF16X3 layout

@@ -460,7 +460,7 @@ struct X3Cfg {
 static const X3Cfg kX3Tiles[] = {
     {{256, 256, 2, 8, 1, 1}, 365.f, 1}, {{128, 128, 2, 8, 1, 1}, 295.f, 2}, {{64, 128, 2, 8, 1, 1}, 255.f, 3},
     {{128, 64, 2, 4, 1, 1}, 230.f, 3},  {{64, 64, 2, 4, 1, 1}, 200.f, 4},   {{128, 32, 4, 4, 1, 1}, 150.f, 4},
-    {{256, 128, 4, 8, 1, 1}, 285.f, 1}};
+    {{256, 128, 4, 8, 1, 1}, 285.f, 1}, {{256, 64, 8, 8, 1, 1}, 250.f, 2}};
 constexpr int kNumX3 = sizeof(kX3Tiles) / sizeof(kX3Tiles[0]);
 
 static const TileCfg &tile_cfg(const s2v_conv_params *p, int tile);
@@ -552,6 +552,7 @@ static Plan make_plan_x3(const s2v_conv_params *p, int M, Plan pl) {
         const X3Cfg &c = kX3Tiles[i];
         if (p->b_kn && c.t.nw != 4) continue;
         if (c.t.bm == 256 && c.t.bn == 256 && am != 0 && am != 3) continue;   // generic gathers spill there
+        if (c.t.bm == 256 && c.t.bn == 64 && am != 0) continue;   // measured slower than 128x64 on per-row gathers
         const long long tiles = (long long)cdiv(M, c.t.bm) * cdiv(p->cout, c.t.bn) * batch;
         const double slots = (double)cus * c.bpc;
         for (int s = 1; s <= 16; s *= 2) {

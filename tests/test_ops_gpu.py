@@ -105,6 +105,9 @@ CONV_CASES = [
     # bf16x3 256x128 8-wave tile (force_tile 7; the f32 table has 6 tiles)
     (2, 64, 18, 16, 128, 3, 1, 1, 1, "direct", "zero", 7, 0),
     (2, 96, 10, 11, 72, 3, 1, 1, 1, "up2", "reflect", 7, 2),
+    # bf16x3 256x64 8-wave tile (force_tile 8: large-M, 64-channel layers)
+    (2, 64, 20, 18, 64, 3, 1, 1, 1, "direct", "reflect", 8, 0),
+    (1, 32, 17, 23, 40, 3, 2, 1, 1, "direct", "zero", 8, 3),
 ]
 
 
@@ -112,7 +115,7 @@ CONV_CASES = [
 def test_conv2d(ctx, prec, case):
     n, cin, h, w, cout, k, stride, pad, dil, mode, pad_mode, tile, splits = case
     if tile > 6 and prec == "f32":
-        pytest.skip("tile 7 exists in the bf16x3 table only")
+        pytest.skip("tiles 7-8 exist in the bf16x3 table only")
     kh, kw = (k, k) if isinstance(k, int) else k
     transposed = mode == "transposed"
     wshape = (cin, cout, kh, kw) if transposed else (cout, cin, kh, kw)
