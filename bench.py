@@ -18,6 +18,8 @@ Other workloads (not the headline metric):
                         384x384 frames (s2v_amd.pipeline.LipSyncPipeline.run_batch), plus the
                         host precompute of a 1000-frame clip timed once;
   --workload enhance    one step = B 512x512 faces through GFPGANv1Clean and GPEN-512;
+  --workload lnet       one step = LNet forward alone on B=16 (BASELINE configs[1]): 256x256 crops
+                        bilinear-resized to 96x96 as ENet.py:104 does, then models/LNet.py:122-139;
   --workload mouth      one step = B 720x720 frames through the mouth-region post-process
                         (FaceParse-512 mask of the face box + 10-level Laplacian blend,
                         inference.py:302-313, s2v_amd.post.MouthBlend).
@@ -53,7 +55,7 @@ ARITH = {"bf16x3": "bf16x3: fp32 tensors, conv products as split-fp32 hi*hi+hi*l
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--workload", choices=("lipsync", "pipeline", "enhance", "mouth"), default="lipsync")
+    ap.add_argument("--workload", choices=("lipsync", "lnet", "pipeline", "enhance", "mouth"), default="lipsync")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=0, help="0 = the workload's default (16, or 4 for enhance)")
@@ -187,6 +189,47 @@ class LipSync(Workload):
         return {"value": round(n / el, 4), "unit": "frames/s", "cores": threads, "kind": "port",
                 "sample": f"{n} frames (2-frame batches) of the same ENet(+LNet) {self.size}x{self.size} workload "
                           f"in {el:.1f}s, torch CPU fp32, {threads} threads"}
+
+
+class LNetOnly(Workload):
+    metric = "LNet-only frames/sec/GPU (B=16 synthetic 256x256 crops -> 96x96 LNet, BASELINE configs[1])"
+    gflop_per_unit = 56.14
+
+    def __init__(self, args, dev, rank):
+        from s2v_amd import models, ops, synth
+        from s2v_amd.models import arch
+        self.batch = args.batch or 16
+        self.sd = synth.synth_torch_state_dict(arch.LNetParams())
+        self.model = models.LNet()
+        self.model.load_state_dict(self.sd)
+        self.model.eval()
+        self.size = args.size
+        mel, face, _ = make_inputs(self.batch, args.size, dev, 5000 + rank)
+        self.inputs = [mel, face]
+        self.x96 = torch.empty((self.batch, 6, 96, 96), device=dev)
+        ctx = ops.Ctx(dev)
+
+        def step(m, f):
+            # F.interpolate(face, (96, 96), mode='bilinear') (ENet.py:104) on the device, then LNet
+            ops.resize(ctx, f.data_ptr(), tuple(f.shape), f.stride(), self.x96.data_ptr(), (96, 96), self.x96.stride())
+            return self.model(m, self.x96)
+        self.fn = step
+        self.config = {"workload": f"LNet forward, B={self.batch} synthetic {args.size}x{args.size} 6-channel crops "
+                                   "(lower half of the masked half zeroed) bilinear-resized to 96x96 + [1,80,16] mel "
+                                   "windows (models/LNet.py:122-139)", "crop": args.size}
+
+    def forward(self):
+        return self.fn(*self.inputs)
+
+    def cpu(self, threads, seconds):
+        import torch.nn.functional as F
+        from oracle import nets
+        torch.set_num_threads(threads)
+        mel, face, _ = make_inputs(2, self.size, "cpu", 1234)
+        f96 = F.interpolate(face, (96, 96), mode="bilinear", align_corners=False)
+        n, el = _timed_cpu(lambda: nets.lnet_forward(self.sd, mel, f96), 2, seconds, 64)
+        return {"value": round(n / el, 4), "unit": "frames/s", "cores": threads, "kind": "port",
+                "sample": f"{n} frames (2-frame batches) of LNet at 96x96 in {el:.1f}s, torch CPU fp32, {threads} threads"}
 
 
 class Pipeline(Workload):
@@ -336,7 +379,7 @@ class Mouth(Workload):
                           f"{el:.1f}s, {threads} threads"}
 
 
-WORKLOADS = {"lipsync": LipSync, "pipeline": Pipeline, "enhance": Enhance, "mouth": Mouth}
+WORKLOADS = {"lipsync": LipSync, "lnet": LNetOnly, "pipeline": Pipeline, "enhance": Enhance, "mouth": Mouth}
 
 
 def main():
