@@ -100,6 +100,12 @@ typedef struct s2v_conv_params {
      *                    matrix is split on the fly. */
     int prec;
     const void *wt_x3;
+    /* optional in-launch split-K fold: >= grid tiles (batch x M-tiles x N-tiles) zero-initialised ints.
+     * When given, the last-arriving split block of each output tile sums the tile's partials in split
+     * order (the same sums as the separate reduce) and runs the epilogue; the counters are left zero.
+     * NULL / too short: a separate reduce kernel folds the workspace (faster on MI355X: the fold's
+     * agent-scope release / acquire per split block costs more than the extra launch). */
+    int *tile_counters; int n_counters;
 } s2v_conv_params;
 
 enum { S2V_PREC_F32 = 0, S2V_PREC_BF16X3 = 1 };

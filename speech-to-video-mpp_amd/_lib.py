@@ -40,6 +40,7 @@ class ConvParams(ctypes.Structure):
         ("force_tile", _c_int), ("force_splits", _c_int),
         ("out_step", _c_int), ("out_full_h", _c_int), ("out_full_w", _c_int),
         ("prec", _c_int), ("wt_x3", _vp),
+        ("tile_counters", _vp), ("n_counters", _c_int),
     ]
 
 

@@ -697,6 +697,7 @@ static ConvArgs make_args(const s2v_conv_params *p, int M, int K, const Plan &pl
     a.x_bs = p->x_bs; a.w_bs = p->w_bs; a.y_bs = p->y_bs; a.res_bs = p->res_bs;
     a.M = M; a.K = K; a.ktiles = pl.ktiles; a.splits = pl.splits; a.tps = pl.tps; a.ws = p->ws;
     a.y_step = p->out_step > 1 ? p->out_step : 1; a.y_h = p->out_full_h; a.y_w = p->out_full_w;
+    a.cnt = nullptr;
     return a;
 }
 
@@ -818,6 +819,8 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
     const bool bkn = p->b_kn != 0;
     const TileCfg &t = tile_cfg(p, pl.tile);
     dim3 grid(cdiv(M, t.bm), cdiv(p->cout, t.bn), batch * pl.splits);
+    if (pl.splits > 1 && p->tile_counters && p->n_counters >= (long long)grid.x * grid.y * batch)
+        a.cnt = p->tile_counters;                       // fold in the launch itself
     if (tiled_x3(p)) {
         if (!bkn) a.wt = (const float *)p->wt_x3;
         launch_conv_x3(pl.tile, a, amode, bkn, grid, s);
@@ -830,7 +833,7 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
         default: launch_tile<128, 32, 4>(a, amode, bkn, grid, s); break;
     }
     rc = check_launch("conv_igemm");
-    if (rc || pl.splits <= 1) return rc;
+    if (rc || pl.splits <= 1 || a.cnt) return rc;
     const long long total = (long long)batch * M * (p->cout % 4 == 0 ? p->cout / 4 : p->cout);
     unsigned blocks = cdiv(total, 256);
     if (blocks > 65535u * 4u) blocks = 65535u * 4u;

@@ -34,6 +34,7 @@ struct ConvArgs {
     int M, K, ktiles, splits, tps;
     float *ws;
     int y_step, y_h, y_w;   // strided (polyphase) output, y_step > 1
+    int *cnt;               // split-K tile counters (in-launch fold), or null
 };
 
 // Element offset of output row m (flattened n, oy, ox) for channel 0.
@@ -376,6 +377,38 @@ __device__ __forceinline__ void epilogue_tile(const ConvArgs &a, const floatx16 
         } else {
 #pragma unroll 1
             for (int rr = tid / TPR; rr < clim; rr += RSTEP) store_epilogue(a, bidx, m0 + c0 + rr, n, Cs[rr * LDC + cn]);
+        }
+    }
+    if (a.splits > 1 && a.cnt) {
+        // In-launch split-K fold (cdna_hip_programming.md, "Projection GEMM" item 2): publish this
+        // split's slab (release at agent scope, then the ticket); the tile's last arriver acquires,
+        // sums every slab in split order — the separate reduce's sums — and runs the epilogue.
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        int *flag = (int *)Cs;
+        const int tile = (bidx * gridDim.x + m0 / BM) * gridDim.y + n0 / BN;
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const int old = __hip_atomic_fetch_add(a.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int last = old == a.splits - 1;
+            if (last) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(a.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            flag[0] = last;
+        }
+        __syncthreads();
+        if (!flag[0] || !live) return;
+        const long long slab = (long long)a.M * a.cout;
+        const float *src = a.ws + (long long)bidx * a.splits * slab + n;
+#pragma unroll 1
+        for (int rr = tid / TPR; rr < mlim; rr += RSTEP) {
+            const long long m = m0 + rr;
+            float v = src[m * a.cout];
+            for (int sp = 1; sp < a.splits; ++sp) v += src[sp * slab + m * a.cout];
+            store_epilogue(a, bidx, (int)m, n, v);
         }
     }
 }

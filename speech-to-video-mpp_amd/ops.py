@@ -31,6 +31,13 @@ if PRECISION not in _PRECISIONS:
     raise ValueError(f"S2V_PRECISION must be one of {sorted(_PRECISIONS)}, got {PRECISION!r}")
 
 
+# in-launch split-K fold (s2v_conv_params.tile_counters), opt-in with S2V_SPLITK_FOLD=1.  It gives
+# the separate reduce kernel's sums bit for bit, but its agent-scope release / acquire per split
+# block (L2 writeback + invalidate on this part) measured 1.5x slower end to end on MI355X (lipsync
+# 445 -> 290 frames/s, r01), so the separate reduce launch stays the default.
+USE_TILE_COUNTERS = os.environ.get("S2V_SPLITK_FOLD", "0") == "1"
+
+
 def set_precision(name: str) -> str:
     """Select the conv arithmetic ("bf16x3" or "f32") for launches issued from now on; returns the
     previous setting.  A captured HIP graph keeps the precision it was captured with."""
@@ -101,10 +108,22 @@ class Workspace:
 class Ctx:
     """Execution context: device, stream handle, workspace."""
 
+    N_COUNTERS = 1 << 18
+
     def __init__(self, device):
         self.device = torch.device(device)
         self.ws = Workspace(self.device)
         self.lib = _lib.load()
+        self._counters = None
+
+    def counters(self):
+        """Zeroed split-K tile counters (s2v_conv_params.tile_counters), made once per context
+        (eagerly, before any graph capture replays the convs that use them)."""
+        if self._counters is None:
+            if self.device.type != "cuda" or torch.cuda.is_current_stream_capturing():
+                return None
+            self._counters = torch.zeros(self.N_COUNTERS, dtype=torch.int32, device=self.device)
+        return self._counters
 
     @property
     def stream(self):
@@ -293,6 +312,7 @@ def _conv(ctx, x, cw, y, ohw, out_view, act, alpha, res, res_after, res_offset, 
         p.wt_x3 = cw.wt_x3(ctx).data_ptr()
     need = ctx.lib.s2v_conv2d_ws_bytes(ctypes.byref(p))
     p.ws, p.ws_bytes = ctx.ws.get(need)
+    _set_counters(ctx, p, need)
     if CONV_HOOK is not None:
         # algorithmic MACs: a transposed conv only counts real (non-inserted-zero) taps
         taps = cw.kh * cw.kw
@@ -348,11 +368,21 @@ def gemm_kn(ctx: Ctx, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, ba
     p.force_tile, p.force_splits = force_tile, force_splits
     need = ctx.lib.s2v_conv2d_ws_bytes(ctypes.byref(p))
     p.ws, p.ws_bytes = ctx.ws.get(need)
+    _set_counters(ctx, p, need)
     if CONV_HOOK is not None:   # DFT products: executed work, not reference-algorithmic FLOPs
         CONV_HOOK(ctx, p, 0.0, lambda: check(ctx.lib.s2v_conv2d(ctypes.byref(p), ctx.stream), "s2v_conv2d(gemm)"))
         return out
     check(ctx.lib.s2v_conv2d(ctypes.byref(p), ctx.stream), "s2v_conv2d(gemm)")
     return out
+
+
+def _set_counters(ctx: Ctx, p, ws_need):
+    """Split-K launches fold their partial sums in-launch when the context has tile counters."""
+    if ws_need and USE_TILE_COUNTERS:
+        c = getattr(ctx, "counters", None)
+        t = c() if callable(c) else None
+        if t is not None:
+            p.tile_counters, p.n_counters = t.data_ptr(), t.numel()
 
 
 def _plan(ctx: Ctx, p):

@@ -166,6 +166,29 @@ def test_conv2d(ctx, prec, case):
         assert (err <= lim).all(), f"variant {variant}: max err {err.max():.3e}, rel {(err / lim).max():.2f}"
 
 
+def test_splitk_fold_matches_separate_reduce(ctx, prec):
+    """The in-launch split-K fold (tile counters, last arriver sums) gives the separate reduce
+    kernel's sums bit for bit and leaves the counters zero."""
+    x = rnd(2, 64, 13, 11, seed=21)
+    wt = rnd(96, 64, 3, 3, seed=22) / 24.0
+    cw = ConvW(wt.float(), rnd(96, seed=23).float(), DEV, padding=1)
+    outs = []
+    try:
+        for fold in (True, False):
+            ops.USE_TILE_COUNTERS = fold
+            for tile, splits in ((4, 3), (5, 4), (0, 0)):
+                y = NHWC.empty(2, 13, 11, 96, DEV)
+                ops.conv2d(ctx, nhwc(x.float()), cw, y, act=ops.ACT_LRELU, alpha=0.2, force_tile=tile,
+                           force_splits=splits)
+                outs.append(y.t.cpu())
+    finally:
+        ops.USE_TILE_COUNTERS = True
+    for a, b in zip(outs[:3], outs[3:]):
+        assert torch.equal(a, b)
+    torch.cuda.synchronize()
+    assert int(ctx.counters().abs().sum()) == 0
+
+
 @pytest.mark.parametrize("cfg", [
     dict(n=2, cin=64, h=7, w=9, cout=96, k=3, pad=0, op=0),      # GPEN upsampling modconv (:262-276)
     dict(n=2, cin=32, h=6, w=6, cout=64, k=3, pad=1, op=1),      # DNet ADAINDecoderBlock (base_blocks.py:240-250)
