@@ -7,7 +7,7 @@ set -e
 set -o pipefail
 OUT=${OUT:-gpurun_out/prof}
 PMC_WORKLOADS=${PMC_WORKLOADS:-lipsync}
-STATS_WORKLOADS=${STATS_WORKLOADS:-"lipsync pipeline enhance"}
+STATS_WORKLOADS=${STATS_WORKLOADS:-"lipsync lnet pipeline enhance mouth"}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 for w in $STATS_WORKLOADS; do
