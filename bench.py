@@ -22,7 +22,9 @@ Other workloads (not the headline metric):
                         bilinear-resized to 96x96 as ENet.py:104 does, then models/LNet.py:122-139;
   --workload mouth      one step = B 720x720 frames through the mouth-region post-process
                         (FaceParse-512 mask of the face box + 10-level Laplacian blend,
-                        inference.py:302-313, s2v_amd.post.MouthBlend).
+                        inference.py:302-313, s2v_amd.post.MouthBlend);
+  --workload sr         one step = B 720x720 uint8 frames through RealESRNet x2 (SURVEY.md §8f(2):
+                        FaceEnhancement's srmodel.process on every full frame, s2v_amd.sr).
 """
 from __future__ import annotations
 
@@ -55,7 +57,7 @@ ARITH = {"bf16x3": "bf16x3: fp32 tensors, conv products as split-fp32 hi*hi+hi*l
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--workload", choices=("lipsync", "lnet", "pipeline", "enhance", "mouth"), default="lipsync")
+    ap.add_argument("--workload", choices=tuple(WORKLOADS), default="lipsync")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=0, help="0 = the workload's default (16, or 4 for enhance)")
@@ -379,7 +381,45 @@ class Mouth(Workload):
                           f"{el:.1f}s, {threads} threads"}
 
 
-WORKLOADS = {"lipsync": LipSync, "lnet": LNetOnly, "pipeline": Pipeline, "enhance": Enhance, "mouth": Mouth}
+class SuperRes(Workload):
+    metric = "super-resolved 720x720 -> 1440x1440 frames/sec/GPU (RealESRNet x2, RRDBNet nf=32, 23 blocks)"
+    FRAME = 720
+
+    def __init__(self, args, dev, rank):
+        from s2v_amd import models, synth
+        from s2v_amd.models import sr_arch
+        from s2v_amd.sr import RealESRNet
+        self.batch = args.batch or 2
+        self.gflop_per_unit = round(sr_arch.rrdb_gflop(self.FRAME, self.FRAME, 2), 2)
+        self.sd = synth.synth_torch_state_dict(sr_arch.RRDBNetParams(3, 3, scale=2, num_feat=32), **synth.RRDB_SYNTH)
+        net = models.RRDBNet(3, 3, scale=2, num_feat=32, num_block=23, num_grow_ch=32)
+        net.load_state_dict(self.sd)
+        self.sr = RealESRNet(scale=2, device=dev, net=net)
+        b, S = self.batch, self.FRAME
+        g = torch.Generator(device=dev)
+        g.manual_seed(5000 + rank)
+        self.inputs = [torch.randint(0, 256, (b, S, S, 3), generator=g, device=dev, dtype=torch.uint8)]
+        self.out = torch.empty((b, 2 * S, 2 * S, 3), dtype=torch.uint8, device=dev)
+        self.fn = lambda f: self.sr.process_device(f, self.out)  # noqa: E731
+        self.config = {"workload": f"RealESRNet.process (scale 2, sr_model=None: realesrnet_x2, num_feat 32, 23 RRDB) "
+                                   f"on B={b} synthetic {S}x{S} uint8 BGR frames -> {2 * S}x{2 * S} uint8 "
+                                   "(face_enhancement.py:102-105, real_esrnet.py:99-137)"}
+
+    def forward(self):
+        return self.fn(*self.inputs)
+
+    def cpu(self, threads, seconds):
+        from oracle import sr as OSR
+        torch.set_num_threads(threads)
+        img = self.inputs[0][0].cpu().numpy()
+        n, el = _timed_cpu(lambda: OSR.realesrnet_process(self.sd, img, 2), 1, seconds, 4)
+        return {"value": round(n / el, 4), "unit": "frames/s", "cores": threads, "kind": "port",
+                "sample": f"{n} {self.FRAME}x{self.FRAME} frames through the oracle restatement (torch CPU RRDBNet "
+                          f"+ NumPy uint8 ends) in {el:.1f}s, {threads} threads"}
+
+
+WORKLOADS = {"lipsync": LipSync, "lnet": LNetOnly, "pipeline": Pipeline, "enhance": Enhance, "mouth": Mouth,
+             "sr": SuperRes}
 
 
 def main():

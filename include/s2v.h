@@ -297,6 +297,18 @@ int s2v_parse_mask(const float *x, int n, int h, int w, int c, long long xbs, lo
  * fp32 RGB (img / 255. * 2 - 1, in float64 then rounded) at pixel pitch ycs (>= 3; channel 3 = 0). */
 int s2v_img_u8_to_m11(const unsigned char *x, long long pixels, int flip, float *y, int ycs, s2v_stream_t stream);
 
+/* ---- Super-resolution front / back end (real_esrnet.py:99-137) ---------------- */
+
+/* RealESRNet.process input (real_esrnet.py:100-115): uint8 HWC frames [n,h,w,3] (BGR if ``flip``)
+ * -> fp32 RGB x / 255 at pixel pitch ycs (>= 3; channel 3 = 0) of [n, h+pad_b, w+pad_r],
+ * F.pad 'reflect' on the bottom / right (pad < dimension, as F.pad requires). */
+int s2v_sr_u8_in(const unsigned char *x, int n, int h, int w, int flip, int pad_b, int pad_r, float *y, int ycs,
+                 s2v_stream_t stream);
+/* RealESRNet.process output (:126-131): the top-left h x w crop of an NHWC fp32 image [n,xh,xw,xcs]
+ * -> uint8 [n,h,w,3] = round_half_even(clamp(x, 0, 1) * 255) (channels reversed if ``flip``). */
+int s2v_sr_f32_out(const float *x, int n, int h, int w, int xh, int xw, int xcs, int flip, unsigned char *y,
+                   s2v_stream_t stream);
+
 const char *s2v_last_error(void);
 /* number of compute units of the current device (0 if no device) */
 int s2v_device_cus(void);

@@ -95,6 +95,8 @@ _SIGS = {
                                      _vp]),
     "s2v_parse_mask": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_ll, _c_ll, _c_ll, _vp, _vp, _vp, _vp]),
     "s2v_img_u8_to_m11": (_c_int, [_vp, _c_ll, _c_int, _vp, _c_int, _vp]),
+    "s2v_sr_u8_in": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp]),
+    "s2v_sr_f32_out": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp]),
     "s2v_last_error": (ctypes.c_char_p, []),
     "s2v_device_cus": (_c_int, []),
     "s2v_version": (ctypes.c_char_p, []),

@@ -16,7 +16,7 @@ import torch
 
 from .. import ops
 from ..ops import NHWC
-from . import arch, enhancer_arch, parse_arch
+from . import arch, enhancer_arch, parse_arch, sr_arch
 
 
 def _fold5(x, dim):
@@ -187,6 +187,28 @@ class ParseNet(_EngineMixin, parse_arch.ParseNetParams):
         return eng.forward(ctx, x.float(), mask, img)
 
 
+class RRDBNet(_EngineMixin, sr_arch.RRDBNetParams):
+    """third_part/GPEN/sr_model/rrdbnet_arch.py:63-116 (RealESRNet: RRDBNet(3, 3, num_feat=32,
+    num_block=23, num_grow_ch=32, scale=2|4), real_esrnet.py:22)."""
+
+    def _build_engine(self, sd, device):
+        from ..engine.rrdb import RRDBEngine
+        return RRDBEngine(sd, device, self.scale, self.num_in_ch)
+
+    @torch.no_grad()
+    def forward(self, x):
+        """x [B, num_in_ch, H, W] -> [B, num_out_ch, scale H, scale W] (H, W multiples of the
+        pixel-unshuffle factor for scale 2 / 1, as arch_util.pixel_unshuffle asserts)."""
+        _need_cuda(x)
+        eng, ctx = self._engine(x.device)
+        r = eng.r
+        if x.shape[2] % r or x.shape[3] % r:
+            raise RuntimeError(f"RRDBNet(scale={self.scale}): input size {tuple(x.shape[2:])} must be a multiple of {r}")
+        b, _, h, w = x.shape
+        out = torch.empty((b, self.num_out_ch, h * self.scale, w * self.scale), device=x.device)
+        return eng.forward(ctx, x.float(), out)
+
+
 # ----------------------------------------------------------------------------- loaders
 def _load(path):
     return torch.load(path, map_location="cpu", weights_only=True)
@@ -251,5 +273,13 @@ def load_parsenet(path, size=512):
     return net.eval()
 
 
-__all__ = ["LNet", "ENet", "DNet", "GFPGANv1Clean", "FullGenerator", "ParseNet", "load_checkpoint", "load_network",
-           "load_DNet", "load_gfpgan", "load_gpen", "load_parsenet"]
+def load_srmodel(path, scale=2, num_feat=32):
+    """real_esrnet.py:21-30: RRDBNet(3, 3, num_feat, num_block=23, num_grow_ch=32, scale) with the
+    ``params_ema`` weights, strict=True."""
+    net = RRDBNet(num_in_ch=3, num_out_ch=3, num_feat=num_feat, num_block=23, num_grow_ch=32, scale=scale)
+    net.load_state_dict(_load(path)["params_ema"], strict=True)
+    return net.eval()
+
+
+__all__ = ["LNet", "ENet", "DNet", "GFPGANv1Clean", "FullGenerator", "ParseNet", "RRDBNet", "load_checkpoint",
+           "load_network", "load_DNet", "load_gfpgan", "load_gpen", "load_parsenet", "load_srmodel"]

@@ -153,6 +153,8 @@ GPEN_SYNTH = dict(noise_weight=0.1, equal=True)
 # ParseNet: 18 residual blocks add their branch to the identity level after level; gain 1.0 keeps
 # the synthetic logits O(1..10) so the argmax is not decided by fp32 rounding
 PARSENET_SYNTH = dict(gain=1.0)
+# RRDBNet (RealESRNet): 69 dense blocks, each added back at 0.2; gain 1.0 like ParseNet
+RRDB_SYNTH = dict(gain=1.0)
 
 
 # ----------------------------------------------------------------------------- inputs
@@ -183,6 +185,11 @@ def dnet_inputs(tag: str, batch: int, size: int):
     src = hash_array(f"{tag}.src", (batch, 3, size, size), -1.0, 1.0)
     coeff = hash_array(f"{tag}.coeff", (batch, 73, 26), -1.5, 1.5)
     return src, coeff
+
+
+def sr_frame(tag: str, batch: int, h: int, w: int) -> np.ndarray:
+    """uint8 HWC BGR frames [B,H,W,3] (RealESRNet.process input, real_esrnet.py:99-101)."""
+    return np.floor(hash_array(f"{tag}.frame", (batch, h, w, 3), 0.0, 256.0)).clip(0, 255).astype(np.uint8)
 
 
 def probe_indices(n: int, count: int = 2048, key: str = "probe") -> np.ndarray:

@@ -10,7 +10,7 @@ Import shims (neither touches arithmetic; both documented in SURVEY.md §8c):
     own vendored copy third_part/GPEN/sr_model/arch_util.py (only used for init, which the
     synthetic state_dict overwrites).
 
-Usage:  python tests/golden/make_golden.py [--only lnet,enet,dnet,ops,gfpgan,gpen,parsenet]
+Usage:  python tests/golden/make_golden.py [--only lnet,enet,dnet,ops,gfpgan,gpen,parsenet,rrdbnet]
 """
 import argparse
 import importlib.util
@@ -274,6 +274,41 @@ def gen_parsenet():
                 pr = _probe(t, f"parsenet.{name}")
                 arrays.update({f"{name}_idx": pr["idx"], f"{name}_val": pr["val"], f"{name}_stats": pr["stats"]})
         _save(f"parsenet_b{batch}_{size}", arrays)
+
+
+# RealESRNet cases (tests/helpers.py): (tag, scale, input [B,3,H,W]) for the forward, (tag, scale,
+# frame H, W, tile, tile_pad) for RealESRNet.process on uint8 frames (odd sizes: reflect padding)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+from helpers import RRDB_FORWARD, RRDB_PROCESS  # noqa: E402
+
+
+def gen_rrdbnet():
+    """third_part/GPEN/sr_model (RRDBNet + RealESRNet.process) at the FaceEnhancement configuration
+    num_feat=32, num_block=23, num_grow_ch=32 (face_enhancement.py:58, real_esrnet.py:9-23)."""
+    import tempfile
+    sys.path.insert(0, os.path.join(REF, "third_part/GPEN/sr_model"))
+    from rrdbnet_arch import RRDBNet
+    from real_esrnet import RealESRNet
+    from s2v_amd.models.sr_arch import RRDBNetParams
+    arrays = {}
+    for tag, scale, shape in RRDB_FORWARD:
+        ref = RRDBNet(3, 3, scale=scale, num_feat=32, num_block=23, num_grow_ch=32).eval()
+        _check_keys("rrdbnet" if scale == 2 else f"rrdbnet_x{scale}", ref,
+                    RRDBNetParams(3, 3, scale=scale, num_feat=32, num_block=23, num_grow_ch=32))
+        ref.load_state_dict(synth.synth_torch_state_dict(ref, **synth.RRDB_SYNTH), strict=True)
+        x = synth.hash_array(f"golden.rrdb.{tag}", shape, 0.0, 1.0)
+        with torch.no_grad():
+            arrays[f"fwd_{tag}"] = ref(torch.from_numpy(x)).numpy()
+    for tag, scale, h, w, tile, pad in RRDB_PROCESS:
+        ref = RRDBNet(3, 3, scale=scale, num_feat=32, num_block=23, num_grow_ch=32)
+        with tempfile.TemporaryDirectory() as d:
+            os.makedirs(os.path.join(d, "weights"))
+            torch.save({"params_ema": synth.synth_torch_state_dict(ref, **synth.RRDB_SYNTH)},
+                       os.path.join(d, "weights", f"realesrnet_x{scale}.pth"))
+            sr = RealESRNet(d, None, scale=scale, tile_size=tile, tile_pad=pad, device="cpu")
+        img = synth.sr_frame(f"golden.rrdb.{tag}", 1, h, w)[0]
+        arrays[f"proc_{tag}"] = sr.process(img)
+    _save("rrdbnet_goldens", arrays)
 
 
 if __name__ == "__main__":

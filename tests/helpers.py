@@ -34,6 +34,19 @@ def parsenet_sd(size: int = 512):
     return synth.synth_torch_state_dict(ParseNetParams(**face_parse_net(size)), **synth.PARSENET_SYNTH)
 
 
+# tests/golden/make_golden.py RRDB_FORWARD / RRDB_PROCESS (kept in sync; the GPU box has no reference)
+RRDB_FORWARD = (("s2", 2, (1, 3, 32, 28)), ("s4", 4, (1, 3, 12, 16)), ("s1", 1, (2, 3, 16, 24)))
+RRDB_PROCESS = (("p2", 2, 27, 31, 0, 10), ("p2t", 2, 30, 26, 16, 4), ("p4", 4, 13, 11, 0, 10))
+
+
+@functools.lru_cache(maxsize=None)
+def rrdb_sd(scale: int = 2, num_feat: int = 32):
+    """Synthetic RRDBNet state_dict at the RealESRNet configuration (real_esrnet.py:22)."""
+    from s2v_amd.models.sr_arch import RRDBNetParams
+    return synth.synth_torch_state_dict(RRDBNetParams(3, 3, scale=scale, num_feat=num_feat, num_block=23,
+                                                      num_grow_ch=32), **synth.RRDB_SYNTH)
+
+
 def max_abs(a, b):
     a = a.detach().cpu().double().numpy() if isinstance(a, torch.Tensor) else np.asarray(a, np.float64)
     b = b.detach().cpu().double().numpy() if isinstance(b, torch.Tensor) else np.asarray(b, np.float64)

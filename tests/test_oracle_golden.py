@@ -124,3 +124,41 @@ def test_parsenet_oracle_matches_reference(golden):
             check_probe(img, g, "img", atol=1e-4 * float(g["img_stats"][2]))
         agree = (mask.argmax(1).numpy() == g["argmax"]).mean()
         assert agree > 0.9999, agree
+
+
+def test_rrdbnet_oracle_matches_reference(golden):
+    """oracle/sr.py vs the reference RRDBNet forward (rrdbnet_arch.py) and RealESRNet.process
+    (real_esrnet.py:99-137, incl. reflect padding, tiling and the uint8 rounding) run unmodified."""
+    from helpers import RRDB_FORWARD, RRDB_PROCESS, rrdb_sd
+    from oracle import sr
+    g = golden("rrdbnet_goldens")
+    for tag, scale, shape in RRDB_FORWARD:
+        x = torch.from_numpy(synth.hash_array(f"golden.rrdb.{tag}", shape, 0.0, 1.0))
+        with torch.no_grad():
+            y = sr.rrdbnet_forward(rrdb_sd(scale), x, scale).numpy()
+        ref = g[f"fwd_{tag}"]
+        assert y.shape == ref.shape
+        assert np.abs(y - ref).max() <= 1e-4 * np.abs(ref).max(), tag
+    for tag, scale, h, w, tile, pad in RRDB_PROCESS:
+        img = synth.sr_frame(f"golden.rrdb.{tag}", 1, h, w)[0]
+        out = sr.realesrnet_process(rrdb_sd(scale), img, scale, tile, pad)
+        ref = g[f"proc_{tag}"]
+        # the reference crops only h_pad / w_pad rows / columns off the *upscaled* output
+        # (real_esrnet.py:126-128), so an odd 27x31 frame at x2 gives 55x63, not 54x62
+        hp, wp = (-h) % {2: 2, 1: 4}.get(scale, 1), (-w) % {2: 2, 1: 4}.get(scale, 1)
+        assert out.shape == ref.shape == ((h + hp) * scale - hp, (w + wp) * scale - wp, 3)
+        assert (np.abs(out.astype(int) - ref.astype(int)) <= 1).all() and (out != ref).mean() <= 1e-3, tag
+
+
+def test_rrdbnet_state_dict_layout_matches_reference():
+    """models.sr_arch.RRDBNetParams has the reference's RRDBNet keys and shapes (manifests written by
+    make_golden.py from the reference modules) for every scale."""
+    import json
+    import os
+    from s2v_amd.models.sr_arch import RRDBNetParams
+    here = os.path.join(os.path.dirname(__file__), "golden")
+    for scale, name in ((2, "rrdbnet"), (4, "rrdbnet_x4"), (1, "rrdbnet_x1")):
+        with open(os.path.join(here, f"{name}_keys.json")) as f:
+            ref = json.load(f)
+        mine = {k: list(v.shape) for k, v in RRDBNetParams(3, 3, scale=scale, num_feat=32).state_dict().items()}
+        assert mine == ref
