@@ -553,6 +553,8 @@ static Plan make_plan_x3(const s2v_conv_params *p, int M, Plan pl) {
         if (p->b_kn && c.t.nw != 4) continue;
         if (c.t.bm == 256 && c.t.bn == 256 && am != 0 && am != 3) continue;   // generic gathers spill there
         if (c.t.bm == 256 && c.t.bn == 64 && am != 0) continue;   // measured slower than 128x64 on per-row gathers
+        if (c.t.bm == 64 && c.t.bn == 64 && p->cout <= 32) continue;     // see validate()
+        if (!p->b_kn && (long long)cdiv(p->cout, c.t.bn) * c.t.bn > p->npad) continue;   // weight rows
         const long long tiles = (long long)cdiv(M, c.t.bm) * cdiv(p->cout, c.t.bn) * batch;
         const double slots = (double)cus * c.bpc;
         for (int s = 1; s <= 16; s *= 2) {
@@ -637,6 +639,16 @@ static int validate(const s2v_conv_params *p, int &M, int &K) {
                 "conv2d: bad force_tile %d", p->force_tile);
     S2V_REQUIRE(!(tiled_x3(p) && p->b_kn && p->force_tile > 0 && kX3Tiles[p->force_tile - 1].t.nw != 4),
                 "conv2d: b_kn operands need a 4-wave split-bf16 tile (force_tile 4..6)");
+    if (tiled_x3(p) && p->force_tile > 0) {
+        // a forced tile must not read weight rows past the packed [npad] rows (the planner never
+        // picks such a tile); 64x64 with cout <= 32 faulted in a tuning sweep and is not offered
+        const TileCfg &t = kX3Tiles[p->force_tile - 1].t;
+        S2V_REQUIRE(!p->b_kn ? (long long)cdiv(p->cout, t.bn) * t.bn <= p->npad : true,
+                    "conv2d: force_tile %d (BN %d) needs npad >= %d, got %d", p->force_tile, t.bn,
+                    cdiv(p->cout, t.bn) * t.bn, p->npad);
+        S2V_REQUIRE(!(t.bm == 64 && t.bn == 64 && p->cout <= 32), "conv2d: force_tile %d not offered for cout <= 32",
+                    p->force_tile);
+    }
     if (uses_x3(p))
         S2V_REQUIRE(p->wt_x3 && ((uintptr_t)p->wt_x3 % 16) == 0, "conv2d: prec BF16X3 needs 16B-aligned wt_x3");
     else

@@ -166,7 +166,9 @@ class ConvW:
         K = self.kh * self.kw * self.cin
         self.K = K
         self.kpad = (K + 31) // 32 * 32
-        self.npad = (self.cout + 127) // 128 * 128
+        # rows padded so every N tile the planner may pick (BN <= 128, or 256 when cout > 128) reads
+        # inside the packed buffer: the kernels load whole BN-row slabs of B without a row guard
+        self.npad = (self.cout + 127) // 128 * 128 if self.cout <= 128 else (self.cout + 255) // 256 * 256
         wk = w.permute(0, 2, 3, 1).reshape(self.cout, K)
         self.wt = _pad2(wk, self.npad, self.kpad).to(device)
         scale = shift = None

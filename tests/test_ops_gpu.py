@@ -73,7 +73,7 @@ def conv_bound(x, w, stride, padding, dilation, transposed=False, op=0):
 CONV_CASES = [
     # (n, cin, h, w, cout, k, stride, pad, dil, mode, pad_mode, tile, splits)
     (2, 64, 17, 19, 96, 3, 1, 1, 1, "direct", "zero", 0, 0),
-    (2, 64, 16, 16, 128, 3, 1, 1, 1, "direct", "zero", 1, 0),
+    (2, 64, 16, 16, 256, 3, 1, 1, 1, "direct", "zero", 1, 0),     # 256-wide N tile needs cout > 128
     (2, 64, 16, 16, 128, 3, 1, 1, 1, "direct", "zero", 2, 3),
     (1, 32, 20, 12, 64, 3, 2, 1, 1, "direct", "zero", 3, 0),
     (2, 32, 12, 12, 64, 3, 1, 1, 1, "direct", "zero", 4, 2),
