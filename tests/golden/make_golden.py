@@ -10,7 +10,7 @@ Import shims (neither touches arithmetic; both documented in SURVEY.md §8c):
     own vendored copy third_part/GPEN/sr_model/arch_util.py (only used for init, which the
     synthetic state_dict overwrites).
 
-Usage:  python tests/golden/make_golden.py [--only lnet,enet,dnet,ops,gfpgan,gpen,parsenet,rrdbnet]
+Usage:  python tests/golden/make_golden.py [--only lnet,enet,dnet,ops,gfpgan,gpen,gpen2048,parsenet,rrdbnet]
 """
 import argparse
 import importlib.util
@@ -248,6 +248,26 @@ def gen_gpen():
     p = _probe(img, "gpen.out")
     arrays.update({"out_idx": p["idx"], "out_val": p["val"], "out_stats": p["stats"]})
     _save("gpen_b1_512", arrays)
+
+
+def gen_gpen2048():
+    """GPEN-BFR-2048 (the CLI's `enhancer` face GAN, inference.py:228-231 -> FaceGAN(in_size=2048),
+    face_gan.py:26-28): FullGenerator(2048, 512, 8, 2), probes of the 2048x2048 output."""
+    sys.path.insert(0, os.path.join(REF, "third_part/GPEN/face_model"))
+    from gpen_model import FullGenerator
+    from s2v_amd.models.enhancer_arch import FullGeneratorParams
+    ref = FullGenerator(2048, 512, 8, 2, narrow=1, device="cpu").eval()
+    _check_keys("gpen2048", ref, FullGeneratorParams(2048, 512, 8, 2, narrow=1))
+    ref.load_state_dict(synth.synth_torch_state_dict(ref, **synth.GPEN_SYNTH), strict=True)
+    acts = {}
+    ref.final_linear.register_forward_hook(lambda m, i, o: acts.__setitem__("code", o))
+    x = synth.face_inputs("golden.gpen2048", 1, 2048)
+    with torch.no_grad():
+        img, _ = ref(torch.from_numpy(x))
+    arrays = {"code": acts["code"].numpy()}
+    p = _probe(img, "gpen2048.out")
+    arrays.update({"out_idx": p["idx"], "out_val": p["val"], "out_stats": p["stats"]})
+    _save("gpen_b1_2048", arrays)
 
 
 def gen_parsenet():

@@ -22,6 +22,8 @@ def synth_sd(net: str):
         return synth.synth_torch_state_dict(ea.GFPGANv1CleanParams(**GFPGAN_KW), **synth.GFPGAN_SYNTH)
     if net == "gpen":
         return synth.synth_torch_state_dict(ea.FullGeneratorParams(512, 512, 8, 2), **synth.GPEN_SYNTH)
+    if net == "gpen2048":             # GPEN-BFR-2048, the CLI's enhancer face GAN (inference.py:228-231)
+        return synth.synth_torch_state_dict(ea.FullGeneratorParams(2048, 512, 8, 2), **synth.GPEN_SYNTH)
     mod = {"lnet": lambda: arch.LNetParams(), "enet": lambda: arch.ENetParams(lnet=arch.LNetParams()),
            "dnet": lambda: arch.DNetParams()}[net]()
     return synth.synth_torch_state_dict(mod)

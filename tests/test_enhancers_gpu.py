@@ -95,6 +95,20 @@ def test_gpen_matches_reference(prec, gpen, golden):
     print("gpen out max err", err)
 
 
+def test_gpen2048_matches_reference(prec, golden):
+    """GPEN-BFR-2048 (the CLI's `enhancer` face GAN: FaceGAN(in_size=2048), inference.py:228-231;
+    16/32-channel convs at 2048^2 and 1024^2) against the reference's own output probes."""
+    from s2v_amd import models
+    m = models.FullGenerator(2048, 512, 8, 2)
+    m.load_state_dict(synth_sd("gpen2048"), strict=True)
+    g = golden("gpen_b1_2048")
+    x = torch.from_numpy(synth.face_inputs("golden.gpen2048", 1, 2048)).to(DEV)
+    img, _ = m.eval()(x)
+    assert img.shape == (1, 3, 2048, 2048)
+    err = check_probe(img, g, "out", atol=2e-4)
+    print(f"gpen2048 {prec} out max err {err:.2e} (|out| max {g['out_stats'][2]:.2f})")
+
+
 def test_gpen_batch_vs_oracle(gpen):
     from oracle import enhancers
     x = torch.from_numpy(synth.face_inputs("gpen.b2", 2))

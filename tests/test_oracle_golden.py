@@ -93,6 +93,22 @@ def test_gpen_oracle_matches_reference(golden):
     check_probe(img, g, "out", atol=1e-4, rtol=1e-4)
 
 
+def test_gpen2048_oracle_matches_reference(golden):
+    """GPEN-BFR-2048 (FullGenerator(2048, 512, 8, 2), face_gan.py:26-28) restatement vs the reference."""
+    import json
+    import os
+    from oracle import enhancers
+    from s2v_amd.models.enhancer_arch import FullGeneratorParams
+    with open(os.path.join(os.path.dirname(__file__), "golden", "gpen2048_keys.json")) as f:
+        assert {k: list(v.shape) for k, v in FullGeneratorParams(2048, 512, 8, 2).state_dict().items()} == json.load(f)
+    g = golden("gpen_b1_2048")
+    x = torch.from_numpy(synth.face_inputs("golden.gpen2048", 1, 2048))
+    with torch.no_grad():
+        img, _, code = enhancers.gpen_forward(synth_sd("gpen2048"), x)
+    assert max_abs(code, g["code"])[0] < 1e-5
+    check_probe(img, g, "out", atol=1e-4, rtol=1e-4)
+
+
 def test_upfirdn2d_and_fused_act_oracle_match_reference_fallbacks(golden):
     from oracle import enhancers
     g = golden("ops")
