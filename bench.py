@@ -24,7 +24,8 @@ Other workloads (not the headline metric):
                         (FaceParse-512 mask of the face box + 10-level Laplacian blend,
                         inference.py:302-313, s2v_amd.post.MouthBlend);
   --workload sr         one step = B 720x720 uint8 frames through RealESRNet x2 (SURVEY.md §8f(2):
-                        FaceEnhancement's srmodel.process on every full frame, s2v_amd.sr).
+                        FaceEnhancement's srmodel.process on every full frame, s2v_amd.sr);
+  --workload gpen2048   one step = B 2048x2048 faces through GPEN-BFR-2048 (the CLI's enhancer GAN).
 """
 from __future__ import annotations
 
@@ -418,8 +419,40 @@ class SuperRes(Workload):
                           f"+ NumPy uint8 ends) in {el:.1f}s, {threads} threads"}
 
 
+class GPEN2048(Workload):
+    metric = "enhanced 2048x2048 faces/sec/GPU (GPEN-BFR-2048 FullGenerator, the CLI enhancer face GAN)"
+    unit = "faces/s"
+    gflop_per_unit = 419.97            # torch FlopCounterMode on oracle.enhancers.gpen_forward at 2048 (2*MAC)
+
+    def __init__(self, args, dev, rank):
+        from s2v_amd import models, synth
+        from s2v_amd.models import enhancer_arch as ea
+        self.batch = args.batch or 2
+        self.sd = synth.synth_torch_state_dict(ea.FullGeneratorParams(2048, 512, 8, 2), **synth.GPEN_SYNTH)
+        self.gpen = models.FullGenerator(2048, 512, 8, 2)
+        self.gpen.load_state_dict(self.sd)
+        g = torch.Generator(device=dev)
+        g.manual_seed(6000 + rank)
+        self.inputs = [torch.rand((self.batch, 3, 2048, 2048), generator=g, device=dev) * 2 - 1]
+        self.fn = lambda x: self.gpen(x)[0]  # noqa: E731
+        self.config = {"workload": f"GPEN FullGenerator(2048, 512, 8, 2) on B={self.batch} synthetic 2048x2048 faces "
+                                   "per step (FaceGAN(in_size=2048) of inference.py:228-231, face_gan.py:26-42)"}
+
+    def forward(self):
+        return self.fn(*self.inputs)
+
+    def cpu(self, threads, seconds):
+        from oracle import enhancers
+        torch.set_num_threads(threads)
+        x = self.inputs[0][:1].cpu()
+        n, el = _timed_cpu(lambda: enhancers.gpen_forward(self.sd, x), 1, seconds, 3)
+        return {"value": round(n / el, 4), "unit": "faces/s", "cores": threads, "kind": "port",
+                "sample": f"{n} 2048x2048 faces through GPEN-2048 (oracle restatement) in {el:.1f}s, torch CPU fp32, "
+                          f"{threads} threads"}
+
+
 WORKLOADS = {"lipsync": LipSync, "lnet": LNetOnly, "pipeline": Pipeline, "enhance": Enhance, "mouth": Mouth,
-             "sr": SuperRes}
+             "sr": SuperRes, "gpen2048": GPEN2048}
 
 
 def main():

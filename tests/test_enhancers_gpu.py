@@ -105,7 +105,7 @@ def test_gpen2048_matches_reference(prec, golden):
     x = torch.from_numpy(synth.face_inputs("golden.gpen2048", 1, 2048)).to(DEV)
     img, _ = m.eval()(x)
     assert img.shape == (1, 3, 2048, 2048)
-    err = check_probe(img, g, "out", atol=2e-4)
+    err = check_probe(img, g, "out", atol=1e-4)          # measured 2.8e-6 (f32) / 3.2e-5 (bf16x3)
     print(f"gpen2048 {prec} out max err {err:.2e} (|out| max {g['out_stats'][2]:.2f})")
 
 
