@@ -36,6 +36,15 @@ __device__ __forceinline__ float apply_act(float v, int act, float alpha) {
 }
 
 // F.pad(mode='reflect') index map for one reflection (pad < n)
+// Workgroups are dispatched round-robin over the 8 XCDs (blockIdx % 8), each with its own L2.
+// Remap a 1-D grid so that XCD j runs the j-th contiguous eighth of the logical blocks: blocks that
+// share input (the rows above / below of a 3x3 stencil) then meet in one L2 instead of eight.
+__device__ __forceinline__ unsigned xcd_block(unsigned L, unsigned total) {
+    const unsigned per = total >> 3, rem = total & 7;
+    const unsigned xcd = L & 7, idx = L >> 3;
+    return xcd < rem ? xcd * (per + 1) + idx : rem * (per + 1) + (xcd - rem) * per + idx;
+}
+
 __device__ __forceinline__ int reflect_idx(int i, int n) {
     i = i < 0 ? -i : i;
     return i >= n ? 2 * n - 2 - i : i;

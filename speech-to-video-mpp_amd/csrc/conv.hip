@@ -354,7 +354,8 @@ template <int CO, int TPP, bool LW>
 __global__ __launch_bounds__(256) void conv_small_cpar(ConvArgs a, int batch) {
     extern __shared__ __attribute__((aligned(16))) float wsm_dyn[];
     const long long total = (long long)batch * a.M;
-    const long long gid = (blockIdx.x * 256LL + threadIdx.x) / TPP;
+    const unsigned blk = xcd_block(blockIdx.x, gridDim.x);      // stencil rows share one XCD's L2
+    const long long gid = (blk * 256LL + threadIdx.x) / TPP;
     const int sub = threadIdx.x % TPP;
     const bool live = gid < total;
     const int bidx = live ? (int)(gid / a.M) : 0;
@@ -369,7 +370,7 @@ __global__ __launch_bounds__(256) void conv_small_cpar(ConvArgs a, int batch) {
     if (LW) {
         // every pixel of the block belongs to the batch entry of its first pixel (the host
         // guarantees M % (256 / TPP) == 0 when the weights are per batch entry)
-        const long long g0 = blockIdx.x * (256LL / TPP);
+        const long long g0 = blk * (256LL / TPP);
         const int b0 = (int)((g0 < total ? g0 : 0) / a.M);
         const float *w0 = a.wt + (long long)b0 * a.w_bs;
         for (int e = threadIdx.x; e < CO * a.K; e += 256) {

@@ -21,7 +21,9 @@ __global__ __launch_bounds__(256) void fir2d_kernel(const float *__restrict__ x,
     for (int i = threadIdx.x; i < kh * kw; i += 256) ks[i] = k[kh * kw - 1 - i];   // flipped
     __syncthreads();
     const int cv = VEC ? c / 4 : c;
-    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    // XCD-aware order: the 4x4 FIR's neighbouring rows are read by blocks of the same L2
+    const unsigned blk = xcd_block(blockIdx.x, gridDim.x);
+    for (long long e = blk * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
         const int cc = (int)(e % cv);
         long long t = e / cv;
         const int ox = (int)(t % ow);
