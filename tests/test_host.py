@@ -234,3 +234,34 @@ def test_fft_tables_reproduce_torch_fft():
         y = ar @ iw[0].t() + ai @ iw[1].t()                                # c2r W pass
         ref = torch.fft.irfftn(torch.complex(sr, si), s=(h, w), dim=(-2, -1), norm="ortho")
         assert (y - ref).abs().max() < 1e-5
+
+
+def test_rrdb_unshuffle_fold_equals_pixel_unshuffle_conv():
+    """engine/rrdb.py folds pixel_unshuffle(x, r) + 3x3 conv (rrdbnet_arch.py:105-110) into one
+    (3r)x(3r) stride-r pad-r conv of the image; check the weight permutation on CPU for r = 2, 4."""
+    import torch
+    import torch.nn.functional as F
+    from oracle.sr import pixel_unshuffle
+    from s2v_amd.engine.rrdb import _unshuffle_weight
+    g = torch.Generator().manual_seed(0)
+    for r in (2, 4):
+        x = torch.randn(2, 3, 8 * r, 4 * r, generator=g, dtype=torch.float64)
+        w = torch.randn(5, 3 * r * r, 3, 3, generator=g, dtype=torch.float64)
+        ref = F.conv2d(pixel_unshuffle(x, r), w, None, 1, 1)
+        got = F.conv2d(x, _unshuffle_weight(w, r, 3), None, r, r)
+        assert got.shape == ref.shape and torch.allclose(got, ref, atol=1e-10), r
+
+
+def test_rrdb_gflop_matches_flop_counter():
+    """models.sr_arch.rrdb_gflop (the sr bench's GFLOP per frame) == torch's FlopCounterMode on the
+    oracle forward, for every scale."""
+    import torch
+    from torch.utils.flop_counter import FlopCounterMode
+    from oracle.sr import rrdbnet_forward
+    from s2v_amd.models.sr_arch import RRDBNetParams, rrdb_gflop
+    for scale in (1, 2, 4):
+        sd = {k: v.float() for k, v in RRDBNetParams(3, 3, scale=scale, num_feat=32, num_block=2).state_dict().items()}
+        x = torch.zeros(1, 3, 16, 12)
+        with FlopCounterMode(display=False) as fc, torch.no_grad():
+            rrdbnet_forward(sd, x, scale)
+        assert abs(fc.get_total_flops() / 1e9 - rrdb_gflop(16, 12, scale, num_block=2)) < 1e-9, scale
