@@ -438,8 +438,13 @@ static void launch_small(const ConvArgs &a, int batch, bool cpar, hipStream_t s)
         return;
     }
     // 8 lanes per pixel (each lane walks cin/32 float4s): 3 shuffle levels per output instead of
-    // 5-6 with one float4 per lane, 128-byte contiguous row pieces per load instruction
-    if (a.cin / 4 >= 8) launch_cpar<CO, 8>(a, batch, s);
+    // 5-6 with one float4 per lane, 128-byte contiguous row pieces per load instruction.  Below 128
+    // channels fewer lanes share a pixel so every lane still has >= 4 float4s in flight per tap:
+    // with one float4 per lane (32-channel ToRGB heads at 2048^2, RealESRNet's conv_last) the
+    // kernel was latency-bound at 1.5 TB/s.
+    if (a.cin >= 128) launch_cpar<CO, 8>(a, batch, s);
+    else if (a.cin >= 64) launch_cpar<CO, 4>(a, batch, s);
+    else if (a.cin >= 32) launch_cpar<CO, 2>(a, batch, s);
     else launch_cpar<CO, 4>(a, batch, s);
 }
 
