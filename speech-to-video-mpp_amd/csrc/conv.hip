@@ -430,6 +430,9 @@ static void launch_cpar(const ConvArgs &a, int batch, hipStream_t s) {
     else conv_small_cpar<CO, TPP, false><<<grid, 256, 0, s>>>(a, batch);
 }
 
+// lanes per output pixel of conv_small_cpar (launch_small and the plan report share it)
+static int cpar_lanes(int cin) { return cin >= 128 ? 8 : cin >= 64 ? 4 : cin >= 32 ? 2 : 4; }
+
 template <int CO>
 static void launch_small(const ConvArgs &a, int batch, bool cpar, hipStream_t s) {
     const long long total = (long long)batch * a.M;
@@ -442,10 +445,11 @@ static void launch_small(const ConvArgs &a, int batch, bool cpar, hipStream_t s)
     // channels fewer lanes share a pixel so every lane still has >= 4 float4s in flight per tap:
     // with one float4 per lane (32-channel ToRGB heads at 2048^2, RealESRNet's conv_last) the
     // kernel was latency-bound at 1.5 TB/s.
-    if (a.cin >= 128) launch_cpar<CO, 8>(a, batch, s);
-    else if (a.cin >= 64) launch_cpar<CO, 4>(a, batch, s);
-    else if (a.cin >= 32) launch_cpar<CO, 2>(a, batch, s);
-    else launch_cpar<CO, 4>(a, batch, s);
+    switch (cpar_lanes(a.cin)) {
+        case 8: launch_cpar<CO, 8>(a, batch, s); break;
+        case 2: launch_cpar<CO, 2>(a, batch, s); break;
+        default: launch_cpar<CO, 4>(a, batch, s); break;
+    }
 }
 
 // ------------------------------------------------------------------ host side
@@ -774,9 +778,8 @@ extern "C" int s2v_conv2d_plan(const s2v_conv_params *p, int *out6) {
         const bool cpar = (p->cin % 4 == 0) && (p->xcs % 4 == 0) && (((uintptr_t)p->x % 16) == 0) &&
                           (p->x_bs % 4 == 0) && (!p->in_scale || (p->in_scale_ns % 4 == 0 &&
                                                                   ((uintptr_t)p->in_scale % 16) == 0));
-        const int c4 = p->cin / 4;
         out6[0] = 0; out6[1] = p->cout < 4 ? p->cout : 4;
-        out6[2] = !cpar ? 0 : (c4 >= 8 ? 8 : 4);
+        out6[2] = !cpar ? 0 : cpar_lanes(p->cin);
         out6[3] = 0; out6[4] = 0; out6[5] = 1;
         return 0;
     }
