@@ -6,9 +6,13 @@ synthetic 256x256 face crops + 16 mel windows [1,80,16] (inference.py:393-399 ba
 LNet_batch_size 16), weights from the portable synthetic checkpoint (s2v_amd.synth), inputs
 resident in HBM.  The whole forward is one HIP-graph replay.
 
-Multi-GPU: one process per GPU (torchrun); frames shard across ranks with no data-path collective
-(weak scaling: every rank runs its own B-frame batches); the timed region is bracketed by a barrier
-and synchronize on every rank and the max over ranks is reported.
+Multi-GPU: one process per GPU.  Under torchrun (the driver's N > 1 launch) the ranks come from the
+environment; ``python bench.py --gpus N`` without it spawns N fresh worker processes itself (before
+anything touches a GPU).  Frames shard across ranks with no data-path collective (weak scaling:
+every rank runs its own B-frame batches); the timed region is bracketed by a barrier and synchronize
+on every rank and the max over ranks is reported.  ``--workload clip`` is the strong-scaling form
+(BASELINE configs[3]): one step = a whole 1000-frame clip sharded over the ranks, with the RCCL
+broadcast of the per-clip host data and the uint8 gather to rank 0 inside the step.
 
 Prints ONE JSON line on rank 0 with the live roofline of the dominant kernel (HIP events on the
 stream the kernels run on) and, at N=1, the CPU baseline (oracle restatement on host cores).
@@ -25,7 +29,12 @@ Other workloads (not the headline metric):
                         inference.py:302-313, s2v_amd.post.MouthBlend);
   --workload sr         one step = B 720x720 uint8 frames through RealESRNet x2 (SURVEY.md §8f(2):
                         FaceEnhancement's srmodel.process on every full frame, s2v_amd.sr);
-  --workload gpen2048   one step = B 2048x2048 faces through GPEN-BFR-2048 (the CLI's enhancer GAN).
+  --workload gpen2048   one step = B 2048x2048 faces through GPEN-BFR-2048 (the CLI's enhancer GAN);
+  --workload clip       one step = the 1000-frame clip of configs[3] through pipeline.run_sharded: broadcast
+                        of wav / semantic / expression, mel + windows, coefficient windows, DNet -> ENet ->
+                        uint8 on each rank's contiguous frame range (HIP-graph replay per 16-frame batch),
+                        all-gather of the uint8 frames to rank 0;
+  --workload selftest   (tests only, --device cpu) the launcher / timing / JSON path on the gloo backend.
 """
 from __future__ import annotations
 
@@ -44,13 +53,15 @@ import s2v_import  # noqa: E402,F401
 
 METRIC = "synthesized 256×256 frames/sec/GPU (LNet+ENet path); 1/2/4/8-GPU scaling"
 FP32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 matrix 157.3 TF (spec)
-# bf16x3 kernels issue 3 dense bf16 MFMAs (2.5 PF/s dense, MI355X_MICROARCH.md) per fp32 MAC, so
-# their ceiling in algorithmic (fp32-equivalent) FLOP/s is a third of the bf16 peak
-BF16X3_PEAK_TFLOPS = 2500.0 / 3
+# split-fp32 kernels issue 3 dense 16-bit MFMAs (bf16 / f16: 2.5 PF/s dense, MI355X_MICROARCH.md) per
+# fp32 MAC, so their ceiling in algorithmic (fp32-equivalent) FLOP/s is a third of that peak
+X3_PEAK_TFLOPS = 2500.0 / 3
 REF_GFLOP_PER_FRAME = 407.46       # ENet+LNet algorithmic GFLOP/frame (2*MAC)
 
 
-ARITH = {"bf16x3": "bf16x3: fp32 tensors, conv products as split-fp32 hi*hi+hi*lo+lo*hi on bf16 MFMA "
+ARITH = {"f16x3": "f16x3: fp32 tensors, conv products as split-fp32 hi*hi+hi*lo+lo*hi on f16 MFMA "
+                   "(22 significant bits per operand, <= 3*2^-22 per product), fp32 accumulate; all other ops fp32",
+         "bf16x3": "bf16x3: fp32 tensors, conv products as split-fp32 hi*hi+hi*lo+lo*hi on bf16 MFMA "
                     "(16 significant bits per operand), fp32 accumulate; all other ops fp32",
          "f32": "f32: exact fp32 MFMA (v_mfma_f32_32x32x2_f32) convs; all other ops fp32"}
 
@@ -68,7 +79,9 @@ def parse():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--precision", choices=("bf16x3", "f32"), default="bf16x3",
+    ap.add_argument("--frames", type=int, default=1000, help="clip workload: frames in the clip")
+    ap.add_argument("--device", choices=("cuda", "cpu"), default="cuda", help="cpu: launcher self-test only")
+    ap.add_argument("--precision", choices=("f16x3", "bf16x3", "f32"), default="f16x3",
                     help="conv arithmetic (s2v_amd.ops.set_precision)")
     ap.add_argument("--no-alt", action="store_true", help="skip the timing of the other conv arithmetic")
     return ap.parse_args()
@@ -127,7 +140,7 @@ def live_roofline(forward, workload="lipsync"):
             print(f"  {v['ms']:9.3f} ms  {v['launches']:4d} launches  {tf:7.2f} TF/s  {k}", file=sys.stderr)
     d = per[dom]
     achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12
-    peak = BF16X3_PEAK_TFLOPS if "conv_igemm_x3" in dom else FP32_MFMA_PEAK_TFLOPS
+    peak = X3_PEAK_TFLOPS if "conv_igemm_x3" in dom else FP32_MFMA_PEAK_TFLOPS
     total_ms = sum(v["ms"] for v in per.values())
     total_flops = sum(v["flops"] for v in per.values())
     traffic = None
@@ -143,6 +156,18 @@ def live_roofline(forward, workload="lipsync"):
         "conv_family": {"achieved": round(total_flops / (total_ms * 1e-3) / 1e12, 2),
                         "ms_per_step": round(total_ms, 3), "symbols": len(per)},
     }
+
+
+def host_threads():
+    """The host cores this job may use: OMP_NUM_THREADS when the launcher set it (the GPU box sets
+    the per-GPU CPU share there), else the CPU affinity set of this process."""
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
 
 
 def _timed_cpu(fn, units_per_call, seconds, max_calls):
@@ -163,10 +188,39 @@ class Workload:
     metric = METRIC
     unit = "frames/s"
     gflop_per_unit = REF_GFLOP_PER_FRAME
+    graphable = True          # the step is one HIP-graph replay of ``fn(*inputs)``
+    scaling = "weak"
+
+    def units_per_step(self, world):
+        return world * self.batch
+
+
+class SelfTest(Workload):
+    """Launcher / timing / JSON self-test on the CPU (gloo): each rank sums its shard of a broadcast
+    vector; no GPU work."""
+    metric = "bench launcher self-test (CPU, gloo)"
+    unit = "items/s"
+    gflop_per_unit = 0.0
+    graphable = False
+
+    def __init__(self, args, dev, rank, world):
+        self.batch = args.batch or 4
+        self.world = world
+        self.inputs = []
+        self.config = {"workload": "selftest"}
+
+    def step(self):
+        import torch.distributed as dist
+        v = torch.arange(64, dtype=torch.float32) if self.world == 1 or dist.get_rank() == 0 else torch.empty(64)
+        if self.world > 1:
+            dist.broadcast(v, 0)
+        return v.sum()
+
+    forward = step
 
 
 class LipSync(Workload):
-    def __init__(self, args, dev, rank):
+    def __init__(self, args, dev, rank, world=1):
         from s2v_amd import models, synth
         from s2v_amd.models import arch
         self.batch = args.batch or 16
@@ -198,7 +252,7 @@ class LNetOnly(Workload):
     metric = "LNet-only frames/sec/GPU (B=16 synthetic 256x256 crops -> 96x96 LNet, BASELINE configs[1])"
     gflop_per_unit = 56.14
 
-    def __init__(self, args, dev, rank):
+    def __init__(self, args, dev, rank, world=1):
         from s2v_amd import models, ops, synth
         from s2v_amd.models import arch
         self.batch = args.batch or 16
@@ -239,7 +293,7 @@ class Pipeline(Workload):
     metric = "full DNet->LNet->ENet frames/sec/GPU (uint8 384x384 output)"
     gflop_per_unit = 508.91            # ENet+LNet 407.46 + DNet 101.45 (live)
 
-    def __init__(self, args, dev, rank):
+    def __init__(self, args, dev, rank, world=1):
         import numpy as np
         from s2v_amd import audio, models, pipeline, synth
         from s2v_amd.models import arch
@@ -297,7 +351,7 @@ class Enhance(Workload):
     unit = "faces/s"
     gflop_per_unit = 395.5 + 276.2
 
-    def __init__(self, args, dev, rank):
+    def __init__(self, args, dev, rank, world=1):
         from s2v_amd import models, synth
         from s2v_amd.models import enhancer_arch as ea
         kw = dict(out_size=512, num_style_feat=512, channel_multiplier=2, decoder_load_path=None, fix_decoder=False,
@@ -339,7 +393,7 @@ class Mouth(Workload):
     gflop_per_unit = 468.08            # ParseNet-512 mask path, 2*MAC (469 GF/face)
     FRAME = 720
 
-    def __init__(self, args, dev, rank):
+    def __init__(self, args, dev, rank, world=1):
         from s2v_amd import models, post, synth
         from s2v_amd.models import parse_arch
         self.batch = args.batch or 8
@@ -386,7 +440,7 @@ class SuperRes(Workload):
     metric = "super-resolved 720x720 -> 1440x1440 frames/sec/GPU (RealESRNet x2, RRDBNet nf=32, 23 blocks)"
     FRAME = 720
 
-    def __init__(self, args, dev, rank):
+    def __init__(self, args, dev, rank, world=1):
         from s2v_amd import models, synth
         from s2v_amd.models import sr_arch
         from s2v_amd.sr import RealESRNet
@@ -424,7 +478,7 @@ class GPEN2048(Workload):
     unit = "faces/s"
     gflop_per_unit = 419.97            # torch FlopCounterMode on oracle.enhancers.gpen_forward at 2048 (2*MAC)
 
-    def __init__(self, args, dev, rank):
+    def __init__(self, args, dev, rank, world=1):
         from s2v_amd import models, synth
         from s2v_amd.models import enhancer_arch as ea
         self.batch = args.batch or 2
@@ -451,35 +505,128 @@ class GPEN2048(Workload):
                           f"{threads} threads"}
 
 
+class Clip(Pipeline):
+    """BASELINE configs[3] (configs[2] at N = 1): the 1000-frame clip sharded over the ranks by
+    pipeline.run_sharded — RCCL broadcast of the per-clip host data, device mel + windows, host
+    coefficient windows, DNet -> ENet(+LNet) -> uint8 per rank (graph replay per 16-frame batch),
+    all-gather of the uint8 frames to rank 0.  Total work per step is fixed (strong scaling)."""
+    metric = "full-clip lip-sync frames/sec (1000-frame clip sharded over the GPUs, DNet->LNet->ENet->uint8)"
+    graphable = False
+    scaling = "strong"
+
+    def __init__(self, args, dev, rank, world=1):
+        import numpy as np
+        from s2v_amd import pipeline
+        super().__init__(args, dev, rank, world)
+        self.pipe.graph = not args.no_graph
+        n = args.frames
+        rng = np.random.default_rng(0)
+        t = np.arange(n * 640) / 16000.0                      # 40 s of 16 kHz audio per 1000 frames at 25 fps
+        wav = (0.1 * rng.standard_normal(t.size) + 0.2 * (np.sin(2 * np.pi * 220 * t) + np.sin(2 * np.pi * 440 * t)
+                                                          + np.sin(2 * np.pi * 1000 * t))).astype(np.float32)
+        sem = rng.standard_normal((n, 262)).astype(np.float32)
+        sem[:, -3] = 1.0 + 0.1 * rng.random(n)
+        expr = rng.standard_normal(64).astype(np.float32)
+        self.host = (wav, sem, expr) if rank == 0 else (None, None, None)
+        self.n = n
+        s0, s1 = pipeline.shard_range(n, rank, world)
+        g = torch.Generator(device=dev)
+        g.manual_seed(7000 + rank)
+        self.src = torch.rand((s1 - s0, 3, 256, 256), generator=g, device=dev) * 2 - 1   # resident before timing
+        self.result = None
+        self.config = {"workload": f"run_sharded over a {n}-frame clip (40 ms of 16 kHz audio per frame): broadcast "
+                                   "wav/semantic/expression, mel + 16-column windows, coefficient windows, "
+                                   "DNet -> uint8 ref -> ENet(+LNet) -> uint8 384x384 per rank, all-gather to rank 0 "
+                                   "(inference.py:204-288, facing.py:176-191)", "clip_frames": n}
+
+    def units_per_step(self, world):
+        return self.n
+
+    def step(self):
+        from s2v_amd import pipeline
+        self.result = pipeline.run_sharded(self.pipe, *self.host, lambda s, e: self.src)
+        return self.result
+
+
 WORKLOADS = {"lipsync": LipSync, "lnet": LNetOnly, "pipeline": Pipeline, "enhance": Enhance, "mouth": Mouth,
-             "sr": SuperRes, "gpen2048": GPEN2048}
+             "sr": SuperRes, "gpen2048": GPEN2048, "clip": Clip, "selftest": SelfTest}
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _spawned(rank, args, port):
+    """Entry of a worker started by ``launch`` (a fresh interpreter: nothing has touched a GPU)."""
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    worker(args)
+
+
+def launch(args):
+    """``bench.py --gpus N`` outside torchrun: start N fresh worker processes (spawn, one per GPU)
+    and wait for them; this process never touches a device."""
+    import torch.multiprocessing as mp
+    mp.start_processes(_spawned, args=(args, _free_port()), nprocs=args.gpus, join=True, start_method="spawn")
 
 
 def main():
     args = parse()
+    if args.device == "cpu" and args.workload != "selftest":
+        raise SystemExit("--device cpu runs only the launcher self-test (--workload selftest)")
+    if "WORLD_SIZE" in os.environ:                 # torchrun (the driver's N > 1 launch)
+        if int(os.environ["WORLD_SIZE"]) != args.gpus:
+            print(f"bench: --gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}; using WORLD_SIZE",
+                  file=sys.stderr)
+        return worker(args)
+    if args.gpus > 1:
+        return launch(args)
+    return worker(args)
+
+
+def worker(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    cuda = args.device == "cuda"
+    if cuda:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    else:
+        dev = torch.device("cpu")
+    world_seen = 1
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if cuda:
+            dist.init_process_group("nccl", device_id=dev)     # RCCL
+        else:
+            dist.init_process_group("gloo")
+        world_seen = dist.get_world_size()
     from s2v_amd.runtime import GraphRunner
 
     from s2v_amd import ops
-    wl = WORKLOADS[args.workload](args, dev, rank)
+    wl = WORKLOADS[args.workload](args, dev, rank, world)
 
     def barrier():
         if world > 1:
             torch.distributed.barrier()
-        torch.cuda.synchronize()
+        if cuda:
+            torch.cuda.synchronize()
 
     def timed(prec):
         """Capture (or not) the step in conv arithmetic ``prec``, warm up, time args.steps steps
         between barriers; returns the max over ranks of the elapsed seconds."""
         ops.set_precision(prec)
-        if args.no_graph:
+        if not wl.graphable:
+            step = wl.step
+            for _ in range(max(1, args.warmup)):
+                step()
+        elif args.no_graph:
             step = wl.forward
             for _ in range(max(1, args.warmup)):
                 step()
@@ -495,36 +642,42 @@ def main():
         barrier()
         el = time.perf_counter() - t0
         if world > 1:
-            t = torch.tensor([el], device=dev)
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
             torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
             el = float(t.item())
         return el
 
     elapsed = timed(args.precision)
-    units = world * wl.batch * args.steps
+    units = wl.units_per_step(world) * args.steps
     value = units / elapsed
     config = dict(wl.config)
-    config.update({"global_batch": world * wl.batch, "batch_per_gpu": wl.batch,
+    config.update({"global_batch": wl.units_per_step(world), "batch_per_gpu": wl.batch,
                    "parallelism": f"frame-shard x{world} (no data-path collective)", "graph": not args.no_graph,
+                   "world_size_seen": world_seen,
                    "achieved_tflops_algorithmic": round(value * wl.gflop_per_unit / 1e3, 2),
                    "gflop_per_unit": wl.gflop_per_unit})
+    if args.workload == "clip":
+        config["parallelism"] = (f"frame-shard x{world}: RCCL broadcast of the clip inputs + all-gather of the "
+                                 "uint8 frames inside the step" if world > 1 else "single GPU")
     result = {
         "metric": wl.metric, "value": round(value, 3), "unit": wl.unit, "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic", "config": config,
+        "scaling": wl.scaling, "vs_baseline": None, "dtype": "f32", "data": "synthetic", "config": config,
     }
     config["conv_arith"] = ARITH[args.precision]
-    if world == 1 and not args.no_alt:
-        other = "f32" if args.precision == "bf16x3" else "bf16x3"
-        el = timed(other)
-        result["alt_precision"] = {"conv_arith": ARITH[other], "value": round(units / el, 3),
-                                   "ms_per_step": round(1e3 * el / args.steps, 3)}
+    if world == 1 and not args.no_alt and cuda and wl.graphable:
+        result["alt_precision"] = {}
+        for other in ARITH:
+            if other == args.precision:
+                continue
+            el = timed(other)
+            result["alt_precision"][other] = {"value": round(units / el, 3),
+                                              "ms_per_step": round(1e3 * el / args.steps, 3)}
         ops.set_precision(args.precision)
-    if rank == 0 and not args.no_roofline:
+    if rank == 0 and not args.no_roofline and cuda:
         result["roofline"] = live_roofline(wl.forward, args.workload)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        result["cpu_baseline"] = wl.cpu(threads, args.cpu_seconds)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and cuda:
+        result["cpu_baseline"] = wl.cpu(args.cpu_threads or host_threads(), args.cpu_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -92,12 +92,16 @@ typedef struct s2v_conv_params {
      * is written at y + ((n*out_full_h + oy*out_step)*out_full_w + ox*out_step)*ycs — one parity
      * class of a polyphase transposed conv.  No pix_add; res only in place (res == y). */
     int out_step; int out_full_h, out_full_w;
-    /* arithmetic of the implicit-GEMM kernels (the Cout <= 4 VALU kernels are always fp32):
+    /* arithmetic of the implicit-GEMM kernels (the Cout <= 4 VALU and K <= 64 kernels are always fp32):
      *   S2V_PREC_F32     v_mfma_f32_32x32x2_f32, exact fp32 products (reads ``wt``);
      *   S2V_PREC_BF16X3  split-fp32 on v_mfma_f32_32x32x16_bf16: a*b ~ ah*bh + ah*bl + al*bh with
-     *                    ah = bf16(a), al = bf16(a - ah); <= 3*2^-16 relative error per product.  Packed
-     *                    weights are read from ``wt_x3`` (s2v_split_weights_x3 layout); a b_kn
-     *                    matrix is split on the fly. */
+     *                    ah = bf16(a), al = bf16(a - ah); <= 3*2^-16 relative error per product, any range;
+     *   S2V_PREC_F16X3   the same split on v_mfma_f32_32x32x16_f16 (ah = f16(a), al = f16(a - ah)):
+     *                    <= 3*2^-22 relative per product for operands in the f16 normal range
+     *                    (|a| < 65504; smaller values keep an absolute error <= 2^-25).
+     * Packed weights are read from ``wt_x3`` (s2v_split_weights layout of the same precision, the
+     * weights multiplied by ``wt_scale`` before the split — a power of two, 0 means 1 — which the
+     * kernel divides out of the accumulators exactly); a b_kn matrix is split on the fly. */
     int prec;
     const void *wt_x3;
     /* optional in-launch split-K fold: >= grid tiles (batch x M-tiles x N-tiles) zero-initialised ints.
@@ -106,9 +110,10 @@ typedef struct s2v_conv_params {
      * NULL / too short: a separate reduce kernel folds the workspace (faster on MI355X: the fold's
      * agent-scope release / acquire per split block costs more than the extra launch). */
     int *tile_counters; int n_counters;
+    float wt_scale;
 } s2v_conv_params;
 
-enum { S2V_PREC_F32 = 0, S2V_PREC_BF16X3 = 1 };
+enum { S2V_PREC_F32 = 0, S2V_PREC_BF16X3 = 1, S2V_PREC_F16X3 = 2 };
 
 /* Replaces the nn.Conv2d / ConvTranspose2d / Conv1d / Linear calls of models/LNet.py,
  * ENet.py, DNet.py, base_blocks.py, ffc.py, transformer.py (inventory: SURVEY.md App. A). */
@@ -116,13 +121,17 @@ int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream);
 size_t s2v_conv2d_ws_bytes(const s2v_conv_params *p);
 /* The launch plan s2v_conv2d would use: out10 = {BM, BN, WAVES_M, AVEC, B_KN, splits, prec, NW, KS, PF}
  * of the conv_igemm<BM,BN,WAVES_M,AVEC,B_KN> (prec 0) or
- * conv_igemm_x3<BM,BN,WAVES_M,NW,KS,PF,AVEC,B_KN> (prec 1) instance, or {0, CO, TPP, 0, 0, 1, 0, 0, 0, 0}
- * for conv_small_cpar<CO,TPP> (conv_direct_small<CO> when TPP == 0).  force_tile: 0 = planner,
- * 1..6 (f32) / 1..8 (bf16x3) a fixed tile of the selected precision's table (tests / tuning). */
+ * conv_igemm_x3<BM,BN,WAVES_M,NW,KS,PF,AVEC,B_KN,prec-1> (prec 1 / 2) instance, or
+ * {0, CO, TPP, LW, 0, 1, 0, 0, 0, 0} for conv_small_cpar<CO,TPP,LW> (conv_direct_small<CO> when
+ * TPP == 0), or {0, cout, -QPT, 0, 0, 1, ...} for conv_smallk<QPT>.  force_tile: 0 = planner,
+ * 1..6 (f32) / 1..8 (split precisions) a fixed tile of the selected precision's table (tests / tuning). */
 int s2v_conv2d_plan(const s2v_conv_params *p, int *out10);
 
-/* Split packed fp32 weights [rows][kpad] (kpad % 32 == 0) into the S2V_PREC_BF16X3 layout
- * [rows][kpad/32][hi 32 | lo 32] bf16 (same byte size), hi = bf16_rne(w), lo = bf16_rne(w - hi). */
+/* Split packed fp32 weights [rows][kpad] (kpad % 32 == 0) into the layout of ``prec``
+ * (S2V_PREC_BF16X3 / S2V_PREC_F16X3): [rows][kpad/32][hi 32 | lo 32] 16-bit (same byte size),
+ * v = w * scale (a power of two), hi = T_rne(v), lo = T_rne(v - hi).  Pass ``scale`` as the conv's
+ * wt_scale.  s2v_split_weights_x3 = the bf16 form with scale 1. */
+int s2v_split_weights(const float *w, int rows, int kpad, int prec, float scale, void *out, s2v_stream_t stream);
 int s2v_split_weights_x3(const float *w, int rows, int kpad, void *out, s2v_stream_t stream);
 
 /* LayerNorm2d (base_blocks.py:52-69) over (H,W,C) per sample, fused affine + act
@@ -231,7 +240,11 @@ int s2v_irfft2(const float *spec, int n, int h, int w, int c, int scs, const flo
  * out is [batch][npad][kpad]; run the conv with batch = B, n = 1 and w_bs = npad * kpad. */
 int s2v_modulate_weights(const float *wt, int npad, int kpad, int K, int cin, int cout, const float *s, int s_ns,
                          const float *d, int d_ns, int batch, float *out, s2v_stream_t stream);
-/* Same, written in the S2V_PREC_BF16X3 split layout (kpad % 32 == 0): pass ``out`` as wt_x3. */
+/* Same, times ``scale`` (a power of two: the conv's wt_scale), written in the split layout of ``prec``
+ * (kpad % 32 == 0): pass ``out`` as wt_x3.  s2v_modulate_weights_x3 = bf16, scale 1. */
+int s2v_modulate_weights_split(const float *wt, int npad, int kpad, int K, int cin, int cout, const float *s,
+                               int s_ns, const float *d, int d_ns, int batch, int prec, float scale, void *out,
+                               s2v_stream_t stream);
 int s2v_modulate_weights_x3(const float *wt, int npad, int kpad, int K, int cin, int cout, const float *s, int s_ns,
                             const float *d, int d_ns, int batch, void *out, s2v_stream_t stream);
 

@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libs2v.so")
 ACT_NONE, ACT_RELU, ACT_LRELU, ACT_SIGMOID, ACT_TANH, ACT_GELU_TANH = range(6)
 IN_DIRECT, IN_NEAREST_UP2, IN_TRANSPOSED = range(3)
 PAD_ZERO, PAD_REFLECT = range(2)
-PREC_F32, PREC_BF16X3 = range(2)
+PREC_F32, PREC_BF16X3, PREC_F16X3 = range(3)
 
 _c_int, _c_float, _c_ll, _c_size, _vp = ctypes.c_int, ctypes.c_float, ctypes.c_longlong, ctypes.c_size_t, ctypes.c_void_p
 
@@ -41,6 +41,7 @@ class ConvParams(ctypes.Structure):
         ("out_step", _c_int), ("out_full_h", _c_int), ("out_full_w", _c_int),
         ("prec", _c_int), ("wt_x3", _vp),
         ("tile_counters", _vp), ("n_counters", _c_int),
+        ("wt_scale", _c_float),
     ]
 
 
@@ -77,7 +78,10 @@ _SIGS = {
     "s2v_fft_tables_floats": (_c_size, [_c_int, _c_int]),
     "s2v_rfft2": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_int, _vp]),
     "s2v_irfft2": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_int, _vp, _c_int, _vp]),
+    "s2v_split_weights": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_float, _vp, _vp]),
     "s2v_split_weights_x3": (_c_int, [_vp, _c_int, _c_int, _vp, _vp]),
+    "s2v_modulate_weights_split": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp, _c_int,
+                                            _c_int, _c_int, _c_float, _vp, _vp]),
     "s2v_modulate_weights_x3": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp, _c_int,
                                          _c_int, _vp, _vp]),
     "s2v_modulate_weights": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp, _c_int, _c_int,

@@ -21,7 +21,8 @@
 
 namespace s2v {
 
-void launch_conv_x3(int tile, const ConvArgs &a, int amode, bool bkn, dim3 grid, hipStream_t s);   // conv_x3.hip
+template <int ELT>   // 0 = bf16, 1 = f16 halves (conv_x3_impl.hpp; instances in conv_x3_{bf16,f16}.hip)
+void launch_conv_x3(int tile, const ConvArgs &a, int amode, bool bkn, dim3 grid, hipStream_t s);
 
 template <int BM, int BN, int AR, int BR, int BKN>
 __device__ __forceinline__ void store_ab(float *As, float *Bs, int tid, const f4 (&ra)[AR],
@@ -419,14 +420,18 @@ __global__ __launch_bounds__(256) void conv_small_cpar(ConvArgs a, int batch) {
 }
 
 // LDS weights when the filter is small next to the block's input (<= 16 KB: ToRGB 1x1s); the 7x7
-// heads keep global (L1-resident) weight reads
+// heads keep global (L1-resident) weight reads.  Per-batch-entry weights need every block inside
+// one entry (M % pixels-per-block == 0).  s2v_conv2d_plan reports the same flag.
+static bool cpar_lw(int co, int K, long long w_bs, int batch, int M, int tpp) {
+    return (size_t)co * K * sizeof(float) <= 16 * 1024 && (w_bs == 0 || batch == 1 || M % (256 / tpp) == 0);
+}
+
 template <int CO, int TPP>
 static void launch_cpar(const ConvArgs &a, int batch, hipStream_t s) {
     const long long total = (long long)batch * a.M;
     const unsigned grid = cdiv(total * TPP, 256);
     const size_t wbytes = (size_t)CO * a.K * sizeof(float);
-    const bool lw = wbytes <= 16 * 1024 && (a.w_bs == 0 || batch == 1 || a.M % (256 / TPP) == 0);
-    if (lw) conv_small_cpar<CO, TPP, true><<<grid, 256, wbytes, s>>>(a, batch);
+    if (cpar_lw(CO, a.K, a.w_bs, batch, a.M, TPP)) conv_small_cpar<CO, TPP, true><<<grid, 256, wbytes, s>>>(a, batch);
     else conv_small_cpar<CO, TPP, false><<<grid, 256, 0, s>>>(a, batch);
 }
 
@@ -459,7 +464,7 @@ struct TileCfg {
 static const TileCfg kTiles[] = {
     {128, 128, 2, 4, 1, 2}, {128, 64, 2, 4, 1, 2}, {64, 128, 2, 4, 1, 2}, {64, 64, 2, 4, 1, 2}, {256, 32, 4, 4, 1, 2},
     {128, 32, 4, 4, 1, 2}};
-// split-bf16 (S2V_PREC_BF16X3) configurations, conv_x3.hip launch_conv_x3, with the sustained
+// split-fp32 (S2V_PREC_BF16X3 / F16X3) configurations, conv_x3_impl.hpp launch_conv_x3, with the sustained
 // throughput each reaches on a full chip (TFLOP/s fp32-equivalent, MI355X, tools/conv_micro.py r01)
 // and resident blocks per CU (LDS / waves) for the planner's cost model
 struct X3Cfg {
@@ -519,7 +524,7 @@ static bool is_smallk(const s2v_conv_params *p) {
     return m < (1LL << 31) && k <= 64 && smallk_cfg(p, (int)m, (int)k, tppx, qpt);
 }
 static bool tiled_x3(const s2v_conv_params *p) {
-    return p->prec == S2V_PREC_BF16X3 && !(use_direct(p) && !p->force_tile) && !is_smallk(p);
+    return p->prec != S2V_PREC_F32 && !(use_direct(p) && !p->force_tile) && !is_smallk(p);
 }
 static bool uses_x3(const s2v_conv_params *p) { return tiled_x3(p) && !p->b_kn; }
 
@@ -563,7 +568,6 @@ static Plan make_plan_x3(const s2v_conv_params *p, int M, Plan pl) {
         if (p->b_kn && c.t.nw != 4) continue;
         if (c.t.bm == 256 && c.t.bn == 256 && am != 0 && am != 3) continue;   // generic gathers spill there
         if (c.t.bm == 256 && c.t.bn == 64 && am != 0) continue;   // measured slower than 128x64 on per-row gathers
-        if (c.t.bm == 64 && c.t.bn == 64 && p->cout <= 32) continue;     // see validate()
         if (!p->b_kn && (long long)cdiv(p->cout, c.t.bn) * c.t.bn > p->npad) continue;   // weight rows
         const long long tiles = (long long)cdiv(M, c.t.bm) * cdiv(p->cout, c.t.bn) * batch;
         const double slots = (double)cus * c.bpc;
@@ -644,23 +648,27 @@ static Plan make_plan(const s2v_conv_params *p, int M, int K) {
 
 static int validate(const s2v_conv_params *p, int &M, int &K) {
     S2V_REQUIRE(p && p->x && p->y, "conv2d: null pointer");
-    S2V_REQUIRE(p->prec == S2V_PREC_F32 || p->prec == S2V_PREC_BF16X3, "conv2d: bad prec %d", p->prec);
+    S2V_REQUIRE(p->prec == S2V_PREC_F32 || p->prec == S2V_PREC_BF16X3 || p->prec == S2V_PREC_F16X3,
+                "conv2d: bad prec %d", p->prec);
+    {
+        int e;
+        S2V_REQUIRE(p->wt_scale == 0.f || (p->wt_scale > 0.f && std::frexp(p->wt_scale, &e) == 0.5f),
+                    "conv2d: wt_scale must be 0 or a positive power of two, got %g", p->wt_scale);
+    }
     S2V_REQUIRE(p->force_tile >= 0 && p->force_tile <= (tiled_x3(p) ? kNumX3 : kNumTiles),
                 "conv2d: bad force_tile %d", p->force_tile);
     S2V_REQUIRE(!(tiled_x3(p) && p->b_kn && p->force_tile > 0 && kX3Tiles[p->force_tile - 1].t.nw != 4),
                 "conv2d: b_kn operands need a 4-wave split-bf16 tile (force_tile 4..6)");
     if (tiled_x3(p) && p->force_tile > 0) {
         // a forced tile must not read weight rows past the packed [npad] rows (the planner never
-        // picks such a tile); 64x64 with cout <= 32 faulted in a tuning sweep and is not offered
+        // picks such a tile: the kernels load whole BN-row slabs of B without a row guard)
         const TileCfg &t = kX3Tiles[p->force_tile - 1].t;
         S2V_REQUIRE(!p->b_kn ? (long long)cdiv(p->cout, t.bn) * t.bn <= p->npad : true,
                     "conv2d: force_tile %d (BN %d) needs npad >= %d, got %d", p->force_tile, t.bn,
                     cdiv(p->cout, t.bn) * t.bn, p->npad);
-        S2V_REQUIRE(!(t.bm == 64 && t.bn == 64 && p->cout <= 32), "conv2d: force_tile %d not offered for cout <= 32",
-                    p->force_tile);
     }
     if (uses_x3(p))
-        S2V_REQUIRE(p->wt_x3 && ((uintptr_t)p->wt_x3 % 16) == 0, "conv2d: prec BF16X3 needs 16B-aligned wt_x3");
+        S2V_REQUIRE(p->wt_x3 && ((uintptr_t)p->wt_x3 % 16) == 0, "conv2d: split precisions need 16B-aligned wt_x3");
     else
         S2V_REQUIRE(p->wt != nullptr, "conv2d: null weights");
     S2V_REQUIRE(p->n > 0 && p->h > 0 && p->w > 0 && p->cin > 0 && p->cout > 0 && p->oh > 0 && p->ow > 0,
@@ -720,6 +728,7 @@ static ConvArgs make_args(const s2v_conv_params *p, int M, int K, const Plan &pl
     a.M = M; a.K = K; a.ktiles = pl.ktiles; a.splits = pl.splits; a.tps = pl.tps; a.ws = p->ws;
     a.y_step = p->out_step > 1 ? p->out_step : 1; a.y_h = p->out_full_h; a.y_w = p->out_full_w;
     a.cnt = nullptr;
+    a.acc_scale = (tiled_x3(p) && !p->b_kn && p->wt_scale > 0.f) ? 1.f / p->wt_scale : 1.f;
     return a;
 }
 
@@ -778,9 +787,12 @@ extern "C" int s2v_conv2d_plan(const s2v_conv_params *p, int *out6) {
         const bool cpar = (p->cin % 4 == 0) && (p->xcs % 4 == 0) && (((uintptr_t)p->x % 16) == 0) &&
                           (p->x_bs % 4 == 0) && (!p->in_scale || (p->in_scale_ns % 4 == 0 &&
                                                                   ((uintptr_t)p->in_scale % 16) == 0));
-        out6[0] = 0; out6[1] = p->cout < 4 ? p->cout : 4;
-        out6[2] = !cpar ? 0 : cpar_lanes(p->cin);
-        out6[3] = 0; out6[4] = 0; out6[5] = 1;
+        const int co = p->cout < 4 ? p->cout : 4, tpp = cpar_lanes(p->cin);
+        const int batch = p->batch > 0 ? p->batch : 1;
+        out6[0] = 0; out6[1] = co;
+        out6[2] = !cpar ? 0 : tpp;
+        out6[3] = cpar && cpar_lw(co, K, p->w_bs, batch, M, tpp);
+        out6[4] = 0; out6[5] = 1;
         return 0;
     }
     const TileCfg &t = tile_cfg(p, pl.tile);
@@ -788,7 +800,7 @@ extern "C" int s2v_conv2d_plan(const s2v_conv_params *p, int *out6) {
     out6[3] = a_mode(p);
     out6[4] = p->b_kn != 0;
     out6[5] = pl.splits;
-    out6[6] = tiled_x3(p) ? 1 : 0;
+    out6[6] = tiled_x3(p) ? p->prec : 0;
     out6[7] = t.nw; out6[8] = t.ks; out6[9] = t.pf;
     return 0;
 }
@@ -844,7 +856,8 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
         a.cnt = p->tile_counters;                       // fold in the launch itself
     if (tiled_x3(p)) {
         if (!bkn) a.wt = (const float *)p->wt_x3;
-        launch_conv_x3(pl.tile, a, amode, bkn, grid, s);
+        if (p->prec == S2V_PREC_BF16X3) launch_conv_x3<0>(pl.tile, a, amode, bkn, grid, s);
+        else launch_conv_x3<1>(pl.tile, a, amode, bkn, grid, s);
     } else switch (pl.tile) {
         case 0: launch_tile<128, 128, 2>(a, amode, bkn, grid, s); break;
         case 1: launch_tile<128, 64, 2>(a, amode, bkn, grid, s); break;

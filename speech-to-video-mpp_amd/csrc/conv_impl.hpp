@@ -35,6 +35,7 @@ struct ConvArgs {
     float *ws;
     int y_step, y_h, y_w;   // strided (polyphase) output, y_step > 1
     int *cnt;               // split-K tile counters (in-launch fold), or null
+    float acc_scale;        // accumulator factor before the epilogue (1 / the split weights' pre-scale)
 };
 
 // Element offset of output row m (flattened n, oy, ox) for channel 0.
@@ -348,7 +349,7 @@ __device__ __forceinline__ void epilogue_tile(const ConvArgs &a, const floatx16 
             for (int j = 0; j < TN; ++j)
 #pragma unroll
                 for (int r = 0; r < 16; ++r)
-                    Cs[(r0 + (r & 3) + 8 * (r >> 2) + 4 * lh) * LDC + wn * WTN + j * 32 + li] = acc[i][j][r];
+                    Cs[(r0 + (r & 3) + 8 * (r >> 2) + 4 * lh) * LDC + wn * WTN + j * 32 + li] = acc[i][j][r] * a.acc_scale;
         }
         __syncthreads();
         const int clim = min(CH, mlim - c0);

@@ -1,428 +1,24 @@
-// Implicit-GEMM convolution on gfx950 bf16 MFMA with split-fp32 operands ("bf16x3").
-//
-// Every fp32 operand v is carried as two bf16 halves, hi = bf16(v) and lo = bf16(v - hi) (RNE both:
-// |v - hi - lo| <= 2^-16 |v|, i.e. 16 significant bits), and a product as hi*hi + hi*lo + lo*hi
-// (the dropped lo*lo term is <= 2^-16 |a*b|), accumulated in fp32 by v_mfma_f32_32x32x16_bf16
-// (bf16 x bf16 products are exact in fp32).  Worst case 3 * 2^-16 relative per product, typically
-// ~1e-5: 32x tighter per operand than TF32 (10 explicit mantissa bits), the arithmetic cuDNN uses
-// for these fp32 convolutions by default on the reference's own GPU path.  Measured model-level
-// error vs the reference CPU goldens: DESIGN.md §3.  Three bf16 MFMAs cost 96 cycles per 32x32x16
-// block against 512 for eight v_mfma_f32_32x32x2_f32.
-//
-// Same GEMM view, gather loaders, K-slice order, XCD-aware tile order and epilogue as the fp32
-// kernel (conv.hip / conv_impl.hpp).  Differences:
-//   * B (packed weights) is pre-split on the host side into [npad][kpad/32][hi 32 | lo 32] bf16
-//     (s2v_split_weights_x3 / s2v_modulate_weights_x3: same bytes as fp32), so a 128-byte weight
-//     row slice lands in LDS unchanged;
-//   * A is split in registers after its global load, while the MFMAs of the previous slice run;
-//   * LDS rows are 128 B (eight 16-byte slots: hi k0-7, k8-15, k16-23, k24-31, then lo), slot s of
-//     row r stored at s ^ ((r >> 1) & 7): the 16 rows of each ds_read_b128 lane group hit 16
-//     distinct slots of the 256-byte bank row (conflict-free operand reads).
-#include "conv_impl.hpp"
+// Weight preparation for the split-fp32 convolutions (conv_x3_impl.hpp): packed fp32 weights, or
+// StyleGAN2 per-sample modulated weights, written once in the [rows][kpad/32][hi 32 | lo 32]
+// 16-bit layout the kernels stage into LDS unchanged.  ``scale`` (a power of two) multiplies the
+// weights before the split; the conv divides it out of the accumulators (s2v_conv_params.wt_scale).
+#include "conv_x3_impl.hpp"
+
+#include <cmath>
 
 namespace s2v {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ unsigned pack_bf16(float a, float b) {
-    bf16x2 v = {(__bf16)a, (__bf16)b};   // v_cvt_pk_bf16_f32 (round to nearest even)
-    return __builtin_bit_cast(unsigned, v);
-}
-
-// 4 fp32 -> 4 bf16 hi (8 bytes) + 4 bf16 lo (8 bytes)
-__device__ __forceinline__ void split4(const f4 &v, u32x2 &hi, u32x2 &lo) {
-    hi.x = pack_bf16(v.x, v.y);
-    hi.y = pack_bf16(v.z, v.w);
-    const float h0 = __uint_as_float(hi.x << 16), h1 = __uint_as_float(hi.x & 0xffff0000u);
-    const float h2 = __uint_as_float(hi.y << 16), h3 = __uint_as_float(hi.y & 0xffff0000u);
-    lo.x = pack_bf16(v.x - h0, v.y - h1);
-    lo.y = pack_bf16(v.z - h2, v.w - h3);
-}
-
-__device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
-
-// byte offset of 16-byte slot ``slot`` (0..7) of LDS row ``row``
-__device__ __forceinline__ int slot_off(int row, int slot) { return row * 128 + ((slot ^ swz(row)) << 4); }
-
-// A rows ar + RS*j of the tile: 4 k-values per thread (slot q>>1, bytes (q&1)*8)
-template <int AR, int RS>
-__device__ __forceinline__ void store_a_x3(char *As, int tid, const f4 (&ra)[AR]) {
-    const int ar = tid >> 3, q = tid & 7;
-#pragma unroll
-    for (int j = 0; j < AR; ++j) {
-        const int row = ar + RS * j;
-        u32x2 hi, lo;
-        split4(ra[j], hi, lo);
-        const int off = slot_off(row, q >> 1) + (q & 1) * 8;
-        *(u32x2 *)(As + off) = hi;
-        *(u32x2 *)(As + (off ^ 64)) = lo;          // slot ^ 4 == the lo slot (slot < 4)
-    }
-}
-
-// Wide A staging (AMODE 0/3): a thread owns 8 consecutive k (two float4 loads) of AR8 rows and
-// writes each as one 16-byte hi slot + one 16-byte lo slot (ds_write_b128).  Lane t of a pass
-// takes row 16 (t >> 6) + ((t >> 3) & 7) + 8 ((t >> 2) & 1): the two rows of every 8-lane store
-// group are r and r + 8, whose swizzles differ in bit 2, so their four slots land in disjoint
-// halves of the 128-byte bank window (no write conflicts); 4 lanes cover a 128-byte row piece.
-template <int NT>
-__device__ __forceinline__ int a_row8(int t, int j) {
-    return j * (NT / 4) + ((t >> 6) << 4) + ((t >> 3) & 7) + 8 * ((t >> 2) & 1);
-}
-
-template <int AR8, int NT>
-__device__ __forceinline__ void store_a8_x3(char *As, int tid, const f4 (&ra)[2 * AR8]) {
-    const int q = tid & 3;
-#pragma unroll
-    for (int j = 0; j < AR8; ++j) {
-        u32x2 h0, l0, h1, l1;
-        split4(ra[2 * j], h0, l0);
-        split4(ra[2 * j + 1], h1, l1);
-        const u32x4 hi = {h0.x, h0.y, h1.x, h1.y}, lo = {l0.x, l0.y, l1.x, l1.y};
-        const int off = slot_off(a_row8<NT>(tid, j), q);
-        *(u32x4 *)(As + off) = hi;
-        *(u32x4 *)(As + (off ^ 64)) = lo;
-    }
-}
-
-// pre-split packed weights: thread loads 16 bytes (one slot) of rows br + RS j
-template <int BR, int RS>
-__device__ __forceinline__ void load_b_x3(const ConvArgs &a, const char *__restrict__ wt, int kt, int n0, int tid,
-                                          u32x4 (&rb)[BR]) {
-    const int br = tid >> 3, sl = tid & 7;
-    const char *p = wt + ((long long)(n0 + br) * a.kpad + kt * 32) * 4 + sl * 16;
-#pragma unroll
-    for (int j = 0; j < BR; ++j) rb[j] = *(const u32x4 *)(p + (long long)RS * j * a.kpad * 4);
-}
-
-template <int BR, int RS>
-__device__ __forceinline__ void store_b_x3(char *Bs, int tid, const u32x4 (&rb)[BR]) {
-    const int br = tid >> 3, sl = tid & 7;
-#pragma unroll
-    for (int j = 0; j < BR; ++j) *(u32x4 *)(Bs + slot_off(br + RS * j, sl)) = rb[j];
-}
-
-// activation B ([K][ldb] fp32, b_kn, 256 threads): split on the fly, scattered 2-byte stores
-// (small GEMMs only)
-template <int BN, int BR>
-__device__ __forceinline__ void store_b_kn_x3(char *Bs, int tid, const f4 (&rb)[BR]) {
-    constexpr int NV = BN / 4, RPP = 256 / NV;
-    const int kr = tid / NV, nn = (tid - (tid / NV) * NV) * 4;
-#pragma unroll
-    for (int j = 0; j < BR; ++j) {
-        const int k = kr + RPP * j;
-        const float v[4] = {rb[j].x, rb[j].y, rb[j].z, rb[j].w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const __bf16 h = (__bf16)v[e];
-            const __bf16 l = (__bf16)(v[e] - (float)h);
-            const int off = slot_off(nn + e, k >> 3) + (k & 7) * 2;
-            *(__bf16 *)(Bs + off) = h;
-            *(__bf16 *)(Bs + (off ^ 64)) = l;
-        }
-    }
-}
-
-// K-slice cursor.  Slice kt = tap * nsl + cs covers channels [32 cs, 32 cs + 32) of filter tap
-// ``tap`` = ky * kw + kx.  With ``kperm`` (AMODE 0/3 multi-tap convs) slices are visited
-// channel-slice-major — all taps of one 32-channel slice in a row, so a 3x3 neighbourhood is
-// re-read from L2 right away; the weights are indexed by the same kt, so the sum is the same up
-// to fp32 summation order.  Otherwise in natural k order.  Advancing needs no division.
-struct SliceIt {
-    int i, tap, cs, ky, kx;
-    __device__ __forceinline__ void init(int i0, bool kperm, int taps, int nsl, int kw) {
-        i = i0;
-        if (kperm) { tap = i0 % taps; cs = i0 / taps; }
-        else if (nsl > 0) { tap = i0 / nsl; cs = i0 - tap * nsl; }
-        else { tap = 0; cs = 0; }                 // generic gathers only use i
-        ky = tap / kw;
-        kx = tap - ky * kw;
-    }
-    __device__ __forceinline__ void next(bool kperm, int taps, int nsl, int kw) {
-        ++i;
-        if (kperm) {
-            ++tap; ++kx;
-            if (kx == kw) { kx = 0; ++ky; }
-            if (tap == taps) { tap = 0; ky = 0; kx = 0; ++cs; }
-        } else {
-            ++cs;
-            if (cs == nsl) { cs = 0; ++tap; ++kx; if (kx == kw) { kx = 0; ++ky; } }
-        }
-    }
-    __device__ __forceinline__ int kt(int nsl) const { return tap * nsl + cs; }
-};
-
-constexpr int x3_chunk(int bm, int bn, int smem) {
-    int ch = bm;
-    while (ch > 32 && ch * (bn + 4) * 4 > smem) ch /= 2;
-    return ch;
-}
-
-// BM x BN tile, NW waves (WAVES_M x NW/WAVES_M), KS 32-deep K-slices per LDS stage (two stages),
-// PF register stages of prefetch (1: slice group t+1 in flight during group t; 2: t+2).
-// Measured on MI355X (tools/conv_micro.py, r01): KS = 1, PF = 1 with 8 waves (two or more waves
-// per SIMD hide each other's load waits) beats deeper register prefetch (PF = 2 costs ~64 VGPRs and
-// drops to one wave per SIMD: -40 %) and BK = 64 stages (KS = 2: LDS for one block per CU: -40 %).
-template <int BM, int BN, int WAVES_M, int NW, int KS, int PF, int AMODE, int BKN>
-__global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3(ConvArgs a) {
-    constexpr int NT = 64 * NW, RS = NT / 8;
-    constexpr int WAVES_N = NW / WAVES_M;
-    constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
-    constexpr int TM = WTM / 32, TN = WTN / 32;
-    constexpr int AR = BM / RS;
-    constexpr int BR = BN / RS;
-    constexpr int SUB = (BM + BN) * 128;                      // one K-slice of A and B (bytes)
-    constexpr int STAGE = KS * SUB;
-    constexpr int OPS = 2 * STAGE;
-    constexpr int CH = x3_chunk(BM, BN, OPS > 65536 ? OPS : 65536);
-    constexpr int CBYTES = CH * (BN + 4) * 4;                 // epilogue C staging
-    constexpr int SMEM = OPS > CBYTES ? OPS : CBYTES;
-    static_assert(TM >= 1 && TN >= 1 && WTM % 32 == 0 && WTN % 32 == 0 && AR >= 1 && BR >= 1, "tile");
-    static_assert(!BKN || NW == 4, "b_kn operands only with 4 waves");
-    static_assert(SMEM <= 160 * 1024, "LDS");
-    constexpr int BKR = BKN ? BN / 32 : 1;                    // b_kn loader rows (256 threads)
-
-    __shared__ __attribute__((aligned(16))) char smem[SMEM];
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63, wave = tid >> 6;
-    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
-    int mt, nt, bz;
-    {   // XCD-aware tile order (see conv.hip)
-        const int gx = gridDim.x, gy = gridDim.y;
-        const int total = gx * gy * gridDim.z;
-        const int L = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
-        const int per = total >> 3, rem = total & 7;
-        const int xcd = L & 7, idx = L >> 3;
-        const int Lp = xcd < rem ? xcd * (per + 1) + idx : rem * (per + 1) + (xcd - rem) * per + idx;
-        nt = Lp % gy;
-        const int t = Lp / gy;
-        mt = t % gx;
-        bz = t / gx;
-    }
-    const int m0 = mt * BM, n0 = nt * BN;
-    const int bidx = bz / a.splits, split = bz - bidx * a.splits;
-    const float *__restrict__ x = a.x + (long long)bidx * a.x_bs;
-    const float *__restrict__ wtf = a.wt + (long long)bidx * a.w_bs;      // fp32 view (b_kn)
-    const char *__restrict__ wtb = (const char *)wtf;                      // split-bf16 view (packed)
-    const int kt0 = split * a.tps;
-    const int kt1 = min(a.ktiles, kt0 + a.tps);
-    const int taps = a.kh * a.kw, nsl = a.cin >> 5;
-    const bool kperm = (AMODE == 0 || AMODE == 3) && !BKN && taps > 1;
-    const int ak = (tid & 7) * 4;
-
-    constexpr bool A8 = (AMODE == 0 || AMODE == 3) && !BKN && BM % (NT / 4) == 0;
-    constexpr int AR8 = A8 ? BM / (NT / 4) : 1;
-    ARows<A8 ? AR8 : AR, AMODE> R;
-    if constexpr (A8) {
-        int rows[AR8];
-#pragma unroll
-        for (int j = 0; j < AR8; ++j) rows[j] = a_row8<NT>(tid, j);
-        a_rows_init_at<AR8, AMODE>(a, m0, rows, R);
-    } else {
-        a_rows_init<AR, AMODE, RS>(a, m0, tid >> 3, R);
-    }
-    static_assert(!A8 || 2 * AR8 == AR, "wide A staging: same float4 count");
-
-    f4 ra[PF][KS][AR];
-    int rc[PF][KS];                  // A8: channel base of the staged slice (for the deferred prologue)
-    u32x4 rbp[PF][KS][BKN ? 1 : BR];
-    f4 rbk[PF][KS][BKN ? BKR : 1];
-    floatx16 acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-    SliceIt ld;                      // the next K-slice to load
-    ld.init(kt0, kperm, taps, nsl, a.kw);
-    // load one group of KS slices into register set p (slices past the end re-load the last one;
-    // their products are never formed)
-    auto issue = [&](int p) {
-#pragma unroll
-        for (int u = 0; u < KS; ++u) {
-            const int kt = (AMODE == 0 || AMODE == 3) ? ld.kt(nsl) : ld.i;
-            if constexpr (A8) {
-                f4 t0[AR8], t1[AR8];
-                const int c8 = ld.cs * 32 + 8 * (tid & 3);
-                rc[p][u] = c8;
-                load_a_tap<AR8, AMODE, false>(a, x, ld.ky, ld.kx, c8, R, t0);
-                load_a_tap<AR8, AMODE, false>(a, x, ld.ky, ld.kx, c8 + 4, R, t1);
-#pragma unroll
-                for (int j = 0; j < AR8; ++j) {
-                    ra[p][u][2 * j] = t0[j];
-                    ra[p][u][2 * j + 1] = t1[j];
-                }
-            } else if constexpr (AMODE == 0 || AMODE == 3) {
-                load_a_tap<AR, AMODE>(a, x, ld.ky, ld.kx, ld.cs * 32 + ak, R, ra[p][u]);
-            } else {
-                load_a<AR, AMODE>(a, x, kt, ak, R, ra[p][u]);
-            }
-            if constexpr (BKN) load_b<BN, BKR, 1>(a, wtf, kt, n0, tid, rbk[p][u]);
-            else load_b_x3<BR, RS>(a, wtb, kt, n0, tid, rbp[p][u]);
-            if (ld.i < kt1 - 1) ld.next(kperm, taps, nsl, a.kw);
-        }
-    };
-    auto store = [&](char *st, int p) {
-#pragma unroll
-        for (int u = 0; u < KS; ++u) {
-            char *sb = st + u * SUB;
-            if constexpr (A8) {
-                if (a.in_scale || a.pre_act) {
-#pragma unroll
-                    for (int j = 0; j < AR8; ++j) {
-                        prologue4<AR8, AMODE>(a, R, j, rc[p][u], ra[p][u][2 * j]);
-                        prologue4<AR8, AMODE>(a, R, j, rc[p][u] + 4, ra[p][u][2 * j + 1]);
-                    }
-                }
-                store_a8_x3<AR8, NT>(sb, tid, ra[p][u]);
-            }
-            else store_a_x3<AR, RS>(sb, tid, ra[p][u]);
-            if constexpr (BKN) store_b_kn_x3<BN, BKR>(sb + BM * 128, tid, rbk[p][u]);
-            else store_b_x3<BR, RS>(sb + BM * 128, tid, rbp[p][u]);
-        }
-    };
-
-    const int li = lane & 31, lh = lane >> 5;
-    const int rsw = swz(li);     // rows wm*WTM + i*32 + li share li's swizzle (tile bases are multiples of 32)
-    // multiply ``nv`` (<= KS) slices of one stage
-    auto compute = [&](const char *st, int nv) {
-#pragma unroll
-        for (int u = 0; u < KS; ++u) {
-            if (u >= nv) break;
-            const char *As = st + u * SUB;
-            const char *Bs = As + BM * 128;
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                const int hs = ((2 * s + lh) ^ rsw) << 4, ls = hs ^ 64;
-                bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
-#pragma unroll
-                for (int i = 0; i < TM; ++i) {
-                    const char *p = As + (wm * WTM + i * 32 + li) * 128;
-                    ah[i] = *(const bf16x8 *)(p + hs);
-                    al[i] = *(const bf16x8 *)(p + ls);
-                }
-#pragma unroll
-                for (int j = 0; j < TN; ++j) {
-                    const char *p = Bs + (wn * WTN + j * 32 + li) * 128;
-                    bh[j] = *(const bf16x8 *)(p + hs);
-                    bl[j] = *(const bf16x8 *)(p + ls);
-                }
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) {
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-                    }
-            }
-        }
-    };
-
-    const int n = kt1 - kt0;
-    const int ng = (n + KS - 1) / KS;            // stage groups
-    if (ng > 0) {
-        issue(0);
-        store(smem, 0);
-        __syncthreads();
-        if (PF == 1) {
-            // group g: load g+1 into the registers, multiply stage g%2, store g+1 into the other
-            // stage (last read before the previous barrier).  In 8-wave blocks the two waves that
-            // share a SIMD run each step in opposite phase orders (the upper half: store the group
-            // loaded one step earlier, load the next, multiply), so one wave's split + LDS-store
-            // phase overlaps its partner's MFMAs instead of both leaving the matrix pipe idle at
-            // the same time (MI355X_MICROARCH.md, two waves per SIMD, item 9).  Either order stores
-            // into the buffer last read before the previous barrier and multiplies the one
-            // completed before it.
-            const bool late = NW == 8 && __builtin_amdgcn_readfirstlane(wave) >= NW / 2;
-            if (late) {
-                issue(0);                                        // group 1
-                for (int g = 0; g < ng; ++g) {
-                    store(smem + ((g + 1) & 1) * STAGE, 0);       // group g+1
-                    issue(0);                                    // group g+2
-                    __builtin_amdgcn_sched_barrier(0);
-                    compute(smem + (g & 1) * STAGE, min(KS, n - g * KS));
-                    __syncthreads();
-                }
-            } else {
-                for (int g = 0; g < ng; ++g) {
-                    issue(0);
-                    __builtin_amdgcn_sched_barrier(0);
-                    compute(smem + (g & 1) * STAGE, min(KS, n - g * KS));
-                    store(smem + ((g + 1) & 1) * STAGE, 0);
-                    __syncthreads();
-                }
-            }
-        } else {
-            issue(PF - 1);
-            // group g: load g+2 into set g%2, multiply stage g%2, store set (g+1)%2 (group g+1)
-            for (int g = 0; g < ng; g += 2) {
-                issue(0);
-                __builtin_amdgcn_sched_barrier(0);
-                compute(smem, min(KS, n - g * KS));
-                store(smem + STAGE, PF - 1);
-                __syncthreads();
-                if (g + 1 >= ng) break;
-                issue(PF - 1);
-                __builtin_amdgcn_sched_barrier(0);
-                compute(smem + STAGE, min(KS, n - (g + 1) * KS));
-                store(smem, 0);
-                __syncthreads();
-            }
-        }
-    }
-    epilogue_tile<BM, BN, WAVES_M, TM, TN, NW, CH>(a, acc, (float *)smem, tid, m0, n0, bz, bidx);
-}
-
-template <int BM, int BN, int WM, int NW, int KS, int PF>
-static void launch_x3(const ConvArgs &a, int amode, bool bkn, dim3 grid, hipStream_t s) {
-    constexpr int NT = 64 * NW;
-    if (bkn) {
-        if constexpr (NW == 4) {
-            if (amode == 0) conv_igemm_x3<BM, BN, WM, NW, KS, PF, 0, 1><<<grid, NT, 0, s>>>(a);
-            else if (amode == 1) conv_igemm_x3<BM, BN, WM, NW, KS, PF, 1, 1><<<grid, NT, 0, s>>>(a);
-            else conv_igemm_x3<BM, BN, WM, NW, KS, PF, 2, 1><<<grid, NT, 0, s>>>(a);
-        }
-        return;
-    }
-    switch (amode) {
-        case 0: conv_igemm_x3<BM, BN, WM, NW, KS, PF, 0, 0><<<grid, NT, 0, s>>>(a); break;
-        case 1: conv_igemm_x3<BM, BN, WM, NW, KS, PF, 1, 0><<<grid, NT, 0, s>>>(a); break;
-        case 2: conv_igemm_x3<BM, BN, WM, NW, KS, PF, 2, 0><<<grid, NT, 0, s>>>(a); break;
-        default: conv_igemm_x3<BM, BN, WM, NW, KS, PF, 3, 0><<<grid, NT, 0, s>>>(a); break;
-    }
-}
-
-// x3 kernel configurations (index = the host planner's tile id, conv.hip kX3Tiles)
-void launch_conv_x3(int cfg, const ConvArgs &a, int amode, bool bkn, dim3 grid, hipStream_t s) {
-    switch (cfg) {
-        case 0: launch_x3<256, 256, 2, 8, 1, 1>(a, amode, bkn, grid, s); break;
-        case 1: launch_x3<128, 128, 2, 8, 1, 1>(a, amode, bkn, grid, s); break;
-        case 2: launch_x3<64, 128, 2, 8, 1, 1>(a, amode, bkn, grid, s); break;
-        case 3: launch_x3<128, 64, 2, 4, 1, 1>(a, amode, bkn, grid, s); break;
-        case 4: launch_x3<64, 64, 2, 4, 1, 1>(a, amode, bkn, grid, s); break;
-        case 5: launch_x3<128, 32, 4, 4, 1, 1>(a, amode, bkn, grid, s); break;
-        case 6: launch_x3<256, 128, 4, 8, 1, 1>(a, amode, bkn, grid, s); break;
-        default: launch_x3<256, 64, 8, 8, 1, 1>(a, amode, bkn, grid, s); break;   // 7
-    }
-}
-
-// ---------------------------------------------------------------- weight splitting kernels
-// [rows][kpad] fp32 -> [rows][kpad/32][hi 32 | lo 32] bf16 (kpad % 32 == 0)
+// [rows][kpad] fp32 -> [rows][kpad/32][hi 32 | lo 32] (kpad % 32 == 0)
+template <int ELT>
 __global__ __launch_bounds__(256) void split_weights_kernel(const float *__restrict__ w, long long slices,
-                                                            char *__restrict__ out) {
+                                                            float scale, char *__restrict__ out) {
     // one thread per 4 consecutive k of one 32-k slice
     for (long long e = blockIdx.x * 256LL + threadIdx.x; e < slices * 8; e += (long long)gridDim.x * 256) {
         const long long sl = e >> 3;
         const int q = (int)(e & 7);
-        const f4 v = *(const f4 *)(w + sl * 32 + q * 4);
+        const f4 v = *(const f4 *)(w + sl * 32 + q * 4) * scale;
         u32x2 hi, lo;
-        split4(v, hi, lo);
+        split4<ELT>(v, hi, lo);
         char *o = out + sl * 128 + q * 8;
         *(u32x2 *)o = hi;
         *(u32x2 *)(o + 64) = lo;
@@ -430,11 +26,12 @@ __global__ __launch_bounds__(256) void split_weights_kernel(const float *__restr
 }
 
 // StyleGAN2 per-sample weights (s2v_modulate_weights) written directly in the split layout
+template <int ELT>
 __global__ __launch_bounds__(256) void modulate_weights_x3_kernel(const float *__restrict__ wt, int npad, int kpad,
                                                                   int K, int cin, int cout,
                                                                   const float *__restrict__ s, int s_ns,
                                                                   const float *__restrict__ d, int d_ns, int batch,
-                                                                  char *__restrict__ out) {
+                                                                  float scale, char *__restrict__ out) {
     const long long per = (long long)npad * kpad;
     const long long total = per * batch;
     for (long long e = (blockIdx.x * 256LL + threadIdx.x) * 4; e < total; e += (long long)gridDim.x * 256 * 4) {
@@ -442,13 +39,13 @@ __global__ __launch_bounds__(256) void modulate_weights_x3_kernel(const float *_
         const long long r = e - b * per;
         const int o = (int)(r / kpad), k = (int)(r - (long long)o * kpad);
         f4 w = *(const f4 *)(wt + r);
-        const float dd = (d && o < cout) ? d[(long long)b * d_ns + o] : 1.f;
+        const float dd = ((d && o < cout) ? d[(long long)b * d_ns + o] : 1.f) * scale;
         float f[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) f[j] = (k + j < K) ? s[(long long)b * s_ns + (k + j) % cin] * dd : 0.f;
         w.x *= f[0]; w.y *= f[1]; w.z *= f[2]; w.w *= f[3];
         u32x2 hi, lo;
-        split4(w, hi, lo);
+        split4<ELT>(w, hi, lo);
         char *ob = out + (e >> 5) * 128 + (k & 31) * 2;    // slice e/32, k-offset within it
         *(u32x2 *)ob = hi;
         *(u32x2 *)(ob + 64) = lo;
@@ -461,26 +58,55 @@ static unsigned grid_x3(long long total) {
     return (unsigned)(b < 1 ? 1 : b);
 }
 
+static bool pow2_scale(float s) {
+    int e;
+    return s > 0.f && std::frexp(s, &e) == 0.5f;
+}
+
 }  // namespace s2v
 
 using namespace s2v;
 
-extern "C" int s2v_split_weights_x3(const float *w, int rows, int kpad, void *out, s2v_stream_t stream) {
-    S2V_REQUIRE(w && out && rows > 0 && kpad > 0 && kpad % 32 == 0, "split_weights_x3: bad args");
-    S2V_REQUIRE(((uintptr_t)w % 16) == 0 && ((uintptr_t)out % 16) == 0, "split_weights_x3: 16-byte alignment");
+extern "C" int s2v_split_weights(const float *w, int rows, int kpad, int prec, float scale, void *out,
+                                 s2v_stream_t stream) {
+    S2V_REQUIRE(w && out && rows > 0 && kpad > 0 && kpad % 32 == 0, "split_weights: bad args");
+    S2V_REQUIRE(prec == S2V_PREC_BF16X3 || prec == S2V_PREC_F16X3, "split_weights: prec must be BF16X3 or F16X3");
+    S2V_REQUIRE(pow2_scale(scale), "split_weights: scale must be a positive power of two, got %g", scale);
+    S2V_REQUIRE(((uintptr_t)w % 16) == 0 && ((uintptr_t)out % 16) == 0, "split_weights: 16-byte alignment");
     const long long slices = (long long)rows * (kpad / 32);
-    split_weights_kernel<<<grid_x3(slices * 8), 256, 0, (hipStream_t)stream>>>(w, slices, (char *)out);
-    return check_launch("split_weights_x3");
+    if (prec == S2V_PREC_BF16X3)
+        split_weights_kernel<0><<<grid_x3(slices * 8), 256, 0, (hipStream_t)stream>>>(w, slices, scale, (char *)out);
+    else
+        split_weights_kernel<1><<<grid_x3(slices * 8), 256, 0, (hipStream_t)stream>>>(w, slices, scale, (char *)out);
+    return check_launch("split_weights");
+}
+
+extern "C" int s2v_split_weights_x3(const float *w, int rows, int kpad, void *out, s2v_stream_t stream) {
+    return s2v_split_weights(w, rows, kpad, S2V_PREC_BF16X3, 1.f, out, stream);
+}
+
+extern "C" int s2v_modulate_weights_split(const float *wt, int npad, int kpad, int K, int cin, int cout,
+                                          const float *s, int s_ns, const float *d, int d_ns, int batch, int prec,
+                                          float scale, void *out, s2v_stream_t stream) {
+    S2V_REQUIRE(wt && s && out && npad > 0 && kpad > 0 && K > 0 && K <= kpad && cin > 0 && cout > 0 && cout <= npad &&
+                batch > 0 && s_ns >= cin && (!d || d_ns >= cout), "modulate_weights_split: bad args");
+    S2V_REQUIRE(prec == S2V_PREC_BF16X3 || prec == S2V_PREC_F16X3, "modulate_weights_split: prec must be BF16X3 or F16X3");
+    S2V_REQUIRE(pow2_scale(scale), "modulate_weights_split: scale must be a positive power of two, got %g", scale);
+    S2V_REQUIRE(kpad % 32 == 0 && ((uintptr_t)wt % 16) == 0 && ((uintptr_t)out % 16) == 0,
+                "modulate_weights_split: kpad %% 32 and 16-byte aligned buffers required");
+    const unsigned g = grid_x3((long long)npad * kpad * batch / 4);
+    if (prec == S2V_PREC_BF16X3)
+        modulate_weights_x3_kernel<0><<<g, 256, 0, (hipStream_t)stream>>>(wt, npad, kpad, K, cin, cout, s, s_ns, d,
+                                                                           d_ns, batch, scale, (char *)out);
+    else
+        modulate_weights_x3_kernel<1><<<g, 256, 0, (hipStream_t)stream>>>(wt, npad, kpad, K, cin, cout, s, s_ns, d,
+                                                                           d_ns, batch, scale, (char *)out);
+    return check_launch("modulate_weights_split");
 }
 
 extern "C" int s2v_modulate_weights_x3(const float *wt, int npad, int kpad, int K, int cin, int cout, const float *s,
                                        int s_ns, const float *d, int d_ns, int batch, void *out,
                                        s2v_stream_t stream) {
-    S2V_REQUIRE(wt && s && out && npad > 0 && kpad > 0 && K > 0 && K <= kpad && cin > 0 && cout > 0 && cout <= npad &&
-                batch > 0 && s_ns >= cin && (!d || d_ns >= cout), "modulate_weights_x3: bad args");
-    S2V_REQUIRE(kpad % 32 == 0 && ((uintptr_t)wt % 16) == 0 && ((uintptr_t)out % 16) == 0,
-                "modulate_weights_x3: kpad %% 32 and 16-byte aligned buffers required");
-    modulate_weights_x3_kernel<<<grid_x3((long long)npad * kpad * batch / 4), 256, 0, (hipStream_t)stream>>>(
-        wt, npad, kpad, K, cin, cout, s, s_ns, d, d_ns, batch, (char *)out);
-    return check_launch("modulate_weights_x3");
+    return s2v_modulate_weights_split(wt, npad, kpad, K, cin, cout, s, s_ns, d, d_ns, batch, S2V_PREC_BF16X3, 1.f,
+                                      out, stream);
 }

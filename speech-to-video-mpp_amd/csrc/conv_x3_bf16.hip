@@ -1,0 +1,6 @@
+// bf16 instances of the split-fp32 implicit-GEMM convolution (S2V_PREC_BF16X3; conv_x3_impl.hpp).
+#include "conv_x3_impl.hpp"
+
+namespace s2v {
+template void launch_conv_x3<0>(int cfg, const ConvArgs &a, int amode, bool bkn, dim3 grid, hipStream_t s);
+}  // namespace s2v

@@ -107,8 +107,11 @@ class ENet(_EngineMixin, arch.ENetParams):
         eng.forward(ctx, audio_sequences.float(), face_sequences.float(), gt_sequences.float(), out, low, noises)
         if five:
             out = torch.stack(torch.split(out, b, 0), 2)
-            low = torch.nn.functional.interpolate(low, out.shape[3:])
-            low = torch.stack(torch.split(low, b, 0), 2)
+            # F.interpolate(low_res_img, outputs.size()[3:]) (default mode 'nearest', ENet.py:134)
+            up = torch.empty((n, 3) + tuple(out.shape[3:]), device=dev)
+            ops.resize(ctx, low.data_ptr(), tuple(low.shape), low.stride(), up.data_ptr(), tuple(out.shape[3:]),
+                       up.stride(), mode=1)
+            low = torch.stack(torch.split(up, b, 0), 2)
         return out, low
 
 

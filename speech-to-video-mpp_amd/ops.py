@@ -17,16 +17,23 @@ import torch
 
 from . import _lib
 from ._lib import (ACT_GELU_TANH, ACT_LRELU, ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_TANH,  # noqa: F401
-                   IN_DIRECT, IN_NEAREST_UP2, IN_TRANSPOSED, PAD_REFLECT, PAD_ZERO, PREC_BF16X3, PREC_F32, check)
+                   IN_DIRECT, IN_NEAREST_UP2, IN_TRANSPOSED, PAD_REFLECT, PAD_ZERO, PREC_BF16X3, PREC_F16X3, PREC_F32,
+                   check)
 
 F32 = 4
 
-# Arithmetic of the implicit-GEMM convolutions (s2v_conv_params.prec): "bf16x3" = split-fp32 on the
-# bf16 MFMA (16 significant bits per operand, <= 3*2^-16 relative error per product, the default),
-# "f32" = exact fp32 MFMA.  The
-# S2V_PRECISION environment variable sets the process default; set_precision() changes it.
-_PRECISIONS = {"bf16x3": PREC_BF16X3, "f32": PREC_F32}
-PRECISION = os.environ.get("S2V_PRECISION", "bf16x3")
+# Arithmetic of the implicit-GEMM convolutions (s2v_conv_params.prec):
+#   "f16x3"  (default) split-fp32 on the f16 MFMA: 22 significant bits per operand, <= 3*2^-22
+#            relative error per product for operands in the f16 normal range (weights are pre-scaled
+#            into it by a power of two, undone exactly in the epilogue);
+#   "bf16x3" split-fp32 on the bf16 MFMA: 16 significant bits per operand, <= 3*2^-16 per product,
+#            any fp32 range;
+#   "f32"    exact fp32 MFMA.
+# All three run fp32 tensors with fp32 accumulation.  The S2V_PRECISION environment variable sets
+# the process default; set_precision() changes it.
+_PRECISIONS = {"f16x3": PREC_F16X3, "bf16x3": PREC_BF16X3, "f32": PREC_F32}
+SPLIT_PRECISIONS = ("f16x3", "bf16x3")
+PRECISION = os.environ.get("S2V_PRECISION", "f16x3")
 if PRECISION not in _PRECISIONS:
     raise ValueError(f"S2V_PRECISION must be one of {sorted(_PRECISIONS)}, got {PRECISION!r}")
 
@@ -39,7 +46,7 @@ USE_TILE_COUNTERS = os.environ.get("S2V_SPLITK_FOLD", "0") == "1"
 
 
 def set_precision(name: str) -> str:
-    """Select the conv arithmetic ("bf16x3" or "f32") for launches issued from now on; returns the
+    """Select the conv arithmetic ("f16x3", "bf16x3" or "f32") for launches issued from now on; returns the
     previous setting.  A captured HIP graph keeps the precision it was captured with."""
     global PRECISION
     if name not in _PRECISIONS:
@@ -187,18 +194,31 @@ class ConvW:
         self.scale = None if scale is None else scale.contiguous().to(device)
         self.shift = None if shift is None else shift.contiguous().to(device)
 
-    _wt_x3 = None
+    _split = None
 
-    def wt_x3(self, ctx: "Ctx") -> torch.Tensor:
-        """The packed weights in the S2V_PREC_BF16X3 split layout (built once, on first use)."""
-        if self._wt_x3 is None:
+    def split_scale(self, prec: int) -> float:
+        """Power-of-two pre-scale of the split weights (s2v_conv_params.wt_scale): f16 halves get
+        max|W| into [2^13, 2^14) so every weight and its lo half stay in the f16 normal range; bf16
+        has fp32's exponent range and needs none."""
+        if prec != PREC_F16X3:
+            return 1.0
+        if getattr(self, "_f16_scale", None) is None:
+            m = float(self.wt.abs().max())
+            self._f16_scale = 1.0 if m == 0.0 else float(2.0 ** math.floor(math.log2(16384.0 / m)))
+        return self._f16_scale
+
+    def wt_x3(self, ctx: "Ctx", prec: int = PREC_BF16X3) -> torch.Tensor:
+        """The packed weights in the split layout of ``prec`` (built once per precision, on first use)."""
+        if self._split is None:
+            self._split = {}
+        if prec not in self._split:
             if self.wt.is_cuda and torch.cuda.is_current_stream_capturing():
                 raise _lib.S2VError("split weights must be built by an eager run before graph capture")
             out = torch.empty(self.wt.shape, dtype=torch.float32, device=self.wt.device)
-            check(ctx.lib.s2v_split_weights_x3(self.wt.data_ptr(), self.npad, self.kpad, out.data_ptr(), ctx.stream),
-                  "s2v_split_weights_x3")
-            self._wt_x3 = out
-        return self._wt_x3
+            check(ctx.lib.s2v_split_weights(self.wt.data_ptr(), self.npad, self.kpad, prec, self.split_scale(prec),
+                                            out.data_ptr(), ctx.stream), "s2v_split_weights")
+            self._split[prec] = out
+        return self._split[prec]
 
     def make_polyphase(self, device):
         """Polyphase plan of a stride-2 ConvTranspose2d: output parity class (ry, rx) is a stride-1
@@ -300,18 +320,19 @@ def _conv(ctx, x, cw, y, ohw, out_view, act, alpha, res, res_after, res_offset, 
         if res is not None:
             p.res_bs = res.h * res.w * res.cs
     use_x3 = False
-    if p.prec == PREC_BF16X3:
+    if p.prec != PREC_F32:
         p.wt_x3 = p.wt                   # placeholder: the plan query only checks it is set
         use_x3 = bool(_plan(ctx, p)[6]) and not p.b_kn
         p.wt_x3 = None
     if per_sample_wt is not None:
-        wb = per_sample_wt(use_x3)       # split or fp32 per-sample weights, as the kernel reads them
+        wb, wscale = per_sample_wt(p.prec if use_x3 else PREC_F32)   # as the kernel reads them
         if use_x3:
-            p.wt, p.wt_x3 = None, wb.data_ptr()
+            p.wt, p.wt_x3, p.wt_scale = None, wb.data_ptr(), wscale
         else:
             p.wt = wb.data_ptr()
     elif use_x3:                         # implicit-GEMM path: pre-split packed weights
-        p.wt_x3 = cw.wt_x3(ctx).data_ptr()
+        p.wt_x3 = cw.wt_x3(ctx, p.prec).data_ptr()
+        p.wt_scale = cw.split_scale(p.prec)
     need = ctx.lib.s2v_conv2d_ws_bytes(ctypes.byref(p))
     p.ws, p.ws_bytes = ctx.ws.get(need)
     _set_counters(ctx, p, need)
@@ -337,14 +358,23 @@ def modulated_conv2d(ctx: Ctx, x: NHWC, cw: ConvW, y: NHWC, s: torch.Tensor, d: 
     assert x.c == cw.cin and (y.n, y.h, y.w, y.c) == (x.n, oh, ow, cw.cout)
     b = x.n
 
-    def weights(x3):
-        # the split-bf16 implicit GEMM reads split weights; the VALU kernels (small K / Cout) fp32
+    def weights(prec):
+        # the split implicit GEMM reads split weights; the VALU kernels (small K / Cout) fp32.
+        # Demodulated rows have |w * s * d| <= post (ENet / GFPGAN / GPEN: sqrt 2), so f16 halves
+        # take a fixed 2^11 pre-scale (room up to |w| < 32); without demodulation the range is open
+        # and the weights go unscaled (f16 subnormal halves keep an absolute error <= 2^-25).
         wb = torch.empty((b, cw.npad, cw.kpad), device=cw.wt.device)
-        fn = ctx.lib.s2v_modulate_weights_x3 if x3 else ctx.lib.s2v_modulate_weights
-        check(fn(cw.wt.data_ptr(), cw.npad, cw.kpad, cw.K, cw.cin, cw.cout, s.data_ptr(), s.stride(0),
-                 None if d is None else d.data_ptr(), 0 if d is None else d.stride(0), b, wb.data_ptr(), ctx.stream),
-              "s2v_modulate_weights")
-        return wb
+        dp, dns = (None, 0) if d is None else (d.data_ptr(), d.stride(0))
+        if prec == PREC_F32:
+            check(ctx.lib.s2v_modulate_weights(cw.wt.data_ptr(), cw.npad, cw.kpad, cw.K, cw.cin, cw.cout, s.data_ptr(),
+                                               s.stride(0), dp, dns, b, wb.data_ptr(), ctx.stream),
+                  "s2v_modulate_weights")
+            return wb, 1.0
+        scale = 2048.0 if (prec == PREC_F16X3 and d is not None) else 1.0
+        check(ctx.lib.s2v_modulate_weights_split(cw.wt.data_ptr(), cw.npad, cw.kpad, cw.K, cw.cin, cw.cout,
+                                                 s.data_ptr(), s.stride(0), dp, dns, b, prec, scale, wb.data_ptr(),
+                                                 ctx.stream), "s2v_modulate_weights_split")
+        return wb, scale
     return _conv(ctx, x, cw, y, (oh, ow), None, act, alpha, res, res_after, (0, 0), None, None, ACT_NONE, 0.0,
                  pix_add, pix_w, None, shift, 0, 0, per_sample_wt=weights)
 
@@ -400,10 +430,11 @@ def conv_symbol(ctx: Ctx, p) -> str:
         if wm < 0:
             return f"void s2v::conv_smallk<{-wm}>(s2v::ConvArgs, int, int, int, int)"
         if wm:
-            return f"void s2v::conv_small_cpar<{bn}, {wm}>(s2v::ConvArgs, int)"
+            return f"void s2v::conv_small_cpar<{bn}, {wm}, {'true' if avec else 'false'}>(s2v::ConvArgs, int)"
         return f"void s2v::conv_direct_small<{bn}>(s2v::ConvArgs, int)"
     if x3:
-        return f"void s2v::conv_igemm_x3<{bm}, {bn}, {wm}, {nw}, {ks}, {pf}, {avec}, {bkn}>(s2v::ConvArgs)"
+        return (f"void s2v::conv_igemm_x3<{bm}, {bn}, {wm}, {nw}, {ks}, {pf}, {avec}, {bkn}, {x3 - 1}>"
+                "(s2v::ConvArgs)")
     return f"void s2v::conv_igemm<{bm}, {bn}, {wm}, {avec}, {bkn}>(s2v::ConvArgs)"
 
 

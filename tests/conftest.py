@@ -25,10 +25,10 @@ def golden():
     return load
 
 
-@pytest.fixture(params=["f32", "bf16x3"])
+@pytest.fixture(params=["f32", "bf16x3", "f16x3"])
 def prec(request):
     """Run a test once per conv arithmetic mode (s2v_amd.ops.set_precision): exact fp32 MFMA and
-    the split-fp32 bf16 MFMA default."""
+    the split-fp32 forms on the bf16 and f16 MFMAs (f16x3 is the default)."""
     from s2v_amd import ops
     prev = ops.set_precision(request.param)
     yield request.param

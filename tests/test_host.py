@@ -59,15 +59,16 @@ def test_invalid_arguments_are_rejected_without_a_device():
 def test_conv_params_struct_layout_matches_header(tmp_path):
     src = tmp_path / "sz.c"
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "%s"\n'
-                   'int main(){printf("%%zu %%zu %%zu %%zu %%zu %%zu\\n", sizeof(s2v_conv_params),'
+                   'int main(){printf("%%zu %%zu %%zu %%zu %%zu %%zu %%zu\\n", sizeof(s2v_conv_params),'
                    'offsetof(s2v_conv_params, ws), offsetof(s2v_conv_params, x_bs),'
                    'offsetof(s2v_conv_params, res), offsetof(s2v_conv_params, force_splits),'
-                   'offsetof(s2v_conv_params, b_kn));return 0;}' % HEADER)
+                   'offsetof(s2v_conv_params, b_kn), offsetof(s2v_conv_params, wt_scale));return 0;}' % HEADER)
     exe = tmp_path / "sz"
     subprocess.run(["gcc", str(src), "-o", str(exe)], check=True)
     got = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
     P = _lib.ConvParams
-    assert got == [ctypes.sizeof(P), P.ws.offset, P.x_bs.offset, P.res.offset, P.force_splits.offset, P.b_kn.offset]
+    assert got == [ctypes.sizeof(P), P.ws.offset, P.x_bs.offset, P.res.offset, P.force_splits.offset, P.b_kn.offset,
+                   P.wt_scale.offset]
 
 
 @pytest.mark.parametrize("name,ctor", [("lnet", lambda: arch.LNetParams()),

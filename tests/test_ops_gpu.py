@@ -6,7 +6,9 @@ run in both arithmetic modes (``prec`` fixture):
            relative to that sum for K <= 10^4, cdna_hip_programming.md §3 'FP32-input MFMA');
   * bf16x3 (split-fp32 on v_mfma_f32_32x32x16_bf16): 5e-5 * sum|a*b| — worst case per product:
            each operand's hi + lo is within 2^-16 of it and the dropped |al*bl| <= 2^-16 |a*b|,
-           so 3 * 2^-16 = 4.6e-5 relative, plus the fp32 sums.
+           so 3 * 2^-16 = 4.6e-5 relative, plus the fp32 sums;
+  * f16x3  (the same split on v_mfma_f32_32x32x16_f16): 3e-6 * sum|a*b| — 3 * 2^-22 = 7.2e-7 per
+           product in the f16 normal range (weights pre-scaled into it), plus the fp32 sums.
 """
 import math
 
@@ -25,7 +27,7 @@ from s2v_amd.ops import NHWC, ConvW  # noqa: E402
 DEV = "cuda"
 
 
-REL = {"f32": 2e-6, "bf16x3": 5e-5}
+REL = {"f32": 2e-6, "bf16x3": 5e-5, "f16x3": 3e-6}
 
 
 @pytest.fixture(scope="module")
@@ -77,6 +79,9 @@ CONV_CASES = [
     (2, 64, 16, 16, 128, 3, 1, 1, 1, "direct", "zero", 2, 3),
     (1, 32, 20, 12, 64, 3, 2, 1, 1, "direct", "zero", 3, 0),
     (2, 32, 12, 12, 64, 3, 1, 1, 1, "direct", "zero", 4, 2),
+    # 64x64 tile (force_tile 5) with cout 32 < BN: the N tail of the B loads and the epilogue
+    (2, 32, 12, 12, 32, 3, 1, 1, 1, "direct", "zero", 5, 0),
+    (2, 64, 17, 15, 32, 3, 1, 1, 1, "direct", "reflect", 5, 2),
     (2, 96, 10, 10, 200, 3, 1, 1, 1, "direct", "reflect", 5, 0),
     (2, 48, 12, 12, 40, 3, 1, 1, 1, "direct", "reflect", 6, 4),
     (1, 3, 24, 24, 64, 7, 1, 3, 1, "direct", "zero", 0, 0),
@@ -173,6 +178,7 @@ def test_splitk_fold_matches_separate_reduce(ctx, prec):
     wt = rnd(96, 64, 3, 3, seed=22) / 24.0
     cw = ConvW(wt.float(), rnd(96, seed=23).float(), DEV, padding=1)
     outs = []
+    prev = ops.USE_TILE_COUNTERS
     try:
         for fold in (True, False):
             ops.USE_TILE_COUNTERS = fold
@@ -182,7 +188,7 @@ def test_splitk_fold_matches_separate_reduce(ctx, prec):
                            force_splits=splits)
                 outs.append(y.t.cpu())
     finally:
-        ops.USE_TILE_COUNTERS = True
+        ops.USE_TILE_COUNTERS = prev
     for a, b in zip(outs[:3], outs[3:]):
         assert torch.equal(a, b)
     torch.cuda.synchronize()
@@ -478,10 +484,12 @@ def test_melspectrogram_matches_restatement(pad_mode):
         assert np.array_equal(chunks[i, 0], exp[:, s: s + 16].astype(np.float32))
 
 
-@pytest.mark.parametrize("cin,k,cout", [(64, 7, 3), (128, 1, 3), (256, 1, 3), (256, 7, 2), (12, 3, 1)])
+@pytest.mark.parametrize("cin,k,cout", [(64, 7, 3), (128, 1, 3), (256, 1, 3), (256, 7, 2), (12, 3, 1),
+                                        (32, 1, 3), (36, 3, 3), (44, 1, 2), (96, 3, 3)])
 def test_small_cout_conv(ctx, prec, cin, k, cout):
     """Cout <= 4 heads (LNet/DNet final 7x7, ToRGB 1x1 with modulation, flow head): channel-parallel
-    kernel with in_scale prologue and in-place residual."""
+    kernel with in_scale prologue and in-place residual.  cin 32..63 runs 2 lanes per pixel, 64..127
+    4 lanes (36 / 44 leave the lanes' channel loops uneven), >= 128 8 lanes."""
     n, h, w = 2, 13, 11
     wt = rnd(cout, cin, k, k, seed=40) / math.sqrt(cin * k * k)
     bias = rnd(cout, seed=41)
@@ -494,3 +502,45 @@ def test_small_cout_conv(ctx, prec, cin, k, cout):
     ref = F.conv2d(x * s[:, :, None, None], wt, bias, padding=k // 2) + res
     bound = conv_bound(x * s[:, :, None, None], wt, 1, k // 2, 1)
     assert ((to_nchw(y) - ref).abs() <= 2e-6 * (bound + 1) + 1e-6).all()
+
+
+@pytest.mark.parametrize("n,hw,cin", [(2, (16, 8), 32), (2, (13, 11), 32), (3, (8, 16), 64), (2, (9, 7), 96)])
+def test_small_cout_per_sample_weights(ctx, n, hw, cin):
+    """Per-sample (modulated) weights on the small-Cout kernel: LDS-staged weights need every block
+    inside one batch entry (M % pixels-per-block == 0, 16x8 = 128 pixels); other M take the global
+    weight path.  Both against the grouped per-sample conv of the reference (base_blocks.py:487-508)."""
+    h, w = hw
+    cout = 3
+    wt = rnd(cout, cin, 1, 1, seed=45) / math.sqrt(cin)
+    bias = rnd(cout, seed=46)
+    x = rnd(n, cin, h, w, seed=47)
+    s = rnd(n, cin, seed=48, lo=0.5, hi=1.5)
+    res = rnd(n, cout, h, w, seed=49)
+    cw = ConvW(wt.float(), bias.float(), DEV)
+    y = nhwc(res.float())
+    ops.modulated_conv2d(ctx, nhwc(x.float()), cw, y, s.float().to(DEV), res=y)
+    wb = wt[None] * s[:, None, :, None, None]
+    ref = torch.stack([F.conv2d(x[i:i + 1], wb[i], bias)[0] for i in range(n)]) + res
+    bound = conv_bound(x * s[:, :, None, None], wt, 1, 0, 1)
+    assert ((to_nchw(y) - ref).abs() <= 2e-6 * (bound + 1) + 1e-6).all()
+
+
+@pytest.mark.parametrize("mag", [1e-2, 30.0])
+def test_f16x3_operand_range(ctx, mag):
+    """f16x3 keeps its 3 * 2^-22 per-product bound away from unit scale: activations of magnitude
+    1e-2 (their lo halves are f16 subnormals: a flushing MFMA would lose 2^-12 of each) and 30 (weights
+    pre-scaled by a power of two, undone in the epilogue), weights scaled by 1 / mag."""
+    prev = ops.set_precision("f16x3")
+    try:
+        n, cin, h, w, cout = 2, 64, 12, 12, 96
+        wt = rnd(cout, cin, 3, 3, seed=51) / math.sqrt(cin * 9) / mag
+        x = rnd(n, cin, h, w, seed=52) * mag
+        cw = ConvW(wt.float(), None, DEV, padding=1)
+        y = NHWC.empty(n, h, w, cout, DEV)
+        ops.conv2d(ctx, nhwc(x.float()), cw, y)
+        ref = F.conv2d(x.float().double(), wt.float().double(), padding=1)
+        bound = conv_bound(x.float().double(), wt.float().double(), 1, 1, 1)
+        err = (to_nchw(y) - ref).abs()
+        assert (err <= REL["f16x3"] * bound + 1e-12).all(), f"max rel {(err / (bound + 1e-30)).max():.3e}"
+    finally:
+        ops.set_precision(prev)

@@ -19,8 +19,8 @@ from s2v_amd import synth
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-FWD_REL = {"f32": 1e-5, "bf16x3": 1e-4}          # measured on MI355X: 1.4e-6 / 1.7e-5
-FLIP_FRAC = {"f32": 1e-3, "bf16x3": 5e-3}        # measured: 2e-4 / 1.5e-3
+FWD_REL = {"f32": 1e-5, "bf16x3": 1e-4, "f16x3": 1e-5}          # measured on MI355X: 1.4e-6 / 1.7e-5
+FLIP_FRAC = {"f32": 1e-3, "bf16x3": 5e-3, "f16x3": 1e-3}        # measured: 2e-4 / 1.5e-3
 
 
 def _net(scale):

@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
-"""Measured error of the HIP models against the reference goldens (tests/golden) in both conv
-arithmetic modes (exact fp32 MFMA, split-fp32 bf16x3).  Prints one JSON line per (net, mode).
+"""Measured error of the HIP models against the reference goldens (tests/golden) in every conv
+arithmetic mode (exact fp32 MFMA, split-fp32 bf16x3 / f16x3).  ENet is also reported on the
+clamp(0, 1) output the caller consumes (inference.py:267) and on the B=16 bench batch against the
+CPU oracle.  Prints one JSON line per (net, mode).
 
     python tools/precision_report.py [--out gpurun_out/precision.json]
 """
@@ -29,6 +31,13 @@ def err(a, b):
     return {"max": float(d.max()), "mean": float(d.mean())}
 
 
+def clamped(a, b):
+    a = a.detach().cpu().double().clamp(0, 1).numpy()
+    b = np.clip(np.asarray(b, np.float64), 0, 1)
+    d = np.abs(a - b)
+    return {"max": float(d.max()), "mean": float(d.mean())}
+
+
 def probe_err(t, g, name):
     flat = t.detach().cpu().reshape(-1).double().numpy()
     d = np.abs(flat[g[f"{name}_idx"]] - g[f"{name}_val"].astype(np.float64))
@@ -51,7 +60,11 @@ def main():
     gpen = models.FullGenerator(512, 512, 8, 2)
     gpen.load_state_dict(synth_sd("gpen"))
     rows = []
-    for mode in ("f32", "bf16x3"):
+    from oracle import nets
+    mel16, face16, gt16 = synth.lipsync_inputs("enet.b16", 16, 256)
+    with torch.no_grad():
+        ro16, _ = nets.enet_forward(synth_sd("enet"), *(torch.from_numpy(a[:2]) for a in (mel16, face16, gt16)))
+    for mode in ("f32", "bf16x3", "f16x3"):
         ops.set_precision(mode)
         g = G("lnet_b2_96")
         mel, face, _ = synth.lipsync_inputs("golden.lnet", 2, 96)
@@ -61,8 +74,14 @@ def main():
             g = G(f"enet_b1_{size}")
             mel, face, gt = synth.lipsync_inputs(f"golden.enet{size}", 1, size)
             out, low = enet(*(torch.from_numpy(a).to(DEV) for a in (mel, face, gt)))
-            rows.append({"net": f"ENet b1 {size}", "mode": mode, "low": err(low, g["low"]),
-                         "out": err(out, g["out"]) if "out" in g.files else probe_err(out, g, "out")})
+            r = {"net": f"ENet b1 {size}", "mode": mode, "low": err(low, g["low"]),
+                 "out": err(out, g["out"]) if "out" in g.files else probe_err(out, g, "out")}
+            if "out" in g.files:
+                r["out_clamped01"] = clamped(out, g["out"])
+            rows.append(r)
+        out16, _ = enet(*(torch.from_numpy(a).to(DEV) for a in (mel16, face16, gt16)))
+        rows.append({"net": "ENet b16 256 (frames 0-1 vs CPU oracle)", "mode": mode, "out": err(out16[:2], ro16),
+                     "out_clamped01": clamped(out16[:2], ro16)})
         for size, b in ((128, 2), (256, 1)):
             g = G(f"dnet_b{b}_{size}")
             src, coeff = synth.dnet_inputs(f"golden.dnet{size}", b, size)
