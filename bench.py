@@ -540,11 +540,12 @@ class Clip(Pipeline):
                                    "(inference.py:204-288, facing.py:176-191)", "clip_frames": n}
 
     def units_per_step(self, world):
-        return self.n
+        # the clip's mel windows (inference.py:209-222: 997 for 40 s); only rank 0 holds the frames
+        return int(self.result.shape[0]) if self.result is not None else 0
 
     def step(self):
         from s2v_amd import pipeline
-        self.result = pipeline.run_sharded(self.pipe, *self.host, lambda s, e: self.src)
+        self.result = pipeline.run_sharded(self.pipe, *self.host, lambda s, e: self.src[: e - s])
         return self.result
 
 

@@ -131,14 +131,24 @@ class LipSyncPipeline:
 
 
 # ----------------------------------------------------------------------------- distributed helpers
+def _dist():
+    """(rank, world) of the default process group; (0, 1) when none is initialised (one GPU)."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
 def broadcast_tensor(t: torch.Tensor | None, shape, dtype, device, src: int = 0) -> torch.Tensor:
     """Broadcast a per-clip host tensor from ``src`` (RCCL on GPU, gloo on CPU)."""
     import torch.distributed as dist
-    if dist.get_rank() == src:
+    rank, world = _dist()
+    if rank == src:
         buf = t.to(device=device, dtype=dtype).contiguous()
     else:
         buf = torch.empty(shape, dtype=dtype, device=device)
-    dist.broadcast(buf, src)
+    if world > 1:
+        dist.broadcast(buf, src)
     return buf
 
 
@@ -146,7 +156,9 @@ def gather_frames(local: torch.Tensor, n_total: int, dst: int = 0):
     """Gather contiguous frame shards (shard_range layout) to ``dst``; returns [n_total, ...] on
     dst, None elsewhere.  Uses all_gather_into_tensor on equal, padded shards."""
     import torch.distributed as dist
-    world, rank = dist.get_world_size(), dist.get_rank()
+    rank, world = _dist()
+    if world == 1:
+        return local
     per = (n_total + world - 1) // world
     pad = torch.zeros((per,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
     pad[: local.shape[0]] = local
@@ -174,10 +186,11 @@ def run_sharded(pipeline: LipSyncPipeline, wav, semantic, expression, src_provid
     [n,3,256,256] on its device.  Returns the uint8 frames [n_chunks, 3, 384, 384] on rank 0."""
     import torch.distributed as dist
     dev = pipeline.device
-    rank = dist.get_rank()
+    rank, world = _dist()
     meta = torch.tensor([0 if wav is None else len(wav), 0 if semantic is None else semantic.shape[0]],
                         dtype=torch.int64, device=dev)
-    dist.broadcast(meta, 0)
+    if world > 1:
+        dist.broadcast(meta, 0)
     ns, nf = int(meta[0]), int(meta[1])
     wav_t = broadcast_tensor(None if rank else torch.as_tensor(wav), (ns,), torch.float32, dev)
     sem_t = broadcast_tensor(None if rank else torch.as_tensor(semantic), (nf, 262), torch.float32, dev)
@@ -185,7 +198,7 @@ def run_sharded(pipeline: LipSyncPipeline, wav, semantic, expression, src_provid
     mel = audio.melspectrogram(wav_t)
     chunks = audio.mel_chunks(mel, fps=fps)
     n = min(chunks.shape[0], nf)                       # inference.py:220-222 truncation
-    start, stop = shard_range(n, dist.get_rank(), dist.get_world_size())
+    start, stop = shard_range(n, rank, world)
     sem = sem_t.cpu().numpy()[:n]
     coeffs = torch.from_numpy(dnet_coefficients(sem, exp_t.cpu().numpy(), one_shot, start, stop)).to(dev)
     local = pipeline.run(chunks, src_provider(start, stop), coeffs, start, stop)
