@@ -262,6 +262,12 @@ int s2v_fir2d(const float *x, int n, int ih, int iw, int c, int xcs, const float
  * base_blocks.py:528-531): y[i] = BoxMuller(splitmix64(seed ^ splitmix64(offset + i))). */
 int s2v_gaussian_noise(float *y, long long n, unsigned long long seed, unsigned long long offset,
                        s2v_stream_t stream);
+/* Same with the offset advanced by (*ctr << shift), ctr a device counter read when the kernel runs,
+ * and the counter bump that goes with it (ctr[0] += inc): a captured HIP graph that bumps the counter
+ * and then draws draws fresh noise on every replay, like the reference's per-call normal_(). */
+int s2v_gaussian_noise_ctr(float *y, long long n, unsigned long long seed, unsigned long long offset,
+                           const unsigned long long *ctr, int shift, s2v_stream_t stream);
+int s2v_counter_add(unsigned long long *ctr, unsigned long long inc, s2v_stream_t stream);
 
 /* Full-clip pipeline glue.  DNet fake [n,3,h,w] in [-1,1] -> uint8 reference frames
  * (preprocessing/facing.py:190-191) and the ENet inputs built from them and the original crops src

@@ -10,7 +10,9 @@ import ctypes
 import os
 import threading
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libs2v.so")
+# S2V_LIB names an alternative in-tree build (kernel-variant experiments, tools/); the default is
+# the package's libs2v.so
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), os.environ.get("S2V_LIB", "libs2v.so"))
 
 ACT_NONE, ACT_RELU, ACT_LRELU, ACT_SIGMOID, ACT_TANH, ACT_GELU_TANH = range(6)
 IN_DIRECT, IN_NEAREST_UP2, IN_TRANSPOSED = range(3)
@@ -87,6 +89,8 @@ _SIGS = {
     "s2v_modulate_weights": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp, _c_int, _c_int,
                                       _vp, _vp]),
     "s2v_gaussian_noise": (_c_int, [_vp, _c_ll, ctypes.c_uint64, ctypes.c_uint64, _vp]),
+    "s2v_gaussian_noise_ctr": (_c_int, [_vp, _c_ll, ctypes.c_uint64, ctypes.c_uint64, _vp, _c_int, _vp]),
+    "s2v_counter_add": (_c_int, [_vp, ctypes.c_uint64, _vp]),
     "s2v_lipsync_inputs": (_c_int, [_vp, _vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp]),
     "s2v_to_u8": (_c_int, [_vp, _c_ll, _c_float, _c_float, _c_float, _c_float, _vp, _vp]),
     "s2v_eltwise": (_c_int, [_vp, _c_int, _vp, _c_int, _vp, _c_int, _vp, _c_ll, _c_int, _c_float, _c_int, _c_float,

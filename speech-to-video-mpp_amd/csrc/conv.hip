@@ -757,6 +757,20 @@ static int a_mode(const s2v_conv_params *p) {
     return 1;
 }
 
+// The split-precision kernels' A-operand mode: AMODE 0 becomes 4 (buffer loads, conv_x3_impl.hpp)
+// when the tile stages A wide (BM a multiple of 16 * waves), the filter has <= 32 taps and the x
+// slab / packed weights fit the 2^31-byte offsets.
+static long long x_extent_bytes(const s2v_conv_params *p) {
+    return ((long long)p->n * p->h * p->w - 1) * p->xcs * 4 + (long long)p->cin * 4;
+}
+
+static int x3_amode(const s2v_conv_params *p, const TileCfg &t) {
+    const int am = a_mode(p);
+    if (am != 0 || p->b_kn || p->kh * p->kw > 32 || t.bm % (16 * t.nw) != 0) return am;
+    if (x_extent_bytes(p) >= (1LL << 31) || (long long)p->npad * p->kpad * 4 >= (1LL << 31)) return am;
+    return 4;
+}
+
 }  // namespace s2v
 
 using namespace s2v;
@@ -797,7 +811,7 @@ extern "C" int s2v_conv2d_plan(const s2v_conv_params *p, int *out6) {
     }
     const TileCfg &t = tile_cfg(p, pl.tile);
     out6[0] = t.bm; out6[1] = t.bn; out6[2] = t.wm;
-    out6[3] = a_mode(p);
+    out6[3] = tiled_x3(p) ? x3_amode(p, t) : a_mode(p);
     out6[4] = p->b_kn != 0;
     out6[5] = pl.splits;
     out6[6] = tiled_x3(p) ? p->prec : 0;
@@ -856,8 +870,13 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
         a.cnt = p->tile_counters;                       // fold in the launch itself
     if (tiled_x3(p)) {
         if (!bkn) a.wt = (const float *)p->wt_x3;
-        if (p->prec == S2V_PREC_BF16X3) launch_conv_x3<0>(pl.tile, a, amode, bkn, grid, s);
-        else launch_conv_x3<1>(pl.tile, a, amode, bkn, grid, s);
+        const int am = x3_amode(p, t);
+        if (am == 4) {
+            a.x_bytes = (unsigned)x_extent_bytes(p);
+            a.w_bytes = (unsigned)((long long)p->npad * p->kpad * 4);
+        }
+        if (p->prec == S2V_PREC_BF16X3) launch_conv_x3<0>(pl.tile, a, am, bkn, grid, s);
+        else launch_conv_x3<1>(pl.tile, a, am, bkn, grid, s);
     } else switch (pl.tile) {
         case 0: launch_tile<128, 128, 2>(a, amode, bkn, grid, s); break;
         case 1: launch_tile<128, 64, 2>(a, amode, bkn, grid, s); break;

@@ -36,6 +36,7 @@ struct ConvArgs {
     int y_step, y_h, y_w;   // strided (polyphase) output, y_step > 1
     int *cnt;               // split-K tile counters (in-launch fold), or null
     float acc_scale;        // accumulator factor before the epilogue (1 / the split weights' pre-scale)
+    unsigned x_bytes, w_bytes;   // buffer-load extents of one batch slab of x / of the weights (AMODE 4)
 };
 
 // Element offset of output row m (flattened n, oy, ox) for channel 0.
@@ -311,22 +312,17 @@ __device__ __forceinline__ void load_b(const ConvArgs &a, const float *__restric
     }
 }
 
-// Epilogue of one BM x BN output tile held as 32x32 MFMA accumulators (C/D map: lane owns column
-// li of each tile, rows (r&3) + 8(r>>2) + 4 lh) by NW waves.  The tile is staged through LDS
-// (``Cs``, at least CH*(BN+4) floats) CH rows at a time with static indices, then every thread walks
-// the chunk row by row (consecutive threads -> consecutive output channels: coalesced stores).
-// Split-K launches write raw partial sums to the workspace instead.
-template <int BM, int BN, int WAVES_M, int TM, int TN, int NW = 4, int CH = BM>
-__device__ __forceinline__ void epilogue_tile(const ConvArgs &a, const floatx16 (&acc)[TM][TN], float *Cs, int tid,
-                                              int m0, int n0, int bz, int bidx) {
+// Epilogue of one BM x BN output tile.  The accumulators are staged through LDS (``Cs``, at least
+// CH*(BN+4) floats) CH rows at a time by ``stage(Cs, c0)`` (rows [c0, c0 + CH) of the tile, static
+// register indices), then every thread walks the chunk row by row (consecutive threads ->
+// consecutive output channels: coalesced stores).  Split-K launches write raw partial sums to the
+// workspace instead.
+template <int BM, int BN, int NW, int CH, class Stage>
+__device__ __forceinline__ void epilogue_tile_fn(const ConvArgs &a, float *Cs, int tid, int m0, int n0, int bz,
+                                                 int bidx, Stage stage) {
     constexpr int NT = 64 * NW;
-    constexpr int WAVES_N = NW / WAVES_M;
-    constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
     constexpr int LDC = BN + 4;
-    static_assert(CH % 32 == 0 && BM % CH == 0, "epilogue chunk");
-    const int lane = tid & 63, wave = tid >> 6;
-    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
-    const int li = lane & 31, lh = lane >> 5;
+    static_assert(CH % 16 == 0 && BM % CH == 0, "epilogue chunk");
     const Epi &e = a.epi;
     constexpr int TPR = BN < NT ? BN : NT;   // threads per tile row
     constexpr int RSTEP = NT / TPR;
@@ -341,16 +337,7 @@ __device__ __forceinline__ void epilogue_tile(const ConvArgs &a, const floatx16 
 #pragma unroll 1
     for (int c0 = 0; c0 < BM; c0 += CH) {
         __syncthreads();   // operand stages (first chunk) / the previous chunk are no longer read
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-            const int r0 = wm * WTM + i * 32 - c0;
-            if (r0 < 0 || r0 >= CH) continue;
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-#pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    Cs[(r0 + (r & 3) + 8 * (r >> 2) + 4 * lh) * LDC + wn * WTN + j * 32 + li] = acc[i][j][r] * a.acc_scale;
-        }
+        stage(Cs, c0);
         __syncthreads();
         const int clim = min(CH, mlim - c0);
         if (!live || clim <= 0) continue;
@@ -412,6 +399,31 @@ __device__ __forceinline__ void epilogue_tile(const ConvArgs &a, const floatx16 
             store_epilogue(a, bidx, (int)m, n, v);
         }
     }
+}
+
+// 32x32 MFMA accumulators (C/D map: lane owns column li of each tile, rows (r&3) + 8(r>>2) + 4 lh)
+// held by NW waves laid out WAVES_M x NW/WAVES_M
+template <int BM, int BN, int WAVES_M, int TM, int TN, int NW = 4, int CH = BM>
+__device__ __forceinline__ void epilogue_tile(const ConvArgs &a, const floatx16 (&acc)[TM][TN], float *Cs, int tid,
+                                              int m0, int n0, int bz, int bidx) {
+    constexpr int WAVES_N = NW / WAVES_M;
+    constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
+    constexpr int LDC = BN + 4;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+    const int li = lane & 31, lh = lane >> 5;
+    epilogue_tile_fn<BM, BN, NW, CH>(a, Cs, tid, m0, n0, bz, bidx, [&](float *C, int c0) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int r0 = wm * WTM + i * 32 - c0;
+            if (r0 < 0 || r0 >= CH) continue;
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    C[(r0 + (r & 3) + 8 * (r >> 2) + 4 * lh) * LDC + wn * WTN + j * 32 + li] = acc[i][j][r] * a.acc_scale;
+        }
+    });
 }
 
 }  // namespace s2v

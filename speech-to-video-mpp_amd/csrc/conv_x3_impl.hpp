@@ -60,16 +60,50 @@ __device__ __forceinline__ void unpack2(unsigned u, float &a, float &b) {
     }
 }
 
+// f16 residual pair: {f16(a - h.lo), f16(b - h.hi)} with one rounding each (v_fma_mix computes
+// -h + a exactly from the f16 source and rounds once): 2 VALU instead of unpack + subtract + pack
+__device__ __forceinline__ unsigned f16_residual2(unsigned h, float a, float b) {
+    unsigned r;
+    asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(a));
+    asm("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(r) : "v"(h), "v"(b));
+    return r;
+}
+
 // 4 fp32 -> 4 hi halves (8 bytes) + 4 lo halves (8 bytes)
 template <int ELT>
 __device__ __forceinline__ void split4(const f4 &v, u32x2 &hi, u32x2 &lo) {
     hi.x = pack2<ELT>(v.x, v.y);
     hi.y = pack2<ELT>(v.z, v.w);
-    float h0, h1, h2, h3;
-    unpack2<ELT>(hi.x, h0, h1);
-    unpack2<ELT>(hi.y, h2, h3);
-    lo.x = pack2<ELT>(v.x - h0, v.y - h1);
-    lo.y = pack2<ELT>(v.z - h2, v.w - h3);
+    if constexpr (ELT == 1) {
+        lo.x = f16_residual2(hi.x, v.x, v.y);
+        lo.y = f16_residual2(hi.y, v.z, v.w);
+    } else {
+        float h0, h1, h2, h3;
+        unpack2<ELT>(hi.x, h0, h1);
+        unpack2<ELT>(hi.y, h2, h3);
+        lo.x = pack2<ELT>(v.x - h0, v.y - h1);
+        lo.y = pack2<ELT>(v.z - h2, v.w - h3);
+    }
+}
+
+// Main-loop MFMA shape: 16x16x32 (default) or 32x32x16 (X3_MFMA16=0).  Same FLOP per cycle and
+// the same LDS reads per MFMA cycle; on MI355X the 16x16x32 loop holds a higher clock under load
+// (MI355X_MICROARCH.md, DVFS give-back item 7): 256x256 f16x3 372 -> 389 TFLOP/s, 128x128 291 -> 309
+// (tools/conv_micro.py, 16x200x200x256 3x3).
+#ifndef X3_MFMA16
+#define X3_MFMA16 1
+#endif
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+// one 16x16x32 MFMA on 16-byte fragments holding 8 halves of type ELT each
+template <int ELT>
+__device__ __forceinline__ floatx4 mfma16x16(const u32x4 &a, const u32x4 &b, const floatx4 &c) {
+    if constexpr (ELT == 0)
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b),
+                                                      c, 0, 0, 0);
+    else
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c,
+                                                     0, 0, 0);
 }
 
 // one 32x32x16 MFMA on 16-byte fragments holding 8 halves of type ELT each
@@ -207,8 +241,16 @@ constexpr int x3_chunk(int bm, int bn, int smem) {
 // Measured on MI355X (tools/conv_micro.py, r01): KS = 1, PF = 1 with 8 waves (two or more waves
 // per SIMD hide each other's load waits) beats deeper register prefetch (PF = 2 costs ~64 VGPRs and
 // drops to one wave per SIMD: -40 %) and BK = 64 stages (KS = 2: LDS for one block per CU: -40 %).
-template <int BM, int BN, int WAVES_M, int NW, int KS, int PF, int AMODE, int BKN, int ELT>
+// AMODE 4 is AMODE 0 (direct conv, zero padding, cin % 32 == 0, wide A staging) with buffer loads:
+// per A row a precomputed 32-bit offset and a mask of the filter taps that land inside the image
+// (out-of-image taps load from an offset past the buffer's extent, which returns zeros — no
+// branches, no zero fills), the tap / channel-slice offset a wave-uniform scalar; the B rows as
+// loop-invariant offsets plus a scalar K offset.  The host picks it when the x slab and the weights
+// fit 2^31 bytes and the filter has <= 32 taps.
+template <int BM, int BN, int WAVES_M, int NW, int KS, int PF, int AMODE_, int BKN, int ELT>
 __global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3(ConvArgs a) {
+    constexpr bool BUF = AMODE_ == 4;
+    constexpr int AMODE = BUF ? 0 : AMODE_;
     constexpr int NT = 64 * NW, RS = NT / 8;
     constexpr int WAVES_N = NW / WAVES_M;
     constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
@@ -267,18 +309,52 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3(ConvArgs a) {
         a_rows_init<AR, AMODE, RS>(a, m0, tid >> 3, R);
     }
     static_assert(!A8 || 2 * AR8 == AR, "wide A staging: same float4 count");
+    static_assert(!BUF || (A8 && !BKN), "buffer loads: wide A staging, packed B");
+
+    // buffer-load state (AMODE 4)
+    __amdgpu_buffer_rsrc_t xrs, wrs;
+    int rowoff[BUF ? AR8 : 1];
+    unsigned tmask[BUF ? AR8 : 1];
+    int boff[BUF ? BR : 1];
+    if constexpr (BUF) {
+        xrs = __builtin_amdgcn_make_buffer_rsrc((void *)x, 0, (int)a.x_bytes, 0x00020000);
+        wrs = __builtin_amdgcn_make_buffer_rsrc((void *)wtb, 0, (int)a.w_bytes, 0x00020000);
+#pragma unroll
+        for (int j = 0; j < AR8; ++j) {
+            rowoff[j] = (int)((R.base[j] + 8 * (tid & 3)) * 4);
+            unsigned m = 0;
+            if (R.ok[j])
+                for (int ky = 0; ky < a.kh; ++ky)
+                    for (int kx = 0; kx < a.kw; ++kx)
+                        if ((unsigned)(R.iy0[j] + ky * a.dh) < (unsigned)a.h &&
+                            (unsigned)(R.ix0[j] + kx * a.dw) < (unsigned)a.w)
+                            m |= 1u << (ky * a.kw + kx);
+            tmask[j] = m;
+        }
+#pragma unroll
+        for (int j = 0; j < BR; ++j) boff[j] = ((n0 + (tid >> 3) + RS * j) * a.kpad) * 4 + (tid & 7) * 16;
+    }
 
     f4 ra[PF][KS][AR];
     int rc[PF][KS];                  // A8: channel base of the staged slice (for the deferred prologue)
     u32x4 rbp[PF][KS][BKN ? 1 : BR];
     f4 rbk[PF][KS][BKN ? BKR : 1];
-    floatx16 acc[TM][TN];
+    constexpr bool M16 = X3_MFMA16;
+    constexpr int TM16 = WTM / 16, TN16 = WTN / 16;
+    floatx16 acc[M16 ? 1 : TM][M16 ? 1 : TN];
+    floatx4 acc4[M16 ? TM16 : 1][M16 ? TN16 : 1];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+            for (int r = 0; r < 16; ++r) if (!M16) acc[i][j][r] = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM16; ++i)
+#pragma unroll
+        for (int j = 0; j < TN16; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) if (M16) acc4[i][j][r] = 0.f;
 
     SliceIt ld;                      // the next K-slice to load
     ld.init(kt0, kperm, taps, nsl, a.kw);
@@ -288,7 +364,21 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3(ConvArgs a) {
 #pragma unroll
         for (int u = 0; u < KS; ++u) {
             const int kt = (AMODE == 0 || AMODE == 3) ? ld.kt(nsl) : ld.i;
-            if constexpr (A8) {
+            if constexpr (BUF) {
+                const int c8 = ld.cs * 32 + 8 * (tid & 3);
+                rc[p][u] = c8;
+                const int toff = ((ld.ky * a.dh * a.w + ld.kx * a.dw) * a.xcs + ld.cs * 32) * 4;
+#pragma unroll
+                for (int j = 0; j < AR8; ++j) {
+                    const int vo = ((tmask[j] >> ld.tap) & 1u) ? rowoff[j] + toff : (int)0x80000000;
+                    ra[p][u][2 * j] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(xrs, vo, 0, 0));
+                    ra[p][u][2 * j + 1] =
+                        __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(xrs, vo + 16, 0, 0));
+                }
+#pragma unroll
+                for (int j = 0; j < BR; ++j)
+                    rbp[p][u][j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wrs, boff[j], kt * 128, 0));
+            } else if constexpr (A8) {
                 f4 t0[AR8], t1[AR8];
                 const int c8 = ld.cs * 32 + 8 * (tid & 3);
                 rc[p][u] = c8;
@@ -305,7 +395,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3(ConvArgs a) {
                 load_a<AR, AMODE>(a, x, kt, ak, R, ra[p][u]);
             }
             if constexpr (BKN) load_b<BN, BKR, 1>(a, wtf, kt, n0, tid, rbk[p][u]);
-            else load_b_x3<BR, RS>(a, wtb, kt, n0, tid, rbp[p][u]);
+            else if constexpr (!BUF) load_b_x3<BR, RS>(a, wtb, kt, n0, tid, rbp[p][u]);
             if (ld.i < kt1 - 1) ld.next(kperm, taps, nsl, a.kw);
         }
     };
@@ -331,6 +421,9 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3(ConvArgs a) {
 
     const int li = lane & 31, lh = lane >> 5;
     const int rsw = swz(li);     // rows wm*WTM + i*32 + li share li's swizzle (tile bases are multiples of 32)
+    // 16x16x32 fragments: lane l reads row l & 15, hi slot l >> 4 (k 8(l>>4) .. +7) and its lo slot
+    const int l16 = lane & 15;
+    const int hs16 = ((lane >> 4) ^ swz(l16)) << 4, ls16 = hs16 ^ 64;
     // multiply ``nv`` (<= KS) slices of one stage
     auto compute = [&](const char *st, int nv) {
 #pragma unroll
@@ -338,6 +431,28 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3(ConvArgs a) {
             if (u >= nv) break;
             const char *As = st + u * SUB;
             const char *Bs = As + BM * 128;
+            if constexpr (M16) {
+                u32x4 bh[TN16], bl[TN16];
+#pragma unroll
+                for (int j = 0; j < TN16; ++j) {
+                    const char *p = Bs + (wn * WTN + j * 16 + l16) * 128;
+                    bh[j] = *(const u32x4 *)(p + hs16);
+                    bl[j] = *(const u32x4 *)(p + ls16);
+                }
+#pragma unroll
+                for (int i = 0; i < TM16; ++i) {
+                    const char *p = As + (wm * WTM + i * 16 + l16) * 128;
+                    const u32x4 ah = *(const u32x4 *)(p + hs16);
+                    const u32x4 al = *(const u32x4 *)(p + ls16);
+#pragma unroll
+                    for (int j = 0; j < TN16; ++j) {
+                        acc4[i][j] = mfma16x16<ELT>(al, bh[j], acc4[i][j]);
+                        acc4[i][j] = mfma16x16<ELT>(ah, bl[j], acc4[i][j]);
+                        acc4[i][j] = mfma16x16<ELT>(ah, bh[j], acc4[i][j]);
+                    }
+                }
+                continue;
+            }
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
                 const int hs = ((2 * s + lh) ^ rsw) << 4, ls = hs ^ 64;
@@ -418,7 +533,24 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3(ConvArgs a) {
             }
         }
     }
-    epilogue_tile<BM, BN, WAVES_M, TM, TN, NW, CH>(a, acc, (float *)smem, tid, m0, n0, bz, bidx);
+    if constexpr (M16) {
+        // stage the 16x16 accumulators (col = lane & 15, row = 4 (lane >> 4) + r) chunk by chunk
+        epilogue_tile_fn<BM, BN, NW, CH>(a, (float *)smem, tid, m0, n0, bz, bidx, [&](float *Cs, int c0) {
+            constexpr int LDC = BN + 4;
+#pragma unroll
+            for (int i = 0; i < TM16; ++i) {
+                const int r0 = wm * WTM + i * 16 - c0;
+                if (r0 < 0 || r0 >= CH) continue;
+#pragma unroll
+                for (int j = 0; j < TN16; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        Cs[(r0 + 4 * (lane >> 4) + r) * LDC + wn * WTN + j * 16 + l16] = acc4[i][j][r] * a.acc_scale;
+            }
+        });
+    } else {
+        epilogue_tile<BM, BN, WAVES_M, TM, TN, NW, CH>(a, acc, (float *)smem, tid, m0, n0, bz, bidx);
+    }
 }
 
 template <int BM, int BN, int WM, int NW, int KS, int PF, int ELT>
@@ -433,6 +565,9 @@ static void launch_x3(const ConvArgs &a, int amode, bool bkn, dim3 grid, hipStre
         return;
     }
     switch (amode) {
+        case 4:
+            if constexpr (BM % (16 * NW) == 0) conv_igemm_x3<BM, BN, WM, NW, KS, PF, 4, 0, ELT><<<grid, NT, 0, s>>>(a);
+            break;
         case 0: conv_igemm_x3<BM, BN, WM, NW, KS, PF, 0, 0, ELT><<<grid, NT, 0, s>>>(a); break;
         case 1: conv_igemm_x3<BM, BN, WM, NW, KS, PF, 1, 0, ELT><<<grid, NT, 0, s>>>(a); break;
         case 2: conv_igemm_x3<BM, BN, WM, NW, KS, PF, 2, 0, ELT><<<grid, NT, 0, s>>>(a); break;

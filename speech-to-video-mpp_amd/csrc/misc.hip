@@ -359,7 +359,9 @@ __device__ __forceinline__ unsigned long long splitmix64(unsigned long long z) {
 }
 
 __global__ __launch_bounds__(256) void gaussian_kernel(float *__restrict__ y, long long n, unsigned long long seed,
-                                                       unsigned long long offset) {
+                                                       unsigned long long offset, const unsigned long long *ctr,
+                                                       int shift) {
+    if (ctr) offset += *ctr << shift;          // device-side draw counter: fresh noise per graph replay
     for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
         const unsigned long long z = splitmix64(seed ^ splitmix64(offset + (unsigned long long)i));
         const float u1 = ((float)(z >> 40) + 0.5f) * (1.0f / 16777216.0f);
@@ -562,8 +564,26 @@ extern "C" int s2v_gaussian_noise(float *y, long long n, unsigned long long seed
                                   s2v_stream_t stream) {
     S2V_REQUIRE(y && n >= 0, "gaussian_noise: bad args");
     if (n == 0) return 0;
-    gaussian_kernel<<<grid_for(n), 256, 0, (hipStream_t)stream>>>(y, n, seed, offset);
+    gaussian_kernel<<<grid_for(n), 256, 0, (hipStream_t)stream>>>(y, n, seed, offset, nullptr, 0);
     return check_launch("gaussian_noise");
+}
+
+extern "C" int s2v_gaussian_noise_ctr(float *y, long long n, unsigned long long seed, unsigned long long offset,
+                                      const unsigned long long *ctr, int shift, s2v_stream_t stream) {
+    S2V_REQUIRE(y && ctr && n >= 0 && shift >= 0 && shift < 64, "gaussian_noise_ctr: bad args");
+    if (n == 0) return 0;
+    gaussian_kernel<<<grid_for(n), 256, 0, (hipStream_t)stream>>>(y, n, seed, offset, ctr, shift);
+    return check_launch("gaussian_noise_ctr");
+}
+
+__global__ void counter_add_kernel(unsigned long long *ctr, unsigned long long inc) {
+    if (threadIdx.x == 0) ctr[0] += inc;
+}
+
+extern "C" int s2v_counter_add(unsigned long long *ctr, unsigned long long inc, s2v_stream_t stream) {
+    S2V_REQUIRE(ctr && ((uintptr_t)ctr % 8) == 0, "counter_add: bad args");
+    counter_add_kernel<<<1, 64, 0, (hipStream_t)stream>>>(ctr, inc);
+    return check_launch("counter_add");
 }
 
 extern "C" int s2v_lipsync_inputs(const float *src, const float *fake, int n, int h, int w, unsigned char *ref_u8,

@@ -80,7 +80,7 @@ class ENetEngine:
         self.mod = ConvW(torch.cat(ws, 0), torch.cat(bs, 0), dev)
         self.mod_offs = offs
         self.noise_seed = 0x5EED
-        self.calls = 0
+        self.noise_ctr = ops.NoiseCounter()
 
     def style_code(self, ctx, ref: torch.Tensor):
         """ref: NCHW [B,3,H,W] device tensor -> style [B,1,1,512] (ENet.py:94-101)."""
@@ -130,7 +130,9 @@ class ENetEngine:
         cur = NHWC.empty(b, 100, 100, 4, dev)
         ops.pad_reflect(ctx, lo, cur, (2, 2, 2, 2))
         skip = cur.slice(0, 3)
-        self.calls += 1
+        ctr = None
+        if noises is None and any(L.noise_w for L in self.layers):
+            ctr = self.noise_ctr.bump(ctx)             # one draw per forward, also under graph replay
         for st in range(2):
             for li in range(2):
                 L = self.layers[3 * st + li]
@@ -148,7 +150,7 @@ class ENetEngine:
                         noise = noises[2 * st + li].contiguous()
                     else:
                         noise = torch.empty((b, x.h, x.w), device=dev)
-                        ops.gaussian_noise(ctx, noise, self.noise_seed, (self.calls << 40) + ((2 * st + li) << 36))
+                        ops.gaussian_noise(ctx, noise, self.noise_seed, (2 * st + li) << 36, ctr=ctr, shift=40)
                 ops.modulated_conv2d(ctx, x, L.conv, y, s2[:, off: off + L.cin], d, act=ops.ACT_LRELU, alpha=LRELU,
                                      pix_add=noise, pix_w=L.noise_w or 0.0)
                 cur = y

@@ -68,7 +68,8 @@ class GFPGANEngine:
             L.mod = ConvW(L.mod_w, L.mod_b, dev)
         self.noise_bufs = [sd[f"{d}noises.noise{i}"].float().reshape(-1).to(dev) for i in range(2 * nd + 1)]
         self._noise_cache = {}
-        self.noise_seed, self.calls = 0x6F9A, 0
+        self.noise_seed = 0x6F9A
+        self.noise_ctr = ops.NoiseCounter()
 
     def _stored_noise(self, b):
         """Stored noise buffers [1,1,H,W] broadcast over the batch (randomize_noise=False)."""
@@ -157,12 +158,12 @@ class GFPGANEngine:
         if noises is not None:
             noise = [None if t is None else t.reshape(b, -1).contiguous() for t in noises]
         elif randomize_noise:
-            self.calls += 1
+            ctr = self.noise_ctr.bump(ctx)                 # fresh draws per call, also under graph replay
             noise = []
             for j in range(nl):
                 r = 2 ** ((j + 5) // 2)
                 t = torch.empty((b, r * r), device=dev)
-                ops.gaussian_noise(ctx, t, self.noise_seed, (self.calls << 40) + (j << 34))
+                ops.gaussian_noise(ctx, t, self.noise_seed, j << 34, ctr=ctr, shift=40)
                 noise.append(t)
         else:
             noise = self._stored_noise(b)

@@ -574,10 +574,35 @@ def pad_cin(w: torch.Tensor, cin: int) -> torch.Tensor:
     return torch.cat([w, z], 1)
 
 
-def gaussian_noise(ctx: Ctx, out: torch.Tensor, seed: int, offset: int = 0):
-    check(ctx.lib.s2v_gaussian_noise(out.data_ptr(), out.numel(), seed & (2 ** 64 - 1), offset & (2 ** 64 - 1),
-                                     ctx.stream), "s2v_gaussian_noise")
+def gaussian_noise(ctx: Ctx, out: torch.Tensor, seed: int, offset: int = 0, ctr: torch.Tensor | None = None,
+                   shift: int = 40):
+    """N(0,1) into ``out``; with a device counter ``ctr`` (int64 [1]) the stream offset advances by
+    ctr << shift, read when the kernel runs (fresh draws on every graph replay)."""
+    if ctr is None:
+        check(ctx.lib.s2v_gaussian_noise(out.data_ptr(), out.numel(), seed & (2 ** 64 - 1), offset & (2 ** 64 - 1),
+                                         ctx.stream), "s2v_gaussian_noise")
+    else:
+        check(ctx.lib.s2v_gaussian_noise_ctr(out.data_ptr(), out.numel(), seed & (2 ** 64 - 1),
+                                             offset & (2 ** 64 - 1), ctr.data_ptr(), shift, ctx.stream),
+              "s2v_gaussian_noise_ctr")
     return out
+
+
+class NoiseCounter:
+    """Device-side draw counter of an engine's random noise (StyleConv / GFPGAN randomize_noise):
+    bumped by a kernel at the start of each forward, so a captured graph draws fresh noise per
+    replay.  Created on the first (eager) forward, never inside a capture."""
+
+    def __init__(self):
+        self.t = None
+
+    def bump(self, ctx: Ctx) -> torch.Tensor:
+        if self.t is None:
+            if torch.cuda.is_current_stream_capturing():
+                raise _lib.S2VError("noise counter must be created by an eager run before graph capture")
+            self.t = torch.zeros(1, dtype=torch.int64, device=ctx.device)
+        check(ctx.lib.s2v_counter_add(self.t.data_ptr(), 1, ctx.stream), "s2v_counter_add")
+        return self.t
 
 
 # ----------------------------------------------------------------------------- DFT matrices

@@ -33,7 +33,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--sweep", action="store_true")
     ap.add_argument("--splits", type=int, default=0)
-    ap.add_argument("--prec", default="both", choices=("f32", "bf16x3", "both"))
+    ap.add_argument("--prec", default="both", choices=("f32", "bf16x3", "f16x3", "both", "split"))
     ap.add_argument("--tiles", default="", help="comma list of force_tile values (101.. = x3 variants)")
     a = ap.parse_args()
     dev = torch.device("cuda")
@@ -46,7 +46,8 @@ def main():
     y = NHWC.empty(a.n, oh, ow, a.cout, dev)
     flops = 2.0 * a.n * oh * ow * a.k * a.k * a.cin * a.cout
     tiles = [int(t) for t in a.tiles.split(",")] if a.tiles else (range(1, 7) if a.sweep else [0])
-    for prec, t in [(p, t) for p in (("f32", "bf16x3") if a.prec == "both" else (a.prec,)) for t in tiles
+    precs = {"both": ("f32", "f16x3"), "split": ("bf16x3", "f16x3")}.get(a.prec, (a.prec,))
+    for prec, t in [(p, t) for p in precs for t in tiles
                     if not (t > 100 and p == "f32")]:
         ops.set_precision(prec)
         kw = dict(act=ops.ACT_LRELU, alpha=0.2, force_tile=t, force_splits=a.splits)
