@@ -111,6 +111,11 @@ typedef struct s2v_conv_params {
      * agent-scope release / acquire per split block costs more than the extra launch). */
     int *tile_counters; int n_counters;
     float wt_scale;
+    /* 2x2 average-pooled output (ResBlock 'down': lrelu(conv1) then F.interpolate(x0.5, bilinear) ==
+     * the mean of each 2x2 quad, base_blocks.py:40-49): y is [n][oh/2][ow/2] (pitch ycs) and holds
+     * 0.25 * sum of the four epilogue values (act included) of each quad.  oh, ow even; implicit-GEMM
+     * path only; no res / nc_scale / pix_add / strided output; one K split. */
+    int out_pool;
 } s2v_conv_params;
 
 enum { S2V_PREC_F32 = 0, S2V_PREC_BF16X3 = 1, S2V_PREC_F16X3 = 2 };
@@ -123,7 +128,7 @@ size_t s2v_conv2d_ws_bytes(const s2v_conv_params *p);
  * of the conv_igemm<BM,BN,WAVES_M,AVEC,B_KN> (prec 0) or
  * conv_igemm_x3<BM,BN,WAVES_M,NW,KS,PF,AVEC,B_KN,prec-1> (prec 1 / 2) instance, or
  * {0, CO, TPP, LW, 0, 1, 0, 0, 0, 0} for conv_small_cpar<CO,TPP,LW> (conv_direct_small<CO> when
- * TPP == 0), or {0, cout, -QPT, 0, 0, 1, ...} for conv_smallk<QPT>.  force_tile: 0 = planner,
+ * TPP == 0), or {0, cout, -QPT, PX, 0, 1, ...} for conv_smallk<QPT,PX>.  force_tile: 0 = planner,
  * 1..6 (f32) / 1..8 (split precisions) a fixed tile of the selected precision's table (tests / tuning). */
 int s2v_conv2d_plan(const s2v_conv_params *p, int *out10);
 

@@ -44,6 +44,7 @@ class ConvParams(ctypes.Structure):
         ("prec", _c_int), ("wt_x3", _vp),
         ("tile_counters", _vp), ("n_counters", _c_int),
         ("wt_scale", _c_float),
+        ("out_pool", _c_int),
     ]
 
 

@@ -212,19 +212,22 @@ __device__ __forceinline__ void store_epilogue4(const ConvArgs &a, int bidx, int
 }
 
 // Small-K direct convolution (K = kh*kw*cin <= 64: the 4-channel image-input layers and the
-// 4-channel StyleConv input): tppx threads per pixel, each QPT x 4 output channels; a block walks
-// iters x (256 / tppx) pixels of one batch entry with that entry's filter [K][cout] staged in LDS
-// once; one float4 of input per tap and channel group; fp32 VALU; 16-byte output stores.  These
-// layers are bound by their output write; the implicit GEMM pads K to 32 per slice and stages
-// every output tile through LDS (3-27 TFLOP/s measured on them).
-template <int QPT>
+// 4-channel StyleConv input): tppx threads per pixel group, each QPT x 4 output channels of PX
+// consecutive pixels (register blocking over pixels: every weight float4 read from LDS feeds PX
+// pixels, 1 LDS byte per FMA at PX = 4 instead of 4); a block walks iters x (256 / tppx) groups of
+// one batch entry with that entry's filter [K][cout] staged in LDS once; one float4 of input per
+// tap and channel group; fp32 VALU; 16-byte output stores.  These layers are bound by their
+// output write; the implicit GEMM pads K to 32 per slice and stages every output tile through LDS
+// (3-27 TFLOP/s measured on them).
+template <int QPT, int PX>
 __global__ __launch_bounds__(256) void conv_smallk(ConvArgs a, int batch, int tppx, int iters, int vec) {
     extern __shared__ __attribute__((aligned(16))) float wk[];   // [K][cout]
-    const int ppi = 256 / tppx;
-    const long long total = (long long)batch * a.M;
-    const long long g0 = (long long)blockIdx.x * ppi * iters;
+    const int gpb = 256 / tppx;
+    const long long total = (long long)batch * a.M;          // pixels (M % PX == 0: groups stay in one entry)
+    const long long g0 = (long long)blockIdx.x * gpb * iters;  // first pixel group of the block
     {
-        const int b0 = (int)((g0 < total ? g0 : 0) / a.M);
+        const long long p0 = g0 * PX;
+        const int b0 = (int)((p0 < total ? p0 : 0) / a.M);
         const float *w0 = a.wt + (long long)b0 * a.w_bs;
         for (int e = threadIdx.x; e < a.K * a.cout; e += 256) {
             const int k = e / a.cout, o = e - k * a.cout;
@@ -235,48 +238,73 @@ __global__ __launch_bounds__(256) void conv_smallk(ConvArgs a, int batch, int tp
     const int tq = threadIdx.x % tppx;
     const int hw = a.oh * a.ow;
     for (int it = 0; it < iters; ++it) {
-        const long long gid = g0 + (long long)it * ppi + threadIdx.x / tppx;
-        if (gid >= total) break;
-        const int bidx = (int)(gid / a.M);
-        const int m = (int)(gid - (long long)bidx * a.M);
-        const int img = m / hw, rem = m - img * hw;
-        const int oy = rem / a.ow, ox = rem - oy * a.ow;
+        const long long g = g0 + (long long)it * gpb + threadIdx.x / tppx;
+        if (g * PX >= total) break;
+        const int bidx = (int)(g * PX / a.M);
+        const int mbase = (int)(g * PX - (long long)bidx * a.M);
         const float *x = a.x + (long long)bidx * a.x_bs;
-        f4 acc[QPT];
+        int img[PX], oy[PX], ox[PX];
 #pragma unroll
-        for (int q = 0; q < QPT; ++q) acc[q] = f4{0.f, 0.f, 0.f, 0.f};
+        for (int p = 0; p < PX; ++p) {
+            const int m = mbase + p;
+            img[p] = m / hw;
+            const int rem = m - img[p] * hw;
+            oy[p] = rem / a.ow;
+            ox[p] = rem - oy[p] * a.ow;
+        }
+        f4 acc[PX][QPT];
+#pragma unroll
+        for (int p = 0; p < PX; ++p)
+#pragma unroll
+            for (int q = 0; q < QPT; ++q) acc[p][q] = f4{0.f, 0.f, 0.f, 0.f};
         for (int ky = 0; ky < a.kh; ++ky)
             for (int kx = 0; kx < a.kw; ++kx) {
-                int iy, ix;
-                if (!map_tap(a, oy, ox, ky, kx, iy, ix)) continue;
-                const float *px = x + ((long long)(img * a.h + iy) * a.w + ix) * a.xcs;
+                const float *px[PX];
+                bool ok[PX];
+#pragma unroll
+                for (int p = 0; p < PX; ++p) {
+                    int iy, ix;
+                    ok[p] = map_tap(a, oy[p], ox[p], ky, kx, iy, ix);
+                    px[p] = x + ((long long)(img[p] * a.h + (ok[p] ? iy : 0)) * a.w + (ok[p] ? ix : 0)) * a.xcs;
+                }
                 const int kb = (ky * a.kw + kx) * a.cin;
                 for (int c = 0; c < a.cin; c += 4) {
-                    f4 v = *(const f4 *)(px + c);
-                    if (a.in_scale) v *= *(const f4 *)(a.in_scale + (long long)img * a.in_scale_ns + c);
-                    if (a.pre_act) {
-                        v.x = apply_act(v.x, a.pre_act, a.pre_alpha);
-                        v.y = apply_act(v.y, a.pre_act, a.pre_alpha);
-                        v.z = apply_act(v.z, a.pre_act, a.pre_alpha);
-                        v.w = apply_act(v.w, a.pre_act, a.pre_alpha);
+                    f4 v[PX];
+#pragma unroll
+                    for (int p = 0; p < PX; ++p) {
+                        v[p] = ok[p] ? *(const f4 *)(px[p] + c) : f4{0.f, 0.f, 0.f, 0.f};
+                        if (a.in_scale) v[p] *= *(const f4 *)(a.in_scale + (long long)img[p] * a.in_scale_ns + c);
+                        if (a.pre_act) {
+                            v[p].x = apply_act(v[p].x, a.pre_act, a.pre_alpha);
+                            v[p].y = apply_act(v[p].y, a.pre_act, a.pre_alpha);
+                            v[p].z = apply_act(v[p].z, a.pre_act, a.pre_alpha);
+                            v[p].w = apply_act(v[p].w, a.pre_act, a.pre_alpha);
+                        }
+                        if (!ok[p]) v[p] = f4{0.f, 0.f, 0.f, 0.f};   // zero padding stays zero after the prologue
                     }
-                    const float vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
                         const float *wr = wk + (kb + c + e) * a.cout + 4 * tq;
 #pragma unroll
                         for (int q = 0; q < QPT; ++q) {
                             const f4 w4 = *(const f4 *)(wr + 4 * tppx * q);
-                            acc[q].x = fmaf(vv[e], w4.x, acc[q].x);
-                            acc[q].y = fmaf(vv[e], w4.y, acc[q].y);
-                            acc[q].z = fmaf(vv[e], w4.z, acc[q].z);
-                            acc[q].w = fmaf(vv[e], w4.w, acc[q].w);
+#pragma unroll
+                            for (int p = 0; p < PX; ++p) {
+                                const float ve = e == 0 ? v[p].x : e == 1 ? v[p].y : e == 2 ? v[p].z : v[p].w;
+                                acc[p][q].x = fmaf(ve, w4.x, acc[p][q].x);
+                                acc[p][q].y = fmaf(ve, w4.y, acc[p][q].y);
+                                acc[p][q].z = fmaf(ve, w4.z, acc[p][q].z);
+                                acc[p][q].w = fmaf(ve, w4.w, acc[p][q].w);
+                            }
                         }
                     }
                 }
             }
 #pragma unroll
-        for (int q = 0; q < QPT; ++q) store_epilogue4(a, bidx, m, 4 * (tq + tppx * q), acc[q], vec != 0);
+        for (int p = 0; p < PX; ++p)
+#pragma unroll
+            for (int q = 0; q < QPT; ++q)
+                store_epilogue4(a, bidx, mbase + p, 4 * (tq + tppx * q), acc[p][q], vec != 0);
     }
 }
 
@@ -493,25 +521,31 @@ static bool vec4_input(const s2v_conv_params *p) {
            (!p->in_scale || (p->in_scale_ns % 4 == 0 && ((uintptr_t)p->in_scale % 16) == 0));
 }
 
+static int smallk_px(int M);
+
 // conv_smallk geometry: threads per pixel (cout / 4 channel quads, at most 64) and quads per thread
 static bool smallk_cfg(const s2v_conv_params *p, int M, int K, int &tppx, int &qpt) {
-    if (p->b_kn || p->force_tile || p->cout < 8 || (p->cout & 3) || K > 64 || !vec4_input(p)) return false;
+    if (p->b_kn || p->force_tile || p->out_pool || p->cout < 8 || (p->cout & 3) || K > 64 || !vec4_input(p)) return false;
     const int quads = p->cout / 4;
     if (quads & (quads - 1)) return false;                       // power of two
     tppx = quads < 64 ? quads : 64;
     qpt = quads / tppx;
     if (qpt > 2 || (size_t)K * p->cout * sizeof(float) > 64 * 1024) return false;
     const int batch = p->batch > 0 ? p->batch : 1;
-    return p->w_bs == 0 || batch == 1 || M % (256 / tppx) == 0;
+    return p->w_bs == 0 || batch == 1 || (M / smallk_px(M)) % (256 / tppx) == 0;
 }
 
-// pixels per block = iters x (256 / tppx): up to 16 iterations, and a divisor of M when each
+// pixels per thread group: 4 when M % 4 == 0 (register blocking over pixels), else 1
+static int smallk_px(int M) { return M % 4 == 0 ? 4 : 1; }
+
+// groups per block = iters x (256 / tppx): up to 16 iterations, and a divisor of M / px when each
 // batch entry has its own weights (a block never straddles two entries)
 static int smallk_iters(const s2v_conv_params *p, int M, int tppx) {
     const int batch = p->batch > 0 ? p->batch : 1;
     const bool per_entry = p->w_bs != 0 && batch > 1;
+    const int px = smallk_px(M);
     int it = 16;
-    while (it > 1 && per_entry && M % (it * (256 / tppx)) != 0) it /= 2;
+    while (it > 1 && per_entry && (M / px) % (it * (256 / tppx)) != 0) it /= 2;
     return it;
 }
 
@@ -591,7 +625,10 @@ static Plan make_plan_x3(const s2v_conv_params *p, int M, Plan pl) {
     return pl;
 }
 
-static Plan make_plan(const s2v_conv_params *p, int M, int K) {
+static Plan make_plan(const s2v_conv_params *p_in, int M, int K) {
+    s2v_conv_params q = *p_in;
+    if (q.out_pool) q.force_splits = 1;          // the pooled epilogue needs whole-K tiles
+    const s2v_conv_params *p = &q;
     Plan pl{};
     pl.ktiles = (K + 31) / 32;
     if (use_direct(p) && !p->force_tile) {
@@ -698,6 +735,12 @@ static int validate(const s2v_conv_params *p, int &M, int &K) {
         S2V_REQUIRE(uses_x3(p) || ((uintptr_t)p->wt % 16) == 0, "conv2d: weights must be 16B aligned");
     }
     if (p->res) S2V_REQUIRE(p->res_cs >= p->cout, "conv2d: res_cs < cout");
+    if (p->out_pool) {
+        S2V_REQUIRE(p->oh % 2 == 0 && p->ow % 2 == 0, "conv2d: out_pool needs even output sizes");
+        S2V_REQUIRE(!p->res && !p->nc_scale && !p->pix_add && p->out_step <= 1 && p->force_splits <= 1,
+                    "conv2d: out_pool takes no res / nc_scale / pix_add / strided output / K split");
+        S2V_REQUIRE(!(use_direct(p) && !p->force_tile) && !is_smallk(p), "conv2d: out_pool needs the implicit-GEMM path");
+    }
     if (p->out_step > 1) {
         S2V_REQUIRE(!p->pix_add, "conv2d: strided output cannot take pix_add");
         S2V_REQUIRE(!p->res || (p->res == p->y && p->res_cs == p->ycs && p->res_oy == 0 && p->res_ox == 0),
@@ -729,6 +772,7 @@ static ConvArgs make_args(const s2v_conv_params *p, int M, int K, const Plan &pl
     a.y_step = p->out_step > 1 ? p->out_step : 1; a.y_h = p->out_full_h; a.y_w = p->out_full_w;
     a.cnt = nullptr;
     a.acc_scale = (tiled_x3(p) && !p->b_kn && p->wt_scale > 0.f) ? 1.f / p->wt_scale : 1.f;
+    a.pool = p->out_pool != 0;
     return a;
 }
 
@@ -794,7 +838,7 @@ extern "C" int s2v_conv2d_plan(const s2v_conv_params *p, int *out6) {
         int tppx, qpt;
         smallk_cfg(p, M, K, tppx, qpt);
         out6[0] = 0; out6[1] = p->cout; out6[2] = -qpt;
-        out6[3] = 0; out6[4] = 0; out6[5] = 1;
+        out6[3] = smallk_px(M); out6[4] = 0; out6[5] = 1;
         return 0;
     }
     if (pl.tile < 0) {
@@ -831,14 +875,20 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
         int tppx, qpt;
         smallk_cfg(p, M, K, tppx, qpt);
         const int iters = smallk_iters(p, M, tppx);
-        const long long total = (long long)batch * M;
-        const unsigned grid = cdiv(total, (256 / tppx) * iters);
+        const int px = smallk_px(M);
+        const long long groups = (long long)batch * M / px;
+        const unsigned grid = cdiv(groups, (256 / tppx) * iters);
         const size_t lds = (size_t)K * p->cout * sizeof(float);
         const int vec = p->ycs % 4 == 0 && ((uintptr_t)p->y % 16) == 0 && p->y_bs % 4 == 0 &&
                         (!p->res || (p->res_cs % 4 == 0 && ((uintptr_t)p->res % 16) == 0 && p->res_bs % 4 == 0)) &&
                         (!p->scale || ((uintptr_t)p->scale % 16) == 0) && (!p->shift || ((uintptr_t)p->shift % 16) == 0);
-        if (qpt == 1) conv_smallk<1><<<grid, 256, lds, s>>>(a, batch, tppx, iters, vec);
-        else conv_smallk<2><<<grid, 256, lds, s>>>(a, batch, tppx, iters, vec);
+        if (px == 4) {
+            if (qpt == 1) conv_smallk<1, 4><<<grid, 256, lds, s>>>(a, batch, tppx, iters, vec);
+            else conv_smallk<2, 4><<<grid, 256, lds, s>>>(a, batch, tppx, iters, vec);
+        } else {
+            if (qpt == 1) conv_smallk<1, 1><<<grid, 256, lds, s>>>(a, batch, tppx, iters, vec);
+            else conv_smallk<2, 1><<<grid, 256, lds, s>>>(a, batch, tppx, iters, vec);
+        }
         return check_launch("conv_smallk");
     }
     if (pl.tile < 0) {

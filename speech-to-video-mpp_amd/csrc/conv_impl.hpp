@@ -37,6 +37,8 @@ struct ConvArgs {
     int *cnt;               // split-K tile counters (in-launch fold), or null
     float acc_scale;        // accumulator factor before the epilogue (1 / the split weights' pre-scale)
     unsigned x_bytes, w_bytes;   // buffer-load extents of one batch slab of x / of the weights (AMODE 4)
+    int pool;               // 2x2 average-pooled output: M runs over 2x2 output quads (quad-major),
+                            // the epilogue writes act(v) averaged over each quad to pixel m / 4
 };
 
 // Element offset of output row m (flattened n, oy, ox) for channel 0.
@@ -144,10 +146,20 @@ __device__ __forceinline__ void a_rows_init_at(const ConvArgs &a, int m0, const 
         const int m = m0 + rows[j];
         R.ok[j] = m < a.M;
         const int mm = R.ok[j] ? m : 0;
-        const int img = mm / hw;
-        const int rem = mm - img * hw;
-        const int oy = rem / a.ow;
-        const int ox = rem - oy * a.ow;
+        int img, oy, ox;
+        if (a.pool) {       // quad-major order: m = 4 * pooled pixel + (dy * 2 + dx)
+            const int q = mm >> 2, hq = hw >> 2, wq = a.ow >> 1;
+            img = q / hq;
+            const int rq = q - img * hq;
+            const int qy = rq / wq;
+            oy = 2 * qy + ((mm >> 1) & 1);
+            ox = 2 * (rq - qy * wq) + (mm & 1);
+        } else {
+            img = mm / hw;
+            const int rem = mm - img * hw;
+            oy = rem / a.ow;
+            ox = rem - oy * a.ow;
+        }
         R.img[j] = img;
         R.oy[j] = oy;
         R.ox[j] = ox;
@@ -341,6 +353,19 @@ __device__ __forceinline__ void epilogue_tile_fn(const ConvArgs &a, float *Cs, i
         __syncthreads();
         const int clim = min(CH, mlim - c0);
         if (!live || clim <= 0) continue;
+        if (a.pool) {
+            // 2x2 average of the activated outputs (ResBlock: lrelu(conv1) then bilinear x0.5 ==
+            // the quad mean, base_blocks.py:40-49); rows 4r..4r+3 of the chunk are one quad
+            float *__restrict__ yb = a.y + (long long)bidx * a.y_bs + n;
+#pragma unroll 1
+            for (int rq = tid / TPR; 4 * rq < clim; rq += RSTEP) {
+                float v = 0.f;
+#pragma unroll
+                for (int d = 0; d < 4; ++d) v += fast_act(Cs[(4 * rq + d) * LDC + cn] * sc + sh, e.act, slope);
+                yb[(long long)((m0 + c0) / 4 + rq) * a.ycs] = 0.25f * v;
+            }
+            continue;
+        }
         if (a.splits > 1) {
             float *w = a.ws + (long long)bz * a.M * a.cout;
 #pragma unroll 1
@@ -349,8 +374,28 @@ __device__ __forceinline__ void epilogue_tile_fn(const ConvArgs &a, float *Cs, i
         } else if (simple) {
             float *__restrict__ yb = a.y + (long long)bidx * a.y_bs + n;
             const float *rsrc = e.res ? e.res + (long long)bidx * a.res_bs + n : nullptr;
+            int rr0 = tid / TPR;
+            if (rsrc && a.y_step <= 1) {
+                // residual rows: four loads in flight before their adds (a dependent load per
+                // row left the store loop latency-bound)
 #pragma unroll 1
-            for (int rr = tid / TPR; rr < clim; rr += RSTEP) {
+                for (; rr0 + 3 * RSTEP < clim; rr0 += 4 * RSTEP) {
+                    float rv[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) rv[q] = rsrc[(long long)(m0 + c0 + rr0 + q * RSTEP) * e.res_cs];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const long long m = m0 + c0 + rr0 + q * RSTEP;
+                        float v = Cs[(rr0 + q * RSTEP) * LDC + cn] * sc + sh;
+                        if (!e.res_after) v += rv[q];
+                        v = fast_act(v, e.act, slope);
+                        if (e.res_after) v += rv[q];
+                        yb[m * a.ycs] = v;
+                    }
+                }
+            }
+#pragma unroll 1
+            for (int rr = rr0; rr < clim; rr += RSTEP) {
                 const long long m = m0 + c0 + rr;
                 float v = Cs[rr * LDC + cn] * sc + sh;
                 float rv = 0.f;

@@ -53,9 +53,13 @@ class ENetEngine:
         self.down = []
         for i in range(6):
             p = f"conv_body_down.{i}."
+            # skip(interpolate(x, 0.5)) == a 2x2 stride-2 conv with the 1x1 weights / 4 on every tap
+            # (bilinear x0.5 is the 2x2 mean and commutes with the 1x1 conv): no pooled copy of x
+            sw = sd[p + "skip.weight"].float()
+            skip2 = (sw / 4.0).expand(-1, -1, 2, 2).contiguous()
             self.down.append((ConvW(sd[p + "conv1.weight"], sd[p + "conv1.bias"], dev, padding=1),
                               ConvW(sd[p + "conv2.weight"], sd[p + "conv2.bias"], dev, padding=1),
-                              ConvW(sd[p + "skip.weight"], None, dev)))
+                              ConvW(skip2, None, dev, stride=2)))
         self.final_conv = ConvW(sd["final_conv.weight"], sd["final_conv.bias"], dev, padding=1)
         # final_linear consumes feat.reshape(B, -1) in NCHW (c, h, w) order; our feature is NHWC
         # (h, w, c): permute the weight columns once.
@@ -92,14 +96,10 @@ class ENetEngine:
         ops.conv2d(ctx, x, self.first, f, act=ops.ACT_LRELU, alpha=LRELU)
         for c1, c2, sk in self.down:                                # ResBlock(mode='down'), base_blocks.py:40-49
             h, w = f.h, f.w
-            t = NHWC.empty(b, h, w, c1.cout, dev)
-            ops.conv2d(ctx, f, c1, t, act=ops.ACT_LRELU, alpha=LRELU)
-            td = NHWC.empty(b, h // 2, w // 2, c1.cout, dev)
-            ops.resize_nhwc(ctx, t, td, scale_factor=0.5)
-            fd = NHWC.empty(b, h // 2, w // 2, f.c, dev)
-            ops.resize_nhwc(ctx, f, fd, scale_factor=0.5)
+            td = NHWC.empty(b, h // 2, w // 2, c1.cout, dev)         # interpolate(lrelu(conv1(x)), 0.5):
+            ops.conv2d(ctx, f, c1, td, act=ops.ACT_LRELU, alpha=LRELU, pool=True)   # pooled in the epilogue
             out = NHWC.empty(b, h // 2, w // 2, c2.cout, dev)
-            ops.conv2d(ctx, fd, sk, out)                            # skip(x_down)
+            ops.conv2d(ctx, f, sk, out)                             # skip(interpolate(x, 0.5))
             ops.conv2d(ctx, td, c2, out, act=ops.ACT_LRELU, alpha=LRELU, res=out, res_after=True)
             f = out
         g = NHWC.empty(b, f.h, f.w, self.final_conv.cout, dev)

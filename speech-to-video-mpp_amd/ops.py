@@ -258,9 +258,10 @@ def _ptr(t):
 
 def conv2d(ctx: Ctx, x: NHWC, cw: ConvW, y: NHWC, *, act=ACT_NONE, alpha=0.0, res: NHWC | None = None,
            res_after=False, res_offset=(0, 0), nc_scale=None, in_scale=None, pre_act=ACT_NONE, pre_alpha=0.0,
-           pix_add=None, pix_w=0.0, scale=None, shift=None, force_tile=0, force_splits=0):
+           pix_add=None, pix_w=0.0, scale=None, shift=None, force_tile=0, force_splits=0, pool=False):
     """Fused conv (see s2v_conv_params).  nc_scale / in_scale: [N, C] device tensors.  A transposed
-    ConvW with a polyphase plan (``cw.poly``) runs as one stride-1 conv per output parity class."""
+    ConvW with a polyphase plan (``cw.poly``) runs as one stride-1 conv per output parity class.
+    ``pool``: y is the 2x2 average pool of the activated conv output (half the conv's size)."""
     if getattr(cw, "poly", None) is not None:
         assert pix_add is None, "polyphase transposed conv: no pix_add epilogue"
         assert res is None or (res.t.data_ptr() == y.t.data_ptr() and res.coff == y.coff and not res_after), \
@@ -279,13 +280,15 @@ def conv2d(ctx: Ctx, x: NHWC, cw: ConvW, y: NHWC, *, act=ACT_NONE, alpha=0.0, re
         return y
     oh, ow = cw.out_hw(x.h, x.w)
     assert x.c == cw.cin, f"conv: input has {x.c} channels, weights expect {cw.cin}"
-    assert (y.n, y.h, y.w, y.c) == (x.n, oh, ow, cw.cout), f"conv: output view {(y.n, y.h, y.w, y.c)} != {(x.n, oh, ow, cw.cout)}"
+    f = 2 if pool else 1
+    assert (y.n, y.h * f, y.w * f, y.c) == (x.n, oh, ow, cw.cout), \
+        f"conv: output view {(y.n, y.h, y.w, y.c)} != {(x.n, oh // f, ow // f, cw.cout)}"
     return _conv(ctx, x, cw, y, (oh, ow), None, act, alpha, res, res_after, res_offset, nc_scale, in_scale, pre_act,
-                 pre_alpha, pix_add, pix_w, scale, shift, force_tile, force_splits)
+                 pre_alpha, pix_add, pix_w, scale, shift, force_tile, force_splits, pool=pool)
 
 
 def _conv(ctx, x, cw, y, ohw, out_view, act, alpha, res, res_after, res_offset, nc_scale, in_scale, pre_act,
-          pre_alpha, pix_add, pix_w, scale, shift, force_tile, force_splits, per_sample_wt=None):
+          pre_alpha, pix_add, pix_w, scale, shift, force_tile, force_splits, per_sample_wt=None, pool=False):
     oh, ow = ohw
     p = _lib.ConvParams()
     p.x, p.n, p.h, p.w, p.cin, p.xcs = x.ptr, x.n, x.h, x.w, x.c, x.cs
@@ -310,13 +313,14 @@ def _conv(ctx, x, cw, y, ohw, out_view, act, alpha, res, res_after, res_offset, 
     p.act, p.alpha = act, alpha
     p.batch = 1
     p.force_tile, p.force_splits = force_tile, force_splits
+    p.out_pool = int(pool)
     if out_view is not None:
         p.out_step, p.out_full_h, p.out_full_w = out_view
     if per_sample_wt is not None:        # batch mode: one image per batch entry, its own weights
         assert in_scale is None and nc_scale is None and out_view is None
         p.n, p.batch = 1, x.n
         p.w_bs = cw.npad * cw.kpad
-        p.x_bs, p.y_bs = x.h * x.w * x.cs, oh * ow * y.cs
+        p.x_bs, p.y_bs = x.h * x.w * x.cs, y.h * y.w * y.cs
         if res is not None:
             p.res_bs = res.h * res.w * res.cs
     use_x3 = False
@@ -428,7 +432,7 @@ def conv_symbol(ctx: Ctx, p) -> str:
     bm, bn, wm, avec, bkn, splits, x3, nw, ks, pf = _plan(ctx, p)
     if bm == 0:
         if wm < 0:
-            return f"void s2v::conv_smallk<{-wm}>(s2v::ConvArgs, int, int, int, int)"
+            return f"void s2v::conv_smallk<{-wm}, {avec}>(s2v::ConvArgs, int, int, int, int)"
         if wm:
             return f"void s2v::conv_small_cpar<{bn}, {wm}, {'true' if avec else 'false'}>(s2v::ConvArgs, int)"
         return f"void s2v::conv_direct_small<{bn}>(s2v::ConvArgs, int)"

@@ -544,3 +544,37 @@ def test_f16x3_operand_range(ctx, mag):
         assert (err <= REL["f16x3"] * bound + 1e-12).all(), f"max rel {(err / (bound + 1e-30)).max():.3e}"
     finally:
         ops.set_precision(prev)
+
+
+@pytest.mark.parametrize("n,cin,h,w,cout,tile", [(2, 64, 12, 16, 96, 0), (2, 32, 8, 8, 64, 5), (1, 256, 16, 16, 256, 1),
+                                                 (3, 4, 10, 6, 40, 0), (2, 64, 6, 10, 48, 8)])
+def test_conv2d_pooled_epilogue(ctx, prec, n, cin, h, w, cout, tile):
+    """out_pool: the 2x2 mean of lrelu(conv + b) (ResBlock conv1 + bilinear x0.5, base_blocks.py:40-49)
+    written at half size; M runs over 2x2 quads, so every tile holds whole quads."""
+    if tile > 6 and prec == "f32":
+        pytest.skip("tiles 7-8 exist in the split-precision table only")
+    wt = rnd(cout, cin, 3, 3, seed=61) / math.sqrt(cin * 9)
+    bias = rnd(cout, seed=62)
+    x = rnd(n, cin, h, w, seed=63)
+    cw = ConvW(wt.float(), bias.float(), DEV, padding=1)
+    y = NHWC.empty(n, h // 2, w // 2, cout + 3, DEV).slice(1, cout)
+    ops.conv2d(ctx, nhwc(x.float()), cw, y, act=ops.ACT_LRELU, alpha=0.2, pool=True, force_tile=tile)
+    full = F.leaky_relu(F.conv2d(x, wt, bias, 1, 1), 0.2)
+    ref = F.interpolate(full, scale_factor=0.5, mode="bilinear", align_corners=False)
+    bound = F.avg_pool2d(conv_bound(x, wt, 1, 1, 1), 2)
+    err = (to_nchw(y) - ref).abs()
+    assert (err <= REL[prec] * (bound + 1) + 1e-6).all(), f"max err {err.max():.3e}"
+
+
+def test_resblock_skip_as_strided_conv(ctx, prec):
+    """skip(interpolate(x, 0.5)) of a 1x1 conv == a 2x2 stride-2 conv with W / 4 on each tap
+    (engine/enet.py): against the reference order of operations."""
+    n, cin, h, w, cout = 2, 64, 12, 10, 96
+    wt = rnd(cout, cin, 1, 1, seed=64) / math.sqrt(cin)
+    x = rnd(n, cin, h, w, seed=65)
+    cw = ConvW((wt.float() / 4).expand(-1, -1, 2, 2).contiguous(), None, DEV, stride=2)
+    y = NHWC.empty(n, h // 2, w // 2, cout, DEV)
+    ops.conv2d(ctx, nhwc(x.float()), cw, y)
+    ref = F.conv2d(F.interpolate(x, scale_factor=0.5, mode="bilinear", align_corners=False), wt)
+    bound = F.conv2d(F.avg_pool2d(x.abs(), 2), wt.abs())
+    assert ((to_nchw(y) - ref).abs() <= REL[prec] * (bound + 1) + 1e-6).all()
