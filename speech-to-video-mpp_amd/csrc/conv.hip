@@ -501,9 +501,9 @@ struct X3Cfg {
     int bpc;
 };
 static const X3Cfg kX3Tiles[] = {
-    {{256, 256, 2, 8, 1, 1}, 365.f, 1}, {{128, 128, 2, 8, 1, 1}, 295.f, 2}, {{64, 128, 2, 8, 1, 1}, 255.f, 3},
-    {{128, 64, 2, 4, 1, 1}, 230.f, 3},  {{64, 64, 2, 4, 1, 1}, 200.f, 4},   {{128, 32, 4, 4, 1, 1}, 150.f, 4},
-    {{256, 128, 4, 8, 1, 1}, 285.f, 1}, {{256, 64, 8, 8, 1, 1}, 250.f, 2}};
+    {{256, 256, 2, 8, 1, 1}, 400.f, 1}, {{128, 128, 2, 8, 1, 1}, 330.f, 2}, {{64, 128, 2, 8, 1, 1}, 260.f, 3},
+    {{128, 64, 2, 4, 1, 1}, 290.f, 3},  {{64, 64, 2, 4, 1, 1}, 265.f, 4},   {{128, 32, 4, 4, 1, 1}, 235.f, 4},
+    {{256, 128, 4, 8, 1, 1}, 335.f, 1}, {{256, 64, 8, 8, 1, 1}, 300.f, 2},  {{512, 128, 4, 8, 1, 1}, 330.f, 1}};
 constexpr int kNumX3 = sizeof(kX3Tiles) / sizeof(kX3Tiles[0]);
 
 static const TileCfg &tile_cfg(const s2v_conv_params *p, int tile);
@@ -528,6 +528,8 @@ static bool smallk_cfg(const s2v_conv_params *p, int M, int K, int &tppx, int &q
     if (p->b_kn || p->force_tile || p->out_pool || p->cout < 8 || (p->cout & 3) || K > 64 || !vec4_input(p)) return false;
     const int quads = p->cout / 4;
     if (quads & (quads - 1)) return false;                       // power of two
+    // one output quad per thread, up to 64 threads per pixel (measured on MI355X: 64 lanes x 1 quad
+    // beat 4 lanes x 16 quads and 4-pixel register blocking on the 256-channel image layers, r02)
     tppx = quads < 64 ? quads : 64;
     qpt = quads / tppx;
     if (qpt > 2 || (size_t)K * p->cout * sizeof(float) > 64 * 1024) return false;
@@ -536,7 +538,7 @@ static bool smallk_cfg(const s2v_conv_params *p, int M, int K, int &tppx, int &q
 }
 
 // pixels per thread group: 4 when M % 4 == 0 (register blocking over pixels), else 1
-static int smallk_px(int M) { return M % 4 == 0 ? 4 : 1; }
+static int smallk_px(int M) { (void)M; return 1; }
 
 // groups per block = iters x (256 / tppx): up to 16 iterations, and a divisor of M / px when each
 // batch entry has its own weights (a block never straddles two entries)
@@ -600,7 +602,7 @@ static Plan make_plan_x3(const s2v_conv_params *p, int M, Plan pl) {
     for (int i = 0; i < kNumX3; ++i) {
         const X3Cfg &c = kX3Tiles[i];
         if (p->b_kn && c.t.nw != 4) continue;
-        if (c.t.bm == 256 && c.t.bn == 256 && am != 0 && am != 3) continue;   // generic gathers spill there
+        if (c.t.bm >= 256 && c.t.bn >= 128 && am != 0 && am != 3) continue;   // generic gathers spill there
         if (c.t.bm == 256 && c.t.bn == 64 && am != 0) continue;   // measured slower than 128x64 on per-row gathers
         if (!p->b_kn && (long long)cdiv(p->cout, c.t.bn) * c.t.bn > p->npad) continue;   // weight rows
         const long long tiles = (long long)cdiv(M, c.t.bm) * cdiv(p->cout, c.t.bn) * batch;
@@ -882,13 +884,8 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
         const int vec = p->ycs % 4 == 0 && ((uintptr_t)p->y % 16) == 0 && p->y_bs % 4 == 0 &&
                         (!p->res || (p->res_cs % 4 == 0 && ((uintptr_t)p->res % 16) == 0 && p->res_bs % 4 == 0)) &&
                         (!p->scale || ((uintptr_t)p->scale % 16) == 0) && (!p->shift || ((uintptr_t)p->shift % 16) == 0);
-        if (px == 4) {
-            if (qpt == 1) conv_smallk<1, 4><<<grid, 256, lds, s>>>(a, batch, tppx, iters, vec);
-            else conv_smallk<2, 4><<<grid, 256, lds, s>>>(a, batch, tppx, iters, vec);
-        } else {
-            if (qpt == 1) conv_smallk<1, 1><<<grid, 256, lds, s>>>(a, batch, tppx, iters, vec);
-            else conv_smallk<2, 1><<<grid, 256, lds, s>>>(a, batch, tppx, iters, vec);
-        }
+        if (qpt == 1) conv_smallk<1, 1><<<grid, 256, lds, s>>>(a, batch, tppx, iters, vec);
+        else conv_smallk<2, 1><<<grid, 256, lds, s>>>(a, batch, tppx, iters, vec);
         return check_launch("conv_smallk");
     }
     if (pl.tile < 0) {

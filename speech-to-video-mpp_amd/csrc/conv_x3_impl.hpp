@@ -586,7 +586,8 @@ void launch_conv_x3(int cfg, const ConvArgs &a, int amode, bool bkn, dim3 grid, 
         case 4: launch_x3<64, 64, 2, 4, 1, 1, ELT>(a, amode, bkn, grid, s); break;
         case 5: launch_x3<128, 32, 4, 4, 1, 1, ELT>(a, amode, bkn, grid, s); break;
         case 6: launch_x3<256, 128, 4, 8, 1, 1, ELT>(a, amode, bkn, grid, s); break;
-        default: launch_x3<256, 64, 8, 8, 1, 1, ELT>(a, amode, bkn, grid, s); break;   // 7
+        case 7: launch_x3<256, 64, 8, 8, 1, 1, ELT>(a, amode, bkn, grid, s); break;
+        default: launch_x3<512, 128, 4, 8, 1, 1, ELT>(a, amode, bkn, grid, s); break;  // 8: N = 128 layers
     }
 }
 

@@ -47,37 +47,41 @@ __global__ __launch_bounds__(256) void resize_kernel(const float *__restrict__ x
 }
 
 // NHWC fast path: channel-contiguous views (xsc == ysc == 1), c % 4 == 0, 16-byte aligned:
-// one float4 of channels per thread, 32-bit index math.
+// one float4 of channels per thread; one output row per blockIdx.y (grid-stride), 32-bit index
+// math only (the per-element 64-bit divisions of a flat index dominated this HBM-bound kernel).
 __global__ __launch_bounds__(256) void resize_nhwc4_kernel(const float *__restrict__ x, int n, int c4, int ih,
                                                            int iw, long long xsn, int xsy, int xsx,
                                                            float *__restrict__ y, int oh, int ow, long long ysn,
                                                            int ysy, int ysx, float sh, float sw, int mode) {
-    const long long total = (long long)n * oh * ow * c4;
-    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
-        const int cq = (int)(e % c4);
-        const long long t = e / c4;
-        const int pix = (int)(t % ((long long)oh * ow));
-        const int nn = (int)(t / ((long long)oh * ow));
-        const int oy = pix / ow, ox = pix - (pix / ow) * ow;
-        const float *xb = x + nn * xsn + 4 * cq;
-        float4 v;
-        if (mode == 0) {
-            int y0, y1, x0, x1;
-            float ly0, ly1, lx0, lx1;
-            bilin_index(sh, oy, ih, y0, y1, ly0, ly1);
-            bilin_index(sw, ox, iw, x0, x1, lx0, lx1);
-            const float4 a = *(const float4 *)(xb + y0 * xsy + x0 * xsx), b = *(const float4 *)(xb + y0 * xsy + x1 * xsx);
-            const float4 cc = *(const float4 *)(xb + y1 * xsy + x0 * xsx), d = *(const float4 *)(xb + y1 * xsy + x1 * xsx);
-            v.x = ly0 * (lx0 * a.x + lx1 * b.x) + ly1 * (lx0 * cc.x + lx1 * d.x);
-            v.y = ly0 * (lx0 * a.y + lx1 * b.y) + ly1 * (lx0 * cc.y + lx1 * d.y);
-            v.z = ly0 * (lx0 * a.z + lx1 * b.z) + ly1 * (lx0 * cc.z + lx1 * d.z);
-            v.w = ly0 * (lx0 * a.w + lx1 * b.w) + ly1 * (lx0 * cc.w + lx1 * d.w);
-        } else {
-            const int sy = min((int)floorf((float)oy * sh), ih - 1);
-            const int sx = min((int)floorf((float)ox * sw), iw - 1);
-            v = *(const float4 *)(xb + sy * xsy + sx * xsx);
+    const int row_elems = ow * c4;
+    for (int r = blockIdx.y; r < n * oh; r += gridDim.y) {
+        const int nn = r / oh, oy = r - nn * oh;
+        const float *xb = x + nn * xsn;
+        float *yr = y + nn * ysn + (long long)oy * ysy;
+        int y0 = 0, y1 = 0, sy = 0;
+        float ly0 = 1.f, ly1 = 0.f;
+        if (mode == 0) bilin_index(sh, oy, ih, y0, y1, ly0, ly1);
+        else sy = min((int)floorf((float)oy * sh), ih - 1);
+        for (int e = blockIdx.x * 256 + threadIdx.x; e < row_elems; e += gridDim.x * 256) {
+            const int ox = e / c4, cq = e - ox * c4;
+            float4 v;
+            if (mode == 0) {
+                int x0, x1;
+                float lx0, lx1;
+                bilin_index(sw, ox, iw, x0, x1, lx0, lx1);
+                const float *b0 = xb + (long long)y0 * xsy + 4 * cq, *b1 = xb + (long long)y1 * xsy + 4 * cq;
+                const float4 a = *(const float4 *)(b0 + x0 * xsx), b = *(const float4 *)(b0 + x1 * xsx);
+                const float4 cc = *(const float4 *)(b1 + x0 * xsx), d = *(const float4 *)(b1 + x1 * xsx);
+                v.x = ly0 * (lx0 * a.x + lx1 * b.x) + ly1 * (lx0 * cc.x + lx1 * d.x);
+                v.y = ly0 * (lx0 * a.y + lx1 * b.y) + ly1 * (lx0 * cc.y + lx1 * d.y);
+                v.z = ly0 * (lx0 * a.z + lx1 * b.z) + ly1 * (lx0 * cc.z + lx1 * d.z);
+                v.w = ly0 * (lx0 * a.w + lx1 * b.w) + ly1 * (lx0 * cc.w + lx1 * d.w);
+            } else {
+                const int sx = min((int)floorf((float)ox * sw), iw - 1);
+                v = *(const float4 *)(xb + (long long)sy * xsy + sx * xsx + 4 * cq);
+            }
+            *(float4 *)(yr + ox * ysx + 4 * cq) = v;
         }
-        *(float4 *)(y + nn * ysn + oy * ysy + ox * ysx + 4 * cq) = v;
     }
 }
 
@@ -469,8 +473,14 @@ extern "C" int s2v_resize(const float *x, int n, int c, int ih, int iw, long lon
                     ysy % 4 == 0 && xsn % 4 == 0 && ysn % 4 == 0 && ((uintptr_t)x % 16) == 0 &&
                     ((uintptr_t)y % 16) == 0 && xsy < (1LL << 31) && ysy < (1LL << 31);
     if (v4) {
-        resize_nhwc4_kernel<<<grid_for((long long)n * oh * ow * (c / 4)), 256, 0, (hipStream_t)stream>>>(
-            x, n, c / 4, ih, iw, xsn, (int)xsy, (int)xsx, y, oh, ow, ysn, (int)ysy, (int)ysx, scale_h, scale_w, mode);
+        // ~4 float4 per thread along a row, a few rows per block (grid-stride over rows)
+        const long long row = (long long)ow * (c / 4);
+        const unsigned gx = (unsigned)((row + 1023) / 1024);
+        const long long rows = (long long)n * oh;
+        const long long gy = (rows + 3) / 4;
+        dim3 grid(gx, (unsigned)(gy < 65535 ? gy : 65535));
+        resize_nhwc4_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(x, n, c / 4, ih, iw, xsn, (int)xsy, (int)xsx, y, oh,
+                                                                  ow, ysn, (int)ysy, (int)ysx, scale_h, scale_w, mode);
         return check_launch("resize");
     }
     resize_kernel<<<grid_for((long long)n * oh * ow * c), 256, 0, (hipStream_t)stream>>>(

@@ -129,7 +129,7 @@ class ENetEngine:
         # F.pad(reflect, 2) -> StyleConv / ToRGB stages (ENet.py:119-129)
         cur = NHWC.empty(b, 100, 100, 4, dev)
         ops.pad_reflect(ctx, lo, cur, (2, 2, 2, 2))
-        skip = cur.slice(0, 3)
+        skip = cur               # RGB + a finite pad channel: the x2 skip upsample takes the float4 path
         ctr = None
         if noises is None and any(L.noise_w for L in self.layers):
             ctr = self.noise_ctr.bump(ctx)             # one draw per forward, also under graph replay
@@ -156,9 +156,9 @@ class ENetEngine:
                 cur = y
             R = self.layers[3 * st + 2]
             off = self.mod_offs[3 * st + 2]
-            rgb = NHWC.empty(b, cur.h, cur.w, 3, dev)
+            rgb = NHWC.empty(b, cur.h, cur.w, 4, dev)
             ops.resize_nhwc(ctx, skip, rgb, scale_factor=2)          # skip upsample (base_blocks.py:552)
-            ops.modulated_conv2d(ctx, cur, R.conv, rgb, s2[:, off: off + R.cin], res=rgb)
+            ops.modulated_conv2d(ctx, cur, R.conv, rgb.slice(0, 3), s2[:, off: off + R.cin], res=rgb.slice(0, 3))
             skip = rgb
-        ops.nhwc_to_nchw(ctx, skip, out, crop=(8, 8))                # [:, :, 8:-8, 8:-8]
+        ops.nhwc_to_nchw(ctx, skip.slice(0, 3), out, crop=(8, 8))    # [:, :, 8:-8, 8:-8]
         return out, low

@@ -266,3 +266,22 @@ def test_rrdb_gflop_matches_flop_counter():
         with FlopCounterMode(display=False) as fc, torch.no_grad():
             rrdbnet_forward(sd, x, scale)
         assert abs(fc.get_total_flops() / 1e9 - rrdb_gflop(16, 12, scale, num_block=2)) < 1e-9, scale
+
+
+def test_torch_custom_ops_registered_hip_only():
+    """TORCH_LIBRARY(s2v) (csrc/torch_ops.cpp): every op is registered with the reference's schema for
+    the GPEN drop-ins, and a CPU tensor raises (no CPU kernel, no fallback)."""
+    from s2v_amd import torch_ops
+    ns = torch_ops.load()
+    for name in torch_ops.OPS:
+        assert hasattr(ns, name), name
+    assert str(ns.fused_bias_act.default._schema) == (
+        "s2v::fused_bias_act(Tensor input, Tensor bias, Tensor refer, int act, int grad, float alpha, "
+        "float scale) -> Tensor")
+    assert str(ns.upfirdn2d.default._schema) == (
+        "s2v::upfirdn2d(Tensor input, Tensor kernel, int up_x, int up_y, int down_x, int down_y, int pad_x0, "
+        "int pad_x1, int pad_y0, int pad_y1) -> Tensor")
+    with pytest.raises(NotImplementedError):
+        torch_ops.fused.fused_bias_act(torch.zeros(2, 3), torch.zeros(3), torch.zeros(0), 3, 0, 0.2, 1.0)
+    with pytest.raises(NotImplementedError):
+        torch_ops.upfirdn2d(torch.zeros(1, 2, 4, 4), torch.ones(2, 2))

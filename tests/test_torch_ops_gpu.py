@@ -1,0 +1,139 @@
+"""PyTorch custom ops (TORCH_LIBRARY(s2v), csrc/torch_ops.cpp) on the device.
+
+* The GPEN native-op drop-ins with the exact call forms of the reference (gpen_model.py:54 Upsample,
+  :76 Downsample, :96 Blur, :162 EqualLinear + fused_leaky_relu; op/fused_act.py:60-66,
+  op/upfirdn2d.py:114-124) against tests/golden/ops.npz — outputs of the reference's own CPU
+  fallbacks (fused_leaky_relu / upfirdn2d_native).
+* The model-path ops against fp64 / torch references and against the ctypes engine path (same
+  kernels, so bit-identical where the launch is identical).
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import s2v_import  # noqa: F401
+from s2v_amd import ops, synth, torch_ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _blur_kernel(up):
+    k = torch.tensor([1.0, 3.0, 3.0, 1.0])
+    k = (k[None, :] * k[:, None]) / 64.0
+    return (k * (4 if up == 2 else 1)).to(DEV)      # make_kernel, Upsample's factor**2 (gpen_model.py:37-44)
+
+
+def test_gpen_call_forms_match_reference_goldens(golden):
+    g = golden("ops")
+    x = torch.from_numpy(synth.hash_array("golden.fba.x", (2, 8, 5, 7))).to(DEV)
+    b = torch.from_numpy(synth.hash_array("golden.fba.b", (8,))).to(DEV)
+    # FusedLeakyReLU.forward -> fused_leaky_relu (fused_act.py:77-96, device branch)
+    got = torch_ops.fused_leaky_relu(x, b, 0.2, 2 ** 0.5)
+    assert np.abs(got.cpu().numpy() - g["fba_out"]).max() < 1e-6
+    # EqualLinear(activation) (gpen_model.py:160-162): 2-D input, bias per column
+    x2 = torch.from_numpy(synth.hash_array("golden.fba.x2", (3, 16))).to(DEV)
+    b2 = torch.from_numpy(synth.hash_array("golden.fba.b2", (16,))).to(DEV)
+    assert np.abs(torch_ops.fused_leaky_relu(x2, b2).cpu().numpy() - g["fba2_out"]).max() < 1e-6
+    # the raw op with the FusedLeakyReLUFunction.forward arguments (fused_act.py:60-61)
+    raw = torch_ops.fused.fused_bias_act(x, b, x.new_empty(0), 3, 0, 0.2, 2 ** 0.5)
+    assert torch.equal(raw, got)
+    xi = torch.from_numpy(synth.hash_array("golden.ufd.x", (2, 3, 9, 11))).to(DEV)
+    forms = {"up2": (2, 1, (2, 1)),        # Upsample (gpen_model.py:54)
+             "down2": (1, 2, (1, 1)),      # Downsample (:76)
+             "blur22": (1, 1, (2, 2)),     # Blur before the stride-2 encoder convs (:96, :572-581)
+             "blur11": (1, 1, (1, 1))}     # Blur after the transposed modulated conv (:257-268)
+    for name, (up, down, pad) in forms.items():
+        out = torch_ops.upfirdn2d(xi, _blur_kernel(up), up=up, down=down, pad=pad)
+        exp = g[f"ufd_{name}"]
+        assert out.shape == exp.shape, (name, out.shape, exp.shape)
+        assert np.abs(out.cpu().numpy() - exp).max() < 1e-6, name
+
+
+def test_upfirdn2d_op_minor_and_errors():
+    from oracle.enhancers import upfirdn2d as ref_upfirdn2d
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(2, 7, 9, 3, generator=g)                     # [major, H, W, minor]
+    k = torch.randn(3, 4, generator=g)
+    out = torch_ops.upfirdn2d_op.upfirdn2d(x.to(DEV), k.to(DEV), 2, 2, 1, 1, 2, 1, 2, 1)
+    ref = ref_upfirdn2d(x.permute(0, 3, 1, 2), k, up=2, down=1, pad=(2, 1)).permute(0, 2, 3, 1)
+    assert out.shape == ref.shape and (out.cpu() - ref).abs().max() < 1e-5
+    with pytest.raises(RuntimeError):                            # empty output: the reference returned garbage
+        torch_ops.upfirdn2d_op.upfirdn2d(x.to(DEV), torch.ones(16, 16, device=DEV), 1, 1, 1, 1, 0, 0, 0, 0)
+
+
+@pytest.mark.parametrize("prec", ["f32", "f16x3"])
+def test_conv2d_nhwc_op_matches_engine_path(prec):
+    ctx = ops.Ctx(DEV)
+    n, cin, h, w, cout = 2, 64, 14, 12, 96
+    g = torch.Generator().manual_seed(5)
+    wt = torch.randn(cout, cin, 3, 3, generator=g) / math.sqrt(cin * 9)
+    bias = torch.randn(cout, generator=g)
+    x = torch.randn(n, h, w, cin, generator=g).to(DEV)
+    cw = ops.ConvW(wt, bias, DEV, padding=1)
+    code = {"f32": ops.PREC_F32, "f16x3": ops.PREC_F16X3}[prec]
+    split = cw.wt_x3(ctx, code) if code != ops.PREC_F32 else None
+    y = torch_ops.load().conv2d_nhwc(x, cw.wt, split, cw.split_scale(code), cout, 3, 3, [1, 1], [1, 1], [1, 1],
+                                     ops.IN_DIRECT, ops.PAD_ZERO, cw.scale, cw.shift, ops.ACT_LRELU, 0.2, None, False,
+                                     code, False)
+    prev = ops.set_precision(prec)
+    try:
+        ye = ops.NHWC.empty(n, h, w, cout, DEV)
+        ops.conv2d(ctx, ops.NHWC(x), cw, ye, act=ops.ACT_LRELU, alpha=0.2)
+    finally:
+        ops.set_precision(prev)
+    assert torch.equal(y, ye.t)
+    ref = F.leaky_relu(F.conv2d(x.permute(0, 3, 1, 2).double().cpu(), wt.double(), bias.double(), padding=1), 0.2)
+    assert (y.permute(0, 3, 1, 2).double().cpu() - ref).abs().max() < 1e-4
+    # pooled form (ResBlock conv1 + x0.5)
+    yp = torch_ops.load().conv2d_nhwc(x, cw.wt, split, cw.split_scale(code), cout, 3, 3, [1, 1], [1, 1], [1, 1],
+                                      ops.IN_DIRECT, ops.PAD_ZERO, cw.scale, cw.shift, ops.ACT_LRELU, 0.2, None, False,
+                                      code, True)
+    assert (yp.permute(0, 3, 1, 2).double().cpu() - F.avg_pool2d(ref, 2)).abs().max() < 1e-4
+
+
+def test_norm_attention_fft_resize_ops():
+    s2v = torch_ops.load()
+    g = torch.Generator().manual_seed(7)
+    x = (torch.randn(2, 12, 10, 40, generator=g) * 3 + 1).to(DEV)
+    wgt, b = torch.randn(40, generator=g).to(DEV), torch.randn(40, generator=g).to(DEV)
+    y = s2v.layernorm2d(x, wgt, b, 1e-5, ops.ACT_LRELU, 0.1, False)
+    xc = x.permute(0, 3, 1, 2).double().cpu()
+    ref = F.leaky_relu(F.layer_norm(xc, xc.shape[1:], wgt.double().cpu()[:, None, None].expand(xc.shape[1:]),
+                                    b.double().cpu()[:, None, None].expand(xc.shape[1:]), 1e-5), 0.1)
+    assert (y.permute(0, 3, 1, 2).double().cpu() - ref).abs().max() < 2e-5
+    gam, bet = torch.randn(2, 40, generator=g).to(DEV), torch.randn(2, 40, generator=g).to(DEV)
+    y = s2v.instnorm_adain(x, gam, bet, 1e-5, ops.ACT_LRELU, 0.01)
+    ref = F.leaky_relu(F.instance_norm(xc, eps=1e-5) * (1 + gam.double().cpu()[:, :, None, None])
+                       + bet.double().cpu()[:, :, None, None], 0.01)
+    assert (y.permute(0, 3, 1, 2).double().cpu() - ref).abs().max() < 2e-5
+    q, k, v = (torch.randn(2, 144, 256, generator=g).to(DEV) for _ in range(3))
+    o = s2v.attention(q, k, v, 4, 0.125)
+    qq, kk, vv = (t.double().cpu().reshape(2, 144, 4, 64).transpose(1, 2) for t in (q, k, v))
+    ref = (torch.softmax(qq @ kk.transpose(-1, -2) * 0.125, -1) @ vv).transpose(1, 2).reshape(2, 144, 256)
+    assert (o.double().cpu() - ref).abs().max() < 1e-5
+    xf = torch.randn(2, 12, 12, 32, generator=g).to(DEV)
+    tables = ops.fft_tables(12, 12, DEV)
+    spec = s2v.rfft2(xf, tables)
+    back = s2v.irfft2(spec, tables, 12, 12, xf)
+    assert (back - 2 * xf).abs().max() < 1e-4                 # irfft2(rfft2(x)) + x
+    img = torch.rand(2, 3, 384, 384, generator=g).to(DEV)
+    r = s2v.resize_bilinear(img, 96, 96, 4.0, 4.0, 0)
+    assert (r.cpu() - F.interpolate(img.cpu(), (96, 96), mode="bilinear", align_corners=False)).abs().max() < 2e-6
+
+
+def test_flow_warp_and_mel_ops(golden):
+    from oracle import audio as ref_audio
+    from s2v_amd import audio
+    s2v = torch_ops.load()
+    gd = golden("ops")
+    flow = torch.from_numpy(synth.hash_array("golden.flow", (2, 2, 16, 16), -3.0, 3.0)).to(DEV)
+    src = torch.from_numpy(synth.hash_array("golden.flow.src", (2, 3, 64, 64))).to(DEV)
+    assert np.abs(s2v.flow_warp(flow, src).cpu().numpy() - gd["warp"]).max() < 2e-5
+    t = np.arange(16000) / 16000.0
+    wav = (0.2 * np.sin(2 * np.pi * 440 * t)).astype(np.float32)
+    mel = s2v.mel_spectrogram(torch.from_numpy(wav).to(DEV), audio.tables(torch.device(DEV)), False)
+    assert np.abs(mel.cpu().numpy() - ref_audio.melspectrogram(wav)).max() < 1e-3

@@ -49,7 +49,7 @@ def main():
         y = NHWC.empty(n, oh, ow, cout, dev)
         flops = 2.0 * n * oh * ow * k * k * cin * cout
         row = []
-        for t in [0] + list(range(1, 9)):
+        for t in [0] + list(range(1, 10)):
             try:
                 ops.conv2d(ctx, x, cw, y, force_tile=t)
             except Exception:        # tile not offered for this shape (weight rows past npad)
