@@ -155,6 +155,8 @@ GPEN_SYNTH = dict(noise_weight=0.1, equal=True)
 PARSENET_SYNTH = dict(gain=1.0)
 # RRDBNet (RealESRNet): 69 dense blocks, each added back at 0.2; gain 1.0 like ParseNet
 RRDB_SYNTH = dict(gain=1.0)
+# RetinaFace-R50: 16 bottlenecks add onto the identity; gain 1.0 keeps the features O(1..10)
+RETINA_SYNTH = dict(gain=1.0)
 
 
 # ----------------------------------------------------------------------------- inputs

@@ -10,7 +10,13 @@ Import shims (neither touches arithmetic; both documented in SURVEY.md §8c):
     own vendored copy third_part/GPEN/sr_model/arch_util.py (only used for init, which the
     synthetic state_dict overwrites).
 
-Usage:  python tests/golden/make_golden.py [--only lnet,enet,dnet,ops,gfpgan,gpen,gpen2048,parsenet,rrdbnet]
+Face detection / alignment (gen_face) adds import-only stubs: ``torchvision`` (retinaface.py /
+net.py import it at module level; the FPN / SSH / head classes and RetinaFace.forward never call it:
+the ResNet-50 body, the only torchvision user, is replaced by the features under test), ``cv2`` and
+``skimage`` (imported by data/ and align_faces.py; cv2.warpAffine is stubbed to None inside
+warp_and_crop_face, whose numpy transform math is what the fixture pins).
+
+Usage:  python tests/golden/make_golden.py [--only lnet,enet,dnet,ops,gfpgan,gpen,gpen2048,parsenet,rrdbnet,face]
 """
 import argparse
 import importlib.util
@@ -329,6 +335,84 @@ def gen_rrdbnet():
         img = synth.sr_frame(f"golden.rrdb.{tag}", 1, h, w)[0]
         arrays[f"proc_{tag}"] = sr.process(img)
     _save("rrdbnet_goldens", arrays)
+
+
+from helpers import FACE_IMG_HW, FACE_LANDMARKS, retina_head_outputs, retina_tail_inputs  # noqa: E402
+
+
+def _face_stubs():
+    class _Any(types.ModuleType):
+        def __getattr__(self, name):
+            if name.startswith("__"):
+                raise AttributeError(name)
+            return None
+    for name in ("torchvision", "torchvision.models", "torchvision.models._utils",
+                 "torchvision.models.detection", "torchvision.models.detection.backbone_utils",
+                 "skimage", "skimage.transform"):
+        sys.modules.setdefault(name, _Any(name))
+        if "." in name:
+            parent, child = name.rsplit(".", 1)
+            object.__setattr__(sys.modules[parent], child, sys.modules[name])
+    cv2 = _Any("cv2")
+    cv2.warpAffine = lambda *a, **k: None
+    sys.modules["cv2"] = cv2
+    for sub in ("face_detect", "face_detect/facemodels", ""):
+        path = os.path.join(REF, "third_part/GPEN", sub)
+        if path not in sys.path:
+            sys.path.insert(0, path)
+
+
+def gen_face():
+    """RetinaFace-R50 detection tail + post-processing and the similarity alignment, from the
+    reference's own modules (see the module docstring for the import stubs)."""
+    from collections import OrderedDict
+    _face_stubs()
+    import net as ref_net
+    import retinaface as ref_rf
+    from data import cfg_re50
+    import retinaface_detection as ref_det
+    import align_faces as ref_align
+    from s2v_amd.models.retinaface_arch import RetinaFaceParams
+    arrays = {}
+    # FPN + SSH + heads through RetinaFace.forward with the body bypassed (features given)
+    rf = ref_rf.RetinaFace.__new__(ref_rf.RetinaFace)
+    torch.nn.Module.__init__(rf)
+    rf.phase = "test"
+    c, oc = cfg_re50["in_channel"], cfg_re50["out_channel"]
+    rf.fpn = ref_net.FPN([c * 2, c * 4, c * 8], oc)
+    rf.ssh1, rf.ssh2, rf.ssh3 = (ref_net.SSH(oc, oc) for _ in range(3))
+    rf.ClassHead = rf._make_class_head(fpn_num=3, inchannels=oc)
+    rf.BboxHead = rf._make_bbox_head(fpn_num=3, inchannels=oc)
+    rf.LandmarkHead = rf._make_landmark_head(fpn_num=3, inchannels=oc)
+    rf.eval()
+    mine = {k: list(v.shape) for k, v in RetinaFaceParams().state_dict().items() if not k.startswith("body.")}
+    if mine != _manifest(rf):
+        raise SystemExit("retinaface: FPN / SSH / head state_dict layout mismatch")
+    rf.load_state_dict(synth.synth_torch_state_dict(rf, **synth.RETINA_SYNTH), strict=True)
+    rf.body = lambda feats: feats
+    feats = retina_tail_inputs()
+    with torch.no_grad():
+        loc, conf, landms = rf(OrderedDict((str(i), torch.from_numpy(f)) for i, f in enumerate(feats)))
+    arrays.update(tail_loc=loc.numpy(), tail_conf=conf.numpy(), tail_landms=landms.numpy())
+    # RetinaFaceDetection.detect post-processing with the net's outputs given
+    det = ref_det.RetinaFaceDetection.__new__(ref_det.RetinaFaceDetection)
+    det.cfg, det.device = cfg_re50, "cpu"
+    hl, hc, hm = retina_head_outputs()
+    det.net = lambda x: (torch.from_numpy(hl)[None], torch.from_numpy(hc)[None], torch.from_numpy(hm)[None])
+    dets, lms = det.detect(np.zeros(FACE_IMG_HW + (3,), np.uint8))
+    arrays.update(det_dets=np.asarray(dets, np.float32), det_landms=np.asarray(lms, np.float32))
+    print(f"face: detect keeps {len(dets)} of {int((hc[:, 1] > 0.9).sum())} candidates")
+    # alignment: reference points and the similarity transforms of warp_and_crop_face
+    for size in (512, 2048):
+        arrays[f"ref5_{size}"] = np.asarray(ref_align.get_reference_facial_points((size, size), 0.25, (0, 0), True))
+    for i, pts in enumerate(FACE_LANDMARKS):
+        for size in (512, 2048):
+            ref = arrays[f"ref5_{size}"]
+            _, tfm_inv = ref_align.warp_and_crop_face(None, np.array(pts), reference_pts=ref, crop_size=(size, size))
+            params, _ = ref_align._umeyama(np.float32(np.array(pts)).T, np.float32(ref))
+            arrays[f"tfm_{i}_{size}"] = np.asarray(params[:2, :], np.float64)
+            arrays[f"tfm_inv_{i}_{size}"] = np.asarray(tfm_inv, np.float64)
+    _save("face_goldens", arrays)
 
 
 if __name__ == "__main__":

@@ -24,6 +24,9 @@ def synth_sd(net: str):
         return synth.synth_torch_state_dict(ea.FullGeneratorParams(512, 512, 8, 2), **synth.GPEN_SYNTH)
     if net == "gpen2048":             # GPEN-BFR-2048, the CLI's enhancer face GAN (inference.py:228-231)
         return synth.synth_torch_state_dict(ea.FullGeneratorParams(2048, 512, 8, 2), **synth.GPEN_SYNTH)
+    if net == "retinaface":           # RetinaFace-R50 (face_detect/retinaface_detection.py:19-30)
+        from s2v_amd.models.retinaface_arch import RetinaFaceParams
+        return synth.synth_torch_state_dict(RetinaFaceParams(), **synth.RETINA_SYNTH)
     mod = {"lnet": lambda: arch.LNetParams(), "enet": lambda: arch.ENetParams(lnet=arch.LNetParams()),
            "dnet": lambda: arch.DNetParams()}[net]()
     return synth.synth_torch_state_dict(mod)
@@ -65,3 +68,37 @@ def check_probe(t, g, name, atol, rtol=0.0):
     lim = atol + rtol * np.abs(val)
     assert (err <= lim).all(), f"{name}: max err {err.max():.3e} (limit {lim.max():.3e})"
     return float(err.max())
+
+
+# ----------------------------------------------------------------------------- face detection
+# RetinaFace fixture sizes: image (H, W) of the detection tail case (feature maps ceil(H / 8, 16, 32))
+FACE_IMG_HW = (100, 120)
+# synthetic 5-point landmark sets (x0..x4, y0..y4: the reshape(2, 5) layout FaceEnhancement passes)
+FACE_LANDMARKS = (
+    [[430.2, 560.9, 497.0, 440.1, 551.3], [512.5, 508.1, 590.2, 660.4, 655.0]],
+    [[100.0, 160.0, 131.0, 108.0, 152.0], [120.0, 124.0, 150.0, 181.0, 184.0]],
+    [[812.7, 870.2, 851.9, 800.4, 846.6], [300.1, 321.8, 352.0, 381.7, 399.5]],   # rolled face
+    [[30.3, 41.0, 35.2, 31.9, 40.1], [50.7, 50.9, 56.1, 61.5, 61.8]],             # small face
+)
+
+
+def retina_tail_inputs(hw=FACE_IMG_HW):
+    """Synthetic backbone features (layer2 / layer3 / layer4 outputs) for the FPN + SSH + heads case."""
+    h, w = hw
+    sizes = [(-(-h // s), -(-w // s)) for s in (8, 16, 32)]
+    return [synth.hash_array(f"golden.retina.f{i}", (1, c, a, b), 0.0, 2.0)
+            for i, (c, (a, b)) in enumerate(zip((512, 1024, 2048), sizes))]
+
+
+def retina_head_outputs(hw=FACE_IMG_HW):
+    """Synthetic (loc, conf, landms) for RetinaFaceDetection.detect's post-processing: clusters of
+    confident, overlapping anchors so the threshold, the sort and the NMS all act."""
+    from oracle.face import prior_box
+    pr = prior_box(hw).numpy()
+    P = pr.shape[0]
+    loc = synth.hash_array("golden.retina.loc", (P, 4), -0.5, 0.5)
+    lm = synth.hash_array("golden.retina.lm", (P, 10), -1.0, 1.0)
+    u = (synth.hash_array("golden.retina.score", (P,), 0.0, 1.0)).astype(np.float64)
+    s = np.where(u > 0.92, 0.9 + 0.1 * (u - 0.92) / 0.08, 0.95 * u)
+    conf = np.stack([1.0 - s, s], 1).astype(np.float32)
+    return loc, conf, lm
