@@ -298,9 +298,14 @@ int s2v_fill(float *y, long long n, float value, s2v_stream_t stream);
  * element (b, y, x, ch) at x + b*xis + y*xrs + x*c + ch (pitches in elements; ROIs of larger frames
  * are plain pointer offsets).  mode 0: uint8 -> uint8 (11-bit fixed-point weights), 1: fp32 -> fp32,
  * 2: fp32 -> uint8 truncated (np.uint8 of the float result, inference.py:313), 3: uint8 -> fp32
- * (v == 255 ? 1 : 0: the mask paste of inference.py:305-308, resized / 255. stored into uint8). */
+ * (v == 255 ? 1 : 0: the mask paste of inference.py:305-308, resized / 255. stored into uint8),
+ * 4: fp64 -> fp64 (double sums, float coefficients: FaceEnhancement's mask_sharp). */
 int s2v_resize_linear(const void *x, int n, int h, int w, int c, long long xrs, long long xis, void *y, int oh,
                       int ow, long long yrs, long long yis, int mode, s2v_stream_t stream);
+/* The same for cv2.resize(src, (0, 0), fx=fx, fy=fy): (ow, oh) = (round(w fx), round(h fy)) chosen by
+ * the caller, source coordinates scaled by 1 / fx, 1 / fy (OpenCV keeps the given factors). */
+int s2v_resize_linear_fxfy(const void *x, int n, int h, int w, int c, long long xrs, long long xis, void *y, int oh,
+                           int ow, long long yrs, long long yis, int mode, double fx, double fy, s2v_stream_t stream);
 
 /* Laplacian_Pyramid_Blending_with_mask (futils/inference_utils.py:181-222): A, B uint8 [n][h][w][c],
  * m fp32 [n][h][w] -> out fp32 [n][h][w][c]; cv2.pyrDown / pyrUp semantics (reflect-101 borders,
@@ -332,6 +337,66 @@ int s2v_sr_u8_in(const unsigned char *x, int n, int h, int w, int flip, int pad_
  * -> uint8 [n,h,w,3] = round_half_even(clamp(x, 0, 1) * 255) (channels reversed if ``flip``). */
 int s2v_sr_f32_out(const float *x, int n, int h, int w, int xh, int xw, int xcs, int flip, unsigned char *y,
                    s2v_stream_t stream);
+
+/* ---- Face detection / alignment / paste-back (face_enhancement.py:91-193) ----- */
+
+/* RetinaFaceDetection.detect input (retinaface_detection.py:59-73): BGR pixels (xtype 0 uint8,
+ * 1 fp32) -> fp32 NHWC4 (b - 104, g - 117, r - 123, 0); y 16-byte aligned. */
+int s2v_bgr_mean_nhwc4(const void *x, int xtype, long long pixels, float *y, s2v_stream_t stream);
+/* F.max_pool2d(x, k, s, p) on NHWC fp32 (c % 4 == 0; the ResNet-50 stem pool: 3, 2, 1). */
+int s2v_maxpool2d_nhwc(const float *x, int n, int h, int w, int c, int k, int s, int p, float *y, int oh, int ow,
+                       s2v_stream_t stream);
+/* RetinaFace priors + decode + threshold (prior_box.py:20-34, box_utils.py:209-247,
+ * retinaface_detection.py:81-104) for cfg_re50 (steps 8/16/32, min sizes 16,32 / 64,128 / 256,512,
+ * variances 0.1 / 0.2).  heads[l]: level l fused head output, NHWC [hs[l]][ws[l]][cs] with channels
+ * [box anchor0 (4) | box anchor1 (4) | class logits a0 (2) | a1 (2) | landmarks a0 (10) | a1 (10)]
+ * (cs >= 32); hs / ws must be ceil(im / step).  Every prior whose softmax score > thresh is written
+ * to cand as 16 floats [prior index (int bits), x1, y1, x2, y2 (pixels), score, 5 x (x, y)] at
+ * slot atomicAdd(count): the order of the slots is arbitrary (the host sorts by prior index).
+ * max_cand must be >= the number of priors. */
+int s2v_retina_decode(const float *const *heads, const int *hs, const int *ws, int cs, int im_h, int im_w,
+                      float thresh, float *cand, int *count, int max_cand, s2v_stream_t stream);
+/* RetinaFace.forward's outputs in phase 'test' (retinaface.py:115-124) from the same head maps for n
+ * images (image b of level l at heads[l] + b*hs[l]*ws[l]*cs): loc [n][P][4], conf = softmax [n][P][2],
+ * landms [n][P][10], priors in PriorBox order. */
+int s2v_retina_split(const float *const *heads, const int *hs, const int *ws, int cs, int im_h, int im_w, int n,
+                     float *loc, float *conf, float *landms, s2v_stream_t stream);
+/* cv2.warpAffine(src, M, (ow, oh), flags=INTER_LINEAR or INTER_AREA, BORDER_CONSTANT 0) on n HWC
+ * images (dtype 0 uint8, 1 fp32, 2 fp64; pitches in elements): M = n device 2x3 fp64 forward
+ * matrices, inverted on the device (invertAffineTransform); OpenCV's fixed-point source coordinates
+ * (AB_BITS 10, INTER_BITS 5), uint8 through 15-bit weights, float in tap order. */
+int s2v_warp_affine(const void *x, int n, int h, int w, int c, long long xrs, long long xis, int dtype,
+                    const double *M, void *y, int oh, int ow, long long yrs, long long yis, s2v_stream_t stream);
+/* FaceEnhancement paste-back (face_enhancement.py:143-157) with both warps fused: for frame pixels
+ * in [y0, y0+wh) x [x0, x0+ww): t = warpAffine(mask fp32 [S][S], M); where t > full_mask:
+ * full_mask = t and full_img (uint8 [H][W][3]) = warpAffine(face uint8 [S][S][3], M).  Pixels
+ * outside the window must be ones where the warped mask is 0 (the window bounds the warped crop). */
+int s2v_face_paste(const float *mask, const unsigned char *face, int S, const double *M, float *full_mask,
+                   unsigned char *full_img, int H, int W, int y0, int x0, int wh, int ww, s2v_stream_t stream);
+/* cv2.GaussianBlur on one [h][w] channel, BORDER_REFLECT_101, separable with the ksize taps of
+ * ``kern`` (work type dtype: 1 fp32, 2 fp64; kern in that type, device memory): row pass in tap
+ * order, column pass as SymmColumnFilter.  xtype 0: uint8 input read as v / 255. (mask_postprocess's
+ * mask_sharp), else the work type; zero_border > 0 zeroes the input outside [zb, h-zb) x [zb, w-zb)
+ * first (face_enhancement.py:84-85).  ytype 1 fp32 / 2 fp64 (fp64 -> fp32 is one rounding).
+ * ws >= s2v_gaussian_blur_ws_bytes(h, w, dtype). */
+size_t s2v_gaussian_blur_ws_bytes(int h, int w, int dtype);
+int s2v_gaussian_blur(const void *x, int xtype, int h, int w, int zero_border, const void *kern, int ksize, void *y,
+                      int ytype, int dtype, void *ws, size_t ws_bytes, s2v_stream_t stream);
+/* cv2.filter2D(img, -1, kern 3x3 fp32) on uint8 HWC, BORDER_REFLECT_101, cvRound + saturate. */
+int s2v_filter3x3_u8(const unsigned char *x, int h, int w, int c, const float *kern, unsigned char *y,
+                     s2v_stream_t stream);
+/* FaceGAN.img2tensor / tensor2img (face_gan.py:44-59): uint8 HWC BGR [n][h][w][3] <-> fp32 NCHW
+ * RGB [n][3][h][w] in [-1, 1]; the way back is np.clip(x * 0.5 + 0.5, 0, 1) * 255 truncated. */
+int s2v_u8_to_gan(const unsigned char *x, int n, int h, int w, float *y, s2v_stream_t stream);
+int s2v_gan_to_u8(const float *x, int n, int h, int w, unsigned char *y, s2v_stream_t stream);
+/* y = x / 255. as float64 (mask_sharp, face_enhancement.py:137). */
+int s2v_u8_div255_f64(const unsigned char *x, long long n, double *y, s2v_stream_t stream);
+/* Final blend of FaceEnhancement.process on uint8 HWC frames (3 channels): mask_sharp == NULL:
+ * convertScaleAbs(base * (1 - full_mask) + full_img * full_mask) (use_sr, :175-176); else
+ * img = that (base = ori_img), then convertScaleAbs(ori * (1 - mask_sharp) + img * mask_sharp) with
+ * the fp64 mask_sharp (:189-191). */
+int s2v_face_blend(const unsigned char *base, const float *full_mask, const unsigned char *full_img,
+                   const double *mask_sharp, unsigned char *out, long long pixels, s2v_stream_t stream);
 
 const char *s2v_last_error(void);
 /* number of compute units of the current device (0 if no device) */

@@ -399,3 +399,107 @@ def mask_postprocess(mask, thres=26):
 def convert_scale_abs(x):
     """cv2.convertScaleAbs: saturate_cast<uchar>(|x|) with round-half-even."""
     return np.clip(np.rint(np.abs(x)), 0, 255).astype(np.uint8)
+
+
+# ----------------------------------------------------------------------------- FaceEnhancement
+FACE_MM = [0, 255, 255, 255, 255, 255, 255, 255, 0, 0, 255, 255, 255, 0, 0, 0, 0, 0, 0]   # face_enhancement.py:136
+SMALL_FACE_KERNEL = np.array([[0.0625, 0.125, 0.0625], [0.125, 0.25, 0.125], [0.0625, 0.125, 0.0625]], np.float32)
+
+
+def filter2d_u8(img, kern):
+    """cv2.filter2D(img, -1, kern 3x3 fp32) on uint8, BORDER_REFLECT_101, fp32 sum in row-major tap
+    order, cvRound, saturated."""
+    h, w = img.shape[:2]
+    ys = _reflect101(np.arange(h)[:, None] + np.arange(-1, 2)[None, :], h)
+    xs = _reflect101(np.arange(w)[:, None] + np.arange(-1, 2)[None, :], w)
+    s = np.zeros(img.shape, np.float32)
+    for dy in range(3):
+        for dx in range(3):
+            s = s + kern[dy, dx] * img[ys[:, dy]][:, xs[:, dx]].astype(np.float32)
+    return np.clip(np.rint(s), 0, 255).astype(np.uint8)
+
+
+def paste_window(tfm_inv, S, H, W):
+    """Frame window holding every pixel whose warped crop value can be non-zero (the image of the
+    crop square (-1, S) x (-1, S) under tfm_inv, padded for the fixed-point rounding)."""
+    M = np.asarray(tfm_inv, np.float64)
+    cs = np.array([[-2.0, -2.0], [S + 1.0, -2.0], [-2.0, S + 1.0], [S + 1.0, S + 1.0]])
+    p = cs @ M[:, :2].T + M[:, 2]
+    pad = 2.0 + 2.0 * max(1.0, float(np.abs(M[:, :2]).sum(1).max()))
+    x0, y0 = int(max(0, np.floor(p[:, 0].min() - pad))), int(max(0, np.floor(p[:, 1].min() - pad)))
+    x1, y1 = int(min(W, np.ceil(p[:, 0].max() + pad))), int(min(H, np.ceil(p[:, 1].max() + pad)))
+    return y0, x0, max(0, y1 - y0), max(0, x1 - x0)
+
+
+def enhance_process(img, ori_img, *, detect, facegan, parse, sr, use_sr, in_size, face_enhance=True, bbox=None,
+                    possion_blending=False, threshold=0.9, blend=None):
+    """FaceEnhancement.process (face_enhancement.py:91-193) with the networks given as callables
+    (detect: uint8 frame -> (dets, landms); facegan: uint8 S x S face -> uint8 face; parse: uint8
+    face -> uint8 512 x 512 mask with FACE_MM; sr: uint8 frame -> uint8 frame or None) and every
+    OpenCV call restated above.  ``blend``: the Laplacian pyramid blend (possion_blending branch).
+    Returns (img, orig_faces, enhanced_faces)."""
+    from . import post as opost
+    orig_faces, enhanced_faces = [], []
+    img_sr = None
+    if use_sr:
+        img_sr = sr(img)
+        if img_sr is not None:
+            img = opost.resize_linear(img, img_sr.shape[:2][::-1])
+    facebs, landms = detect(img)
+    height, width = img.shape[:2]
+    full_mask = np.zeros((height, width), dtype=np.float32)
+    full_img = np.zeros(ori_img.shape, dtype=np.uint8)
+    ref5 = get_reference_facial_points((in_size, in_size))
+    mask_sharp = None
+    for faceb, facial5points in zip(facebs, landms):
+        if faceb[4] < threshold:
+            continue
+        fh, fw = (faceb[3] - faceb[1]), (faceb[2] - faceb[0])
+        tfm, tfm_inv = similarity_transforms(np.reshape(facial5points, (2, 5)), ref5)
+        of = warp_affine(img, tfm, (in_size, in_size))
+        ef = facegan(of) if face_enhance else of
+        orig_faces.append(of)
+        enhanced_faces.append(ef)
+        mask_sharp = parse(ef) / 255.
+        tmp_mask = mask_postprocess(mask_sharp)
+        tmp_mask = opost.resize_linear(tmp_mask, (in_size, in_size))
+        tmp_mask = warp_affine(tmp_mask, tfm_inv, (width, height))
+        mask_sharp = opost.resize_linear(mask_sharp, ef.shape[:2])
+        mask_sharp = warp_affine(mask_sharp, tfm_inv, (width, height))
+        if min(fh, fw) < 100:
+            ef = filter2d_u8(ef, SMALL_FACE_KERNEL)
+        tmp_img = warp_affine(ef, tfm_inv, (width, height))
+        sel = (tmp_mask - full_mask) > 0
+        full_mask[sel] = tmp_mask[sel]
+        full_img[sel] = tmp_img[sel]
+    if mask_sharp is None:
+        raise UnboundLocalError("local variable 'mask_sharp' referenced before assignment (no face above the "
+                                "threshold: face_enhancement.py:165 fails the same way)")
+    mask_sharp = gaussian_blur(mask_sharp, 0, 1.0)
+    full_mask = full_mask[:, :, np.newaxis]
+    mask_sharp = mask_sharp[:, :, np.newaxis]
+    if use_sr and img_sr is not None:
+        return convert_scale_abs(img_sr * (1 - full_mask) + full_img * full_mask), orig_faces, enhanced_faces
+    if possion_blending:
+        if bbox is not None:
+            y1, y2, x1, x2 = bbox
+            mask_bbox = np.zeros_like(mask_sharp)
+            mask_bbox[y1:y2 - 5, x1:x2] = 1
+            full_img, ori_img, full_mask = [opost.resize_linear(x, (512, 512)) for x in
+                                            (full_img, ori_img, np.float32(mask_sharp * mask_bbox)[..., 0])]
+        else:
+            full_img, ori_img, full_mask = [opost.resize_linear(x, (512, 512)) for x in
+                                            (full_img, ori_img, full_mask[..., 0])]
+        out = blend(full_img, ori_img, full_mask, 6)
+        out = np.clip(out, 0, 255)
+        return opost.resize_linear(out.astype(np.float32), (width, height)).astype(np.uint8), orig_faces, \
+            enhanced_faces
+    out = convert_scale_abs(ori_img * (1 - full_mask) + full_img * full_mask)
+    out = convert_scale_abs_f64(ori_img * (1 - mask_sharp) + out * mask_sharp)
+    return out, orig_faces, enhanced_faces
+
+
+def convert_scale_abs_f64(x):
+    """cv2.convertScaleAbs of a float64 image as OpenCV's vector path does it: each value rounded to
+    fp32 first, then |.|, round half to even, saturated."""
+    return convert_scale_abs(np.asarray(x, np.float64).astype(np.float32))

@@ -113,8 +113,8 @@ def laplacian_blend(A, B, m, num_levels=6):
     return ls_.astype(F32)
 
 
-def _coords(n_out, n_in, clamp):
-    scale = 1.0 / (n_out / n_in)
+def _coords(n_out, n_in, clamp, inv_scale=None):
+    scale = 1.0 / (n_out / n_in) if inv_scale is None else 1.0 / inv_scale
     f = ((np.arange(n_out) + 0.5) * scale - 0.5).astype(F32)
     s = np.floor(f).astype(np.int64)
     f = (f - s.astype(F32)).astype(F32)
@@ -126,13 +126,15 @@ def _coords(n_out, n_in, clamp):
     return np.clip(s, 0, n_in - 1), np.clip(s + 1, 0, n_in - 1), f
 
 
-def resize_linear(img, dsize):
+def resize_linear(img, dsize, fxfy=None):
     """cv2.resize(img, dsize=(W, H)) with INTER_LINEAR (resize.cpp resizeGeneric_): uint8 with the
-    11-bit fixed-point weights and OpenCV's vector column pass, float32 in float arithmetic."""
+    11-bit fixed-point weights and OpenCV's vector column pass, float32 in float arithmetic, float64
+    in double arithmetic with the float coefficients.  ``fxfy``: cv2.resize(img, (0, 0), fx, fy)
+    (dsize = the rounded product; the factors themselves scale the coordinates)."""
     W, H = dsize
     h, w = img.shape[:2]
-    x0, x1, fx = _coords(W, w, True)
-    y0, y1, fy = _coords(H, h, False)
+    x0, x1, fx = _coords(W, w, True, None if fxfy is None else fxfy[0])
+    y0, y1, fy = _coords(H, h, False, None if fxfy is None else fxfy[1])
     ex = (1,) * (img.ndim - 2)
     if img.dtype == np.uint8:
         a0 = np.rint((F32(1) - fx) * F32(2048)).astype(np.int64).reshape((1, W) + ex)
@@ -143,6 +145,11 @@ def resize_linear(img, dsize):
         D = S[:, x0] * a0 + S[:, x1] * a1
         v = (((D[y0] >> 4) * b0) >> 16) + (((D[y1] >> 4) * b1) >> 16)
         return np.clip((v + 2) >> 2, 0, 255).astype(np.uint8)
+    if img.dtype == np.float64:
+        a0, a1 = (F32(1) - fx).astype(np.float64).reshape((1, W) + ex), fx.astype(np.float64).reshape((1, W) + ex)
+        b0, b1 = (F32(1) - fy).astype(np.float64).reshape((H, 1) + ex), fy.astype(np.float64).reshape((H, 1) + ex)
+        D = img[:, x0] * a0 + img[:, x1] * a1
+        return D[y0] * b0 + D[y1] * b1
     S = img.astype(F32)
     a0, a1 = (F32(1) - fx).reshape((1, W) + ex), fx.reshape((1, W) + ex)
     b0, b1 = (F32(1) - fy).reshape((H, 1) + ex), fy.reshape((H, 1) + ex)

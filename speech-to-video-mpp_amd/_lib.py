@@ -99,6 +99,8 @@ _SIGS = {
     "s2v_fill": (_c_int, [_vp, _c_ll, _c_float, _vp]),
     "s2v_resize_linear": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_ll, _c_ll, _vp, _c_int, _c_int, _c_ll,
                                    _c_ll, _c_int, _vp]),
+    "s2v_resize_linear_fxfy": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_ll, _c_ll, _vp, _c_int, _c_int, _c_ll,
+                                        _c_ll, _c_int, ctypes.c_double, ctypes.c_double, _vp]),
     "s2v_laplacian_blend_ws_bytes": (_c_size, [_c_int, _c_int, _c_int, _c_int, _c_int]),
     "s2v_laplacian_blend": (_c_int, [_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_size,
                                      _vp]),
@@ -106,6 +108,21 @@ _SIGS = {
     "s2v_img_u8_to_m11": (_c_int, [_vp, _c_ll, _c_int, _vp, _c_int, _vp]),
     "s2v_sr_u8_in": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp]),
     "s2v_sr_f32_out": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp]),
+    "s2v_bgr_mean_nhwc4": (_c_int, [_vp, _c_int, _c_ll, _vp, _vp]),
+    "s2v_maxpool2d_nhwc": (_c_int, [_vp] + [_c_int] * 7 + [_vp, _c_int, _c_int, _vp]),
+    "s2v_retina_decode": (_c_int, [_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_float, _vp, _vp, _c_int, _vp]),
+    "s2v_retina_split": (_c_int, [_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp]),
+    "s2v_warp_affine": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_ll, _c_ll, _c_int, _vp, _vp, _c_int, _c_int,
+                                 _c_ll, _c_ll, _vp]),
+    "s2v_face_paste": (_c_int, [_vp, _vp, _c_int, _vp, _vp, _vp] + [_c_int] * 6 + [_vp]),
+    "s2v_gaussian_blur_ws_bytes": (_c_size, [_c_int, _c_int, _c_int]),
+    "s2v_gaussian_blur": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp, _c_int, _c_int, _vp, _c_size,
+                                   _vp]),
+    "s2v_filter3x3_u8": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _vp, _vp]),
+    "s2v_u8_to_gan": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _vp]),
+    "s2v_gan_to_u8": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _vp]),
+    "s2v_u8_div255_f64": (_c_int, [_vp, _c_ll, _vp, _vp]),
+    "s2v_face_blend": (_c_int, [_vp, _vp, _vp, _vp, _vp, _c_ll, _vp]),
     "s2v_last_error": (ctypes.c_char_p, []),
     "s2v_device_cus": (_c_int, []),
     "s2v_version": (ctypes.c_char_p, []),

@@ -166,7 +166,7 @@ __global__ __launch_bounds__(256) void lap_level_kernel(const float *__restrict_
 //   (v + 2) >> 2 saturated.  fp32: float weights, S0*a0 + S1*a1 and D0*b0 + D1*b1.
 // mode 0: u8 -> u8, 1: f32 -> f32, 2: f32 -> u8 truncated (np.uint8 of the float result,
 // inference.py:313), 3: u8 -> f32 (v == 255 ? 1 : 0): the mask paste at inference.py:305-308,
-// which assigns resized/255. into a uint8 array (so only 255 survives, as 1).
+// which assigns resized/255. into a uint8 array (so only 255 survives, as 1); 4: f64 -> f64.
 template <int MODE>
 __global__ __launch_bounds__(256) void resize_linear_kernel(const void *__restrict__ xv, int n, int h, int w, int c,
                                                             long long xrs, long long xis, void *__restrict__ yv,
@@ -201,6 +201,14 @@ __global__ __launch_bounds__(256) void resize_linear_kernel(const void *__restri
             const int v = min(max(((((d0 >> 4) * b0) >> 16) + (((d1 >> 4) * b1) >> 16) + 2) >> 2, 0), 255);
             if (MODE == 0) ((unsigned char *)yv)[yo] = (unsigned char)v;
             else ((float *)yv)[yo] = v == 255 ? 1.f : 0.f;
+        } else if (MODE == 4) {
+            // CV_64F: double sums with the float coefficients (HResizeLinear / VResizeLinear<double, .., float>)
+            const double *xb = (const double *)xv + (long long)b * xis + ch;
+            const double a0 = (double)(1.f - fx), b0 = (double)(1.f - fy), a1 = (double)fx, b1 = (double)fy;
+            const double *r0 = xb + (long long)y0 * xrs, *r1 = xb + (long long)y1 * xrs;
+            const double d0 = r0[x0 * c] * a0 + r0[x1 * c] * a1;
+            const double d1 = r1[x0 * c] * a0 + r1[x1 * c] * a1;
+            ((double *)yv)[yo] = d0 * b0 + d1 * b1;
         } else {
             const float *xb = (const float *)xv + (long long)b * xis + ch;
             const float a0 = 1.f - fx, b0 = 1.f - fy;
@@ -340,23 +348,38 @@ extern "C" int s2v_laplacian_blend(const unsigned char *a, const unsigned char *
     return check_launch("laplacian_blend");
 }
 
-extern "C" int s2v_resize_linear(const void *x, int n, int h, int w, int c, long long xrs, long long xis, void *y,
-                                 int oh, int ow, long long yrs, long long yis, int mode, s2v_stream_t stream) {
+static int resize_linear_scaled(const void *x, int n, int h, int w, int c, long long xrs, long long xis, void *y,
+                                int oh, int ow, long long yrs, long long yis, int mode, double sy, double sx,
+                                s2v_stream_t stream) {
     S2V_REQUIRE(x && y && n > 0 && h > 0 && w > 0 && c > 0 && oh > 0 && ow > 0, "resize_linear: bad args");
-    S2V_REQUIRE(mode >= 0 && mode <= 3, "resize_linear: bad mode %d", mode);
+    S2V_REQUIRE(mode >= 0 && mode <= 4, "resize_linear: bad mode %d", mode);
     S2V_REQUIRE(xrs >= (long long)w * c && yrs >= (long long)ow * c && (n == 1 || (xis >= xrs * h && yis >= yrs * oh)),
                 "resize_linear: row / image pitches smaller than the rows / images");
-    // cv::resize: inv_scale = dsize / ssize, scale = 1 / inv_scale (both double)
-    const double sy = 1.0 / ((double)oh / h), sx = 1.0 / ((double)ow / w);
     const unsigned g = grid_for((long long)n * oh * ow * c);
     hipStream_t s = (hipStream_t)stream;
     switch (mode) {
         case 0: resize_linear_kernel<0><<<g, 256, 0, s>>>(x, n, h, w, c, xrs, xis, y, oh, ow, yrs, yis, sy, sx); break;
         case 1: resize_linear_kernel<1><<<g, 256, 0, s>>>(x, n, h, w, c, xrs, xis, y, oh, ow, yrs, yis, sy, sx); break;
         case 2: resize_linear_kernel<2><<<g, 256, 0, s>>>(x, n, h, w, c, xrs, xis, y, oh, ow, yrs, yis, sy, sx); break;
-        default: resize_linear_kernel<3><<<g, 256, 0, s>>>(x, n, h, w, c, xrs, xis, y, oh, ow, yrs, yis, sy, sx); break;
+        case 3: resize_linear_kernel<3><<<g, 256, 0, s>>>(x, n, h, w, c, xrs, xis, y, oh, ow, yrs, yis, sy, sx); break;
+        default: resize_linear_kernel<4><<<g, 256, 0, s>>>(x, n, h, w, c, xrs, xis, y, oh, ow, yrs, yis, sy, sx); break;
     }
     return check_launch("resize_linear");
+}
+
+extern "C" int s2v_resize_linear(const void *x, int n, int h, int w, int c, long long xrs, long long xis, void *y,
+                                 int oh, int ow, long long yrs, long long yis, int mode, s2v_stream_t stream) {
+    // cv::resize with dsize: inv_scale = dsize / ssize, scale = 1 / inv_scale (both double)
+    return resize_linear_scaled(x, n, h, w, c, xrs, xis, y, oh, ow, yrs, yis, mode, 1.0 / ((double)oh / h),
+                                1.0 / ((double)ow / w), stream);
+}
+
+extern "C" int s2v_resize_linear_fxfy(const void *x, int n, int h, int w, int c, long long xrs, long long xis,
+                                      void *y, int oh, int ow, long long yrs, long long yis, int mode, double fx,
+                                      double fy, s2v_stream_t stream) {
+    // cv::resize(src, (0, 0), fx, fy): dsize = round(size * f), inv_scale = f itself
+    S2V_REQUIRE(fx > 0 && fy > 0, "resize_linear_fxfy: scale factors must be positive");
+    return resize_linear_scaled(x, n, h, w, c, xrs, xis, y, oh, ow, yrs, yis, mode, 1.0 / fy, 1.0 / fx, stream);
 }
 
 extern "C" int s2v_parse_mask(const float *x, int n, int h, int w, int c, long long xbs, long long ps, long long cs,

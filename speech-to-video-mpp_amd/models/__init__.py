@@ -16,7 +16,7 @@ import torch
 
 from .. import ops
 from ..ops import NHWC
-from . import arch, enhancer_arch, parse_arch, sr_arch
+from . import arch, enhancer_arch, parse_arch, retinaface_arch, sr_arch
 
 
 def _fold5(x, dim):
@@ -213,6 +213,60 @@ class RRDBNet(_EngineMixin, sr_arch.RRDBNetParams):
 
 
 # ----------------------------------------------------------------------------- loaders
+class RetinaFace(_EngineMixin, retinaface_arch.RetinaFaceParams):
+    """third_part/GPEN/face_detect/facemodels/retinaface.py:47-125 with cfg_re50 (the only
+    configuration RetinaFaceDetection builds, retinaface_detection.py:19-27)."""
+
+    def __init__(self, cfg=None, phase="test"):
+        cfg = retinaface_arch.CFG_RE50 if cfg is None else cfg
+        if cfg.get("name", "Resnet50") != "Resnet50":
+            raise NotImplementedError("RetinaFace: only the Resnet50 backbone (cfg_re50) is on the GPEN path")
+        super().__init__(cfg)
+        self.phase = phase
+
+    def _build_engine(self, sd, device):
+        from ..engine.retinaface import RetinaFaceEngine
+        return RetinaFaceEngine(sd, device)
+
+    def head_maps(self, x4: NHWC):
+        """x4: NHWC [B,H,W,4] fp32 (BGR minus means, channel 3 zero) -> per-level fused head maps."""
+        eng, ctx = self._engine(x4.t.device)
+        return eng.forward_maps(ctx, x4), ctx
+
+    @torch.no_grad()
+    def forward(self, inputs):
+        """inputs [B,3,H,W] fp32 (BGR minus (104, 117, 123)) -> (loc [B,P,4], conf [B,P,2] softmaxed in
+        phase 'test' (raw logits in 'train'), landms [B,P,10]) (retinaface.py:108-125)."""
+        _need_cuda(inputs)
+        b, c, h, w = inputs.shape
+        if c != 3:
+            raise RuntimeError(f"RetinaFace: expected 3 input channels, got {c}")
+        eng, ctx = self._engine(inputs.device)
+        x4 = NHWC.empty(b, h, w, 4, inputs.device)
+        ops.fill(ctx, x4.t)
+        ops.nchw_to_nhwc(ctx, inputs.float(), x4.slice(0, 3))
+        maps = eng.forward_maps(ctx, x4)
+        if self.phase != "test":
+            return eng.split_heads(maps)
+        return retina_outputs(ctx, maps, h, w)
+
+
+def retina_outputs(ctx, maps, im_h, im_w):
+    """Head maps -> (loc, softmax conf, landms) via s2v_retina_split (phase 'test')."""
+    import ctypes
+    n, dev = maps[0].n, maps[0].t.device
+    P = sum(2 * m.h * m.w for m in maps)
+    loc = torch.empty((n, P, 4), device=dev)
+    conf = torch.empty((n, P, 2), device=dev)
+    lms = torch.empty((n, P, 10), device=dev)
+    heads = (ctypes.c_void_p * 3)(*[m.ptr for m in maps])
+    hs = (ctypes.c_int * 3)(*[m.h for m in maps])
+    ws = (ctypes.c_int * 3)(*[m.w for m in maps])
+    ops.check(ctx.lib.s2v_retina_split(heads, hs, ws, maps[0].cs, im_h, im_w, n, loc.data_ptr(), conf.data_ptr(),
+                                       lms.data_ptr(), ctx.stream), "s2v_retina_split")
+    return loc, conf, lms
+
+
 def _load(path):
     return torch.load(path, map_location="cpu", weights_only=True)
 
@@ -276,6 +330,20 @@ def load_parsenet(path, size=512):
     return net.eval()
 
 
+def load_retinaface(path):
+    """RetinaFaceDetection.load_model (retinaface_detection.py:45-58): ``state_dict`` entry or bare
+    dict, ``module.`` prefix stripped, strict=False."""
+    net = RetinaFace(retinaface_arch.CFG_RE50, phase="test")
+    sd = _load(path)
+    if "state_dict" in sd:
+        sd = sd["state_dict"]
+    sd = {(k.split("module.", 1)[-1] if k.startswith("module.") else k): v for k, v in sd.items()}
+    if not set(sd) & set(net.state_dict()):
+        raise AssertionError("load NONE from pretrained checkpoint")
+    net.load_state_dict(sd, strict=False)
+    return net.eval()
+
+
 def load_srmodel(path, scale=2, num_feat=32):
     """real_esrnet.py:21-30: RRDBNet(3, 3, num_feat, num_block=23, num_grow_ch=32, scale) with the
     ``params_ema`` weights, strict=True."""
@@ -285,4 +353,5 @@ def load_srmodel(path, scale=2, num_feat=32):
 
 
 __all__ = ["LNet", "ENet", "DNet", "GFPGANv1Clean", "FullGenerator", "ParseNet", "RRDBNet", "load_checkpoint",
-           "load_network", "load_DNet", "load_gfpgan", "load_gpen", "load_parsenet", "load_srmodel"]
+           "load_network", "load_DNet", "load_gfpgan", "load_gpen", "load_parsenet", "load_srmodel", "RetinaFace",
+           "load_retinaface"]

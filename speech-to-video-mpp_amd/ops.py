@@ -106,7 +106,7 @@ class Workspace:
         if nbytes <= 0:
             return None, 0
         if self.buf.numel() < nbytes:
-            if torch.cuda.is_current_stream_capturing():
+            if torch.device(self.device).type == "cuda" and torch.cuda.is_current_stream_capturing():
                 raise _lib.S2VError("workspace must be sized by an eager run before graph capture")
             self.buf = torch.empty(int(nbytes * 1.25) + 256, dtype=torch.uint8, device=self.device)
         return self.buf.data_ptr(), self.buf.numel()
@@ -602,7 +602,7 @@ class NoiseCounter:
 
     def bump(self, ctx: Ctx) -> torch.Tensor:
         if self.t is None:
-            if torch.cuda.is_current_stream_capturing():
+            if ctx.device.type == "cuda" and torch.cuda.is_current_stream_capturing():
                 raise _lib.S2VError("noise counter must be created by an eager run before graph capture")
             self.t = torch.zeros(1, dtype=torch.int64, device=ctx.device)
         check(ctx.lib.s2v_counter_add(self.t.data_ptr(), 1, ctx.stream), "s2v_counter_add")

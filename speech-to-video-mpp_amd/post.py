@@ -26,7 +26,11 @@ MASK_COLORMAP = [0] * 10 + [255, 255, 255] + [0] * 6          # face_parsing.py:
 PROCESS_MM = [0] + [255] * 12 + [0] * 6                        # face_parsing.py:39 (process default)
 MOUTH_MM = [0] * 10 + [255, 255, 255] + [0] * 6                # inference.py:304
 
-RS_U8, RS_F32, RS_F32_TO_U8, RS_U8_EQ255 = range(4)
+RS_U8, RS_F32, RS_F32_TO_U8, RS_U8_EQ255, RS_F64 = range(5)
+_RS_IN = {RS_U8: torch.uint8, RS_F32: torch.float32, RS_F32_TO_U8: torch.float32, RS_U8_EQ255: torch.uint8,
+          RS_F64: torch.float64}
+_RS_OUT = {RS_U8: torch.uint8, RS_F32: torch.float32, RS_F32_TO_U8: torch.uint8, RS_U8_EQ255: torch.float32,
+           RS_F64: torch.float64}
 
 _CTX = {}
 
@@ -62,18 +66,19 @@ def _hwc(t: torch.Tensor):
     return n, h, w, c, sh, sn
 
 
-def resize_linear(x: torch.Tensor, dsize, out: torch.Tensor | None = None, mode: int | None = None):
+def resize_linear(x: torch.Tensor, dsize, out: torch.Tensor | None = None, mode: int | None = None, fxfy=None):
     """cv2.resize(x, dsize=(W, H), interpolation=INTER_LINEAR) on a device image ([H,W], [H,W,C] or a
-    batch [N,H,W,C], uint8 or float32).  ``out`` may be a view into a larger frame.  mode (default
-    by dtype): RS_U8, RS_F32, RS_F32_TO_U8 (np.uint8 of the float result), RS_U8_EQ255 (1.0 where
-    the resized uint8 value is 255, else 0)."""
+    batch [N,H,W,C], uint8, float32 or float64).  ``out`` may be a view into a larger frame.  mode
+    (default by dtype): RS_U8, RS_F32, RS_F32_TO_U8 (np.uint8 of the float result), RS_U8_EQ255
+    (1.0 where the resized uint8 value is 255, else 0), RS_F64.  ``fxfy``: cv2.resize(x, (0, 0),
+    fx, fy) (dsize must then be (round(w fx), round(h fy)); the factors themselves scale)."""
     W, H = dsize
     if mode is None:
-        mode = RS_U8 if x.dtype == torch.uint8 else RS_F32
-    if x.dtype != (torch.uint8 if mode in (RS_U8, RS_U8_EQ255) else torch.float32):
+        mode = {torch.uint8: RS_U8, torch.float64: RS_F64}.get(x.dtype, RS_F32)
+    if x.dtype != _RS_IN[mode]:
         raise TypeError(f"resize_linear: mode {mode} does not take {x.dtype}")
     n, h, w, c, xrs, xis = _hwc(x)
-    odt = torch.uint8 if mode in (RS_U8, RS_F32_TO_U8) else torch.float32
+    odt = _RS_OUT[mode]
     if out is None:
         shape = {2: (H, W), 3: (H, W, c)}.get(x.dim(), (n, H, W, c))
         out = torch.empty(shape, dtype=odt, device=x.device)
@@ -81,6 +86,10 @@ def resize_linear(x: torch.Tensor, dsize, out: torch.Tensor | None = None, mode:
     if (on, oh, ow, oc) != (n, H, W, c) or out.dtype != odt:
         raise ValueError(f"resize_linear: out {tuple(out.shape)} {out.dtype} != {(n, H, W, c)} {odt}")
     ctx = _ctx(x.device)
+    if fxfy is not None:
+        check(ctx.lib.s2v_resize_linear_fxfy(x.data_ptr(), n, h, w, c, xrs, xis, out.data_ptr(), H, W, yrs, yis, mode,
+                                             float(fxfy[0]), float(fxfy[1]), ctx.stream), "s2v_resize_linear_fxfy")
+        return out
     check(ctx.lib.s2v_resize_linear(x.data_ptr(), n, h, w, c, xrs, xis, out.data_ptr(), H, W, yrs, yis, mode,
                                     ctx.stream), "s2v_resize_linear")
     return out

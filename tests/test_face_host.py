@@ -99,3 +99,59 @@ def test_gaussian_kernel_and_blur():
 def test_convert_scale_abs_rounding():
     x = np.array([-3.5, -0.5, 0.5, 1.5, 2.5, 254.5, 300.0], np.float32)
     assert face.convert_scale_abs(x).tolist() == [4, 0, 0, 2, 2, 254, 255]
+
+
+# ----------------------------------------------------------------------------- product host logic
+def test_product_alignment_and_nms_match_reference(golden):
+    from s2v_amd import face as pface
+    g = golden("face_goldens")
+    for size in (512, 2048):
+        ref5 = pface.get_reference_facial_points((size, size), 0.25, (0, 0), True)
+        assert np.array_equal(ref5, g[f"ref5_{size}"])
+        for i, pts in enumerate(FACE_LANDMARKS):
+            tfm, tfm_inv = pface.similarity_transforms(np.array(pts), ref5)
+            assert np.array_equal(tfm, g[f"tfm_{i}_{size}"]) and np.array_equal(tfm_inv, g[f"tfm_inv_{i}_{size}"])
+    # the device hands over the thresholded candidates in prior order: same NMS result
+    loc, conf, lm = retina_head_outputs()
+    pr = face.prior_box(FACE_IMG_HW)
+    h, w = FACE_IMG_HW
+    boxes = (face.decode(torch.from_numpy(loc), pr, face.CFG["variance"]) * torch.Tensor([w, h, w, h])).numpy()
+    lms = (face.decode_landm(torch.from_numpy(lm), pr, face.CFG["variance"]) * torch.Tensor([w, h] * 5)).numpy()
+    keep = np.where(conf[:, 1] > 0.9)[0]
+    dets, lmk = pface.nms_postprocess(boxes[keep], conf[keep, 1], lms[keep])
+    assert np.array_equal(dets, g["det_dets"]) and np.array_equal(lmk, g["det_landms"])
+
+
+def test_paste_window_bounds_the_warped_crop():
+    from s2v_amd import face as pface
+    rng = np.random.default_rng(1)
+    for S, (H, W), pts in ((64, (90, 120), [[30, 52, 41, 33, 50], [40, 41, 52, 63, 62]]),
+                           (32, (200, 180), [[20, 150, 90, 30, 140], [30, 35, 100, 160, 170]])):
+        ref5 = pface.get_reference_facial_points((S, S), 0.25, (0, 0), True)
+        _, tfm_inv = pface.similarity_transforms(np.array(pts, np.float64), ref5)
+        mask = rng.random((S, S)).astype(np.float32) + 0.01
+        warped = face.warp_affine(mask, tfm_inv, (W, H))
+        y0, x0, wh, ww = pface.paste_window(tfm_inv, S, H, W)
+        outside = np.ones((H, W), bool)
+        outside[y0:y0 + wh, x0:x0 + ww] = False
+        assert (warped[outside] == 0).all() and (warped[~outside] > 0).any()
+
+
+def test_face_entry_points_reject_bad_arguments():
+    from s2v_amd import _lib
+    lib = _lib.load()
+    img = np.zeros((8, 8, 3), np.uint8)
+    out = np.zeros((8, 8, 3), np.uint8)
+    M = np.zeros(6)
+    p = lambda a: a.ctypes.data  # noqa: E731
+    assert lib.s2v_warp_affine(p(img), 1, 8, 8, 3, 24, 192, 3, p(M), p(out), 8, 8, 24, 192, None) == -1
+    assert lib.s2v_warp_affine(p(img), 1, 8, 8, 3, 8, 192, 0, p(M), p(out), 8, 8, 24, 192, None) == -1
+    heads = (_lib.ctypes.c_void_p * 3)(p(img), p(img), p(img))
+    hs = (_lib.ctypes.c_int * 3)(13, 7, 4)
+    ws = (_lib.ctypes.c_int * 3)(15, 8, 5)                     # 120 / 32 -> 4, not 5
+    cand = np.zeros(16 * 1000, np.float32)
+    cnt = np.zeros(1, np.int32)
+    assert lib.s2v_retina_decode(heads, hs, ws, 32, 100, 120, 0.9, p(cand), p(cnt), 1000, None) == -1
+    assert b"level 2" in lib.s2v_last_error()
+    assert lib.s2v_gaussian_blur(p(img), 0, 8, 8, 0, p(M), 4, p(out), 1, 2, p(out), 1 << 20, None) == -1   # even ksize
+    assert lib.s2v_maxpool2d_nhwc(p(cand), 1, 8, 8, 6, 3, 2, 1, p(cand), 4, 4, None) == -1                 # c % 4
