@@ -146,6 +146,13 @@ def test_retinaface_forward_matches_oracle(retina, prec):
     assert torch.allclose(conf.sum(-1).cpu(), torch.ones(1, P), atol=1e-6)
 
 
+def _threshold(conf, frac):
+    """A confidence threshold passing about ``frac`` of the anchors (at least one): synthetic weights
+    saturate many scores, so pick a value strictly below a distinct score."""
+    v = np.unique(conf[:, 1].numpy())
+    return float(v[max(0, len(v) - 1 - max(1, int(len(v) * frac)))])
+
+
 def test_retinaface_detect_matches_oracle_postprocess(retina):
     from s2v_amd import face
     det = face.RetinaFaceDetection(device=DEV, net=retina)
@@ -153,7 +160,7 @@ def test_retinaface_detect_matches_oracle_postprocess(retina):
     maps = det.head_maps(torch.from_numpy(img).to(DEV))
     from s2v_amd.models import retina_outputs
     loc, conf, lms = (t[0].cpu() for t in retina_outputs(face._ctx(DEV), maps, 150, 190))
-    thr = float(np.quantile(conf[:, 1].numpy(), 0.97))          # synthetic weights: a few % of anchors pass
+    thr = _threshold(conf, 0.03)                                 # synthetic weights: a few % of anchors pass
     dets, lmk = det.detect(img, confidence_threshold=thr)
     rd, rl = OF.postprocess(loc, conf, lms, 150, 190, confidence_threshold=thr)
     assert len(dets) == len(rd) and len(dets) > 0
@@ -171,7 +178,7 @@ def test_retinaface_detect_large_frame_branch(retina):
     maps = det.head_maps(torch.from_numpy(small).to(DEV))
     from s2v_amd.models import retina_outputs
     loc, conf, lms = (t[0].cpu() for t in retina_outputs(face._ctx(DEV), maps, *small.shape[:2]))
-    thr = float(np.quantile(conf[:, 1].numpy(), 0.995))
+    thr = _threshold(conf, 0.005)
     dets, lmk = det.detect(img, confidence_threshold=thr)
     rd, rl = OF.postprocess(loc, conf, lms, *small.shape[:2], ss=ss, confidence_threshold=thr)
     assert len(dets) == len(rd)
@@ -221,7 +228,7 @@ def _oracle_run(enh, img, ori, trace, of_dev, ef_dev, **kw):
     out, of, ef = OF.enhance_process(img, ori, detect=lambda im: (trace["dets"], trace["landms"]),
                                      facegan=lambda f: next(efs), parse=lambda f: next(masks),
                                      sr=lambda im: img_sr, use_sr=enh.use_sr, in_size=enh.in_size,
-                                     blend=OP.laplacian_pyramid_blending_with_mask, **kw)
+                                     blend=OP.laplacian_blend, **kw)
     assert len(of) == len(of_dev) == 2
     for a, b in zip(of, of_dev):
         assert np.array_equal(a, b.cpu().numpy())                 # warp_and_crop_face bit-exact
