@@ -102,3 +102,37 @@ def retina_head_outputs(hw=FACE_IMG_HW):
     s = np.where(u > 0.92, 0.9 + 0.1 * (u - 0.92) / 0.08, 0.95 * u)
     conf = np.stack([1.0 - s, s], 1).astype(np.float32)
     return loc, conf, lm
+
+
+# ----------------------------------------------------------------------------- media fixtures
+def write_wav(path, rate=44100, channels=2, seconds=1.0, freq=440.0, amp=0.5):
+    """PCM16 .wav with a sine (left) and its half (right), like examples/audio/1.wav's format."""
+    import wave
+    t = np.arange(int(rate * seconds)) / rate
+    left = amp * np.sin(2 * np.pi * freq * t)
+    chans = [left, 0.5 * left][:channels]
+    pcm = np.clip(np.round(np.stack(chans, 1) * 32767), -32768, 32767).astype("<i2")
+    with wave.open(str(path), "wb") as w:
+        w.setnchannels(channels)
+        w.setsampwidth(2)
+        w.setframerate(rate)
+        w.writeframes(pcm.tobytes())
+    return path
+
+
+def write_mp4_header(path, width=320, height=240, frames=30, timescale=12800, duration=15360):
+    """A minimal ISO BMFF file with one video track header (tkhd / mdhd / hdlr / stts), no media."""
+    import struct
+
+    def box(t, body):
+        return struct.pack(">I4s", 8 + len(body), t.encode()) + body
+    tkhd = bytes(4) + bytes(20) + bytes(8) + bytes(8) + bytes(36) + struct.pack(">II", width << 16, height << 16)
+    mdhd = bytes(4) + bytes(8) + struct.pack(">II", timescale, duration) + bytes(4)
+    hdlr = bytes(4) + bytes(4) + b"vide" + bytes(12) + b"VideoHandler\x00"
+    stts = bytes(4) + struct.pack(">III", 1, frames, duration // frames)
+    stbl = box("stbl", box("stts", stts))
+    mdia = box("mdia", box("mdhd", mdhd) + box("hdlr", hdlr) + box("minf", stbl))
+    moov = box("moov", box("trak", box("tkhd", tkhd) + mdia))
+    with open(path, "wb") as f:
+        f.write(box("ftyp", b"isom" + bytes(4)) + moov)
+    return path
