@@ -186,7 +186,8 @@ __global__ void splitk_reduce(ConvArgs a, int batch) {
 
 // Epilogue of 4 consecutive output channels [n, n + 4) of row m as one 16-byte store (host
 // guarantees 16-byte aligned rows: ycs, res_cs % 4 == 0; n % 4 == 0); per-element otherwise.
-__device__ __forceinline__ void store_epilogue4(const ConvArgs &a, int bidx, int m, int n, f4 v, bool vec) {
+__device__ __forceinline__ void store_epilogue4(const ConvArgs &a, int bidx, int m, int n, f4 v, bool vec,
+                                                bool nt = false) {
     const Epi &e = a.epi;
     if (!vec || e.nc_scale || (e.res && !e.res_simple) || a.y_step > 1) {
         store_epilogue(a, bidx, m, n + 0, v.x);
@@ -208,7 +209,9 @@ __device__ __forceinline__ void store_epilogue4(const ConvArgs &a, int bidx, int
     v.z = apply_act(v.z, e.act, e.alpha);
     v.w = apply_act(v.w, e.act, e.alpha);
     if (e.res && e.res_after) v += r;
-    *(f4 *)(a.y + (long long)bidx * a.y_bs + (long long)m * a.ycs + n) = v;
+    f4 *dst = (f4 *)(a.y + (long long)bidx * a.y_bs + (long long)m * a.ycs + n);
+    if (nt) __builtin_nontemporal_store(v, dst);
+    else *dst = v;
 }
 
 // Small-K direct convolution (K = kh*kw*cin <= 64: the 4-channel image-input layers and the
@@ -219,6 +222,9 @@ __device__ __forceinline__ void store_epilogue4(const ConvArgs &a, int bidx, int
 // tap and channel group; fp32 VALU; 16-byte output stores.  These layers are bound by their
 // output write; the implicit GEMM pads K to 32 per slice and stages every output tile through LDS
 // (3-27 TFLOP/s measured on them).
+#ifndef SMALLK_NT
+#define SMALLK_NT 1      // streaming (non-temporal) output stores: the image-layer outputs exceed L2 / MALL
+#endif
 template <int QPT, int PX>
 __global__ __launch_bounds__(256) void conv_smallk(ConvArgs a, int batch, int tppx, int iters, int vec) {
     extern __shared__ __attribute__((aligned(16))) float wk[];   // [K][cout]
@@ -304,7 +310,7 @@ __global__ __launch_bounds__(256) void conv_smallk(ConvArgs a, int batch, int tp
         for (int p = 0; p < PX; ++p)
 #pragma unroll
             for (int q = 0; q < QPT; ++q)
-                store_epilogue4(a, bidx, mbase + p, 4 * (tq + tppx * q), acc[p][q], vec != 0);
+                store_epilogue4(a, bidx, mbase + p, 4 * (tq + tppx * q), acc[p][q], vec != 0, SMALLK_NT != 0);
     }
 }
 

@@ -6,6 +6,8 @@ place by the two encoder streams, FFC x_l / x_g are channel ranges of the block 
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .. import ops
@@ -14,6 +16,8 @@ from .common import AdainBank, bn_tuple, conv_weight, make_conv
 
 LRELU = 0.1        # LNet.py:91
 LRELU_FFC = 0.01   # FineADAINLama built with nn.LeakyReLU() default (base_blocks.py:369 via :393/:419)
+# FFC products on concurrent side streams (S2V_LNET_BRANCHES=0 serialises them on one stream)
+BRANCHES = os.environ.get("S2V_LNET_BRANCHES", "1") == "1"
 
 AUDIO_CFG = [  # LNet.py:102-120: (stride, padding, residual)
     (1, 1, False), (1, 1, True), (1, 1, True), ((3, 1), 1, False), (1, 1, True), (1, 1, True),
@@ -130,27 +134,63 @@ class FFCLama:
         self.gid = bank.add_group(sd, [(p + "bn_l.", self.cl), (p + "bn_g.", self.cg)])
         self.device = device
 
-    def pre_norm(self, ctx, x: NHWC, y: NHWC):
-        """y <- [l2l(x_l)+g2l(x_g) | l2g(x_l) + spectral(x_g)] (before ADAIN)."""
+    def pre_norm(self, ctx, x: NHWC, y: NHWC, branches=None):
+        """y <- [l2l(x_l)+g2l(x_g) | l2g(x_l) + spectral(x_g)] (before ADAIN).
+
+        The three independent products run as concurrent branches when ``branches`` (two
+        (stream, Ctx) pairs, see Branches) is given: conv_to_l on the calling stream, l2g on the
+        first side stream, the spectral chain st1 -> rfft2 -> fu -> irfft2 on the second; st2 joins
+        them (it accumulates onto l2g's output).  At 12x12 each product fills only a fraction of
+        the 256 CUs, so running them side by side is what fills the chip."""
         b = x.n
-        P = self.h * self.w
         cl, cg, cc, dev = self.cl, self.cg, self.cc, self.device
-        ops.conv2d(ctx, x, self.conv_to_l, y.slice(0, cl))
         yg = y.slice(cl, cg)
-        ops.conv2d(ctx, x.slice(0, cl), self.conv_l2g, yg)
         t1 = NHWC.empty(b, self.h, self.w, cc, dev)
-        ops.conv2d(ctx, x.slice(cl, cg), self.st1, t1, act=ops.ACT_RELU)
         spec = torch.empty((b, self.F, 2 * cc), device=dev)
-        ops.rfft2(ctx, t1, self.fft, spec)                             # rfftn ortho (ffc.py:99-104)
         spec2 = NHWC.empty(b, self.F, 1, 2 * cc, dev)
-        ops.conv2d(ctx, NHWC(spec.view(b, self.F, 1, 2 * cc)), self.fu, spec2, act=ops.ACT_RELU)
         u = NHWC.empty(b, self.h, self.w, cc, dev)
-        ops.irfft2(ctx, spec2.t.view(b, self.F, 2 * cc), self.fft, u, res=t1)   # irfftn + x (ffc.py:120-126, :158)
+
+        def l2g(c):
+            ops.conv2d(c, x.slice(0, cl), self.conv_l2g, yg)
+
+        def spectral(c):
+            ops.conv2d(c, x.slice(cl, cg), self.st1, t1, act=ops.ACT_RELU)
+            ops.rfft2(c, t1, self.fft, spec)                             # rfftn ortho (ffc.py:99-104)
+            ops.conv2d(c, NHWC(spec.view(b, self.F, 1, 2 * cc)), self.fu, spec2, act=ops.ACT_RELU)
+            ops.irfft2(c, spec2.t.view(b, self.F, 2 * cc), self.fft, u, res=t1)   # irfftn + x (ffc.py:120-126, :158)
+
+        if branches is None:
+            ops.conv2d(ctx, x, self.conv_to_l, y.slice(0, cl))
+            l2g(ctx)
+            spectral(ctx)
+        else:
+            branches.run(ctx, lambda c: ops.conv2d(c, x, self.conv_to_l, y.slice(0, cl)), l2g, spectral)
         ops.conv2d(ctx, u, self.st2, yg, res=yg)
 
     def norm(self, ctx, bank: AdainBank, y: NHWC, out: NHWC, res: NHWC | None = None):
         g, bt, ns = bank.gamma_beta(self.gid)
         ops.instnorm(ctx, y, out, g, bt, ns, act=ops.ACT_LRELU, alpha=LRELU_FFC, res=res)
+
+
+class Branches:
+    """Fork / join of independent work on side HIP streams (captured into the same graph when the
+    caller is capturing: the side streams fork from and join back into the calling stream).  Each
+    branch has its own Ctx, so split-K workspaces never alias across concurrent launches."""
+
+    def __init__(self, device, n=2):
+        self.device = torch.device(device)
+        self.side = [(torch.cuda.Stream(self.device), ops.Ctx(self.device)) for _ in range(n)]
+
+    def run(self, ctx, main, *others):
+        cur = torch.cuda.current_stream(self.device)
+        for st, _ in self.side[: len(others)]:
+            st.wait_stream(cur)
+        for (st, c), fn in zip(self.side, others):
+            with torch.cuda.stream(st):
+                fn(c)
+        main(ctx)
+        for st, _ in self.side[: len(others)]:
+            cur.wait_stream(st)
 
 
 class LNetEngine:
@@ -189,6 +229,13 @@ class LNetEngine:
         self.final4 = ConvW(torch.cat([fw, torch.zeros((1,) + tuple(fw.shape[1:]))]),
                             torch.cat([sd[d + "final.model.0.bias"].float(), torch.zeros(1)]), dev, padding=3)
 
+    def _branches(self):
+        if getattr(self, "_br", None) is None:
+            if self.device.type != "cuda":
+                return None
+            self._br = Branches(self.device)
+        return self._br
+
     def forward(self, ctx, audio: torch.Tensor, face6: NHWC, out: NHWC, logits: NHWC | None = None,
                 pad_rgb: bool = False):
         """audio: [B,1,80,16] device tensor; face6: NHWC [B,96,96,6] = [masked | ref];
@@ -225,14 +272,15 @@ class LNetEngine:
         self.bank.run(ctx, z)
         # ---- decoder (LNet.py:67-77)
         cur = cat
+        br = self._branches() if BRANCHES else None
         for lv in self.levels:
             c = lv["c"]
             ya = NHWC.empty(cur.n, cur.h, cur.w, c, dev)
             yb = NHWC.empty(cur.n, cur.h, cur.w, c, dev)
             for l1, l2 in lv["blocks"]:
-                l1.pre_norm(ctx, cur, ya)
+                l1.pre_norm(ctx, cur, ya, br)
                 l1.norm(ctx, self.bank, ya, ya)
-                l2.pre_norm(ctx, ya, yb)
+                l2.pre_norm(ctx, ya, yb, br)
                 l2.norm(ctx, self.bank, yb, cur, res=cur)       # FFCResnetBlock: id + conv2(conv1(x))
             up = lv["up"](ctx, cur)
             skip = skips.pop()
