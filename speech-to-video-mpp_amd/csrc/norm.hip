@@ -204,23 +204,28 @@ __global__ __launch_bounds__(256) void in_apply(const float *__restrict__ x, int
 }
 
 // Vectorised InstanceNorm/ADAIN (c % 4 == 0, 16-byte aligned views): a thread owns 4 channels
-// (one float4) and a pixel phase; 4 independent loads in flight per thread; fp64 partial sums.
-// grid (chunks, ceil(c / 256), n)
+// (one float4) and a pixel phase; a block covers QB = min(64, c / 4) channel quads with
+// 256 / QB pixel phases (so a 128-channel layer keeps every lane busy); 4 independent loads in
+// flight per thread; fp64 partial sums.   grid (chunks, ceil(c / (4 QB)), n)
+__device__ __forceinline__ int in_quads(int c) { return c / 4 < 64 ? c / 4 : 64; }
+
 __global__ __launch_bounds__(256) void in_stats_v(const float *__restrict__ x, int hw, int c, int xcs, int chunks,
                                                   double *__restrict__ part) {
-    const int q4 = threadIdx.x & 63, ph = threadIdx.x >> 6;
-    const int cc = blockIdx.y * 256 + 4 * q4;
+    const int qb = in_quads(c), nph = 256 / qb;
+    const int q4 = threadIdx.x % qb, ph = threadIdx.x / qb;
+    const int cc = (blockIdx.y * qb + q4) * 4;
     const int n = blockIdx.z, ch = blockIdx.x;
     const int per = (hw + chunks - 1) / chunks;
     const int p0 = ch * per, p1 = min(hw, p0 + per);
+    const bool live = ph < nph && cc < c;
     double s[4] = {0.0, 0.0, 0.0, 0.0}, q[4] = {0.0, 0.0, 0.0, 0.0};
-    if (cc < c) {
+    if (live) {
         const float *xb = x + (long long)n * hw * xcs + cc;
         int p = p0 + ph;
-        for (; p + 12 < p1; p += 16) {
+        for (; p + 3 * nph < p1; p += 4 * nph) {
             float4 v[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) v[u] = *(const float4 *)(xb + (long long)(p + 4 * u) * xcs);
+            for (int u = 0; u < 4; ++u) v[u] = *(const float4 *)(xb + (long long)(p + nph * u) * xcs);
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const double a = v[u].x, b = v[u].y, d = v[u].z, e = v[u].w;
@@ -228,25 +233,28 @@ __global__ __launch_bounds__(256) void in_stats_v(const float *__restrict__ x, i
                 q[0] += a * a; q[1] += b * b; q[2] += d * d; q[3] += e * e;
             }
         }
-        for (; p < p1; p += 4) {
+        for (; p < p1; p += nph) {
             const float4 v = *(const float4 *)(xb + (long long)p * xcs);
             const double a = v.x, b = v.y, d = v.z, e = v.w;
             s[0] += a; s[1] += b; s[2] += d; s[3] += e;
             q[0] += a * a; q[1] += b * b; q[2] += d * d; q[3] += e * e;
         }
     }
-    __shared__ double red[4][64][8];
+    __shared__ double red[256][8];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        red[ph][q4][j] = s[j];
-        red[ph][q4][4 + j] = q[j];
+        red[threadIdx.x][j] = s[j];
+        red[threadIdx.x][4 + j] = q[j];
     }
     __syncthreads();
     if (ph == 0 && cc < c) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const double ss = red[0][q4][j] + red[1][q4][j] + red[2][q4][j] + red[3][q4][j];
-            const double qq = red[0][q4][4 + j] + red[1][q4][4 + j] + red[2][q4][4 + j] + red[3][q4][4 + j];
+            double ss = 0.0, qq = 0.0;
+            for (int k = 0; k < nph; ++k) {
+                ss += red[k * qb + q4][j];
+                qq += red[k * qb + q4][4 + j];
+            }
             const long long o = (((long long)n * c + cc + j) * chunks + ch) * 2;
             part[o] = ss;
             part[o + 1] = qq;
@@ -254,32 +262,64 @@ __global__ __launch_bounds__(256) void in_stats_v(const float *__restrict__ x, i
     }
 }
 
+// The block first folds the chunk partials of its channels cooperatively (each pixel phase sums a
+// stride of the chunks, LDS combine), computes (mul, add) per channel once, then applies.
 __global__ __launch_bounds__(256) void in_apply_v(const float *__restrict__ x, int hw, int c, int xcs,
                                                   const float *__restrict__ gamma, const float *__restrict__ beta,
                                                   int gb_ns, float eps, int act, float alpha, const float *res,
                                                   int res_cs, float *y, int ycs, const double *__restrict__ part,
                                                   int chunks, int achunks) {
-    const int q4 = threadIdx.x & 63, ph = threadIdx.x >> 6;
-    const int cc = blockIdx.y * 256 + 4 * q4;
+    const int qb = in_quads(c), nph = 256 / qb;
+    const int q4 = threadIdx.x % qb, ph = threadIdx.x / qb;
+    const int cc = (blockIdx.y * qb + q4) * 4;
     const int n = blockIdx.z;
-    if (cc >= c) return;
+    const bool live = ph < nph && cc < c;
+    __shared__ double red[256][8];
+    __shared__ float coef[64][8];
+    {
+        double s[4] = {0.0, 0.0, 0.0, 0.0}, q[4] = {0.0, 0.0, 0.0, 0.0};
+        if (live) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const long long o = ((long long)n * c + cc + j) * chunks * 2;
+                for (int i = ph; i < chunks; i += nph) {
+                    s[j] += part[o + 2 * i];
+                    q[j] += part[o + 2 * i + 1];
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            red[threadIdx.x][j] = s[j];
+            red[threadIdx.x][4 + j] = q[j];
+        }
+    }
+    __syncthreads();
+    if (ph == 0 && cc < c) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            double sm = 0.0, sq = 0.0;
+            for (int k = 0; k < nph; ++k) {
+                sm += red[k * qb + q4][j];
+                sq += red[k * qb + q4][4 + j];
+            }
+            const double mean = sm / hw;
+            double var = sq / hw - mean * mean;
+            if (var < 0.0) var = 0.0;
+            const float rstd = 1.f / sqrtf((float)(var + (double)eps));   // fp64 moments, fp32 root
+            const float g = gamma ? 1.f + gamma[(long long)n * gb_ns + cc + j] : 1.f;
+            const float b = beta ? beta[(long long)n * gb_ns + cc + j] : 0.f;
+            coef[q4][j] = rstd * g;                                  // (x - mean) * rstd * g + b
+            coef[q4][4 + j] = b - (float)mean * rstd * g;
+        }
+    }
+    __syncthreads();
+    if (!live) return;
     float mul[4], add[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        double s = 0.0, q = 0.0;
-        const long long o = ((long long)n * c + cc + j) * chunks * 2;
-        for (int i = 0; i < chunks; ++i) {
-            s += part[o + 2 * i];
-            q += part[o + 2 * i + 1];
-        }
-        const double mean = s / hw;
-        double var = q / hw - mean * mean;
-        if (var < 0.0) var = 0.0;
-        const float rstd = 1.f / sqrtf((float)(var + (double)eps));   // fp64 moments, fp32 root
-        const float g = gamma ? 1.f + gamma[(long long)n * gb_ns + cc + j] : 1.f;
-        const float b = beta ? beta[(long long)n * gb_ns + cc + j] : 0.f;
-        mul[j] = rstd * g;                                   // (x - mean) * rstd * g + b
-        add[j] = b - (float)mean * rstd * g;
+        mul[j] = coef[q4][j];
+        add[j] = coef[q4][4 + j];
     }
     const int per = (hw + achunks - 1) / achunks;
     const int p0 = blockIdx.x * per, p1 = min(hw, p0 + per);
@@ -287,7 +327,7 @@ __global__ __launch_bounds__(256) void in_apply_v(const float *__restrict__ x, i
     float *yb = y + (long long)n * hw * ycs + cc;
     const float *rb = res ? res + (long long)n * hw * res_cs + cc : nullptr;
 #pragma unroll 4
-    for (int p = p0 + ph; p < p1; p += 4) {
+    for (int p = p0 + ph; p < p1; p += nph) {
         const float4 v = *(const float4 *)(xb + (long long)p * xcs);
         float4 o;
         o.x = apply_act(fmaf(v.x, mul[0], add[0]), act, alpha);
@@ -450,7 +490,8 @@ extern "C" int s2v_instnorm_adain(const float *x, int n, int h, int w, int c, in
             set_error("instnorm: workspace of %zu bytes required", needv);
             return S2V_E_WORKSPACE;
         }
-        const unsigned cq = cdiv(c, 256);
+        const int qb = c / 4 < 64 ? c / 4 : 64;
+        const unsigned cq = cdiv(c, 4 * qb);
         in_stats_v<<<dim3(kv, cq, n), 256, 0, s>>>(x, hw, c, xcs, kv, (double *)ws);
         int rc = check_launch("in_stats");
         if (rc) return rc;

@@ -6,8 +6,8 @@
 set -e
 set -o pipefail
 OUT=${OUT:-gpurun_out/prof}
-PMC_WORKLOADS=${PMC_WORKLOADS:-lipsync}
-STATS_WORKLOADS=${STATS_WORKLOADS:-"lipsync lnet pipeline enhance mouth"}
+PMC_WORKLOADS=${PMC_WORKLOADS-lipsync}
+STATS_WORKLOADS=${STATS_WORKLOADS-"lipsync lnet pipeline enhance mouth"}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 for w in $STATS_WORKLOADS; do
@@ -24,4 +24,5 @@ for w in $PMC_WORKLOADS; do
     echo "pmc $w $c done"
   done
   python3 tools/pmc_traffic.py "$OUT/pmc_${w}_FETCH_SIZE" "$OUT/pmc_${w}_WRITE_SIZE" "$OUT/pmc_$w.json" "$w"
+  if [ -f "$OUT/stats_$w.csv" ]; then python3 tools/hbm_report.py "$OUT/pmc_$w.json" "$OUT/stats_$w.csv" "$OUT/hbm_$w.json" "$w"; fi
 done
