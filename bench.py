@@ -143,14 +143,20 @@ def live_roofline(forward, workload="lipsync"):
     peak = X3_PEAK_TFLOPS if "conv_igemm_x3" in dom else FP32_MFMA_PEAK_TFLOPS
     total_ms = sum(v["ms"] for v in per.values())
     total_flops = sum(v["flops"] for v in per.values())
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", f"pmc_r01_{workload}.json")
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            traffic = json.load(f).get("per_launch_bytes", {}).get(dom)
+    # HBM bytes per launch of the same symbol from the PMC passes of this workload (tools/gpu_profile.sh:
+    # separate FETCH_SIZE / WRITE_SIZE runs of this bench command; the newest round's file wins)
+    traffic, traffic_src = None, None
+    for rnd in ("r02", "r01"):
+        pmc = os.path.join(ROOT, "profiles", f"pmc_{rnd}_{workload}.json")
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                traffic = json.load(f).get("per_launch_bytes", {}).get(dom)
+            if traffic is not None:
+                traffic_src = os.path.relpath(pmc, ROOT)
+                break
     return {
         "bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
-        "frac": round(achieved / peak, 4), "traffic": traffic,
+        "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
         "kernel": dom, "launches": d["launches"], "avg_launch_us": round(1e3 * d["ms"] / d["launches"], 2),
         "flops_per_launch": d["flops"] / d["launches"],
         "conv_family": {"achieved": round(total_flops / (total_ms * 1e-3) / 1e12, 2),

@@ -491,6 +491,113 @@ static void launch_small(const ConvArgs &a, int batch, bool cpar, hipStream_t s)
     }
 }
 
+
+// Halo-tiled direct conv for Cout <= 4 heads with a wide square filter (DNet's 7x7 64 -> 3 tanh
+// head at 256^2, LNet's 7x7 64 -> 3 sigmoid head): a block owns an 8 x 128 output tile; per chunk
+// of 4 input channels it stages the (8 + KS - 1) x (128 + KS - 1) input halo once in LDS (planar
+// per channel), and each thread computes 4 horizontally adjacent pixels x CO outputs from 16-byte
+// LDS row reads, so every staged value feeds up to 4 * KS taps.  The per-pixel gather of
+// conv_small_cpar re-read each input pixel KS^2 times from L1/L2 (DNet head: 1.5 ms per 16 frames
+// at 185 GB/s).  Filter values are block-uniform (scalar loads).  fp32 VALU, exact products.
+#ifndef HALO_SMALL
+#define HALO_SMALL 1
+#endif
+template <int CO, int KS>
+__global__ __launch_bounds__(256) void conv_halo_small(ConvArgs a, int tiles_x, int tiles_y) {
+    constexpr int TH = 8, PX = 4, TW = 32 * PX;
+    constexpr int IH = TH + KS - 1, IW = TW + KS - 1, IWP = (IW + 3) / 4 * 4;
+    constexpr int NV = (PX + KS - 1 + 3) / 4;                 // float4 row reads per (channel, ky)
+    static_assert(4 * 31 + 4 * NV <= IWP, "halo row reads stay inside the padded LDS row");
+    __shared__ __attribute__((aligned(16))) float tile[4][IH][IWP];
+    const int tid = threadIdx.x, r = tid >> 5, cg = tid & 31;
+    int t = blockIdx.x;
+    const int txi = t % tiles_x;
+    t /= tiles_x;
+    const int tyi = t % tiles_y, img = t / tiles_y;
+    const int oy0 = tyi * TH, ox0 = txi * TW;
+    const float *xb = a.x + (long long)img * a.h * a.w * a.xcs;
+    const float *__restrict__ wt = a.wt;
+    float acc[PX][CO];
+#pragma unroll
+    for (int p = 0; p < PX; ++p)
+#pragma unroll
+        for (int o = 0; o < CO; ++o) acc[p][o] = 0.f;
+    const bool refl = a.pad_mode == S2V_PAD_REFLECT;
+    for (int c0 = 0; c0 < a.cin; c0 += 4) {
+        __syncthreads();                                      // the previous chunk has been consumed
+        for (int e = tid; e < IH * IW; e += 256) {
+            const int iy = e / IW, ix = e - iy * IW;
+            int gy = oy0 + iy - a.ph, gx = ox0 + ix - a.pw;
+            if (refl) {
+                gy = reflect_idx(gy, a.h);
+                gx = reflect_idx(gx, a.w);
+            }
+            // halo rows / columns past the image (tiles overhanging the bottom / right edge, or
+            // beyond a single reflection) feed only outputs that are never stored
+            const bool ok = (unsigned)gy < (unsigned)a.h && (unsigned)gx < (unsigned)a.w;
+            f4 v = f4{0.f, 0.f, 0.f, 0.f};
+            if (ok) v = *(const f4 *)(xb + ((long long)gy * a.w + gx) * a.xcs + c0);
+            tile[0][iy][ix] = v.x;
+            tile[1][iy][ix] = v.y;
+            tile[2][iy][ix] = v.z;
+            tile[3][iy][ix] = v.w;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+#pragma unroll
+            for (int ky = 0; ky < KS; ++ky) {
+                float row[4 * NV];
+                const float *src = &tile[c][r + ky][4 * cg];
+#pragma unroll
+                for (int j = 0; j < NV; ++j) *(f4 *)&row[4 * j] = *(const f4 *)(src + 4 * j);
+#pragma unroll
+                for (int kx = 0; kx < KS; ++kx) {
+                    const long long k = (long long)(ky * KS + kx) * a.cin + c0 + c;
+                    float wv[CO];
+#pragma unroll
+                    for (int o = 0; o < CO; ++o) wv[o] = wt[(long long)o * a.kpad + k];
+#pragma unroll
+                    for (int p = 0; p < PX; ++p)
+#pragma unroll
+                        for (int o = 0; o < CO; ++o) acc[p][o] = fmaf(row[p + kx], wv[o], acc[p][o]);
+                }
+            }
+        }
+    }
+    const int oy = oy0 + r;
+    if (oy >= a.oh) return;
+#pragma unroll
+    for (int p = 0; p < PX; ++p) {
+        const int ox = ox0 + 4 * cg + p;
+        if (ox >= a.ow) continue;
+        const int m = (img * a.oh + oy) * a.ow + ox;
+#pragma unroll
+        for (int o = 0; o < CO; ++o) store_epilogue(a, 0, m, o, acc[p][o]);
+    }
+}
+
+// The halo kernel serves plain stride-1 square-filter heads: direct input, zero or reflect
+// padding (pad < filter), no prologue scaling, one shared filter, 16-byte channel quads.
+static int halo_ks(const s2v_conv_params *p) {
+    const int batch = p->batch > 0 ? p->batch : 1;
+    if (p->cout > 4 || p->kh != p->kw || (p->kh != 3 && p->kh != 5 && p->kh != 7)) return 0;
+    if (p->in_mode != S2V_IN_DIRECT || p->sh != 1 || p->sw != 1 || p->dh != 1 || p->dw != 1) return 0;
+    if (p->in_scale || p->pre_act || p->w_bs || batch != 1 || p->b_kn || p->out_step > 1) return 0;
+    if (p->ph >= p->kh || p->pw >= p->kw || p->cin % 4 || p->xcs % 4 || ((uintptr_t)p->x % 16)) return 0;
+    if (p->pad_mode == S2V_PAD_REFLECT && (p->ph >= p->h || p->pw >= p->w)) return 0;
+    return p->kh;
+}
+
+template <int CO>
+static void launch_halo(const ConvArgs &a, int ks, hipStream_t s) {
+    const int tiles_x = (int)cdiv(a.ow, 128), tiles_y = (int)cdiv(a.oh, 8);
+    const unsigned grid = (unsigned)((long long)a.n * tiles_x * tiles_y);
+    if (ks == 3) conv_halo_small<CO, 3><<<grid, 256, 0, s>>>(a, tiles_x, tiles_y);
+    else if (ks == 5) conv_halo_small<CO, 5><<<grid, 256, 0, s>>>(a, tiles_x, tiles_y);
+    else conv_halo_small<CO, 7><<<grid, 256, 0, s>>>(a, tiles_x, tiles_y);
+}
+
 // ------------------------------------------------------------------ host side
 struct TileCfg {
     int bm, bn, wm, nw, ks, pf;   // nw / ks / pf: waves, K-slices per stage, prefetch sets (x3 kernel)
@@ -849,6 +956,12 @@ extern "C" int s2v_conv2d_plan(const s2v_conv_params *p, int *out6) {
         out6[3] = smallk_px(M); out6[4] = 0; out6[5] = 1;
         return 0;
     }
+    if (pl.tile < 0 && HALO_SMALL && halo_ks(p)) {
+        out6[0] = 0; out6[1] = p->cout < 4 ? p->cout : 4;
+        out6[2] = 0; out6[3] = 0;
+        out6[4] = 1000 + halo_ks(p); out6[5] = 1;          // conv_halo_small<CO, KS>
+        return 0;
+    }
     if (pl.tile < 0) {
         const bool cpar = (p->cin % 4 == 0) && (p->xcs % 4 == 0) && (((uintptr_t)p->x % 16) == 0) &&
                           (p->x_bs % 4 == 0) && (!p->in_scale || (p->in_scale_ns % 4 == 0 &&
@@ -893,6 +1006,15 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
         if (qpt == 1) conv_smallk<1, 1><<<grid, 256, lds, s>>>(a, batch, tppx, iters, vec);
         else conv_smallk<2, 1><<<grid, 256, lds, s>>>(a, batch, tppx, iters, vec);
         return check_launch("conv_smallk");
+    }
+    if (pl.tile < 0 && HALO_SMALL && halo_ks(p)) {
+        switch (p->cout) {
+            case 1: launch_halo<1>(a, halo_ks(p), s); break;
+            case 2: launch_halo<2>(a, halo_ks(p), s); break;
+            case 3: launch_halo<3>(a, halo_ks(p), s); break;
+            default: launch_halo<4>(a, halo_ks(p), s); break;
+        }
+        return check_launch("conv_halo_small");
     }
     if (pl.tile < 0) {
         const bool cpar = (p->cin % 4 == 0) && (p->xcs % 4 == 0) && (((uintptr_t)p->x % 16) == 0) &&

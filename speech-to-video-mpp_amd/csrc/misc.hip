@@ -101,6 +101,24 @@ __global__ __launch_bounds__(256) void pad_reflect_kernel(const float *__restric
     }
 }
 
+// float4 form (c, pitches % 4 == 0, 16-byte aligned): one channel quad per thread
+__global__ __launch_bounds__(256) void pad_reflect4_kernel(const float *__restrict__ x, int n, int h, int w, int c4,
+                                                           int xcs, int pt, int pl, int oh, int ow,
+                                                           float *__restrict__ y, int ycs) {
+    const long long total = (long long)n * oh * ow * c4;
+    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+        const int cq = (int)(e % c4);
+        long long t = e / c4;
+        const int ox = (int)(t % ow);
+        t /= ow;
+        const int oy = (int)(t % oh);
+        const int nn = (int)(t / oh);
+        const int iy = reflect_idx(oy - pt, h), ix = reflect_idx(ox - pl, w);
+        *(float4 *)(y + (((long long)nn * oh + oy) * ow + ox) * ycs + 4 * cq) =
+            *(const float4 *)(x + (((long long)nn * h + iy) * w + ix) * xcs + 4 * cq);
+    }
+}
+
 // ------------------------------------------------------------------ attention
 // one block per (b, head); K padded to 65 floats per row (conflict-free column reads)
 __global__ __launch_bounds__(256) void attention_kernel(const float *__restrict__ q, const float *__restrict__ k,
@@ -494,8 +512,12 @@ extern "C" int s2v_pad_reflect(const float *x, int n, int h, int w, int c, int x
     S2V_REQUIRE(pt >= 0 && pb >= 0 && pl >= 0 && pr >= 0 && pt < h && pb < h && pl < w && pr < w,
                 "pad_reflect: padding must be < input size");
     const int oh = h + pt + pb, ow = w + pl + pr;
-    pad_reflect_kernel<<<grid_for((long long)n * oh * ow * c), 256, 0, (hipStream_t)stream>>>(
-        x, n, h, w, c, xcs, pt, pl, oh, ow, y, ycs);
+    if (c % 4 == 0 && xcs % 4 == 0 && ycs % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0)
+        pad_reflect4_kernel<<<grid_for((long long)n * oh * ow * (c / 4)), 256, 0, (hipStream_t)stream>>>(
+            x, n, h, w, c / 4, xcs, pt, pl, oh, ow, y, ycs);
+    else
+        pad_reflect_kernel<<<grid_for((long long)n * oh * ow * c), 256, 0, (hipStream_t)stream>>>(
+            x, n, h, w, c, xcs, pt, pl, oh, ow, y, ycs);
     return check_launch("pad_reflect");
 }
 

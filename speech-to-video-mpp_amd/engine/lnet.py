@@ -18,6 +18,8 @@ LRELU = 0.1        # LNet.py:91
 LRELU_FFC = 0.01   # FineADAINLama built with nn.LeakyReLU() default (base_blocks.py:369 via :393/:419)
 # FFC products on concurrent side streams (S2V_LNET_BRANCHES=0 serialises them on one stream)
 BRANCHES = os.environ.get("S2V_LNET_BRANCHES", "1") == "1"
+# FFC 3x3 reflect convs over a pre-padded input (S2V_LNET_PREPAD=0: reflect addressing in the gather)
+PREPAD = os.environ.get("S2V_LNET_PREPAD", "1") == "1"
 
 AUDIO_CFG = [  # LNet.py:102-120: (stride, padding, residual)
     (1, 1, False), (1, 1, True), (1, 1, True), ((3, 1), 1, False), (1, 1, True), (1, 1, True),
@@ -114,7 +116,9 @@ class FFCLama:
         self.cg = int(c * 0.75)
         self.cl = c - self.cg
         self.cc = self.cg // 2
-        rp = dict(padding=1, pad_mode=ops.PAD_REFLECT)
+        # reflect-padded 3x3 convs run as valid convs over one reflect-padded copy of the block input
+        # (PREPAD): no per-tap reflection in the gather, so they take the buffer-load A path
+        rp = dict(padding=0) if PREPAD else dict(padding=1, pad_mode=ops.PAD_REFLECT)
         w_l2l, w_g2l = sd[f + "convl2l.weight"].float(), sd[f + "convg2l.weight"].float()
         self.conv_to_l = ConvW(torch.cat([w_l2l, w_g2l], 1), None, device, **rp)   # l2l(x_l) + g2l(x_g)
         self.conv_l2g = ConvW(sd[f + "convl2g.weight"], None, device, **rp)
@@ -150,8 +154,13 @@ class FFCLama:
         spec2 = NHWC.empty(b, self.F, 1, 2 * cc, dev)
         u = NHWC.empty(b, self.h, self.w, cc, dev)
 
+        xr = x
+        if PREPAD:
+            xr = NHWC.empty(b, self.h + 2, self.w + 2, x.c, dev)
+            ops.pad_reflect(ctx, x, xr, (1, 1, 1, 1))
+
         def l2g(c):
-            ops.conv2d(c, x.slice(0, cl), self.conv_l2g, yg)
+            ops.conv2d(c, xr.slice(0, cl), self.conv_l2g, yg)
 
         def spectral(c):
             ops.conv2d(c, x.slice(cl, cg), self.st1, t1, act=ops.ACT_RELU)
@@ -160,11 +169,11 @@ class FFCLama:
             ops.irfft2(c, spec2.t.view(b, self.F, 2 * cc), self.fft, u, res=t1)   # irfftn + x (ffc.py:120-126, :158)
 
         if branches is None:
-            ops.conv2d(ctx, x, self.conv_to_l, y.slice(0, cl))
+            ops.conv2d(ctx, xr, self.conv_to_l, y.slice(0, cl))
             l2g(ctx)
             spectral(ctx)
         else:
-            branches.run(ctx, lambda c: ops.conv2d(c, x, self.conv_to_l, y.slice(0, cl)), l2g, spectral)
+            branches.run(ctx, lambda c: ops.conv2d(c, xr, self.conv_to_l, y.slice(0, cl)), l2g, spectral)
         ops.conv2d(ctx, u, self.st2, yg, res=yg)
 
     def norm(self, ctx, bank: AdainBank, y: NHWC, out: NHWC, res: NHWC | None = None):

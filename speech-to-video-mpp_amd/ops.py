@@ -431,6 +431,8 @@ def conv_symbol(ctx: Ctx, p) -> str:
     """Kernel symbol (as rocprofv3 reports it, demangled) the launch of ``p`` runs."""
     bm, bn, wm, avec, bkn, splits, x3, nw, ks, pf = _plan(ctx, p)
     if bm == 0:
+        if bkn >= 1000:
+            return f"void s2v::conv_halo_small<{bn}, {bkn - 1000}>(s2v::ConvArgs, int, int)"
         if wm < 0:
             return f"void s2v::conv_smallk<{-wm}, {avec}>(s2v::ConvArgs, int, int, int, int)"
         if wm:

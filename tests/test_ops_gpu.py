@@ -91,6 +91,13 @@ CONV_CASES = [
     (2, 32, 8, 8, 48, 3, 1, 1, 1, "up2", "zero", 0, 0),
     (2, 64, 6, 7, 32, 3, 2, 1, 1, "transposed", "zero", 0, 0),
     (2, 64, 9, 9, 3, 7, 1, 3, 1, "direct", "zero", 0, 0),     # direct small-N kernel
+    # halo-tiled small-Cout kernel (8 x 128 output tiles): ragged tiles in both directions, reflect
+    # halos, 3 / 5 / 7 filters, 1..4 outputs (DNet's 7x7 64 -> 3 head at 256^2 is the model case)
+    (2, 64, 37, 150, 3, 7, 1, 3, 1, "direct", "zero", 0, 0),
+    (1, 64, 20, 130, 3, 7, 1, 3, 1, "direct", "reflect", 0, 0),
+    (2, 32, 19, 17, 4, 3, 1, 1, 1, "direct", "reflect", 0, 0),
+    (2, 16, 16, 16, 1, 5, 1, 2, 1, "direct", "zero", 0, 0),
+    (1, 8, 9, 260, 2, 7, 1, 2, 1, "direct", "zero", 0, 0),
     (3, 1, 20, 16, 32, 3, (3, 1), 1, 1, "direct", "zero", 0, 0),
     (2, 128, 3, 3, 256, 3, (3, 2), 1, 1, "direct", "zero", 0, 0),
     # small-K direct kernel (K = kh*kw*cin <= 64, cin % 4 == 0): image-input / 4-channel layers
