@@ -11,12 +11,17 @@ namespace s2v {
 
 constexpr int FIR_MAX_TAPS = 64;
 
-template <bool VEC>
+// UP / DOWN / KS > 0: compile-time resampling factors and square filter size (the StyleGAN2 /
+// GPEN cases up2 / down2 / blur with the 4x4 [1 3 3 1] kernel): the zero-insertion test and the
+// index division become shifts and the tap loops unroll; 0 = runtime values (any combination).
+template <bool VEC, int UP = 0, int DOWN = 0, int KS = 0>
 __global__ __launch_bounds__(256) void fir2d_kernel(const float *__restrict__ x, int ih, int iw, int c, int xcs,
-                                                    const float *__restrict__ k, int kh, int kw, int up, int down,
+                                                    const float *__restrict__ k, int kh_, int kw_, int up_, int down_,
                                                     int py0, int px0, float *__restrict__ y, int oh, int ow, int ycs,
                                                     float gain, const float *__restrict__ bias, int act, float alpha,
                                                     float post, long long total) {
+    const int up = UP ? UP : up_, down = DOWN ? DOWN : down_;
+    const int kh = KS ? KS : kh_, kw = KS ? KS : kw_;
     __shared__ float ks[FIR_MAX_TAPS];
     for (int i = threadIdx.x; i < kh * kw; i += 256) ks[i] = k[kh * kw - 1 - i];   // flipped
     __syncthreads();
@@ -32,23 +37,31 @@ __global__ __launch_bounds__(256) void fir2d_kernel(const float *__restrict__ x,
         const int n = (int)(t / oh);
         const float *xb = x + (long long)n * ih * iw * xcs + (VEC ? 4 * cc : cc);
         float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-        for (int i = 0; i < kh; ++i) {
-            const int uy = oy * down + i - py0;
-            if (uy < 0 || uy % up) continue;
-            const int iy = uy / up;
-            if (iy >= ih) continue;
-            for (int j = 0; j < kw; ++j) {
-                const int ux = ox * down + j - px0;
-                if (ux < 0 || ux % up) continue;
-                const int ix = ux / up;
-                if (ix >= iw) continue;
-                const float kv = ks[i * kw + j];
-                const float *src = xb + ((long long)iy * iw + ix) * xcs;
-                if (VEC) {
-                    const float4 v = *(const float4 *)src;
-                    a0 = fmaf(v.x, kv, a0); a1 = fmaf(v.y, kv, a1); a2 = fmaf(v.z, kv, a2); a3 = fmaf(v.w, kv, a3);
-                } else {
-                    a0 = fmaf(*src, kv, a0);
+#pragma unroll
+        for (int i = 0; i < (KS ? KS : 1); ++i) {
+            for (int ii = 0; ii < (KS ? 1 : kh); ++ii) {
+                const int ti = KS ? i : ii;
+                const int uy = oy * down + ti - py0;
+                if (uy < 0 || uy % up) continue;
+                const int iy = uy / up;
+                if (iy >= ih) continue;
+#pragma unroll
+                for (int j = 0; j < (KS ? KS : 1); ++j) {
+                    for (int jj = 0; jj < (KS ? 1 : kw); ++jj) {
+                        const int tj = KS ? j : jj;
+                        const int ux = ox * down + tj - px0;
+                        if (ux < 0 || ux % up) continue;
+                        const int ix = ux / up;
+                        if (ix >= iw) continue;
+                        const float kv = ks[ti * kw + tj];
+                        const float *src = xb + ((long long)iy * iw + ix) * xcs;
+                        if (VEC) {
+                            const float4 v = *(const float4 *)src;
+                            a0 = fmaf(v.x, kv, a0); a1 = fmaf(v.y, kv, a1); a2 = fmaf(v.z, kv, a2); a3 = fmaf(v.w, kv, a3);
+                        } else {
+                            a0 = fmaf(*src, kv, a0);
+                        }
+                    }
                 }
             }
         }
@@ -83,11 +96,19 @@ extern "C" int s2v_fir2d(const float *x, int n, int ih, int iw, int c, int xcs, 
     const long long total = (long long)n * oh * ow * (vec ? c / 4 : c);
     long long blocks = (total + 255) / 256;
     if (blocks > 65535LL * 16) blocks = 65535LL * 16;
-    if (vec)
-        fir2d_kernel<true><<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(
-            x, ih, iw, c, xcs, k, kh, kw, up, down, pad_y0, pad_x0, y, oh, ow, ycs, gain, bias, act, alpha, post, total);
+    hipStream_t st = (hipStream_t)stream;
+#define S2V_FIR_ARGS x, ih, iw, c, xcs, k, kh, kw, up, down, pad_y0, pad_x0, y, oh, ow, ycs, gain, bias, act, alpha, post, total
+    if (vec && kh == 4 && kw == 4 && up == 1 && down == 1)
+        fir2d_kernel<true, 1, 1, 4><<<(unsigned)blocks, 256, 0, st>>>(S2V_FIR_ARGS);
+    else if (vec && kh == 4 && kw == 4 && up == 2 && down == 1)
+        fir2d_kernel<true, 2, 1, 4><<<(unsigned)blocks, 256, 0, st>>>(S2V_FIR_ARGS);
+    else if (vec && kh == 4 && kw == 4 && up == 1 && down == 2)
+        fir2d_kernel<true, 1, 2, 4><<<(unsigned)blocks, 256, 0, st>>>(S2V_FIR_ARGS);
+    else if (vec)
+        fir2d_kernel<true><<<(unsigned)blocks, 256, 0, st>>>(S2V_FIR_ARGS);
     else
         fir2d_kernel<false><<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(
             x, ih, iw, c, xcs, k, kh, kw, up, down, pad_y0, pad_x0, y, oh, ow, ycs, gain, bias, act, alpha, post, total);
+#undef S2V_FIR_ARGS
     return check_launch("fir2d");
 }

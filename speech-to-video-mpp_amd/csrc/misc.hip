@@ -338,11 +338,49 @@ __global__ __launch_bounds__(256) void fused_bias_act_kernel(const float *__rest
     }
 }
 
-// out = down( FIR( zero-pad( zero-insert-up(x) ), flip(k) ) ) per plane, [major][H][W][minor]
+// Row form (step_b % 4 == 0, 16-byte aligned; the GPEN call on [N, C, H, W] has step_b = H*W): a
+// block row walks one (n, c) plane with float4 loads / stores, the bias channel fixed per row — no
+// per-element 64-bit index division.
+__global__ __launch_bounds__(256) void fused_bias_act_rows(const float *__restrict__ x, const float *__restrict__ b,
+                                                           const float *__restrict__ ref, float *__restrict__ y,
+                                                           long long rows, int c, long long step4, int act, int grad,
+                                                           float alpha, float scale) {
+    for (long long r = blockIdx.y; r < rows; r += gridDim.y) {
+        const float bv = b ? b[r % c] : 0.f;
+        const float4 *xr = (const float4 *)x + r * step4;
+        const float4 *rr = ref ? (const float4 *)ref + r * step4 : nullptr;
+        float4 *yr = (float4 *)y + r * step4;
+        for (long long i = blockIdx.x * 256LL + threadIdx.x; i < step4; i += (long long)gridDim.x * 256) {
+            float4 v = xr[i];
+            v.x += bv; v.y += bv; v.z += bv; v.w += bv;
+            float4 o = v;
+            const int mode = act * 10 + grad;
+            if (mode == 30) {
+                o.x = v.x > 0.f ? v.x : v.x * alpha; o.y = v.y > 0.f ? v.y : v.y * alpha;
+                o.z = v.z > 0.f ? v.z : v.z * alpha; o.w = v.w > 0.f ? v.w : v.w * alpha;
+            } else if (mode == 31) {
+                const float4 q = rr[i];
+                o.x = q.x > 0.f ? v.x : v.x * alpha; o.y = q.y > 0.f ? v.y : v.y * alpha;
+                o.z = q.z > 0.f ? v.z : v.z * alpha; o.w = q.w > 0.f ? v.w : v.w * alpha;
+            } else if (mode == 12 || mode == 32) {
+                o = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+            o.x *= scale; o.y *= scale; o.z *= scale; o.w *= scale;
+            yr[i] = o;
+        }
+    }
+}
+
+// out = down( FIR( zero-pad( zero-insert-up(x) ), flip(k) ) ) per plane, [major][H][W][minor].
+// UP / DN / KS > 0 fix the factors and the square filter at compile time (the GPEN Upsample /
+// Downsample / Blur forms with the 4x4 kernel): shifts instead of divisions, unrolled taps.
+template <int UP = 0, int DN = 0, int KS = 0>
 __global__ __launch_bounds__(256) void upfirdn2d_kernel(const float *__restrict__ x, int major, int ih, int iw,
-                                                        int minor, const float *__restrict__ k, int kh, int kw,
-                                                        int upx, int upy, int dnx, int dny, int px0, int py0,
+                                                        int minor, const float *__restrict__ k, int kh_, int kw_,
+                                                        int upx_, int upy_, int dnx_, int dny_, int px0, int py0,
                                                         float *__restrict__ y, int oh, int ow) {
+    const int upx = UP ? UP : upx_, upy = UP ? UP : upy_, dnx = DN ? DN : dnx_, dny = DN ? DN : dny_;
+    const int kh = KS ? KS : kh_, kw = KS ? KS : kw_;
     const long long total = (long long)major * oh * ow * minor;
     for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
         const int mi = (int)(e % minor);
@@ -353,21 +391,86 @@ __global__ __launch_bounds__(256) void upfirdn2d_kernel(const float *__restrict_
         const int mj = (int)(t / oh);
         const float *xb = x + (long long)mj * ih * iw * minor + mi;
         float acc = 0.f;
-        for (int i = 0; i < kh; ++i) {
-            const int uy = oy * dny + i - py0;   // row in the zero-inserted image
-            if (uy < 0 || uy % upy) continue;
-            const int iy = uy / upy;
-            if (iy >= ih) continue;
-            for (int j = 0; j < kw; ++j) {
-                const int ux = ox * dnx + j - px0;
-                if (ux < 0 || ux % upx) continue;
-                const int ix = ux / upx;
-                if (ix >= iw) continue;
-                acc = fmaf(xb[((long long)iy * iw + ix) * minor], k[(kh - 1 - i) * kw + (kw - 1 - j)], acc);
+#pragma unroll
+        for (int i = 0; i < (KS ? KS : 1); ++i) {
+            for (int ii = 0; ii < (KS ? 1 : kh); ++ii) {
+                const int ti = KS ? i : ii;
+                const int uy = oy * dny + ti - py0;   // row in the zero-inserted image
+                if (uy < 0 || uy % upy) continue;
+                const int iy = uy / upy;
+                if (iy >= ih) continue;
+#pragma unroll
+                for (int j = 0; j < (KS ? KS : 1); ++j) {
+                    for (int jj = 0; jj < (KS ? 1 : kw); ++jj) {
+                        const int tj = KS ? j : jj;
+                        const int ux = ox * dnx + tj - px0;
+                        if (ux < 0 || ux % upx) continue;
+                        const int ix = ux / upx;
+                        if (ix >= iw) continue;
+                        acc = fmaf(xb[((long long)iy * iw + ix) * minor], k[(kh - 1 - ti) * kw + (kw - 1 - tj)], acc);
+                    }
+                }
             }
         }
         y[e] = acc;
     }
+}
+
+// Plane form (minor == 1, the NCHW tensors GPEN passes as [N*C, H, W, 1]) with the 4x4 filter:
+// a block owns a 16 x 64 output tile of one plane, stages the input rows it touches in LDS with
+// coalesced row loads (zeros outside the image), and each thread computes 4 adjacent outputs.
+template <int UP, int DN>
+__global__ __launch_bounds__(256) void upfirdn2d_plane4(const float *__restrict__ x, int ih, int iw,
+                                                        const float *__restrict__ k, int px0, int py0,
+                                                        float *__restrict__ y, int oh, int ow, int tiles_x,
+                                                        int tiles_y) {
+    constexpr int TY = 16, TX = 64;
+    // input rows / cols a tile touches: zero-inserted coordinates u = o*DN + t - p, t in [0, 4)
+    constexpr int RH = ((TY - 1) * DN + 3) / UP + 2, RW = ((TX - 1) * DN + 3) / UP + 2;
+    __shared__ float tile[RH][RW + 1];
+    __shared__ float ks[16];
+    if (threadIdx.x < 16) ks[threadIdx.x] = k[15 - threadIdx.x];          // flipped
+    int t = blockIdx.x;
+    const int txi = t % tiles_x;
+    t /= tiles_x;
+    const int tyi = t % tiles_y;
+    const long long plane = t / tiles_y;
+    const int oy0 = tyi * TY, ox0 = txi * TX;
+    // first input row / col of the tile (floor division of the first zero-inserted coordinate)
+    const int uy0 = oy0 * DN - py0, ux0 = ox0 * DN - px0;
+    const int iy0 = uy0 >= 0 ? uy0 / UP : -((-uy0 + UP - 1) / UP);
+    const int ix0 = ux0 >= 0 ? ux0 / UP : -((-ux0 + UP - 1) / UP);
+    const float *xp = x + plane * ih * iw;
+    for (int e = threadIdx.x; e < RH * RW; e += 256) {
+        const int r = e / RW, cidx = e - r * RW;
+        const int gy = iy0 + r, gx = ix0 + cidx;
+        tile[r][cidx] = ((unsigned)gy < (unsigned)ih && (unsigned)gx < (unsigned)iw) ? xp[(long long)gy * iw + gx] : 0.f;
+    }
+    __syncthreads();
+    const int ry = threadIdx.x >> 4, rx = (threadIdx.x & 15) * 4;
+    const int oy = oy0 + ry;
+    if (oy >= oh) return;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int uy = oy * DN + i - py0;
+        if (UP > 1 && (uy % UP + UP) % UP) continue;
+        const int ly = (uy >= 0 ? uy / UP : -((-uy + UP - 1) / UP)) - iy0;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int ux = (ox0 + rx + p) * DN + j - px0;
+                if (UP > 1 && (ux % UP + UP) % UP) continue;
+                const int lx = (ux >= 0 ? ux / UP : -((-ux + UP - 1) / UP)) - ix0;
+                acc[p] = fmaf(tile[ly][lx], ks[i * 4 + j], acc[p]);
+            }
+        }
+    }
+    float *yp = y + plane * oh * ow + (long long)oy * ow;
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+        if (ox0 + rx + p < ow) yp[ox0 + rx + p] = acc[p];
 }
 
 // ------------------------------------------------------------------ noise
@@ -572,8 +675,18 @@ extern "C" int s2v_fused_bias_act(const float *x, const float *b, const float *r
     S2V_REQUIRE(x && y && size >= 0, "fused_bias_act: bad args");
     S2V_REQUIRE(!b || (c > 0 && step_b > 0), "fused_bias_act: bias needs c > 0 and step_b > 0");
     if (size == 0) return 0;
-    fused_bias_act_kernel<<<grid_for(size), 256, 0, (hipStream_t)stream>>>(x, b, ref, y, size, c, step_b, act, grad,
-                                                                             alpha, scale);
+    const bool rows_ok = step_b % 4 == 0 && size % step_b == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0 &&
+                         (!ref || ((uintptr_t)ref & 15) == 0);
+    if (rows_ok) {
+        const long long rows = size / step_b, step4 = step_b / 4;
+        const unsigned gx = (unsigned)((step4 + 255) / 256 < 64 ? (step4 + 255) / 256 : 64);
+        const unsigned gy = (unsigned)(rows < 65535 ? rows : 65535);
+        fused_bias_act_rows<<<dim3(gx, gy), 256, 0, (hipStream_t)stream>>>(x, b, ref, y, rows, b ? c : 1, step4, act,
+                                                                           grad, alpha, scale);
+    } else {
+        fused_bias_act_kernel<<<grid_for(size), 256, 0, (hipStream_t)stream>>>(x, b, ref, y, size, c, step_b, act, grad,
+                                                                                 alpha, scale);
+    }
     return check_launch("fused_bias_act");
 }
 
@@ -587,8 +700,21 @@ extern "C" int s2v_upfirdn2d(const float *x, int major, int in_h, int in_w, int 
     const int ew = (in_w * up_x + pad_x0 + pad_x1 - kw) / down_x + 1;
     S2V_REQUIRE(eh == out_h && ew == out_w && out_h > 0 && out_w > 0,
                 "upfirdn2d: output must be %dx%d (got %dx%d)", eh, ew, out_h, out_w);
-    upfirdn2d_kernel<<<grid_for((long long)major * out_h * out_w * minor), 256, 0, (hipStream_t)stream>>>(
-        x, major, in_h, in_w, minor, k, kh, kw, up_x, up_y, down_x, down_y, pad_x0, pad_y0, y, out_h, out_w);
+    const unsigned g = grid_for((long long)major * out_h * out_w * minor);
+    hipStream_t st = (hipStream_t)stream;
+    const bool k4 = kh == 4 && kw == 4 && up_x == up_y && down_x == down_y;
+#define S2V_UFD_ARGS x, major, in_h, in_w, minor, k, kh, kw, up_x, up_y, down_x, down_y, pad_x0, pad_y0, y, out_h, out_w
+    if (k4 && minor == 1 && pad_x0 >= 0 && pad_y0 >= 0 && ((up_x == 1 && down_x <= 2) || (up_x == 2 && down_x == 1))) {
+        const int tx = (out_w + 63) / 64, ty = (out_h + 15) / 16;
+        const unsigned gp = (unsigned)((long long)major * tx * ty);
+        if (up_x == 2) upfirdn2d_plane4<2, 1><<<gp, 256, 0, st>>>(x, in_h, in_w, k, pad_x0, pad_y0, y, out_h, out_w, tx, ty);
+        else if (down_x == 2) upfirdn2d_plane4<1, 2><<<gp, 256, 0, st>>>(x, in_h, in_w, k, pad_x0, pad_y0, y, out_h, out_w, tx, ty);
+        else upfirdn2d_plane4<1, 1><<<gp, 256, 0, st>>>(x, in_h, in_w, k, pad_x0, pad_y0, y, out_h, out_w, tx, ty);
+    } else if (k4 && up_x == 1 && down_x == 1) upfirdn2d_kernel<1, 1, 4><<<g, 256, 0, st>>>(S2V_UFD_ARGS);
+    else if (k4 && up_x == 2 && down_x == 1) upfirdn2d_kernel<2, 1, 4><<<g, 256, 0, st>>>(S2V_UFD_ARGS);
+    else if (k4 && up_x == 1 && down_x == 2) upfirdn2d_kernel<1, 2, 4><<<g, 256, 0, st>>>(S2V_UFD_ARGS);
+    else upfirdn2d_kernel<><<<g, 256, 0, st>>>(S2V_UFD_ARGS);
+#undef S2V_UFD_ARGS
     return check_launch("upfirdn2d");
 }
 

@@ -137,3 +137,36 @@ def test_flow_warp_and_mel_ops(golden):
     wav = (0.2 * np.sin(2 * np.pi * 440 * t)).astype(np.float32)
     mel = s2v.mel_spectrogram(torch.from_numpy(wav).to(DEV), audio.tables(torch.device(DEV)), False)
     assert np.abs(mel.cpu().numpy() - ref_audio.melspectrogram(wav)).max() < 1e-3
+
+
+@pytest.mark.parametrize("up,down,pad", [(1, 1, (2, 1)), (1, 1, (1, 1)), (2, 1, (2, 1)), (1, 2, (1, 1)),
+                                         (1, 2, (2, 2)), (2, 1, (1, 2))])
+def test_upfirdn2d_plane_tiles_ragged(up, down, pad):
+    """The LDS-tiled plane kernel (NCHW inputs, 4x4 filter, 16 x 64 output tiles): sizes that leave
+    partial tiles in both directions, asymmetric pads, against the reference's CPU upfirdn2d."""
+    from oracle.enhancers import upfirdn2d as ref_upfirdn2d
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(2, 5, 37, 150, generator=g)
+    k = torch.randn(4, 4, generator=g)
+    got = torch_ops.upfirdn2d(x.to(DEV), k.to(DEV), up=up, down=down, pad=pad)
+    ref = ref_upfirdn2d(x, k, up=up, down=down, pad=pad)
+    assert got.shape == ref.shape
+    assert (got.cpu() - ref).abs().max() < 1e-5
+
+
+def test_fused_bias_act_row_form():
+    """The float4 row kernel (step_b % 4 == 0: every [N, C, H, W] activation of GPEN) in all the
+    act / grad modes the reference's kernel implements (fused_bias_act_kernel.cu:36-45)."""
+    g = torch.Generator().manual_seed(13)
+    x = torch.randn(2, 8, 8, 12, generator=g)
+    b = torch.randn(8, generator=g)
+    ref_in = torch.randn(2, 8, 8, 12, generator=g)
+    op = torch_ops.fused.fused_bias_act
+    xb = x + b[None, :, None, None]
+    exp = {(3, 0): torch.where(xb > 0, xb, xb * 0.2) * 1.5, (3, 1): torch.where(ref_in > 0, xb, xb * 0.2) * 1.5,
+           (1, 0): xb * 1.5}
+    for (act, grad), e in exp.items():
+        got = op(x.to(DEV), b.to(DEV), ref_in.to(DEV) if grad else x.new_empty(0).to(DEV), act, grad, 0.2, 1.5)
+        assert (got.cpu() - e).abs().max() < 1e-6, (act, grad)
+    got = torch_ops.fused_leaky_relu(x.to(DEV), b.to(DEV), 0.2, 2 ** 0.5)
+    assert (got.cpu() - torch.where(xb > 0, xb, xb * 0.2) * 2 ** 0.5).abs().max() < 1e-5
