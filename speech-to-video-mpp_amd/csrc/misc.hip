@@ -547,6 +547,36 @@ __global__ __launch_bounds__(256) void eltwise_kernel(const float *__restrict__ 
     }
 }
 
+// float4 form (c, pitches % 4 == 0, 16-byte aligned views, < 2^31 quads): one channel quad per
+// thread, 32-bit index math
+__global__ __launch_bounds__(256) void eltwise4_kernel(const float *__restrict__ x, int xcs, const float *__restrict__ mul,
+                                                       int mcs, const float *__restrict__ add, int acs,
+                                                       const float *__restrict__ bias, unsigned quads, unsigned c4,
+                                                       float a, int act, float alpha, float post,
+                                                       float *__restrict__ y, int ycs) {
+    for (unsigned e = blockIdx.x * 256u + threadIdx.x; e < quads; e += gridDim.x * 256u) {
+        const unsigned p = e / c4, q = e - p * c4;
+        const long long pp = (long long)p;
+        float4 v = *(const float4 *)(x + pp * xcs + 4 * q);
+        v.x *= a; v.y *= a; v.z *= a; v.w *= a;
+        if (mul) {
+            const float4 m = *(const float4 *)(mul + pp * mcs + 4 * q);
+            v.x *= m.x; v.y *= m.y; v.z *= m.z; v.w *= m.w;
+        }
+        if (add) {
+            const float4 d = *(const float4 *)(add + pp * acs + 4 * q);
+            v.x += d.x; v.y += d.y; v.z += d.z; v.w += d.w;
+        }
+        if (bias) {
+            const float4 b = *(const float4 *)(bias + 4 * q);
+            v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+        }
+        v.x = apply_act(v.x, act, alpha) * post; v.y = apply_act(v.y, act, alpha) * post;
+        v.z = apply_act(v.z, act, alpha) * post; v.w = apply_act(v.w, act, alpha) * post;
+        *(float4 *)(y + pp * ycs + 4 * q) = v;
+    }
+}
+
 __global__ __launch_bounds__(256) void fill_kernel(float *__restrict__ y, long long n, float v) {
     for (long long e = blockIdx.x * 256LL + threadIdx.x; e < n; e += (long long)gridDim.x * 256) y[e] = v;
 }
@@ -766,8 +796,17 @@ extern "C" int s2v_eltwise(const float *x, int xcs, const float *mul, int mcs, c
     S2V_REQUIRE(x && y && pixels >= 0 && c > 0 && xcs >= c && ycs >= c && (!mul || mcs >= c) && (!add || acs >= c),
                 "eltwise: bad args");
     if (pixels == 0) return 0;
-    eltwise_kernel<<<grid_for(pixels * c), 256, 0, (hipStream_t)stream>>>(x, xcs, mul, mcs, add, acs, bias, pixels,
-                                                                           c, a, act, alpha, post, y, ycs);
+    const auto al = [](const void *q) { return ((uintptr_t)q & 15) == 0; };
+    const bool v4 = c % 4 == 0 && xcs % 4 == 0 && ycs % 4 == 0 && al(x) && al(y) && (!mul || (mcs % 4 == 0 && al(mul))) &&
+                    (!add || (acs % 4 == 0 && al(add))) && (!bias || al(bias)) && pixels * (c / 4) < (1LL << 31);
+    if (v4) {
+        const unsigned quads = (unsigned)(pixels * (c / 4));
+        eltwise4_kernel<<<grid_for(quads), 256, 0, (hipStream_t)stream>>>(x, xcs, mul, mcs, add, acs, bias, quads,
+                                                                          (unsigned)(c / 4), a, act, alpha, post, y, ycs);
+    } else {
+        eltwise_kernel<<<grid_for(pixels * c), 256, 0, (hipStream_t)stream>>>(x, xcs, mul, mcs, add, acs, bias, pixels,
+                                                                               c, a, act, alpha, post, y, ycs);
+    }
     return check_launch("eltwise");
 }
 
