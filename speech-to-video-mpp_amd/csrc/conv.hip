@@ -314,6 +314,74 @@ __global__ __launch_bounds__(256) void conv_smallk(ConvArgs a, int batch, int tp
     }
 }
 
+// 4-channel inputs with a compile-time tap count (1x1 or 3x3: ENet's conv_body_first and the first
+// StyleConv on the upsampled 4-channel image): every tap's float4 is loaded before any FMA, so a
+// thread has KT loads in flight instead of KT dependent round trips per pixel (the runtime-tap
+// loop of conv_smallk ran the 3x3 StyleConv at 0.66 TB/s of output).
+template <int QPT, int KT>
+__global__ __launch_bounds__(256) void conv_smallk4(ConvArgs a, int batch, int tppx, int iters, int vec) {
+    constexpr int KW = KT == 9 ? 3 : 1;
+    extern __shared__ __attribute__((aligned(16))) float wk[];   // [K][cout]
+    const int gpb = 256 / tppx;
+    const long long total = (long long)batch * a.M;
+    const long long g0 = (long long)blockIdx.x * gpb * iters;
+    {
+        const int b0 = (int)((g0 < total ? g0 : 0) / a.M);
+        const float *w0 = a.wt + (long long)b0 * a.w_bs;
+        for (int e = threadIdx.x; e < KT * 4 * a.cout; e += 256) {
+            const int k = e / a.cout, o = e - k * a.cout;
+            wk[e] = w0[(long long)o * a.kpad + k];
+        }
+    }
+    __syncthreads();
+    const int tq = threadIdx.x % tppx;
+    const int hw = a.oh * a.ow;
+    for (int it = 0; it < iters; ++it) {
+        const long long g = g0 + (long long)it * gpb + threadIdx.x / tppx;
+        if (g >= total) break;
+        const int bidx = (int)(g / a.M);
+        const int m = (int)(g - (long long)bidx * a.M);
+        const float *x = a.x + (long long)bidx * a.x_bs;
+        const int img = m / hw, rem = m - img * hw;
+        const int oy = rem / a.ow, ox = rem - oy * a.ow;
+        f4 v[KT];
+#pragma unroll
+        for (int t = 0; t < KT; ++t) {
+            int iy, ix;
+            const bool ok = map_tap(a, oy, ox, t / KW, t % KW, iy, ix);
+            v[t] = ok ? *(const f4 *)(x + ((long long)(img * a.h + iy) * a.w + ix) * a.xcs) : f4{0.f, 0.f, 0.f, 0.f};
+            if (a.in_scale || a.pre_act) {
+                v[t].x = prologue(a, v[t].x, img, 0);
+                v[t].y = prologue(a, v[t].y, img, 1);
+                v[t].z = prologue(a, v[t].z, img, 2);
+                v[t].w = prologue(a, v[t].w, img, 3);
+                if (!ok) v[t] = f4{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+        f4 acc[QPT];
+#pragma unroll
+        for (int q = 0; q < QPT; ++q) acc[q] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < KT; ++t)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float ve = e == 0 ? v[t].x : e == 1 ? v[t].y : e == 2 ? v[t].z : v[t].w;
+                const float *wr = wk + (t * 4 + e) * a.cout + 4 * tq;
+#pragma unroll
+                for (int q = 0; q < QPT; ++q) {
+                    const f4 w4 = *(const f4 *)(wr + 4 * tppx * q);
+                    acc[q].x = fmaf(ve, w4.x, acc[q].x);
+                    acc[q].y = fmaf(ve, w4.y, acc[q].y);
+                    acc[q].z = fmaf(ve, w4.z, acc[q].z);
+                    acc[q].w = fmaf(ve, w4.w, acc[q].w);
+                }
+            }
+#pragma unroll
+        for (int q = 0; q < QPT; ++q)
+            store_epilogue4(a, bidx, m, 4 * (tq + tppx * q), acc[q], vec != 0, SMALLK_NT != 0);
+    }
+}
+
 // Direct VALU convolution for tiny Cout (final RGB / flow heads, ToRGB): one thread per output
 // pixel, all CO outputs per thread.  Per filter tap the block stages W[:, tap, c0:c0+CCH] in LDS,
 // so every weight read is an LDS broadcast (all lanes read the same address).
@@ -953,7 +1021,9 @@ extern "C" int s2v_conv2d_plan(const s2v_conv_params *p, int *out6) {
         int tppx, qpt;
         smallk_cfg(p, M, K, tppx, qpt);
         out6[0] = 0; out6[1] = p->cout; out6[2] = -qpt;
-        out6[3] = smallk_px(M); out6[4] = 0; out6[5] = 1;
+        out6[3] = smallk_px(M); out6[5] = 1;
+        // conv_smallk4<QPT, KT> for 4-channel 1x1 / 3x3 inputs (reported as 2000 + KT)
+        out6[4] = p->cin == 4 && p->kh == p->kw && (p->kh == 1 || p->kh == 3) ? 2000 + p->kh * p->kw : 0;
         return 0;
     }
     if (pl.tile < 0 && HALO_SMALL && halo_ks(p)) {
@@ -1003,7 +1073,12 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
         const int vec = p->ycs % 4 == 0 && ((uintptr_t)p->y % 16) == 0 && p->y_bs % 4 == 0 &&
                         (!p->res || (p->res_cs % 4 == 0 && ((uintptr_t)p->res % 16) == 0 && p->res_bs % 4 == 0)) &&
                         (!p->scale || ((uintptr_t)p->scale % 16) == 0) && (!p->shift || ((uintptr_t)p->shift % 16) == 0);
-        if (qpt == 1) conv_smallk<1, 1><<<grid, 256, lds, s>>>(a, batch, tppx, iters, vec);
+        const int kt = p->cin == 4 && p->kh == p->kw && (p->kh == 1 || p->kh == 3) ? p->kh * p->kw : 0;
+        if (kt == 9 && qpt == 1) conv_smallk4<1, 9><<<grid, 256, lds, s>>>(a, batch, tppx, iters, vec);
+        else if (kt == 9) conv_smallk4<2, 9><<<grid, 256, lds, s>>>(a, batch, tppx, iters, vec);
+        else if (kt == 1 && qpt == 1) conv_smallk4<1, 1><<<grid, 256, lds, s>>>(a, batch, tppx, iters, vec);
+        else if (kt == 1) conv_smallk4<2, 1><<<grid, 256, lds, s>>>(a, batch, tppx, iters, vec);
+        else if (qpt == 1) conv_smallk<1, 1><<<grid, 256, lds, s>>>(a, batch, tppx, iters, vec);
         else conv_smallk<2, 1><<<grid, 256, lds, s>>>(a, batch, tppx, iters, vec);
         return check_launch("conv_smallk");
     }

@@ -143,7 +143,8 @@ __global__ __launch_bounds__(256) void attention_kernel(const float *__restrict_
     float *ps = qs + 64;
     const float *qb = q + b * bsq + hd * 64;
     float *ob = o + b * bso + hd * 64;
-    for (int i = wv; i < T; i += 4) {
+    // query rows interleave over the blocks of blockIdx.y (row groups) and the 4 waves
+    for (int i = blockIdx.y * 4 + wv; i < T; i += 4 * gridDim.y) {
         qs[lane] = qb[(long long)i * ldq + lane];
         __builtin_amdgcn_wave_barrier();
         float sv[4];
@@ -666,8 +667,12 @@ extern "C" int s2v_attention(const float *q, const float *k, const float *v, int
         (void)hipFuncSetAttribute((const void *)attention_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
-    attention_kernel<<<batch * heads, 256, smem, (hipStream_t)stream>>>(q, k, v, heads, tokens, ld_q, ld_k, ld_v, bs_q,
-                                                                        bs_k, bs_v, scale, o, ld_o, bs_o);
+    // enough row groups per (sample, head) to cover the CUs (LNet: 16 x 4 heads -> 64 x 4 blocks)
+    int rg = 1;
+    while (batch * heads * rg < 2 * device_cus() && 4 * rg * 2 <= tokens && rg < 16) rg *= 2;
+    attention_kernel<<<dim3(batch * heads, rg), 256, smem, (hipStream_t)stream>>>(q, k, v, heads, tokens, ld_q, ld_k,
+                                                                                 ld_v, bs_q, bs_k, bs_v, scale, o, ld_o,
+                                                                                 bs_o);
     return check_launch("attention");
 }
 

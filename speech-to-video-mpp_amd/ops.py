@@ -434,6 +434,8 @@ def conv_symbol(ctx: Ctx, p) -> str:
         if bkn >= 1000:
             return f"void s2v::conv_halo_small<{bn}, {bkn - 1000}>(s2v::ConvArgs, int, int)"
         if wm < 0:
+            if bkn >= 2000:
+                return f"void s2v::conv_smallk4<{-wm}, {bkn - 2000}>(s2v::ConvArgs, int, int, int, int)"
             return f"void s2v::conv_smallk<{-wm}, {avec}>(s2v::ConvArgs, int, int, int, int)"
         if wm:
             return f"void s2v::conv_small_cpar<{bn}, {wm}, {'true' if avec else 'false'}>(s2v::ConvArgs, int)"
