@@ -113,6 +113,11 @@ def live_roofline(forward, workload="lipsync"):
         recs.append((sym, flops, splits, s, e, (p.n, p.h, p.w, p.cin, p.oh, p.ow, p.cout, p.kh, p.kw,
                                                 bool(p.in_scale), bool(p.nc_scale), bool(p.pix_add), bool(p.res))))
 
+    # per-kernel durations are measured with the side-stream branches serialised (engine.lnet
+    # BRANCHES, engine.enet OVERLAP), so concurrent kernels do not inflate each other's time
+    from s2v_amd.engine import enet as _enet, lnet as _lnet
+    saved = (_lnet.BRANCHES, _enet.OVERLAP)
+    _lnet.BRANCHES = _enet.OVERLAP = False
     ops.CONV_HOOK = hook
     try:
         with torch.no_grad():
@@ -120,6 +125,7 @@ def live_roofline(forward, workload="lipsync"):
         torch.cuda.synchronize()
     finally:
         ops.CONV_HOOK = None
+        _lnet.BRANCHES, _enet.OVERLAP = saved
     per = {}
     if os.environ.get("S2V_BENCH_VERBOSE") == "2":
         for sym, flops, splits, s, e, shp in recs:

@@ -10,6 +10,7 @@ in_scale / nc_scale, used where per-sample weights do not apply.)
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -18,6 +19,9 @@ from ..ops import NHWC, ConvW
 from .lnet import LNetEngine
 
 LRELU = 0.2  # ENet.py:94-97, base_blocks.py:41-44, :522
+# the style encoder and LNet are independent until the StyleConvs (ENet.py:94-112): run the style
+# encoder on a side stream beside LNet (S2V_ENET_OVERLAP=0 serialises them)
+OVERLAP = os.environ.get("S2V_ENET_OVERLAP", "1") == "1"
 
 
 class StyleLayer:
@@ -86,6 +90,14 @@ class ENetEngine:
         self.noise_seed = 0x5EED
         self.noise_ctr = ops.NoiseCounter()
 
+    def _side(self):
+        """(stream, Ctx) for the style encoder branch, made once (CUDA devices only)."""
+        if getattr(self, "_side_branch", None) is None:
+            if self.device.type != "cuda":
+                return None
+            self._side_branch = (torch.cuda.Stream(self.device), ops.Ctx(self.device))
+        return self._side_branch
+
     def style_code(self, ctx, ref: torch.Tensor):
         """ref: NCHW [B,3,H,W] device tensor -> style [B,1,1,512] (ENet.py:94-101)."""
         dev, b = self.device, ref.shape[0]
@@ -113,11 +125,18 @@ class ENetEngine:
         out [B,3,384,384], low [B,3,96,96] (NCHW, written in place)."""
         dev = self.device
         b = audio.shape[0]
-        style = self.style_code(ctx, face[:, 3:])
-        if aux is not None:
-            aux["style"] = style.t.view(b, -1)
         svec = NHWC.empty(b, 1, 1, self.mod.cout, dev)
-        ops.conv2d(ctx, style, self.mod, svec)
+        side = self._side() if OVERLAP else None
+        if side is not None:
+            sst, sctx = side
+            cur_st = torch.cuda.current_stream(dev)
+            sst.wait_stream(cur_st)
+            with torch.cuda.stream(sst):
+                style = self.style_code(sctx, face[:, 3:])
+                ops.conv2d(sctx, style, self.mod, svec)
+        else:
+            style = self.style_code(ctx, face[:, 3:])
+            ops.conv2d(ctx, style, self.mod, svec)
         s2 = svec.t.view(b, -1)
         # LNet input: cat(inp, gt) -> bilinear 96x96 (ENet.py:103-104)
         x6 = NHWC.empty(b, 96, 96, 6, dev)
@@ -126,6 +145,10 @@ class ENetEngine:
         lo = NHWC.empty(b, 96, 96, 4, dev)          # channel 3 = sigmoid(0): finite, zero weights
         self.lnet.forward(ctx, audio, x6, lo, pad_rgb=True)
         ops.nhwc_to_nchw(ctx, lo.slice(0, 3), low)
+        if side is not None:
+            torch.cuda.current_stream(dev).wait_stream(side[0])    # style code ready for the StyleConvs
+        if aux is not None:
+            aux["style"] = style.t.view(b, -1)
         # F.pad(reflect, 2) -> StyleConv / ToRGB stages (ENet.py:119-129)
         cur = NHWC.empty(b, 100, 100, 4, dev)
         ops.pad_reflect(ctx, lo, cur, (2, 2, 2, 2))
