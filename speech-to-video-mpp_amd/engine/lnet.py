@@ -238,6 +238,16 @@ class LNetEngine:
         self.final4 = ConvW(torch.cat([fw, torch.zeros((1,) + tuple(fw.shape[1:]))]),
                             torch.cat([sd[d + "final.model.0.bias"].float(), torch.zeros(1)]), dev, padding=3)
 
+    @staticmethod
+    def _shape_after(layers, n, h, w):
+        c = 0
+        for L in layers:
+            h, w = L.conv.out_hw(h, w)
+            if L.pool:
+                h, w = h // 2, w // 2
+            c = L.conv.cout
+        return n, h, w, c
+
     def _branches(self):
         if getattr(self, "_br", None) is None:
             if self.device.type != "cuda":
@@ -252,36 +262,48 @@ class LNetEngine:
         when ``pad_rgb``)."""
         dev = self.device
         b = face6.n
-        # ---- visual encoder (LNet.py:30-43)
-        xm = self.first_inp(ctx, face6.slice(0, 3))
-        xr = self.first_ref(ctx, face6.slice(3, 3))
-        skips = [xm]
-        h = face6.h
-        cat = None
-        for i in range(3):
-            if i < 2:
-                xm = self.inp_down[i](ctx, xm)
-                xr = self.ref_down[i](ctx, xr)
-                skips.append(xm)
-            else:
-                n_, oh, ow, c = self.inp_down[i].out_shape(xm)
-                cat = NHWC.empty(n_, oh, ow, 2 * c, dev)
-                xm2 = self.inp_down[i](ctx, xm)
-                self.ref_down[i](ctx, xr, out=cat.slice(c, c))
-                self.ca2(ctx, xm2, cat.slice(c, c), cat.slice(0, c))
-        # ---- audio encoder (LNet.py:102-120, base_blocks.py:12-26)
-        a = audio.contiguous()
-        x = NHWC(a.view(b, a.shape[2], a.shape[3], 1))
-        for cw, res in self.audio:
-            oh, ow = cw.out_hw(x.h, x.w)
-            y = NHWC.empty(b, oh, ow, cw.cout, dev)
-            ops.conv2d(ctx, x, cw, y, act=ops.ACT_RELU, res=x if res else None)
-            x = y
-        z = x
-        self.bank.run(ctx, z)
+        # ---- visual encoder (LNet.py:30-43) and audio encoder (LNet.py:102-120): the masked-face
+        # stream, the reference stream and the audio encoder (+ the ADAIN heads it feeds) are
+        # independent until the cross attention, so they run as three concurrent branches
+        n_, oh, ow, c = self._shape_after([self.first_ref] + self.ref_down, b, face6.h, face6.w)
+        cat = NHWC.empty(n_, oh, ow, 2 * c, dev)
+        skips = []
+        st = {}
+
+        def masked(cx):
+            xm = self.first_inp(cx, face6.slice(0, 3))
+            skips.append(xm)
+            for i in range(3):
+                xm = self.inp_down[i](cx, xm)
+                if i < 2:
+                    skips.append(xm)
+            st["xm2"] = xm
+
+        def reference(cx):
+            xr = self.first_ref(cx, face6.slice(3, 3))
+            for i in range(3):
+                xr = self.ref_down[i](cx, xr, out=cat.slice(c, c) if i == 2 else None)
+
+        def audio_enc(cx):
+            a = audio.contiguous()
+            x = NHWC(a.view(b, a.shape[2], a.shape[3], 1))
+            for cw, res in self.audio:
+                oh2, ow2 = cw.out_hw(x.h, x.w)
+                y = NHWC.empty(b, oh2, ow2, cw.cout, dev)
+                ops.conv2d(cx, x, cw, y, act=ops.ACT_RELU, res=x if res else None)
+                x = y
+            self.bank.run(cx, x)
+
+        br = self._branches() if BRANCHES else None
+        if br is None:
+            masked(ctx)
+            reference(ctx)
+            audio_enc(ctx)
+        else:
+            br.run(ctx, masked, reference, audio_enc)
+        self.ca2(ctx, st["xm2"], cat.slice(c, c), cat.slice(0, c))
         # ---- decoder (LNet.py:67-77)
         cur = cat
-        br = self._branches() if BRANCHES else None
         for lv in self.levels:
             c = lv["c"]
             ya = NHWC.empty(cur.n, cur.h, cur.w, c, dev)
