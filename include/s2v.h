@@ -116,6 +116,11 @@ typedef struct s2v_conv_params {
      * 0.25 * sum of the four epilogue values (act included) of each quad.  oh, ow even; implicit-GEMM
      * path only; no res / nc_scale / pix_add / strided output; one K split. */
     int out_pool;
+    /* x holds the split layout of ``prec`` (s2v_split_act: per pixel and 32-channel block, 32 hi
+     * halves then 32 lo halves — the fp32 tensor's bytes and pitch): both operands are staged by
+     * LDS-DMA (conv_glds_x3).  Needs prec BF16X3 / F16X3, a direct zero-padded conv with cin % 32 == 0,
+     * <= 32 taps, packed weights, no in_scale / pre_act, xcs % 4 == 0 and a 16-byte aligned x. */
+    int x_split;
 } s2v_conv_params;
 
 enum { S2V_PREC_F32 = 0, S2V_PREC_BF16X3 = 1, S2V_PREC_F16X3 = 2 };
@@ -131,6 +136,15 @@ size_t s2v_conv2d_ws_bytes(const s2v_conv_params *p);
  * TPP == 0), or {0, cout, -QPT, PX, 0, 1, ...} for conv_smallk<QPT,PX>.  force_tile: 0 = planner,
  * 1..6 (f32) / 1..8 (split precisions) a fixed tile of the selected precision's table (tests / tuning). */
 int s2v_conv2d_plan(const s2v_conv_params *p, int *out10);
+/* Planner knobs (tests / tuning; process-wide, not thread-safe against concurrent planning):
+ *   S2V_TUNE_HALO_MIN_BLOCKS  the halo-tiled small-Cout kernel needs at least this many 8x128 tiles
+ *                             (default 512, env S2V_HALO_MIN_BLOCKS); fewer go channel-parallel;
+ *   S2V_TUNE_GLDS_TILE        force an LDS-DMA tile config (-1 = planner, env S2V_GLDS_TILE);
+ *   S2V_TUNE_SMALLK_TILE      1: split-precision convs with K <= 128 on large M take one N tile over
+ *                             cout (default, env S2V_SMALLK_TILE); 0: the throughput model.
+ * Sets ``value``, returns the previous one in *old_value (may be NULL). */
+enum { S2V_TUNE_HALO_MIN_BLOCKS = 0, S2V_TUNE_GLDS_TILE = 1, S2V_TUNE_SMALLK_TILE = 2, S2V_TUNE_COUNT = 3 };
+int s2v_tune(int key, long long value, long long *old_value);
 
 /* Split packed fp32 weights [rows][kpad] (kpad % 32 == 0) into the layout of ``prec``
  * (S2V_PREC_BF16X3 / S2V_PREC_F16X3): [rows][kpad/32][hi 32 | lo 32] 16-bit (same byte size),
@@ -138,6 +152,11 @@ int s2v_conv2d_plan(const s2v_conv_params *p, int *out10);
  * wt_scale.  s2v_split_weights_x3 = the bf16 form with scale 1. */
 int s2v_split_weights(const float *w, int rows, int kpad, int prec, float scale, void *out, s2v_stream_t stream);
 int s2v_split_weights_x3(const float *w, int rows, int kpad, void *out, s2v_stream_t stream);
+/* fp32 NHWC activations [pixels][xcs] -> the split layout of ``prec`` at pitch ocs (floats; the
+ * conv input of s2v_conv_params.x_split): per pixel and 32-channel block [hi 32 | lo 32] 16-bit,
+ * hi = T_rne(v), lo = T_rne(v - hi).  c % 32 == 0, ocs % 32 == 0, out 128-byte aligned. */
+int s2v_split_act(const float *x, long long pixels, int c, int xcs, int prec, float *out, int ocs,
+                  s2v_stream_t stream);
 
 /* LayerNorm2d (base_blocks.py:52-69) over (H,W,C) per sample, fused affine + act
  * (+ 2x2 average pool: DownBlock2d base_blocks.py:95-109) (+ residual after act: Jump + out,

@@ -45,6 +45,7 @@ class ConvParams(ctypes.Structure):
         ("tile_counters", _vp), ("n_counters", _c_int),
         ("wt_scale", _c_float),
         ("out_pool", _c_int),
+        ("x_split", _c_int),
     ]
 
 
@@ -53,6 +54,7 @@ _SIGS = {
     "s2v_conv2d": (_c_int, [ctypes.POINTER(ConvParams), _vp]),
     "s2v_conv2d_ws_bytes": (_c_size, [ctypes.POINTER(ConvParams)]),
     "s2v_conv2d_plan": (_c_int, [ctypes.POINTER(ConvParams), ctypes.POINTER(_c_int)]),
+    "s2v_tune": (_c_int, [_c_int, _c_ll, ctypes.POINTER(_c_ll)]),
     "s2v_layernorm2d": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_float, _c_int, _c_float,
                                  _c_int, _vp, _c_int, _vp, _c_int, _vp, _c_size, _vp]),
     "s2v_layernorm2d_ws_bytes": (_c_size, [_c_int, _c_int, _c_int, _c_int]),
@@ -82,6 +84,7 @@ _SIGS = {
     "s2v_rfft2": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_int, _vp]),
     "s2v_irfft2": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_int, _vp, _c_int, _vp]),
     "s2v_split_weights": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_float, _vp, _vp]),
+    "s2v_split_act": (_c_int, [_vp, _c_ll, _c_int, _c_int, _c_int, _vp, _c_int, _vp]),
     "s2v_split_weights_x3": (_c_int, [_vp, _c_int, _c_int, _vp, _vp]),
     "s2v_modulate_weights_split": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp, _c_int,
                                             _c_int, _c_int, _c_float, _vp, _vp]),

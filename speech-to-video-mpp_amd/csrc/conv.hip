@@ -23,6 +23,8 @@ namespace s2v {
 
 template <int ELT>   // 0 = bf16, 1 = f16 halves (conv_x3_impl.hpp; instances in conv_x3_{bf16,f16}.hip)
 void launch_conv_x3(int tile, const ConvArgs &a, int amode, bool bkn, dim3 grid, hipStream_t s);
+template <int ELT>   // LDS-DMA kernels on split-layout inputs (conv_glds.hip): cfg 0 = 256x256, 1 = 256x128
+void launch_conv_glds(int cfg, const ConvArgs &a, dim3 grid, hipStream_t s);
 
 template <int BM, int BN, int AR, int BR, int BKN>
 __device__ __forceinline__ void store_ab(float *As, float *Bs, int tid, const f4 (&ra)[AR],
@@ -647,6 +649,22 @@ __global__ __launch_bounds__(256) void conv_halo_small(ConvArgs a, int tiles_x, 
 
 // The halo kernel serves plain stride-1 square-filter heads: direct input, zero or reflect
 // padding (pad < filter), no prologue scaling, one shared filter, 16-byte channel quads.
+// planner knobs (s2v_tune; defaults, or S2V_HALO_MIN_BLOCKS / S2V_GLDS_TILE from the environment)
+static long long g_tune[S2V_TUNE_COUNT];
+static bool g_tune_init = false;
+static long long tune_value(int key) {
+    if (!g_tune_init) {
+        const char *e = getenv("S2V_HALO_MIN_BLOCKS");
+        g_tune[S2V_TUNE_HALO_MIN_BLOCKS] = e ? atoll(e) : 512;
+        e = getenv("S2V_GLDS_TILE");
+        g_tune[S2V_TUNE_GLDS_TILE] = e ? atoll(e) : -1;
+        e = getenv("S2V_SMALLK_TILE");
+        g_tune[S2V_TUNE_SMALLK_TILE] = e ? atoll(e) : 1;
+        g_tune_init = true;
+    }
+    return g_tune[key];
+}
+
 static int halo_ks(const s2v_conv_params *p) {
     const int batch = p->batch > 0 ? p->batch : 1;
     if (p->cout > 4 || p->kh != p->kw || (p->kh != 3 && p->kh != 5 && p->kh != 7)) return 0;
@@ -654,6 +672,11 @@ static int halo_ks(const s2v_conv_params *p) {
     if (p->in_scale || p->pre_act || p->w_bs || batch != 1 || p->b_kn || p->out_step > 1) return 0;
     if (p->ph >= p->kh || p->pw >= p->kw || p->cin % 4 || p->xcs % 4 || ((uintptr_t)p->x % 16)) return 0;
     if (p->pad_mode == S2V_PAD_REFLECT && (p->ph >= p->h || p->pw >= p->w)) return 0;
+    // 8 x 128 output tiles: on small images (LNet's 96^2 RGB head, DNet's 64^2 flow head) too few
+    // blocks cover the chip and a 128-wide tile runs part empty; the channel-parallel kernel (lanes
+    // split K per pixel) has the parallelism there.  S2V_HALO_MIN_BLOCKS overrides (tuning).
+    const long long blocks = (long long)p->n * cdiv(p->ow, 128) * cdiv(p->oh, 8);
+    if (blocks < tune_value(S2V_TUNE_HALO_MIN_BLOCKS) || p->ow < 96) return 0;
     return p->kh;
 }
 
@@ -707,6 +730,10 @@ static int smallk_px(int M);
 // conv_smallk geometry: threads per pixel (cout / 4 channel quads, at most 64) and quads per thread
 static bool smallk_cfg(const s2v_conv_params *p, int M, int K, int &tppx, int &qpt) {
     if (p->b_kn || p->force_tile || p->out_pool || p->cout < 8 || (p->cout & 3) || K > 64 || !vec4_input(p)) return false;
+    // multi-tap filters on 4k-channel inputs go to the split-precision implicit GEMM even at K <= 64
+    // (measured on MI355X, r02: 3x3 4 -> 256 at 200^2 776 -> 336 us, 4 -> 64 at 512^2 602 -> 361 us,
+    // at 96^2 74 -> 32 us; the 1x1 4 -> 256 layer stays here, 415 us against 491 us)
+    if (p->prec != S2V_PREC_F32 && p->kh * p->kw > 1) return false;
     const int quads = p->cout / 4;
     if (quads & (quads - 1)) return false;                       // power of two
     // one output quad per thread, up to 64 threads per pixel (measured on MI355X: 64 lanes x 1 quad
@@ -777,6 +804,20 @@ static Plan make_plan_x3(const s2v_conv_params *p, int M, Plan pl) {
         finish_plan(pl, splits);
         return pl;
     }
+    if (pl.ktiles <= 4 && !p->b_kn && tune_value(S2V_TUNE_SMALLK_TILE)) {
+        // K <= 128 (image-input layers): the launch is output-write / gather bound, the throughput
+        // model does not apply.  One N tile covering cout reads A once; measured on MI355X (r02):
+        // 4 -> 256 3x3 at 200^2 256x256 336 us (128x128 497), 4 -> 64 at 96^2 64x64 32 us (128x64 43)
+        // (small M — LNet's 12^2 1x1 convs — keeps the throughput model: it needs the blocks)
+        int t = p->cout > 128 ? 0 : (p->cout > 64 ? 1 : 4);
+        const TileCfg &c = kX3Tiles[t].t;
+        const long long blocks = (long long)cdiv(M, c.bm) * cdiv(p->cout, c.bn) * batch;
+        if ((long long)cdiv(p->cout, c.bn) * c.bn <= p->npad && blocks >= 4LL * cus) {
+            pl.tile = t;
+            finish_plan(pl, 1);
+            return pl;
+        }
+    }
     double best = 1e30;
     int bt = kNumX3 - 1, bs = 1;
     const int am = a_mode(p);
@@ -808,12 +849,48 @@ static Plan make_plan_x3(const s2v_conv_params *p, int M, Plan pl) {
     return pl;
 }
 
+// LDS-DMA kernels (x_split inputs): 256 x BN tiles, BN = 256 when the weight rows allow, else 128
+struct GldsCfg {
+    int bm, bn, wm, nst;
+};
+static const GldsCfg kGlds[] = {{256, 256, 2, 2}, {256, 128, 4, 3}, {512, 128, 4, 2}};
+
+static int glds_cfg(const s2v_conv_params *p) {
+    const int forced = (int)tune_value(S2V_TUNE_GLDS_TILE);   // tuning override (tools/glds_sweep.sh)
+    if (forced >= 0 && forced < (int)(sizeof(kGlds) / sizeof(kGlds[0]))) {
+        const GldsCfg &c = kGlds[forced];
+        if ((long long)cdiv(p->cout, c.bn) * c.bn <= p->npad) return forced;
+    }
+    if (p->cout > 128 && (long long)cdiv(p->cout, 256) * 256 <= p->npad) return 0;
+    // N <= 128: 512x128 (128x64 per wave) over 256x128 (64x64 per wave, 33 % more LDS reads per
+    // MFMA): 400^2 256 -> 128 4330 vs 4648 us, 128 -> 128 2543 vs 2749 us (r02)
+    const long long m = (long long)p->n * p->oh * p->ow * (p->batch > 0 ? p->batch : 1);
+    return m >= 512LL * 1024 ? 2 : 1;
+}
+
+static Plan make_plan_glds(const s2v_conv_params *p, int M, Plan pl) {
+    const int batch = p->batch > 0 ? p->batch : 1;
+    const int cus = device_cus() > 0 ? device_cus() : 256;
+    pl.tile = glds_cfg(p);
+    const GldsCfg &c = kGlds[pl.tile];
+    const long long blocks = (long long)cdiv(M, c.bm) * cdiv(p->cout, c.bn) * batch;
+    int splits = p->force_splits;
+    if (splits <= 0) {
+        splits = 1;
+        if (blocks < cus) splits = (int)((2LL * cus + blocks - 1) / blocks);
+        if (splits > pl.ktiles / 8) splits = pl.ktiles / 8;
+    }
+    finish_plan(pl, splits);
+    return pl;
+}
+
 static Plan make_plan(const s2v_conv_params *p_in, int M, int K) {
     s2v_conv_params q = *p_in;
     if (q.out_pool) q.force_splits = 1;          // the pooled epilogue needs whole-K tiles
     const s2v_conv_params *p = &q;
     Plan pl{};
     pl.ktiles = (K + 31) / 32;
+    if (p->x_split) return make_plan_glds(p, M, pl);
     if (use_direct(p) && !p->force_tile) {
         pl.tile = -1;
         pl.splits = 1;
@@ -887,7 +964,15 @@ static int validate(const s2v_conv_params *p, int &M, int &K) {
                     "conv2d: force_tile %d (BN %d) needs npad >= %d, got %d", p->force_tile, t.bn,
                     cdiv(p->cout, t.bn) * t.bn, p->npad);
     }
-    if (uses_x3(p))
+    if (p->x_split) {
+        S2V_REQUIRE(p->prec == S2V_PREC_BF16X3 || p->prec == S2V_PREC_F16X3, "conv2d: x_split needs prec BF16X3 / F16X3");
+        S2V_REQUIRE(!p->b_kn && p->in_mode == S2V_IN_DIRECT && p->pad_mode == S2V_PAD_ZERO && p->cin % 32 == 0 &&
+                        p->kh * p->kw <= 32 && !p->in_scale && p->pre_act == S2V_ACT_NONE && p->xcs % 4 == 0 &&
+                        ((uintptr_t)p->x % 16) == 0 && p->x_bs % 4 == 0 && p->force_tile == 0,
+                    "conv2d: x_split needs a direct zero-padded conv, cin %% 32 == 0, <= 32 taps, packed weights, "
+                    "no in_scale / pre_act / force_tile, xcs %% 4 == 0 and a 16-byte aligned x");
+        S2V_REQUIRE(p->wt_x3 && ((uintptr_t)p->wt_x3 % 16) == 0, "conv2d: x_split needs 16B-aligned wt_x3");
+    } else if (uses_x3(p))
         S2V_REQUIRE(p->wt_x3 && ((uintptr_t)p->wt_x3 % 16) == 0, "conv2d: split precisions need 16B-aligned wt_x3");
     else
         S2V_REQUIRE(p->wt != nullptr, "conv2d: null weights");
@@ -922,13 +1007,14 @@ static int validate(const s2v_conv_params *p, int &M, int &K) {
         S2V_REQUIRE(p->oh % 2 == 0 && p->ow % 2 == 0, "conv2d: out_pool needs even output sizes");
         S2V_REQUIRE(!p->res && !p->nc_scale && !p->pix_add && p->out_step <= 1 && p->force_splits <= 1,
                     "conv2d: out_pool takes no res / nc_scale / pix_add / strided output / K split");
-        S2V_REQUIRE(!(use_direct(p) && !p->force_tile) && !is_smallk(p), "conv2d: out_pool needs the implicit-GEMM path");
+        S2V_REQUIRE(p->x_split || (!(use_direct(p) && !p->force_tile) && !is_smallk(p)),
+                    "conv2d: out_pool needs the implicit-GEMM path");
     }
     if (p->out_step > 1) {
         S2V_REQUIRE(!p->pix_add, "conv2d: strided output cannot take pix_add");
         S2V_REQUIRE(!p->res || (p->res == p->y && p->res_cs == p->ycs && p->res_oy == 0 && p->res_ox == 0),
                     "conv2d: strided output only takes an in-place residual (res == y)");
-        S2V_REQUIRE(p->cout > 4, "conv2d: strided output needs the implicit-GEMM path (cout > 4)");
+        S2V_REQUIRE(p->cout > 4 || p->x_split, "conv2d: strided output needs the implicit-GEMM path (cout > 4)");
         S2V_REQUIRE(p->out_full_h >= (p->oh - 1) * p->out_step + 1 && p->out_full_w >= (p->ow - 1) * p->out_step + 1,
                     "conv2d: strided output exceeds out_full_h/w");
     }
@@ -954,7 +1040,7 @@ static ConvArgs make_args(const s2v_conv_params *p, int M, int K, const Plan &pl
     a.M = M; a.K = K; a.ktiles = pl.ktiles; a.splits = pl.splits; a.tps = pl.tps; a.ws = p->ws;
     a.y_step = p->out_step > 1 ? p->out_step : 1; a.y_h = p->out_full_h; a.y_w = p->out_full_w;
     a.cnt = nullptr;
-    a.acc_scale = (tiled_x3(p) && !p->b_kn && p->wt_scale > 0.f) ? 1.f / p->wt_scale : 1.f;
+    a.acc_scale = ((p->x_split || tiled_x3(p)) && !p->b_kn && p->wt_scale > 0.f) ? 1.f / p->wt_scale : 1.f;
     a.pool = p->out_pool != 0;
     return a;
 }
@@ -1002,6 +1088,14 @@ static int x3_amode(const s2v_conv_params *p, const TileCfg &t) {
 
 using namespace s2v;
 
+extern "C" int s2v_tune(int key, long long value, long long *old_value) {
+    S2V_REQUIRE(key >= 0 && key < S2V_TUNE_COUNT, "tune: bad key %d", key);
+    const long long prev = tune_value(key);
+    if (old_value) *old_value = prev;
+    g_tune[key] = value;
+    return 0;
+}
+
 extern "C" size_t s2v_conv2d_ws_bytes(const s2v_conv_params *p) {
     int M, K;
     if (validate(p, M, K) != 0) return 0;
@@ -1017,6 +1111,12 @@ extern "C" int s2v_conv2d_plan(const s2v_conv_params *p, int *out6) {
     int rc = validate(p, M, K);
     if (rc) return rc;
     Plan pl = make_plan(p, M, K);
+    if (p->x_split) {                                   // conv_glds_x3<BM, BN, WM, NST, prec-1>
+        const GldsCfg &c = kGlds[pl.tile];
+        out6[0] = c.bm; out6[1] = c.bn; out6[2] = c.wm; out6[3] = 5; out6[4] = 0; out6[5] = pl.splits;
+        out6[6] = p->prec; out6[7] = 8; out6[8] = c.nst; out6[9] = 0;
+        return 0;
+    }
     if (pl.tile == -2) {
         int tppx, qpt;
         smallk_cfg(p, M, K, tppx, qpt);
@@ -1112,6 +1212,13 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
             return S2V_E_WORKSPACE;
         }
     }
+    if (p->x_split) {
+        const GldsCfg &c = kGlds[pl.tile];
+        dim3 grid(cdiv(M, c.bm), cdiv(p->cout, c.bn), batch * pl.splits);
+        a.wt = (const float *)p->wt_x3;
+        if (p->prec == S2V_PREC_BF16X3) launch_conv_glds<0>(pl.tile, a, grid, s);
+        else launch_conv_glds<1>(pl.tile, a, grid, s);
+    } else {
     const int amode = a_mode(p);
     const bool bkn = p->b_kn != 0;
     const TileCfg &t = tile_cfg(p, pl.tile);
@@ -1134,6 +1241,7 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
         case 3: launch_tile<64, 64, 2>(a, amode, bkn, grid, s); break;
         case 4: launch_tile<256, 32, 4>(a, amode, bkn, grid, s); break;
         default: launch_tile<128, 32, 4>(a, amode, bkn, grid, s); break;
+    }
     }
     rc = check_launch("conv_igemm");
     if (rc || pl.splits <= 1 || a.cnt) return rc;

@@ -70,24 +70,28 @@ def _require_cuda(t: torch.Tensor, what: str):
 
 
 class NHWC:
-    """Channel-slice view of a contiguous [N, H, W, Ctot] fp32 device tensor."""
-    __slots__ = ("t", "n", "h", "w", "cs", "coff", "c")
+    """Channel-slice view of a contiguous [N, H, W, Ctot] fp32 device tensor.  ``split``: the
+    tensor holds the split-fp32 layout of the current precision (s2v_split_act; only convolutions
+    with x_split read it)."""
+    __slots__ = ("t", "n", "h", "w", "cs", "coff", "c", "split")
 
-    def __init__(self, t: torch.Tensor, coff: int = 0, c: int | None = None):
+    def __init__(self, t: torch.Tensor, coff: int = 0, c: int | None = None, split: bool = False):
         assert t.dim() == 4 and t.is_contiguous(), "NHWC view needs a contiguous 4-D tensor"
         _require_cuda(t, "NHWC")
         self.t = t
         self.n, self.h, self.w, self.cs = t.shape
         self.coff = coff
         self.c = self.cs - coff if c is None else c
+        self.split = split
         assert 0 <= coff and coff + self.c <= self.cs
+        assert not split or (coff % 32 == 0 and self.c % 32 == 0), "split views cover whole 32-channel blocks"
 
     @property
     def ptr(self) -> int:
         return self.t.data_ptr() + F32 * self.coff
 
     def slice(self, coff: int, c: int) -> "NHWC":
-        return NHWC(self.t, self.coff + coff, c)
+        return NHWC(self.t, self.coff + coff, c, self.split)
 
     @staticmethod
     def empty(n, h, w, c, device) -> "NHWC":
@@ -274,6 +278,7 @@ def conv2d(ctx: Ctx, x: NHWC, cw: ConvW, y: NHWC, *, act=ACT_NONE, alpha=0.0, re
                 continue
             base = NHWC.__new__(NHWC)
             base.t, base.n, base.h, base.w, base.cs, base.c = y.t, y.n, ch, cwid, y.cs, y.c
+            base.split = False
             base.coff = y.coff + (ry * y.w + rx) * y.cs
             _conv(ctx, x, sub, base, (ch, cwid), (2, y.h, y.w), act, alpha, None if res is None else base, False,
                   (0, 0), nc_scale, in_scale, pre_act, pre_alpha, None, 0.0, scale, shift, force_tile, force_splits)
@@ -314,6 +319,9 @@ def _conv(ctx, x, cw, y, ohw, out_view, act, alpha, res, res_after, res_offset, 
     p.batch = 1
     p.force_tile, p.force_splits = force_tile, force_splits
     p.out_pool = int(pool)
+    p.x_split = int(getattr(x, "split", False))
+    if p.x_split:
+        assert p.prec != PREC_F32, "split-layout inputs need a split precision (f16x3 / bf16x3)"
     if out_view is not None:
         p.out_step, p.out_full_h, p.out_full_w = out_view
     if per_sample_wt is not None:        # batch mode: one image per batch entry, its own weights
@@ -353,7 +361,7 @@ def _conv(ctx, x, cw, y, ohw, out_view, act, alpha, res, res_after, res_offset, 
 
 def modulated_conv2d(ctx: Ctx, x: NHWC, cw: ConvW, y: NHWC, s: torch.Tensor, d: torch.Tensor | None = None, *,
                      act=ACT_NONE, alpha=0.0, res: NHWC | None = None, res_after=False, pix_add=None, pix_w=0.0,
-                     shift=None):
+                     shift=None, force_splits=0):
     """StyleGAN2 modulated conv with per-sample weights W * s[b, c] (* d[b, o]) built by
     s2v_modulate_weights, then one batched conv (no prologue / epilogue scaling in the GEMM).
     s: [B, cin] (row stride s.stride(0)); d: [B, cout] demodulation or None."""
@@ -380,7 +388,7 @@ def modulated_conv2d(ctx: Ctx, x: NHWC, cw: ConvW, y: NHWC, s: torch.Tensor, d: 
                                                  ctx.stream), "s2v_modulate_weights_split")
         return wb, scale
     return _conv(ctx, x, cw, y, (oh, ow), None, act, alpha, res, res_after, (0, 0), None, None, ACT_NONE, 0.0,
-                 pix_add, pix_w, None, shift, 0, 0, per_sample_wt=weights)
+                 pix_add, pix_w, None, shift, 0, force_splits, per_sample_wt=weights)
 
 
 def gemm_kn(ctx: Ctx, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, batch: int, a_bs: int, b_bs: int,
@@ -430,13 +438,15 @@ def _plan(ctx: Ctx, p):
 def conv_symbol(ctx: Ctx, p) -> str:
     """Kernel symbol (as rocprofv3 reports it, demangled) the launch of ``p`` runs."""
     bm, bn, wm, avec, bkn, splits, x3, nw, ks, pf = _plan(ctx, p)
+    if avec == 5:
+        return f"void s2v::conv_glds_x3<{bm}, {bn}, {wm}, {ks}, {x3 - 1}>(s2v::ConvArgs)"
     if bm == 0:
-        if bkn >= 1000:
-            return f"void s2v::conv_halo_small<{bn}, {bkn - 1000}>(s2v::ConvArgs, int, int)"
         if wm < 0:
             if bkn >= 2000:
                 return f"void s2v::conv_smallk4<{-wm}, {bkn - 2000}>(s2v::ConvArgs, int, int, int, int)"
             return f"void s2v::conv_smallk<{-wm}, {avec}>(s2v::ConvArgs, int, int, int, int)"
+        if bkn >= 1000:
+            return f"void s2v::conv_halo_small<{bn}, {bkn - 1000}>(s2v::ConvArgs, int, int)"
         if wm:
             return f"void s2v::conv_small_cpar<{bn}, {wm}, {'true' if avec else 'false'}>(s2v::ConvArgs, int)"
         return f"void s2v::conv_direct_small<{bn}>(s2v::ConvArgs, int)"
@@ -444,6 +454,29 @@ def conv_symbol(ctx: Ctx, p) -> str:
         return (f"void s2v::conv_igemm_x3<{bm}, {bn}, {wm}, {nw}, {ks}, {pf}, {avec}, {bkn}, {x3 - 1}>"
                 "(s2v::ConvArgs)")
     return f"void s2v::conv_igemm<{bm}, {bn}, {wm}, {avec}, {bkn}>(s2v::ConvArgs)"
+
+
+def split_act(ctx: Ctx, x: NHWC, out: NHWC | None = None) -> NHWC:
+    """fp32 activations -> the split layout of the current precision (s2v_split_act), the input
+    form of the LDS-DMA convolutions.  ``out``: a whole contiguous tensor of x's shape."""
+    prec = prec_code()
+    assert prec != PREC_F32, "split_act needs a split precision (f16x3 / bf16x3)"
+    if out is None:
+        out = NHWC.empty(x.n, x.h, x.w, x.c, x.t.device)
+    assert (out.n, out.h, out.w, out.c) == (x.n, x.h, x.w, x.c) and out.coff == 0
+    check(ctx.lib.s2v_split_act(x.ptr, x.n * x.h * x.w, x.c, x.cs, prec, out.ptr, out.cs, ctx.stream), "s2v_split_act")
+    out.split = True
+    return out
+
+
+TUNE_HALO_MIN_BLOCKS, TUNE_GLDS_TILE = 0, 1
+
+
+def tune(ctx: Ctx, key: int, value: int) -> int:
+    """Set a planner knob (s2v_tune); returns the previous value."""
+    old = ctypes.c_longlong(0)
+    check(ctx.lib.s2v_tune(key, value, ctypes.byref(old)), "s2v_tune")
+    return old.value
 
 
 def conv_splits(ctx: Ctx, p) -> int:

@@ -92,10 +92,13 @@ CONV_CASES = [
     (2, 64, 6, 7, 32, 3, 2, 1, 1, "transposed", "zero", 0, 0),
     (2, 64, 9, 9, 3, 7, 1, 3, 1, "direct", "zero", 0, 0),     # direct small-N kernel
     # halo-tiled small-Cout kernel (8 x 128 output tiles): ragged tiles in both directions, reflect
-    # halos, 3 / 5 / 7 filters, 1..4 outputs (DNet's 7x7 64 -> 3 head at 256^2 is the model case)
+    # halos, 3 / 5 / 7 filters, 1..4 outputs (DNet's 7x7 64 -> 3 head at 256^2 is the model case);
+    # rows with w >= 96 run it with the planner's block-count floor off (halo_everywhere)
     (2, 64, 37, 150, 3, 7, 1, 3, 1, "direct", "zero", 0, 0),
     (1, 64, 20, 130, 3, 7, 1, 3, 1, "direct", "reflect", 0, 0),
-    (2, 32, 19, 17, 4, 3, 1, 1, 1, "direct", "reflect", 0, 0),
+    (2, 32, 19, 100, 4, 3, 1, 1, 1, "direct", "reflect", 0, 0),
+    (2, 16, 16, 120, 1, 5, 1, 2, 1, "direct", "zero", 0, 0),
+    (2, 32, 19, 17, 4, 3, 1, 1, 1, "direct", "reflect", 0, 0),      # narrow: channel-parallel kernel
     (2, 16, 16, 16, 1, 5, 1, 2, 1, "direct", "zero", 0, 0),
     (1, 8, 9, 260, 2, 7, 1, 2, 1, "direct", "zero", 0, 0),
     (3, 1, 20, 16, 32, 3, (3, 1), 1, 1, "direct", "zero", 0, 0),
@@ -123,9 +126,20 @@ CONV_CASES = [
 ]
 
 
+@pytest.fixture
+def halo_everywhere(ctx):
+    """The halo-tiled small-Cout kernel for every qualifying shape (its block-count floor off), so
+    the small test images exercise it."""
+    prev = ops.tune(ctx, ops.TUNE_HALO_MIN_BLOCKS, 0)
+    yield
+    ops.tune(ctx, ops.TUNE_HALO_MIN_BLOCKS, prev)
+
+
 @pytest.mark.parametrize("case", CONV_CASES, ids=[str(i) for i in range(len(CONV_CASES))])
-def test_conv2d(ctx, prec, case):
+def test_conv2d(ctx, prec, case, request):
     n, cin, h, w, cout, k, stride, pad, dil, mode, pad_mode, tile, splits = case
+    if cout <= 4 and w >= 96:
+        request.getfixturevalue("halo_everywhere")
     if tile > 6 and prec == "f32":
         pytest.skip("tiles 7-8 exist in the bf16x3 table only")
     kh, kw = (k, k) if isinstance(k, int) else k

@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--splits", type=int, default=0)
     ap.add_argument("--prec", default="both", choices=("f32", "bf16x3", "f16x3", "both", "split"))
     ap.add_argument("--tiles", default="", help="comma list of force_tile values (101.. = x3 variants)")
+    ap.add_argument("--glds", action="store_true", help="also time the LDS-DMA kernel on a split-layout input")
     a = ap.parse_args()
     dev = torch.device("cuda")
     ctx = ops.Ctx(dev)
@@ -62,6 +63,29 @@ def main():
         ms = s.elapsed_time(e) / a.iters
         print(f"tile={t} {ops.conv_symbol(ctx, _params(ctx, x, cw, y, t, a.splits))}: {ms * 1e3:9.1f} us  "
               f"{flops / ms / 1e9:7.2f} TFLOP/s", flush=True)
+    if a.glds and not a.up2 and a.stride == 1:
+        ops.set_precision("f16x3")
+        xs = ops.split_act(ctx, x)
+        y2 = NHWC.empty(a.n, oh, ow, a.cout, dev)
+        kw = dict(act=ops.ACT_LRELU, alpha=0.2, force_splits=a.splits)
+        ops.conv2d(ctx, x, cw, y, **kw)
+        ops.conv2d(ctx, xs, cw, y2, **kw)
+        torch.cuda.synchronize()
+        same = bool(torch.equal(y.t, y2.t))
+        md = (y.t - y2.t).abs().max().item()
+        for name, fn in (("split_act", lambda: ops.split_act(ctx, x, xs)),
+                         ("glds conv", lambda: ops.conv2d(ctx, xs, cw, y2, **kw))):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(a.iters):
+                fn()
+            e.record()
+            torch.cuda.synchronize()
+            ms = s.elapsed_time(e) / a.iters
+            extra = f"{flops / ms / 1e9:7.2f} TFLOP/s  bitwise={same} maxdiff={md:.3g}" if name == "glds conv" else \
+                f"{x.t.numel() * 8 / ms / 1e9:7.1f} GB/s"
+            print(f"{name} {ops.conv_symbol(ctx, _params(ctx, xs, cw, y2, 0, a.splits)) if name == 'glds conv' else ''}: "
+                  f"{ms * 1e3:9.1f} us  {extra}", flush=True)
 
 
 def _params(ctx, x, cw, y, tile, splits):

@@ -8,7 +8,7 @@ CONV=${CONV:-"--n 16 --h 200 --w 200 --cin 256 --cout 256 --k 3 --tiles 1 --prec
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 120 python3 tools/conv_micro.py $CONV > "$OUT/time.log" 2>&1
-cat "$OUT/time.log" | grep tile
+grep -E "tile|glds" "$OUT/time.log"
 i=0
 for pass in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA GRBM_GUI_ACTIVE" \
             "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS GRBM_COUNT" $PMC_EXTRA; do
@@ -16,4 +16,4 @@ for pass in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_WAIT_ANY SQ_WAIT
   timeout -s KILL 90 rocprofv3 --pmc $pass --output-format csv -d "$OUT/p$i" -o run -- python3 tools/conv_micro.py $CONV > "$OUT/p$i.log" 2>&1
   echo "pass $i done"
 done
-python3 tools/pmc_counters.py $(ls -d $OUT/p*/ ) --match conv_igemm --out "$OUT/pmc.json"
+python3 tools/pmc_counters.py $(ls -d $OUT/p*/ ) --match "${MATCH:-conv_igemm}" --out "$OUT/pmc.json"
