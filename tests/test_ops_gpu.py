@@ -413,6 +413,17 @@ def test_resize_bilinear(ctx, shape):
     assert (to_nchw(y2) - ref.double()).abs().max() < 2e-6
 
 
+@pytest.mark.parametrize("n,c,h,w,extra", [(2, 64, 7, 9, 0), (3, 4, 100, 100, 0), (1, 32, 13, 5, 8)])
+def test_resize_up2_quads(ctx, n, c, h, w, extra):
+    """Exact x2 upsample (2x2 output quads per thread: the StyleConv / ToRGB upsamples) against
+    F.interpolate, into a channel slice of a wider output (edges clamp on every side)."""
+    x = rnd(n, c, h, w, seed=33).float()
+    ref = F.interpolate(x, scale_factor=2, mode="bilinear", align_corners=False)
+    y = NHWC.empty(n, 2 * h, 2 * w, c + extra, DEV).slice(extra, c)
+    ops.resize_nhwc(ctx, nhwc(x), y, scale_factor=2)
+    assert (to_nchw(y) - ref.double()).abs().max() < 2e-6
+
+
 def test_pad_reflect_and_crop(ctx):
     x = rnd(2, 3, 96, 96, seed=32).float()
     y = NHWC.empty(2, 100, 100, 3, DEV)
