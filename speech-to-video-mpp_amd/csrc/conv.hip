@@ -587,13 +587,16 @@ __global__ __launch_bounds__(256) void conv_halo_small(ConvArgs a, int tiles_x, 
     const int oy0 = tyi * TH, ox0 = txi * TW;
     const float *xb = a.x + (long long)img * a.h * a.w * a.xcs;
     const float *__restrict__ wt = a.wt;
+    // channel split (gridDim.y = a.splits, a.tps channels each): raw partial sums to the split-K
+    // workspace, folded by splitk_reduce with the epilogue (small images: too few tiles otherwise)
+    const int cb = blockIdx.y * a.tps, ce = min(a.cin, cb + a.tps);
     float acc[PX][CO];
 #pragma unroll
     for (int p = 0; p < PX; ++p)
 #pragma unroll
         for (int o = 0; o < CO; ++o) acc[p][o] = 0.f;
     const bool refl = a.pad_mode == S2V_PAD_REFLECT;
-    for (int c0 = 0; c0 < a.cin; c0 += 4) {
+    for (int c0 = cb; c0 < ce; c0 += 4) {
         __syncthreads();                                      // the previous chunk has been consumed
         for (int e = tid; e < IH * IW; e += 256) {
             const int iy = e / IW, ix = e - iy * IW;
@@ -642,6 +645,12 @@ __global__ __launch_bounds__(256) void conv_halo_small(ConvArgs a, int tiles_x, 
         const int ox = ox0 + 4 * cg + p;
         if (ox >= a.ow) continue;
         const int m = (img * a.oh + oy) * a.ow + ox;
+        if (a.splits > 1) {
+            float *w = a.ws + ((long long)blockIdx.y * a.M + m) * a.cout;
+#pragma unroll
+            for (int o = 0; o < CO; ++o) w[o] = acc[p][o];
+            continue;
+        }
 #pragma unroll
         for (int o = 0; o < CO; ++o) store_epilogue(a, 0, m, o, acc[p][o]);
     }
@@ -655,7 +664,7 @@ static bool g_tune_init = false;
 static long long tune_value(int key) {
     if (!g_tune_init) {
         const char *e = getenv("S2V_HALO_MIN_BLOCKS");
-        g_tune[S2V_TUNE_HALO_MIN_BLOCKS] = e ? atoll(e) : 512;
+        g_tune[S2V_TUNE_HALO_MIN_BLOCKS] = e ? atoll(e) : 0;
         e = getenv("S2V_GLDS_TILE");
         g_tune[S2V_TUNE_GLDS_TILE] = e ? atoll(e) : -1;
         e = getenv("S2V_SMALLK_TILE");
@@ -676,14 +685,26 @@ static int halo_ks(const s2v_conv_params *p) {
     // blocks cover the chip and a 128-wide tile runs part empty; the channel-parallel kernel (lanes
     // split K per pixel) has the parallelism there.  S2V_HALO_MIN_BLOCKS overrides (tuning).
     const long long blocks = (long long)p->n * cdiv(p->ow, 128) * cdiv(p->oh, 8);
-    if (blocks < tune_value(S2V_TUNE_HALO_MIN_BLOCKS) || p->ow < 96) return 0;
+    if (blocks < tune_value(S2V_TUNE_HALO_MIN_BLOCKS)) return 0;
     return p->kh;
+}
+
+// channel splits of the halo kernel: about three blocks per CU, at least 8 channels per split
+static int halo_splits(const s2v_conv_params *p, int &per) {
+    const long long blocks = (long long)p->n * cdiv(p->ow, 128) * cdiv(p->oh, 8);
+    const int cus = device_cus() > 0 ? device_cus() : 256;
+    const int quads = p->cin / 4;
+    int s = blocks >= 3LL * cus ? 1 : (int)((3LL * cus + blocks - 1) / blocks);
+    if (s > quads / 2) s = quads / 2;
+    if (s < 1) s = 1;
+    per = 4 * ((quads + s - 1) / s);
+    return (p->cin + per - 1) / per;
 }
 
 template <int CO>
 static void launch_halo(const ConvArgs &a, int ks, hipStream_t s) {
     const int tiles_x = (int)cdiv(a.ow, 128), tiles_y = (int)cdiv(a.oh, 8);
-    const unsigned grid = (unsigned)((long long)a.n * tiles_x * tiles_y);
+    const dim3 grid((unsigned)((long long)a.n * tiles_x * tiles_y), (unsigned)a.splits);
     if (ks == 3) conv_halo_small<CO, 3><<<grid, 256, 0, s>>>(a, tiles_x, tiles_y);
     else if (ks == 5) conv_halo_small<CO, 5><<<grid, 256, 0, s>>>(a, tiles_x, tiles_y);
     else conv_halo_small<CO, 7><<<grid, 256, 0, s>>>(a, tiles_x, tiles_y);
@@ -895,6 +916,7 @@ static Plan make_plan(const s2v_conv_params *p_in, int M, int K) {
         pl.tile = -1;
         pl.splits = 1;
         pl.tps = pl.ktiles;
+        if (HALO_SMALL && halo_ks(p)) pl.splits = halo_splits(p, pl.tps);   // tps: channels per split
         return pl;
     }
     int tppx, qpt;
@@ -1100,7 +1122,7 @@ extern "C" size_t s2v_conv2d_ws_bytes(const s2v_conv_params *p) {
     int M, K;
     if (validate(p, M, K) != 0) return 0;
     Plan pl = make_plan(p, M, K);
-    if (pl.tile < 0 || pl.splits <= 1) return 0;
+    if (pl.splits <= 1 || pl.tile == -2) return 0;
     const int batch = p->batch > 0 ? p->batch : 1;
     return (size_t)batch * pl.splits * (size_t)M * p->cout * sizeof(float);
 }
@@ -1129,7 +1151,7 @@ extern "C" int s2v_conv2d_plan(const s2v_conv_params *p, int *out6) {
     if (pl.tile < 0 && HALO_SMALL && halo_ks(p)) {
         out6[0] = 0; out6[1] = p->cout < 4 ? p->cout : 4;
         out6[2] = 0; out6[3] = 0;
-        out6[4] = 1000 + halo_ks(p); out6[5] = 1;          // conv_halo_small<CO, KS>
+        out6[4] = 1000 + halo_ks(p); out6[5] = pl.splits;  // conv_halo_small<CO, KS>
         return 0;
     }
     if (pl.tile < 0) {
@@ -1183,13 +1205,23 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
         return check_launch("conv_smallk");
     }
     if (pl.tile < 0 && HALO_SMALL && halo_ks(p)) {
+        if (pl.splits > 1) {
+            const size_t need = (size_t)pl.splits * (size_t)M * p->cout * sizeof(float);
+            if (!p->ws || p->ws_bytes < need) {
+                set_error("conv2d: split workspace of %zu bytes required (have %zu)", need, p->ws_bytes);
+                return S2V_E_WORKSPACE;
+            }
+        }
         switch (p->cout) {
             case 1: launch_halo<1>(a, halo_ks(p), s); break;
             case 2: launch_halo<2>(a, halo_ks(p), s); break;
             case 3: launch_halo<3>(a, halo_ks(p), s); break;
             default: launch_halo<4>(a, halo_ks(p), s); break;
         }
-        return check_launch("conv_halo_small");
+        rc = check_launch("conv_halo_small");
+        if (rc || pl.splits <= 1) return rc;
+        splitk_reduce<<<cdiv((long long)M * p->cout, 256), 256, 0, s>>>(a, 1);
+        return check_launch("splitk_reduce");
     }
     if (pl.tile < 0) {
         const bool cpar = (p->cin % 4 == 0) && (p->xcs % 4 == 0) && (((uintptr_t)p->x % 16) == 0) &&
