@@ -138,7 +138,9 @@ size_t s2v_conv2d_ws_bytes(const s2v_conv_params *p);
 int s2v_conv2d_plan(const s2v_conv_params *p, int *out10);
 /* Planner knobs (tests / tuning; process-wide, not thread-safe against concurrent planning):
  *   S2V_TUNE_HALO_MIN_BLOCKS  the halo-tiled small-Cout kernel needs at least this many 8x128 tiles
- *                             (default 512, env S2V_HALO_MIN_BLOCKS); fewer go channel-parallel;
+ *                             (default 0, env S2V_HALO_MIN_BLOCKS; fewer go channel-parallel).  Below
+ *                             ~3 tiles per CU it splits the channels (split-K workspace, see
+ *                             s2v_conv2d_ws_bytes) and folds them with the epilogue;
  *   S2V_TUNE_GLDS_TILE        force an LDS-DMA tile config (-1 = planner, env S2V_GLDS_TILE);
  *   S2V_TUNE_SMALLK_TILE      1: split-precision convs with K <= 128 on large M take one N tile over
  *                             cout (default, env S2V_SMALLK_TILE); 0: the throughput model.
