@@ -419,6 +419,23 @@ int s2v_u8_div255_f64(const unsigned char *x, long long n, double *y, s2v_stream
 int s2v_face_blend(const unsigned char *base, const float *full_mask, const unsigned char *full_img,
                    const double *mask_sharp, unsigned char *out, long long pixels, s2v_stream_t stream);
 
+/* ---- 3DMM coefficient regression front end (facing.py:100-130) ---------------- */
+
+/* face3d util/preprocess.py resize_n_crop_img (:147-167) as align_img (:186-216) calls it, then the
+ * network input of facing.py:120: PIL img.resize((w, h), resample = filter: 2 BILINEAR, 3 BICUBIC)
+ * and img.crop((left, up, left + ow, up + oh)) on n uint8 RGB frames [n][h0][w0][3] (frame stride
+ * xis bytes) with Pillow's Resample.c arithmetic (double taps, 22-bit fixed point, uint8 rows
+ * between the horizontal and vertical pass; crop pixels outside the resized image are 0) ->
+ * fp32 float32(pixel / 255.) NHWC [n][oh][ow][ycs] (channels >= 3 zero).  params: DEVICE int32
+ * [n][4] = (w, h, left, up) per frame; a resample that needs more than 48 taps per output
+ * coordinate (more than an 11.75x bicubic downscale) writes NaN.  Replaces facing.py:118-121
+ * (align_img + np.array(im) / 255. + torch.tensor) for every frame of the clip at once. */
+int s2v_pil_resize_crop(const unsigned char *x, int n, int h0, int w0, long long xis, const int *params, int filter,
+                        float *y, int oh, int ow, int ycs, s2v_stream_t stream);
+/* nn.AdaptiveAvgPool2d((1, 1)) on NHWC fp32: y[b][c] = mean of x[b][0..hw)[c] (fp64 sum)
+ * (face3d models/networks.py ResNet._forward_impl avgpool). */
+int s2v_spatial_mean_nhwc(const float *x, int n, int hw, int c, float *y, s2v_stream_t stream);
+
 const char *s2v_last_error(void);
 /* number of compute units of the current device (0 if no device) */
 int s2v_device_cus(void);

@@ -39,9 +39,9 @@ def _conv_bn(sd, p, x, stride=1, act=None):
     return F.leaky_relu(y, act) if act is not None else y
 
 
-def resnet50_body(sd, x):
-    """torchvision resnet50 conv1..layer4 (Bottleneck v1.5) -> (layer2, layer3, layer4) outputs."""
-    p = "body."
+def resnet50_body(sd, x, p="body."):
+    """torchvision resnet50 conv1..layer4 (Bottleneck v1.5) -> (layer2, layer3, layer4) outputs
+    (parameters under prefix ``p``: ``body.`` in RetinaFace, ``backbone.`` in face3d's ReconNet)."""
     y = F.relu(_bn(sd, p + "bn1.", F.conv2d(x, sd[p + "conv1.weight"], None, 2, 3)))
     y = F.max_pool2d(y, 3, 2, 1)
     outs = []

@@ -126,6 +126,9 @@ _SIGS = {
     "s2v_gan_to_u8": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _vp]),
     "s2v_u8_div255_f64": (_c_int, [_vp, _c_ll, _vp, _vp]),
     "s2v_face_blend": (_c_int, [_vp, _vp, _vp, _vp, _vp, _c_ll, _vp]),
+    "s2v_pil_resize_crop": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_ll, _vp, _c_int, _vp, _c_int, _c_int, _c_int,
+                                     _vp]),
+    "s2v_spatial_mean_nhwc": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _vp]),
     "s2v_last_error": (ctypes.c_char_p, []),
     "s2v_device_cus": (_c_int, []),
     "s2v_version": (ctypes.c_char_p, []),

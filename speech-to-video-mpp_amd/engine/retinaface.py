@@ -82,20 +82,46 @@ class _SSH:
         return o
 
 
-class RetinaFaceEngine:
+class ResNet50Body:
+    """torchvision resnet50 conv1 .. layer4 (Bottleneck v1.5, [3, 4, 6, 3]) with its parameters
+    under ``prefix``: RetinaFace's ``body.`` (IntermediateLayerGetter) and face3d ReconNet's
+    ``backbone.`` (models/networks.py:226-372, the same torchvision layout)."""
     LAYERS = ((3, 1), (4, 2), (6, 2), (3, 2))
-    HEAD_CS = 32
 
-    def __init__(self, sd, device):
-        dev = torch.device(device)
-        self.device = dev
-        b = "body."
+    def __init__(self, sd, prefix, dev):
+        b = prefix
         self.stem = ConvW(ops.pad_cin(sd[b + "conv1.weight"].float(), 4), None, dev, stride=2, padding=3,
                           bn=_bn(sd, b + "bn1."))
         self.layers = []
         for li, (blocks, stride) in enumerate(self.LAYERS):
             self.layers.append([_Bottleneck(sd, f"{b}layer{li + 1}.{j}.", stride if j == 0 else 1, dev)
                                 for j in range(blocks)])
+
+    def __call__(self, ctx, x4: NHWC):
+        """x4 [n,H,W,4] (channel 3 zero) -> (layer1, layer2, layer3, layer4) outputs."""
+        dev = x4.t.device
+        oh, ow = self.stem.out_hw(x4.h, x4.w)
+        s = NHWC.empty(x4.n, oh, ow, 64, dev)
+        ops.conv2d(ctx, x4, self.stem, s, act=RELU)
+        ph, pw = (oh + 2 - 3) // 2 + 1, (ow + 2 - 3) // 2 + 1
+        y = NHWC.empty(x4.n, ph, pw, 64, dev)
+        ops.check(ctx.lib.s2v_maxpool2d_nhwc(s.ptr, s.n, s.h, s.w, 64, 3, 2, 1, y.ptr, ph, pw, ctx.stream),
+                  "s2v_maxpool2d_nhwc")
+        outs = []
+        for blocks in self.layers:
+            for blk in blocks:
+                y = blk(ctx, y)
+            outs.append(y)
+        return outs
+
+
+class RetinaFaceEngine:
+    HEAD_CS = 32
+
+    def __init__(self, sd, device):
+        dev = torch.device(device)
+        self.device = dev
+        self.body = ResNet50Body(sd, "body.", dev)
         f = "fpn."
         self.out = [ConvW(sd[f"{f}output{i}.0.weight"], None, dev, bn=_bn(sd, f"{f}output{i}.1.")) for i in (1, 2, 3)]
         self.merge1 = ConvW(sd[f + "merge1.0.weight"], None, dev, padding=1, bn=_bn(sd, f + "merge1.1."))
@@ -118,21 +144,7 @@ class RetinaFaceEngine:
 
     def backbone(self, ctx, x4: NHWC):
         """x4 [n,H,W,4] (BGR minus means, channel 3 zero) -> (layer2, layer3, layer4) outputs."""
-        dev = x4.t.device
-        oh, ow = self.stem.out_hw(x4.h, x4.w)
-        s = NHWC.empty(x4.n, oh, ow, 64, dev)
-        ops.conv2d(ctx, x4, self.stem, s, act=RELU)
-        ph, pw = (oh + 2 - 3) // 2 + 1, (ow + 2 - 3) // 2 + 1
-        y = NHWC.empty(x4.n, ph, pw, 64, dev)
-        ops.check(ctx.lib.s2v_maxpool2d_nhwc(s.ptr, s.n, s.h, s.w, 64, 3, 2, 1, y.ptr, ph, pw, ctx.stream),
-                  "s2v_maxpool2d_nhwc")
-        outs = []
-        for li, blocks in enumerate(self.layers):
-            for blk in blocks:
-                y = blk(ctx, y)
-            if li >= 1:
-                outs.append(y)
-        return outs
+        return self.body(ctx, x4)[1:]
 
     def fpn(self, ctx, feats):
         """net.py:79-100 -> [output1, output2, output3]."""

@@ -16,7 +16,7 @@ import torch
 
 from .. import ops
 from ..ops import NHWC
-from . import arch, enhancer_arch, parse_arch, retinaface_arch, sr_arch
+from . import arch, enhancer_arch, face3d_arch, parse_arch, retinaface_arch, sr_arch
 
 
 def _fold5(x, dim):
@@ -267,6 +267,39 @@ def retina_outputs(ctx, maps, im_h, im_w):
     return loc, conf, lms
 
 
+class ReconNetWrapper(_EngineMixin, face3d_arch.ReconNetWrapperParams):
+    """third_part/face3d/models/networks.py:66-105 with net_recon='resnet50', use_last_fc=False (the
+    configuration load_face3d_net builds, futils/inference_utils.py:261-267)."""
+
+    def _build_engine(self, sd, device):
+        from ..engine.face3d import ReconNetEngine
+        return ReconNetEngine(sd, device)
+
+    def forward_nhwc(self, x4: NHWC) -> torch.Tensor:
+        """x4: NHWC [B,H,W,4] fp32 (RGB / 255, channel 3 zero) -> coefficients [B, 257] (view)."""
+        eng, ctx = self._engine(x4.t.device)
+        return eng.forward(ctx, x4)
+
+    @torch.no_grad()
+    def forward(self, x):
+        """x [B,3,H,W] fp32 (RGB in [0, 1], facing.py:120) -> [B, 257] =
+        flatten(cat(id 80, exp 64, tex 80, angle 3, gamma 27, tx,ty 2, tz 1)) (networks.py:98-105)."""
+        _need_cuda(x)
+        b, c, h, w = x.shape
+        if c != 3:
+            raise RuntimeError(f"ReconNetWrapper: expected 3 input channels, got {c}")
+        eng, ctx = self._engine(x.device)
+        x4 = NHWC.empty(b, h, w, 4, x.device)
+        ops.fill(ctx, x4.t)
+        ops.nchw_to_nhwc(ctx, x.float(), x4.slice(0, 3))
+        return eng.forward(ctx, x4).clone()
+
+
+def define_net_recon(net_recon, use_last_fc=False, init_path=None):
+    """networks.py:59-60."""
+    return ReconNetWrapper(net_recon, use_last_fc=use_last_fc, init_path=init_path)
+
+
 def _load(path):
     return torch.load(path, map_location="cpu", weights_only=True)
 
@@ -344,6 +377,14 @@ def load_retinaface(path):
     return net.eval()
 
 
+def load_face3d_net(ckpt_path, device):
+    """futils/inference_utils.py:261-267: ReconNetWrapper('resnet50') with checkpoint['net_recon'],
+    strict, eval, on ``device``."""
+    net = define_net_recon(net_recon="resnet50", use_last_fc=False, init_path="").to(device)
+    net.load_state_dict(_load(ckpt_path)["net_recon"])
+    return net.eval()
+
+
 def load_srmodel(path, scale=2, num_feat=32):
     """real_esrnet.py:21-30: RRDBNet(3, 3, num_feat, num_block=23, num_grow_ch=32, scale) with the
     ``params_ema`` weights, strict=True."""
@@ -354,4 +395,4 @@ def load_srmodel(path, scale=2, num_feat=32):
 
 __all__ = ["LNet", "ENet", "DNet", "GFPGANv1Clean", "FullGenerator", "ParseNet", "RRDBNet", "load_checkpoint",
            "load_network", "load_DNet", "load_gfpgan", "load_gpen", "load_parsenet", "load_srmodel", "RetinaFace",
-           "load_retinaface"]
+           "load_retinaface", "ReconNetWrapper", "define_net_recon", "load_face3d_net"]

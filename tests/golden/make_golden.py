@@ -16,7 +16,15 @@ the ResNet-50 body, the only torchvision user, is replaced by the features under
 ``skimage`` (imported by data/ and align_faces.py; cv2.warpAffine is stubbed to None inside
 warp_and_crop_face, whose numpy transform math is what the fixture pins).
 
-Usage:  python tests/golden/make_golden.py [--only lnet,enet,dnet,ops,gfpgan,gpen,gpen2048,parsenet,rrdbnet,face]
+3DMM extraction (gen_face3d) loads third_part/face3d/util/preprocess.py and models/networks.py by
+file path with import-only stubs for ``cv2`` / ``skimage`` / ``kornia`` (none is called by POS,
+resize_n_crop_img or ReconNetWrapper) and one numpy alias: preprocess.py:13 names
+``np.VisibleDeprecationWarning``, which numpy 2 moved to ``np.exceptions``.  align_img itself cannot
+run under numpy >= 1.24 (its ``np.array([w0, h0, s, t[0], t[1]])`` is ragged); the fixture takes
+POS and resize_n_crop_img from the reference and assembles trans_params the way facing.py:119
+reads it under numpy 1.23 (five floats).  Pillow, which resize_n_crop_img calls, is installed.
+
+Usage:  python tests/golden/make_golden.py [--only lnet,enet,dnet,ops,gfpgan,gpen,gpen2048,parsenet,rrdbnet,face,face3d]
 """
 import argparse
 import importlib.util
@@ -413,6 +421,80 @@ def gen_face():
             arrays[f"tfm_{i}_{size}"] = np.asarray(params[:2, :], np.float64)
             arrays[f"tfm_inv_{i}_{size}"] = np.asarray(tfm_inv, np.float64)
     _save("face_goldens", arrays)
+
+
+def gen_face3d():
+    """PIL resize cases, align_img's geometry and pixels, ReconNetWrapper('resnet50') and the
+    facing.py:108-129 semantic rows, from the reference's own functions."""
+    from PIL import Image
+    from helpers import FACE3D_LM3D, PIL_RESIZE_CASES, face3d_frames, face3d_landmarks
+    from s2v_amd.models.face3d_arch import ReconNetWrapperParams
+    _face_stubs()
+    for name in ("kornia", "kornia.geometry"):
+        sys.modules.setdefault(name, types.ModuleType(name))
+    sys.modules["kornia"].geometry = sys.modules["kornia.geometry"]
+    sys.modules["kornia.geometry"].warp_affine = None
+    if not hasattr(np, "VisibleDeprecationWarning"):
+        np.VisibleDeprecationWarning = np.exceptions.VisibleDeprecationWarning
+    f3d = os.path.join(REF, "third_part/face3d")
+    spec = importlib.util.spec_from_file_location("_ref_face3d_pre", os.path.join(f3d, "util/preprocess.py"))
+    pre = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(pre)
+    pkg = types.ModuleType("_ref_face3d_models")
+    pkg.__path__ = [os.path.join(f3d, "models")]
+    sys.modules["_ref_face3d_models"] = pkg
+    spec = importlib.util.spec_from_file_location("_ref_face3d_models.networks", os.path.join(f3d, "models/networks.py"))
+    nets = importlib.util.module_from_spec(spec)
+    sys.modules[spec.name] = nets
+    spec.loader.exec_module(nets)
+    arrays = {}
+    # Pillow resample cases (the arithmetic resize_n_crop_img delegates to)
+    for i, (w0, h0, w, h, flt) in enumerate(PIL_RESIZE_CASES):
+        img = np.floor(synth.hash_array(f"golden.pil.{i}", (h0, w0, 3), 0.0, 256.0)).astype(np.uint8)
+        arrays[f"pil_{i}"] = np.asarray(Image.fromarray(img).resize((w, h), resample=flt))
+    # align_img geometry + pixels, one frame per landmark case (facing.py:110-118)
+    lm3d = FACE3D_LM3D
+    lms = face3d_landmarks()
+    frames = face3d_frames(len(lms))
+    # futils/inference_utils.py:158-181 split_coeff, compiled alone from the reference file (the module
+    # imports cv2 / torchvision / face_detection at the top, none of which split_coeff uses)
+    import ast
+    src = open(os.path.join(REF, "futils/inference_utils.py")).read()
+    fn = next(n for n in ast.parse(src).body if isinstance(n, ast.FunctionDef) and n.name == "split_coeff")
+    ns = {}
+    exec(compile(ast.Module(body=[fn], type_ignores=[]), "futils/inference_utils.py", "exec"), ns)
+    split_coeff = ns["split_coeff"]
+    net = nets.define_net_recon(net_recon="resnet50", use_last_fc=False, init_path="")
+    _check_keys("recon", net, ReconNetWrapperParams())
+    net.load_state_dict(synth.synth_torch_state_dict(net, **synth.RETINA_SYNTH), strict=True)
+    net.eval()
+    rows, ims = [], []
+    for i, (frame, lm) in enumerate(zip(frames, lms)):
+        H, W = frame.shape[:2]
+        lm_idx = lm.reshape([-1, 2]).copy()
+        if np.mean(lm_idx) == -1:
+            lm_idx = (lm3d[:, :2] + 1) / 2.
+            lm_idx = np.concatenate([lm_idx[:, :1] * W, lm_idx[:, 1:2] * H], 1)
+        else:
+            lm_idx[:, -1] = H - 1 - lm_idx[:, -1]
+        lm5p = pre.extract_5p(lm_idx) if lm_idx.shape[0] != 5 else lm_idx
+        t, s = pre.POS(lm5p.transpose(), lm3d.transpose())
+        s = 102. / s
+        im, lm_new, _ = pre.resize_n_crop_img(Image.fromarray(frame), lm_idx, t, s, target_size=224.)
+        w, h = (W * s).astype(np.int32), (H * s).astype(np.int32)
+        trans = np.array([float(W), float(H), float(s), float(t[0][0]), float(t[1][0])]).astype(np.float32)
+        arrays[f"lm_{i}"] = np.asarray(lm_idx, np.float64)
+        arrays[f"box_{i}"] = np.array([w, h, (w / 2 - 112. + float(((t[0] - W / 2) * s)[0])),
+                                       (h / 2 - 112. + float(((H / 2 - t[1]) * s)[0]))], np.float64)
+        arrays[f"im_{i}"] = np.asarray(im)
+        arrays[f"lmnew_{i}"] = np.asarray(lm_new, np.float64)
+        x = torch.tensor(np.array(im) / 255., dtype=torch.float32).permute(2, 0, 1).to("cpu").unsqueeze(0)
+        with torch.no_grad():
+            c = {k: v.numpy() for k, v in split_coeff(net(x)).items()}
+        rows.append(np.concatenate([c["id"], c["exp"], c["tex"], c["angle"], c["gamma"], c["trans"], trans[None]], 1))
+        print(f"face3d case {i}: resized {w}x{h}, box {arrays[f'box_{i}'][2:]}, s={float(s):.4f}")
+    arrays["semantic"] = np.concatenate(rows, 0)
+    _save("face3d_goldens", arrays)
 
 
 if __name__ == "__main__":

@@ -27,6 +27,9 @@ def synth_sd(net: str):
     if net == "retinaface":           # RetinaFace-R50 (face_detect/retinaface_detection.py:19-30)
         from s2v_amd.models.retinaface_arch import RetinaFaceParams
         return synth.synth_torch_state_dict(RetinaFaceParams(), **synth.RETINA_SYNTH)
+    if net == "recon":                # face3d ReconNetWrapper('resnet50') (inference_utils.py:261-267)
+        from s2v_amd.models.face3d_arch import ReconNetWrapperParams
+        return synth.synth_torch_state_dict(ReconNetWrapperParams(), **synth.RETINA_SYNTH)
     mod = {"lnet": lambda: arch.LNetParams(), "enet": lambda: arch.ENetParams(lnet=arch.LNetParams()),
            "dnet": lambda: arch.DNetParams()}[net]()
     return synth.synth_torch_state_dict(mod)
@@ -136,3 +139,47 @@ def write_mp4_header(path, width=320, height=240, frames=30, timescale=12800, du
     with open(path, "wb") as f:
         f.write(box("ftyp", b"isom" + bytes(4)) + moov)
     return path
+
+
+# ----------------------------------------------------------------------------- 3DMM extraction
+FACE3D_HW = (180, 240)
+# stand-in for the 5 standard 3D landmarks of BFM's similarity_Lm3D_all.mat (checkpoints/BFM is not
+# in the reference tree): eye centres, nose tip, mouth corners in the BFM's y-up frame
+FACE3D_LM3D = np.array([[-0.31, 0.29, 0.41], [0.31, 0.29, 0.41], [0.0, 0.0, 0.65], [-0.25, -0.36, 0.44],
+                        [0.25, -0.36, 0.44]], np.float64)
+# (eye distance px, centre x, centre y, roll deg): mild, 2.5x downscale past the border, 2x upscale
+# in a corner, rolled, ~6x downscale; plus one frame with no landmarks (all -1)
+FACE3D_CASES = ((60.0, 120.0, 85.0, 0.0), (150.0, 110.0, 95.0, 4.0), (28.0, 32.0, 40.0, -6.0),
+                (70.0, 140.0, 100.0, 20.0), (420.0, 120.0, 90.0, 0.0), None)
+
+
+def face3d_frames(n, hw=FACE3D_HW):
+    """Synthetic uint8 RGB frames [n, H, W, 3]."""
+    h, w = hw
+    return np.floor(synth.hash_array("golden.face3d.frames", (n, h, w, 3), 0.0, 256.0)).astype(np.uint8)
+
+
+def face3d_landmarks(cases=FACE3D_CASES):
+    """68-point (x, y) landmark sets, image coordinates (y down, as FAN writes them): hash noise with
+    the seven points extract_5p reads (30, 36, 39, 42, 45, 48, 54) placed as a face."""
+    out = []
+    for i, c in enumerate(cases):
+        if c is None:
+            out.append(np.full((68, 2), -1.0, np.float32))
+            continue
+        d, cx, cy, roll = c
+        lm = synth.hash_array(f"golden.face3d.lm{i}", (68, 2), -0.6, 0.6) * d + np.array([cx, cy], np.float32)
+        pts = {30: (0.0, 0.05), 36: (-0.7, -0.45), 39: (-0.3, -0.45), 42: (0.3, -0.45), 45: (0.7, -0.45),
+               48: (-0.42, 0.62), 54: (0.42, 0.62)}
+        a = np.deg2rad(roll)
+        for k, (u, v) in pts.items():
+            x, y = u * d / 1.0, v * d
+            lm[k] = (cx + np.cos(a) * x - np.sin(a) * y, cy + np.sin(a) * x + np.cos(a) * y)
+        out.append(lm.astype(np.float32))
+    return out
+
+
+# (w0, h0, w, h, filter) resize cases pinned directly against Pillow: up, down, one axis unchanged,
+# both unchanged, bilinear
+PIL_RESIZE_CASES = ((37, 29, 61, 45, 3), (90, 70, 23, 31, 3), (40, 33, 40, 70, 3), (40, 33, 17, 33, 3),
+                    (50, 40, 50, 40, 3), (45, 38, 70, 19, 2))
