@@ -517,6 +517,78 @@ class GPEN2048(Workload):
                           f"{threads} threads"}
 
 
+class Face3D(Workload):
+    """facing.py:100-130 face_3dmm_extraction on B frames per step: the PIL
+    bicubic resize + 224 crop of every frame (one s2v_pil_resize_crop launch) and ReconNetWrapper
+    (ResNet-50 + 257-coefficient head).  The per-frame POS fits (host, like NMS) and the box upload
+    are precomputed once for the clip, outside the timed step."""
+    metric = "3DMM coefficient frames/sec/GPU (align_img resize+crop + ReconNetWrapper resnet50, facing.py:100-130)"
+    gflop_per_unit = 8.175             # torch FlopCounterMode on oracle.face3d.recon_forward at 224x224 (2*MAC)
+    FRAME = 700                        # examples/face/1.mp4 is 700x700
+
+    def __init__(self, args, dev, rank, world=1):
+        import numpy as np
+        from s2v_amd import face3d, models, ops, synth
+        from s2v_amd.models.face3d_arch import ReconNetWrapperParams
+        from s2v_amd.ops import NHWC
+        self.batch = b = args.batch or 64
+        self.sd = synth.synth_torch_state_dict(ReconNetWrapperParams(), **synth.RETINA_SYNTH)
+        self.net = models.ReconNetWrapper()
+        self.net.load_state_dict(self.sd)
+        self.net.eval()
+        S = self.FRAME
+        lm3d = np.array([[-0.31, 0.29, 0.41], [0.31, 0.29, 0.41], [0.0, 0.0, 0.65], [-0.25, -0.36, 0.44],
+                         [0.25, -0.36, 0.44]])
+        rng = np.random.default_rng(8000 + rank)
+        t0 = time.perf_counter()
+        boxes = []
+        for i in range(b):             # a face of ~220-300 px eye-to-mouth scale drifting over the frame
+            d = 180 + 60 * rng.random()
+            cx, cy = S / 2 + 40 * rng.standard_normal(2)
+            base = np.array([[-0.5, 0.45], [0.5, 0.45], [0.0, 0.0], [-0.42, -0.62], [0.42, -0.62]])
+            lm5 = base * d + np.array([cx, S - 1 - cy]) + rng.standard_normal((5, 2))
+            _, box, _ = face3d.align_params(S, S, lm5.astype(np.float32), lm3d)
+            boxes.append(box)
+        self.host = {"pos_fits_ms": round(1e3 * (time.perf_counter() - t0), 2)}
+        g = torch.Generator(device=dev)
+        g.manual_seed(8000 + rank)
+        frames = torch.randint(0, 256, (b, S, S, 3), generator=g, device=dev, dtype=torch.uint8)
+        self.params = face3d.box_params(boxes, S, S, dev)
+        self.x4 = NHWC.empty(b, 224, 224, 4, dev)
+        self.out = torch.empty((b, 257), device=dev)
+        self.boxes = boxes
+        ctx = ops.Ctx(dev)
+
+        def step(f):
+            face3d.resize_crop_params(ctx, f, self.params, self.x4)
+            self.out.copy_(self.net.forward_nhwc(self.x4))
+            return self.out
+        self.inputs = [frames]
+        self.fn = step
+        self.config = {"workload": f"face_3dmm_extraction on B={b} synthetic {S}x{S} uint8 RGB frames per step: "
+                                   "PIL bicubic resize + 224x224 crop (s2v_pil_resize_crop) -> ReconNetWrapper "
+                                   "resnet50 -> [B, 257] coefficients", "host_precompute": self.host}
+
+    def forward(self):
+        return self.fn(*self.inputs)
+
+    def cpu(self, threads, seconds):
+        from oracle import face3d as O3
+        torch.set_num_threads(threads)
+        frames = self.inputs[0][:4].cpu().numpy()
+
+        def one(i=[0]):
+            k = i[0] % 4
+            i[0] += 1
+            im = O3.pil_resize_crop(frames[k], self.boxes[k])
+            x = torch.tensor(im / 255., dtype=torch.float32).permute(2, 0, 1)[None]
+            O3.recon_forward(self.sd, x)
+        n, el = _timed_cpu(one, 1, seconds, 64)
+        return {"value": round(n / el, 4), "unit": "frames/s", "cores": threads, "kind": "port",
+                "sample": f"{n} {self.FRAME}x{self.FRAME} frames through the oracle restatement (NumPy Pillow "
+                          f"resample + crop, torch CPU ResNet-50) in {el:.1f}s, {threads} threads"}
+
+
 class Clip(Pipeline):
     """BASELINE configs[3] (configs[2] at N = 1): the 1000-frame clip sharded over the ranks by
     pipeline.run_sharded — RCCL broadcast of the per-clip host data, device mel + windows, host
@@ -562,7 +634,7 @@ class Clip(Pipeline):
 
 
 WORKLOADS = {"lipsync": LipSync, "lnet": LNetOnly, "pipeline": Pipeline, "enhance": Enhance, "mouth": Mouth,
-             "sr": SuperRes, "gpen2048": GPEN2048, "clip": Clip, "selftest": SelfTest}
+             "sr": SuperRes, "gpen2048": GPEN2048, "face3d": Face3D, "clip": Clip, "selftest": SelfTest}
 
 
 def _free_port():

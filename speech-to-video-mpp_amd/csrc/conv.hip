@@ -755,6 +755,8 @@ static bool smallk_cfg(const s2v_conv_params *p, int M, int K, int &tppx, int &q
     // (measured on MI355X, r02: 3x3 4 -> 256 at 200^2 776 -> 336 us, 4 -> 64 at 512^2 602 -> 361 us,
     // at 96^2 74 -> 32 us; the 1x1 4 -> 256 layer stays here, 415 us against 491 us)
     if (p->prec != S2V_PREC_F32 && p->kh * p->kw > 1) return false;
+    // 1x1 convs on >= 32 channels too (ResNet-50 layer1 64 -> 64 / 64 -> 256 at 56^2: VALU-bound here)
+    if (p->prec != S2V_PREC_F32 && K >= 32) return false;
     const int quads = p->cout / 4;
     if (quads & (quads - 1)) return false;                       // power of two
     // one output quad per thread, up to 64 threads per pixel (measured on MI355X: 64 lanes x 1 quad

@@ -119,12 +119,23 @@ def resize_crop(ctx, frames: torch.Tensor, boxes, out: NHWC, filter=PIL_BICUBIC)
         raise ops._lib.S2VError("resize_crop: frames must be a contiguous uint8 [n, H, W, 3] HIP tensor")
     if len(boxes) != n or out.n != n or out.coff != 0:
         raise ValueError("resize_crop: one (w, h, left, up) box and one output image per frame")
+    params = box_params(boxes, W, H, frames.device)
+    resize_crop_params(ctx, frames, params, out, filter)
+    return params
+
+
+def box_params(boxes, W, H, device):
+    """Validated (w, h, left, up) boxes of W x H frames -> the device int32 [n, 4] parameter block."""
     for (w, h, _, _) in boxes:
         _check_scale(W, H, w, h)
-    params = torch.tensor(np.asarray(boxes, np.int32).reshape(n, 4), device=frames.device)
+    return torch.tensor(np.asarray(boxes, np.int32).reshape(len(boxes), 4), device=device)
+
+
+def resize_crop_params(ctx, frames: torch.Tensor, params: torch.Tensor, out: NHWC, filter=PIL_BICUBIC):
+    """resize_crop with the boxes already on the device (box_params): no host work, graph-capturable."""
+    n, H, W, _ = frames.shape
     check(ctx.lib.s2v_pil_resize_crop(frames.data_ptr(), n, H, W, H * W * 3, params.data_ptr(), filter, out.ptr,
                                       out.h, out.w, out.cs, ctx.stream), "s2v_pil_resize_crop")
-    return params
 
 
 def align_img(img, lm, lm3D, mask=None, target_size=float(TARGET), rescale_factor=RESCALE):
