@@ -175,6 +175,12 @@ int s2v_instnorm_adain(const float *x, int n, int h, int w, int c, int xcs,
                        const float *gamma, const float *beta, int gb_ns, float eps, int act, float alpha,
                        const float *res, int res_cs, float *y, int ycs, void *ws, size_t ws_bytes,
                        s2v_stream_t stream);
+/* s2v_instnorm_adain that also writes F.pad(y, (1, 1, 1, 1), 'reflect') to yp ([n][h+2][w+2],
+ * pitch ypcs): the FFC's reflect-padded 3x3 convs read the next block's input without a separate
+ * pad pass.  Vector path only (c % 4 == 0, 4-aligned pitches, 16-byte aligned x / y / yp / res). */
+int s2v_instnorm_adain_pad(const float *x, int n, int h, int w, int c, int xcs, const float *gamma,
+                           const float *beta, int gb_ns, float eps, int act, float alpha, const float *res, int res_cs,
+                           float *y, int ycs, float *yp, int ypcs, void *ws, size_t ws_bytes, s2v_stream_t stream);
 size_t s2v_instnorm_ws_bytes(int n, int h, int w, int c);
 
 /* Segmented GEMV for all ADAIN gamma/beta heads at once (base_blocks.py:148-155):

@@ -60,6 +60,8 @@ _SIGS = {
     "s2v_layernorm2d_ws_bytes": (_c_size, [_c_int, _c_int, _c_int, _c_int]),
     "s2v_instnorm_adain": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_int, _c_float, _c_int,
                                     _c_float, _vp, _c_int, _vp, _c_int, _vp, _c_size, _vp]),
+    "s2v_instnorm_adain_pad": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_int, _c_float,
+                                        _c_int, _c_float, _vp, _c_int, _vp, _c_int, _vp, _c_int, _vp, _c_size, _vp]),
     "s2v_instnorm_ws_bytes": (_c_size, [_c_int, _c_int, _c_int, _c_int]),
     "s2v_adain_params": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _c_int, _vp, _c_int, _vp]),
     "s2v_modconv_demod": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_float, _c_float, _vp, _c_int, _vp]),

@@ -268,7 +268,8 @@ __global__ __launch_bounds__(256) void in_apply_v(const float *__restrict__ x, i
                                                   const float *__restrict__ gamma, const float *__restrict__ beta,
                                                   int gb_ns, float eps, int act, float alpha, const float *res,
                                                   int res_cs, float *y, int ycs, const double *__restrict__ part,
-                                                  int chunks, int achunks) {
+                                                  int chunks, int achunks, int w = 0, float *yp = nullptr,
+                                                  int ypcs = 0) {
     const int qb = in_quads(c), nph = 256 / qb;
     const int q4 = threadIdx.x % qb, ph = threadIdx.x / qb;
     const int cc = (blockIdx.y * qb + q4) * 4;
@@ -339,6 +340,20 @@ __global__ __launch_bounds__(256) void in_apply_v(const float *__restrict__ x, i
             o.x += r.x; o.y += r.y; o.z += r.z; o.w += r.w;
         }
         *(float4 *)(yb + (long long)p * ycs) = o;
+        if (yp) {
+            // reflect pad 1 (F.pad 'reflect'): pixel (r, q) lands at (r + 1, q + 1) and, on the second /
+            // second-to-last row or column, also on the mirrored border row / column
+            const int h = hw / w, r = p / w, q = p - r * w, W2 = w + 2;
+            const int rows[2] = {r + 1, r == 1 ? 0 : (r == h - 2 ? h + 1 : -1)};
+            const int cols[2] = {q + 1, q == 1 ? 0 : (q == w - 2 ? w + 1 : -1)};
+            float *pb = yp + (long long)n * (h + 2) * W2 * ypcs + cc;
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    if (rows[i] >= 0 && cols[j] >= 0)
+                        *(float4 *)(pb + ((long long)rows[i] * W2 + cols[j]) * ypcs) = o;
+        }
     }
 }
 
@@ -505,6 +520,34 @@ extern "C" int s2v_instnorm_adain(const float *x, int n, int h, int w, int c, in
     if (rc) return rc;
     in_apply<<<dim3(chunks, cg, n), 256, 0, s>>>(x, hw, c, xcs, gamma, beta, gb_ns, eps, act, alpha, res, res_cs, y,
                                                  ycs, (const double *)ws, chunks, chunks);
+    return check_launch("in_apply");
+}
+
+extern "C" int s2v_instnorm_adain_pad(const float *x, int n, int h, int w, int c, int xcs, const float *gamma,
+                                      const float *beta, int gb_ns, float eps, int act, float alpha, const float *res,
+                                      int res_cs, float *y, int ycs, float *yp, int ypcs, void *ws, size_t ws_bytes,
+                                      s2v_stream_t stream) {
+    S2V_REQUIRE(x && y && yp && n > 0 && h >= 2 && w >= 2 && c > 0, "instnorm_pad: bad args");
+    S2V_REQUIRE(xcs >= c && ycs >= c && ypcs >= c && (!res || res_cs >= c), "instnorm_pad: bad strides");
+    const bool vec = c % 4 == 0 && xcs % 4 == 0 && ycs % 4 == 0 && ypcs % 4 == 0 && (!res || res_cs % 4 == 0) &&
+                     ((uintptr_t)x % 16) == 0 && ((uintptr_t)y % 16) == 0 && ((uintptr_t)yp % 16) == 0 &&
+                     (!res || ((uintptr_t)res % 16) == 0);
+    S2V_REQUIRE(vec, "instnorm_pad: needs c %% 4 == 0, 4-aligned pitches and 16-byte aligned tensors");
+    const int hw = h * w;
+    const int kv = in_chunks_v(n, hw, c);
+    const size_t need = (size_t)n * c * kv * 2 * sizeof(double);
+    if (!ws || ws_bytes < need) {
+        set_error("instnorm_pad: workspace of %zu bytes required", need);
+        return S2V_E_WORKSPACE;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    const int qb = c / 4 < 64 ? c / 4 : 64;
+    const unsigned cq = cdiv(c, 4 * qb);
+    in_stats_v<<<dim3(kv, cq, n), 256, 0, s>>>(x, hw, c, xcs, kv, (double *)ws);
+    int rc = check_launch("in_stats");
+    if (rc) return rc;
+    in_apply_v<<<dim3(kv, cq, n), 256, 0, s>>>(x, hw, c, xcs, gamma, beta, gb_ns, eps, act, alpha, res, res_cs, y, ycs,
+                                                (const double *)ws, kv, kv, w, yp, ypcs);
     return check_launch("in_apply");
 }
 

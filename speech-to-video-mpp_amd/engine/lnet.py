@@ -20,6 +20,8 @@ LRELU_FFC = 0.01   # FineADAINLama built with nn.LeakyReLU() default (base_block
 BRANCHES = os.environ.get("S2V_LNET_BRANCHES", "1") == "1"
 # FFC 3x3 reflect convs over a pre-padded input (S2V_LNET_PREPAD=0: reflect addressing in the gather)
 PREPAD = os.environ.get("S2V_LNET_PREPAD", "1") == "1"
+# with PREPAD: the InstanceNorm that ends an FFC writes the next FFC's reflect-padded input itself
+FUSED_PAD = os.environ.get("S2V_LNET_FUSED_PAD", "1") == "1"
 
 AUDIO_CFG = [  # LNet.py:102-120: (stride, padding, residual)
     (1, 1, False), (1, 1, True), (1, 1, True), ((3, 1), 1, False), (1, 1, True), (1, 1, True),
@@ -138,7 +140,7 @@ class FFCLama:
         self.gid = bank.add_group(sd, [(p + "bn_l.", self.cl), (p + "bn_g.", self.cg)])
         self.device = device
 
-    def pre_norm(self, ctx, x: NHWC, y: NHWC, branches=None):
+    def pre_norm(self, ctx, x: NHWC, y: NHWC, branches=None, xpad: NHWC | None = None):
         """y <- [l2l(x_l)+g2l(x_g) | l2g(x_l) + spectral(x_g)] (before ADAIN).
 
         The three independent products run as concurrent branches when ``branches`` (two
@@ -155,7 +157,9 @@ class FFCLama:
         u = NHWC.empty(b, self.h, self.w, cc, dev)
 
         xr = x
-        if PREPAD:
+        if PREPAD and xpad is not None:
+            xr = xpad                                  # written by the previous InstanceNorm (norm(pad_out=))
+        elif PREPAD:
             xr = NHWC.empty(b, self.h + 2, self.w + 2, x.c, dev)
             ops.pad_reflect(ctx, x, xr, (1, 1, 1, 1))
 
@@ -176,9 +180,9 @@ class FFCLama:
             branches.run(ctx, lambda c: ops.conv2d(c, xr, self.conv_to_l, y.slice(0, cl)), l2g, spectral)
         ops.conv2d(ctx, u, self.st2, yg, res=yg)
 
-    def norm(self, ctx, bank: AdainBank, y: NHWC, out: NHWC, res: NHWC | None = None):
+    def norm(self, ctx, bank: AdainBank, y: NHWC, out: NHWC, res: NHWC | None = None, pad_out: NHWC | None = None):
         g, bt, ns = bank.gamma_beta(self.gid)
-        ops.instnorm(ctx, y, out, g, bt, ns, act=ops.ACT_LRELU, alpha=LRELU_FFC, res=res)
+        ops.instnorm(ctx, y, out, g, bt, ns, act=ops.ACT_LRELU, alpha=LRELU_FFC, res=res, pad_out=pad_out)
 
 
 class Branches:
@@ -308,11 +312,19 @@ class LNetEngine:
             c = lv["c"]
             ya = NHWC.empty(cur.n, cur.h, cur.w, c, dev)
             yb = NHWC.empty(cur.n, cur.h, cur.w, c, dev)
-            for l1, l2 in lv["blocks"]:
-                l1.pre_norm(ctx, cur, ya, br)
-                l1.norm(ctx, self.bank, ya, ya)
-                l2.pre_norm(ctx, ya, yb, br)
-                l2.norm(ctx, self.bank, yb, cur, res=cur)       # FFCResnetBlock: id + conv2(conv1(x))
+            # the ADAIN that ends each FFC also writes the reflect-padded copy the next FFC's 3x3
+            # convs read (PREPAD), so no separate pad pass runs inside a level
+            pa = pc = None
+            if PREPAD and FUSED_PAD:
+                pa = NHWC.empty(cur.n, cur.h + 2, cur.w + 2, c, dev)
+                pc = NHWC.empty(cur.n, cur.h + 2, cur.w + 2, c, dev)
+            nblk = len(lv["blocks"])
+            for bi, (l1, l2) in enumerate(lv["blocks"]):
+                l1.pre_norm(ctx, cur, ya, br, xpad=pc if bi > 0 else None)
+                l1.norm(ctx, self.bank, ya, ya, pad_out=pa)
+                l2.pre_norm(ctx, ya, yb, br, xpad=pa)
+                l2.norm(ctx, self.bank, yb, cur, res=cur,        # FFCResnetBlock: id + conv2(conv1(x))
+                        pad_out=pc if bi + 1 < nblk else None)
             up = lv["up"](ctx, cur)
             skip = skips.pop()
             lv["jump"](ctx, skip, out=up, res=up)               # jump(skip) + out

@@ -494,13 +494,20 @@ def layernorm2d(ctx: Ctx, x: NHWC, weight, bias, y: NHWC, *, act=ACT_LRELU, alph
 
 
 def instnorm(ctx: Ctx, x: NHWC, y: NHWC, gamma=None, beta=None, gb_ns=0, *, act=ACT_NONE, alpha=0.0,
-             res: NHWC | None = None, eps=1e-5):
-    """gamma/beta: raw device pointers (ints) or None; gb_ns = per-sample row stride."""
+             res: NHWC | None = None, eps=1e-5, pad_out: NHWC | None = None):
+    """gamma/beta: raw device pointers (ints) or None; gb_ns = per-sample row stride.  ``pad_out``
+    ([n, h+2, w+2, c] view) also receives F.pad(y, (1, 1, 1, 1), 'reflect')."""
     need = ctx.lib.s2v_instnorm_ws_bytes(x.n, x.h, x.w, x.c)
     ws, nb = ctx.ws.get(need)
+    rp, rcs = (None, 0) if res is None else (res.ptr, res.cs)
+    if pad_out is not None:
+        assert (pad_out.n, pad_out.h, pad_out.w, pad_out.c) == (x.n, x.h + 2, x.w + 2, x.c)
+        check(ctx.lib.s2v_instnorm_adain_pad(x.ptr, x.n, x.h, x.w, x.c, x.cs, gamma, beta, gb_ns, eps, act, alpha,
+                                             rp, rcs, y.ptr, y.cs, pad_out.ptr, pad_out.cs, ws, nb, ctx.stream),
+              "s2v_instnorm_adain_pad")
+        return y
     check(ctx.lib.s2v_instnorm_adain(x.ptr, x.n, x.h, x.w, x.c, x.cs, gamma, beta, gb_ns, eps, act, alpha,
-                                     None if res is None else res.ptr, 0 if res is None else res.cs, y.ptr, y.cs,
-                                     ws, nb, ctx.stream), "s2v_instnorm_adain")
+                                     rp, rcs, y.ptr, y.cs, ws, nb, ctx.stream), "s2v_instnorm_adain")
     return y
 
 

@@ -356,6 +356,16 @@ def test_instnorm_adain(ctx, c):
                      alpha=0.01, res=nhwc(res.float()))
         ref = F.leaky_relu(F.instance_norm(x, eps=1e-5) * (1 + g[:, :, None, None]) + bt[:, :, None, None], 0.01) + res
         assert (to_nchw(y) - ref).abs().max() < 2e-5
+        if c % 4 == 0:
+            # the padded second output (LNet FFC: the next block's reflect-padded 3x3 input): the same
+            # values as y, laid out as F.pad(y, (1, 1, 1, 1), 'reflect'); y itself unchanged
+            y2 = NHWC.empty(2, h, w, c, DEV)
+            yp = NHWC(torch.full((2, h + 2, w + 2, c), float("nan"), device=DEV))
+            ops.instnorm(ctx, nhwc(x.float()), y2, gb.data_ptr(), gb.data_ptr() + 4 * c, 2 * c, act=ops.ACT_LRELU,
+                         alpha=0.01, res=nhwc(res.float()), pad_out=yp)
+            assert torch.equal(y2.t, y.t)
+            exp = F.pad(y.t.permute(0, 3, 1, 2), (1, 1, 1, 1), mode="reflect").permute(0, 2, 3, 1)
+            assert torch.equal(yp.t, exp)
 
 
 def test_row_layernorm_attention(ctx):
