@@ -378,11 +378,22 @@ __device__ __forceinline__ void epilogue_tile_fn(const ConvArgs &a, float *Cs, i
             if (rsrc && a.y_step <= 1) {
                 // residual rows: four loads in flight before their adds (a dependent load per
                 // row left the store loop latency-bound)
-#pragma unroll 1
-                for (; rr0 + 3 * RSTEP < clim; rr0 += 4 * RSTEP) {
-                    float rv[4];
+                // ... and the next group's loads are issued before this group's stores (vmcnt counts
+                // loads and stores in issue order: a load issued after a store waits for it)
+                float rv[4];
+                if (rr0 + 3 * RSTEP < clim) {
 #pragma unroll
                     for (int q = 0; q < 4; ++q) rv[q] = rsrc[(long long)(m0 + c0 + rr0 + q * RSTEP) * e.res_cs];
+                }
+#pragma unroll 1
+                for (; rr0 + 3 * RSTEP < clim; rr0 += 4 * RSTEP) {
+                    const bool more = rr0 + 7 * RSTEP < clim;
+                    float rn[4];
+                    if (more) {
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            rn[q] = rsrc[(long long)(m0 + c0 + rr0 + (4 + q) * RSTEP) * e.res_cs];
+                    }
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
                         const long long m = m0 + c0 + rr0 + q * RSTEP;
@@ -391,6 +402,10 @@ __device__ __forceinline__ void epilogue_tile_fn(const ConvArgs &a, float *Cs, i
                         v = fast_act(v, e.act, slope);
                         if (e.res_after) v += rv[q];
                         yb[m * a.ycs] = v;
+                    }
+                    if (more) {
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) rv[q] = rn[q];
                     }
                 }
             }

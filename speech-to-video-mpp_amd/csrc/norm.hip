@@ -132,6 +132,49 @@ __global__ __launch_bounds__(256) void ln_apply(const float *__restrict__ x, int
     }
 }
 
+// float4 form without pooling (c, pitches % 4 == 0, 16-byte aligned): one channel quad per thread
+// and no grid-stride loop, so no load waits behind an earlier store of the same wave
+__global__ __launch_bounds__(256) void ln_apply4(const float *__restrict__ x, int hw, int c4, int xcs,
+                                                 const float *__restrict__ weight, const float *__restrict__ bias,
+                                                 float eps, int act, float alpha, const float *res, int res_cs,
+                                                 float *y, int ycs, const double *__restrict__ part, int nblk) {
+    const int n = blockIdx.y;
+    __shared__ float st[2];
+    {
+        double s = 0.0, q = 0.0;
+        for (int i = threadIdx.x; i < nblk; i += 256) {
+            s += part[((long long)n * nblk + i) * 2 + 0];
+            q += part[((long long)n * nblk + i) * 2 + 1];
+        }
+        block_sum2(s, q);
+        if (threadIdx.x == 0) {
+            const double cnt = (double)hw * c4 * 4;
+            const double mean = s / cnt;
+            double var = q / cnt - mean * mean;
+            if (var < 0.0) var = 0.0;
+            st[0] = (float)mean;
+            st[1] = (float)(1.0 / sqrt(var + (double)eps));
+        }
+        __syncthreads();
+    }
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= hw * c4) return;
+    const float mean = st[0], rstd = st[1];
+    const int p = e / c4, cc = (e - p * c4) * 4;
+    const float4 v = *(const float4 *)(x + ((long long)n * hw + p) * xcs + cc);
+    const float4 w = *(const float4 *)(weight + cc), b = *(const float4 *)(bias + cc);
+    float4 o;
+    o.x = apply_act((v.x - mean) * (w.x * rstd) + b.x, act, alpha);
+    o.y = apply_act((v.y - mean) * (w.y * rstd) + b.y, act, alpha);
+    o.z = apply_act((v.z - mean) * (w.z * rstd) + b.z, act, alpha);
+    o.w = apply_act((v.w - mean) * (w.w * rstd) + b.w, act, alpha);
+    if (res) {
+        const float4 r = *(const float4 *)(res + ((long long)n * hw + p) * res_cs + cc);
+        o.x += r.x; o.y += r.y; o.z += r.z; o.w += r.w;
+    }
+    *(float4 *)(y + ((long long)n * hw + p) * ycs + cc) = o;
+}
+
 // ------------------------------------------------------------------ InstanceNorm / ADAIN
 static int in_chunks(long long hw) {
     long long k = (hw + 1023) / 1024;
@@ -327,17 +370,25 @@ __global__ __launch_bounds__(256) void in_apply_v(const float *__restrict__ x, i
     const float *xb = x + (long long)n * hw * xcs + cc;
     float *yb = y + (long long)n * hw * ycs + cc;
     const float *rb = res ? res + (long long)n * hw * res_cs + cc : nullptr;
-#pragma unroll 4
+    // software-pipelined: pixel p + nph is loaded before pixel p is stored (vmcnt counts loads and
+    // stores in issue order: a load issued after a store would wait for that store to complete)
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f), r = v;
+    if (p0 + ph < p1) {
+        v = *(const float4 *)(xb + (long long)(p0 + ph) * xcs);
+        if (rb) r = *(const float4 *)(rb + (long long)(p0 + ph) * res_cs);
+    }
     for (int p = p0 + ph; p < p1; p += nph) {
-        const float4 v = *(const float4 *)(xb + (long long)p * xcs);
         float4 o;
         o.x = apply_act(fmaf(v.x, mul[0], add[0]), act, alpha);
         o.y = apply_act(fmaf(v.y, mul[1], add[1]), act, alpha);
         o.z = apply_act(fmaf(v.z, mul[2], add[2]), act, alpha);
         o.w = apply_act(fmaf(v.w, mul[3], add[3]), act, alpha);
         if (rb) {
-            const float4 r = *(const float4 *)(rb + (long long)p * res_cs);
             o.x += r.x; o.y += r.y; o.z += r.z; o.w += r.w;
+        }
+        if (p + nph < p1) {
+            v = *(const float4 *)(xb + (long long)(p + nph) * xcs);
+            if (rb) r = *(const float4 *)(rb + (long long)(p + nph) * res_cs);
         }
         *(float4 *)(yb + (long long)p * ycs) = o;
         if (yp) {
@@ -398,6 +449,9 @@ __global__ __launch_bounds__(256) void adain_heads(const float *__restrict__ hid
     float acc[BB];
 #pragma unroll
     for (int i = 0; i < BB; ++i) acc[i] = 0.f;
+    // unrolled so the loads of several hidden units are in flight together (one dependent L2 round
+    // trip per unit made this GEMV latency-bound: 222 us for 26 MB of weights)
+#pragma unroll 8
     for (int j = 0; j < nh; ++j) {
         const float wv = w2t[(long long)j * total + o];
 #pragma unroll
@@ -469,6 +523,15 @@ extern "C" int s2v_layernorm2d(const float *x, int n, int h, int w, int c, int x
     ln_stats<<<dim3(nblk, n), 256, 0, s>>>(x, h * w, c, xcs, nblk, (double *)ws);
     int rc = check_launch("ln_stats");
     if (rc) return rc;
+    const bool vec = !pool && c % 4 == 0 && xcs % 4 == 0 && ycs % 4 == 0 && (!res || res_cs % 4 == 0) &&
+                     ((uintptr_t)x % 16) == 0 && ((uintptr_t)y % 16) == 0 && ((uintptr_t)weight % 16) == 0 &&
+                     ((uintptr_t)bias % 16) == 0 && (!res || ((uintptr_t)res % 16) == 0) &&
+                     (long long)h * w * (c / 4) < (1LL << 31);
+    if (vec) {
+        ln_apply4<<<dim3(cdiv((long long)h * w * (c / 4), 256), n), 256, 0, s>>>(
+            x, h * w, c / 4, xcs, weight, bias, eps, act, alpha, res, res_cs, y, ycs, (const double *)ws, nblk);
+        return check_launch("ln_apply");
+    }
     const long long out = (long long)(pool ? (h / 2) * (w / 2) : h * w) * c;
     unsigned gx = cdiv(out, 256 * 4);
     if (gx > 1024) gx = 1024;

@@ -107,6 +107,7 @@ CONV_CASES = [
     (2, 4, 17, 19, 64, 3, 1, 1, 1, "direct", "zero", 0, 0),
     (2, 4, 16, 16, 256, 1, 1, 0, 1, "direct", "zero", 0, 0),
     (1, 4, 9, 9, 512, 1, 1, 0, 1, "direct", "zero", 0, 0),
+    (2, 4, 33, 35, 256, 1, 1, 0, 1, "direct", "zero", 0, 0),        # 1x1 load groups with a ragged tail
     (2, 4, 10, 12, 32, 3, 1, 1, 1, "direct", "reflect", 0, 0),
     (2, 4, 8, 8, 64, 3, 1, 1, 1, "up2", "zero", 0, 0),
     (2, 4, 14, 14, 128, 3, 2, 1, 1, "direct", "zero", 0, 0),
@@ -327,21 +328,22 @@ def test_gemm_kn_batched(ctx, prec):
     assert ((out.double().cpu() - ref).abs() <= REL[prec] * (bound + 1) + 1e-6).all()
 
 
-def test_layernorm2d(ctx):
-    x = rnd(2, 40, 12, 10, seed=13) * 3 + 1
-    wgt, b = rnd(40, seed=14), rnd(40, seed=15)
-    res = rnd(2, 40, 6, 5, seed=16)
+@pytest.mark.parametrize("c", [40, 42])                # float4 apply (no pool), scalar apply
+def test_layernorm2d(ctx, c):
+    x = rnd(2, c, 12, 10, seed=13) * 3 + 1
+    wgt, b = rnd(c, seed=14), rnd(c, seed=15)
     xv = nhwc(x.float())
     for pool in (False, True):
         oh, ow = (6, 5) if pool else (12, 10)
-        y = NHWC.empty(2, oh, ow, 40, DEV)
+        res = rnd(2, c, oh, ow, seed=16 + pool)
+        y = NHWC.empty(2, oh, ow, c, DEV)
         ops.layernorm2d(ctx, xv, wgt.float().to(DEV), b.float().to(DEV), y, act=ops.ACT_LRELU, alpha=0.1, pool=pool,
-                        res=nhwc(res.float()) if pool else None)
+                        res=nhwc(res.float()))
         ref = F.leaky_relu(F.layer_norm(x, x.shape[1:], wgt[:, None, None].expand(x.shape[1:]),
                                         b[:, None, None].expand(x.shape[1:]), 1e-5), 0.1)
         if pool:
-            ref = F.avg_pool2d(ref, 2) + res
-        assert (to_nchw(y) - ref).abs().max() < 2e-5
+            ref = F.avg_pool2d(ref, 2)
+        assert (to_nchw(y) - (ref + res)).abs().max() < 2e-5
 
 
 @pytest.mark.parametrize("c", [70, 72, 300])          # scalar path, float4 path, two 256-channel blocks
