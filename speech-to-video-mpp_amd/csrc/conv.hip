@@ -340,24 +340,29 @@ __global__ __launch_bounds__(256) void conv_smallk4(ConvArgs a, int batch, int t
     const int tq = threadIdx.x % tppx;
     const int hw = a.oh * a.ow;
     if constexpr (KT == 1) {
-        // 1x1, one float4 per pixel, software-pipelined: the loads of pixel group u + 1 are issued before the stores of group u
-        // (vmcnt counts loads and stores in issue order, so a load issued after a store waits for
-        // that store: load -> store -> load chains ran at 0.65 TB/s of output)
-        auto load1 = [&](int it, f4 &v) {
-            const long long g = g0 + (long long)it * gpb + threadIdx.x / tppx;
-            if (it >= iters || g >= total) return;
-            const int bidx = (int)(g / a.M), m = (int)(g - (long long)bidx * a.M);
-            const float *x = a.x + (long long)bidx * a.x_bs;
-            const int img = m / hw, rem = m - img * hw;
-            const int oy = rem / a.ow, ox = rem - oy * a.ow;
+        // 1x1, one float4 per pixel.  Software-pipelined: pixel u + 1 is loaded before pixel u is
+        // stored (vmcnt counts loads and stores in issue order, so a load issued after a store
+        // waits for it).  Pixel positions advance incrementally: one division per thread instead
+        // of per pixel (the per-pixel 64-bit / 32-bit divisions made this loop VALU-bound, ~190
+        // VALU instructions per pixel and wave, 0.65 TB/s of output).
+        struct Pos { int b, m, img, oy, ox; };
+        auto advance = [&](Pos &p) {
+            p.m += gpb;
+            p.ox += gpb;
+            while (p.ox >= a.ow) { p.ox -= a.ow; ++p.oy; }
+            while (p.oy >= a.oh) { p.oy -= a.oh; ++p.img; }
+            while (p.img >= a.n) { p.img -= a.n; ++p.b; p.m -= a.M; }
+        };
+        auto load1 = [&](const Pos &p, f4 &v) {
+            const float *x = a.x + (long long)p.b * a.x_bs;
             int iy, ix;
-            const bool ok = map_tap(a, oy, ox, 0, 0, iy, ix);
-            v = ok ? *(const f4 *)(x + ((long long)(img * a.h + iy) * a.w + ix) * a.xcs) : f4{0.f, 0.f, 0.f, 0.f};
+            const bool ok = map_tap(a, p.oy, p.ox, 0, 0, iy, ix);
+            v = ok ? *(const f4 *)(x + ((long long)(p.img * a.h + iy) * a.w + ix) * a.xcs) : f4{0.f, 0.f, 0.f, 0.f};
             if (a.in_scale || a.pre_act) {
-                v.x = prologue(a, v.x, img, 0);
-                v.y = prologue(a, v.y, img, 1);
-                v.z = prologue(a, v.z, img, 2);
-                v.w = prologue(a, v.w, img, 3);
+                v.x = prologue(a, v.x, p.img, 0);
+                v.y = prologue(a, v.y, p.img, 1);
+                v.z = prologue(a, v.z, p.img, 2);
+                v.w = prologue(a, v.w, p.img, 3);
                 if (!ok) v = f4{0.f, 0.f, 0.f, 0.f};
             }
         };
@@ -371,13 +376,27 @@ __global__ __launch_bounds__(256) void conv_smallk4(ConvArgs a, int batch, int t
             esc[q] = ep.scale ? *(const f4 *)(ep.scale + n) : f4{1.f, 1.f, 1.f, 1.f};
             esh[q] = ep.shift ? *(const f4 *)(ep.shift + n) : f4{0.f, 0.f, 0.f, 0.f};
         }
+        const long long gs = g0 + threadIdx.x / tppx;
+        if (gs >= total) return;
+        const long long left = (total - gs + gpb - 1) / gpb;
+        const int nit = left < iters ? (int)left : iters;
+        Pos pl;
+        pl.b = (int)(gs / a.M);
+        pl.m = (int)(gs - (long long)pl.b * a.M);
+        pl.img = pl.m / hw;
+        {
+            const int rem = pl.m - pl.img * hw;
+            pl.oy = rem / a.ow;
+            pl.ox = rem - pl.oy * a.ow;
+        }
+        Pos ps = pl;
         f4 cur = f4{0.f, 0.f, 0.f, 0.f}, nxt = f4{0.f, 0.f, 0.f, 0.f};
-        load1(0, cur);
-        for (int it = 0; it < iters; ++it) {
-            const long long g = g0 + (long long)it * gpb + threadIdx.x / tppx;
-            if (g >= total) break;
-            load1(it + 1, nxt);
-            const int bidx = (int)(g / a.M), m = (int)(g - (long long)bidx * a.M);
+        load1(pl, cur);
+        for (int it = 0; it < nit; ++it) {
+            if (it + 1 < nit) {
+                advance(pl);
+                load1(pl, nxt);
+            }
             f4 acc[QPT];
 #pragma unroll
             for (int q = 0; q < QPT; ++q) acc[q] = f4{0.f, 0.f, 0.f, 0.f};
@@ -398,7 +417,7 @@ __global__ __launch_bounds__(256) void conv_smallk4(ConvArgs a, int batch, int t
             for (int q = 0; q < QPT; ++q) {
                 const int n = 4 * (tq + tppx * q);
                 if (!plain) {
-                    store_epilogue4(a, bidx, m, n, acc[q], vec != 0, SMALLK_NT != 0);
+                    store_epilogue4(a, ps.b, ps.m, n, acc[q], vec != 0, SMALLK_NT != 0);
                     continue;
                 }
                 f4 v = acc[q] * esc[q] + esh[q];
@@ -406,10 +425,11 @@ __global__ __launch_bounds__(256) void conv_smallk4(ConvArgs a, int batch, int t
                 v.y = apply_act(v.y, ep.act, ep.alpha);
                 v.z = apply_act(v.z, ep.act, ep.alpha);
                 v.w = apply_act(v.w, ep.act, ep.alpha);
-                f4 *dst = (f4 *)(a.y + (long long)bidx * a.y_bs + (long long)m * a.ycs + n);
+                f4 *dst = (f4 *)(a.y + (long long)ps.b * a.y_bs + (long long)ps.m * a.ycs + n);
                 if (SMALLK_NT) __builtin_nontemporal_store(v, dst);
                 else *dst = v;
             }
+            advance(ps);
             cur = nxt;
         }
         return;

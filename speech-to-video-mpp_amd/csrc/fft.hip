@@ -156,7 +156,7 @@ __global__ __launch_bounds__(256) void irfft2_kernel(const float *__restrict__ s
 // VALU register-blocked form this replaces (one thread per output row, 1.4M serial fmas per
 // block), the waves of a block (4, or 8 at 48x48) share every pass.
 typedef float mf16 __attribute__((ext_vector_type(16)));
-constexpr int FCG = 4;   // channels per block
+constexpr int FCG = 4;   // channels per block (2 at 48x48: twice the blocks, a third of the LDS per block)
 
 __device__ __forceinline__ int mf_row(int r, int lh) { return (r & 3) + 8 * (r >> 2) + 4 * lh; }
 
@@ -164,7 +164,11 @@ __device__ __forceinline__ mf16 mfma32(float a, float b, mf16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
-template <int H, int NWV>
+template <int CG> struct VecOf;
+template <> struct VecOf<4> { typedef float4 T; };
+template <> struct VecOf<2> { typedef float2 T; };
+
+template <int H, int NWV, int FCG = 4>
 __global__ __launch_bounds__(64 * NWV) void rfft2_mf(const float *__restrict__ x, int C, int xcs,
                                                 const float *__restrict__ tables, float *__restrict__ spec,
                                                 int scs) {
@@ -185,7 +189,8 @@ __global__ __launch_bounds__(64 * NWV) void rfft2_mf(const float *__restrict__ x
     for (int i = tid; i < H * 2 * H; i += 64 * NWV) Th[i] = T.fh[i];
     for (int p = tid; p < H * W; p += 64 * NWV) {
         const int hh = p / W, ww = p - hh * W;
-        *(float4 *)&X[hh * XS + ww * FCG] = *(const float4 *)&x[((long long)n * H * W + p) * xcs + c0];
+        typedef typename VecOf<FCG>::T V;
+        *(V *)&X[hh * XS + ww * FCG] = *(const V *)&x[((long long)n * H * W + p) * xcs + c0];
     }
     __syncthreads();
     for (int t = wave; t < T1M * T1N; t += NWV) {      // W pass (real -> half spectrum)
@@ -240,7 +245,7 @@ __global__ __launch_bounds__(64 * NWV) void rfft2_mf(const float *__restrict__ x
     }
 }
 
-template <int H, int NWV>
+template <int H, int NWV, int FCG = 4>
 __global__ __launch_bounds__(64 * NWV) void irfft2_mf(const float *__restrict__ spec, int C, int scs,
                                                  const float *__restrict__ tables, const float *__restrict__ res,
                                                  int rcs, float *__restrict__ y, int ycs) {
@@ -261,8 +266,8 @@ __global__ __launch_bounds__(64 * NWV) void irfft2_mf(const float *__restrict__ 
     for (int i = tid; i < H * WF * 2; i += 64 * NWV) {
         const int q = i & 1, f = i >> 1;
         const int u = f / WF, v = f - u * WF;
-        *(float4 *)&Z[(q * H + u) * N1 + v * FCG] =
-            *(const float4 *)&spec[((long long)n * H * WF + f) * scs + q * C + c0];
+        typedef typename VecOf<FCG>::T V;
+        *(V *)&Z[(q * H + u) * N1 + v * FCG] = *(const V *)&spec[((long long)n * H * WF + f) * scs + q * C + c0];
     }
     __syncthreads();
     for (int t = wave; t < T1M * T1N; t += NWV) {      // inverse H pass (complex)
@@ -345,10 +350,11 @@ extern "C" int s2v_rfft2(const float *x, int n, int h, int w, int c, int xcs, co
     hipStream_t st = (hipStream_t)stream;
     if (c % FCG == 0 && aligned && h == w && (h == 12 || h == 24 || h == 48)) {
         const unsigned grid = n * (c / FCG);
-        // 48x48: 8 waves per block (one block per CU by LDS; the blocks barely cover the chip)
+        // 48x48: 2 channels per block (16 x 48 channels -> 384 blocks; 4 channels gave 192 blocks of
+        // 104 KB LDS, one per CU, three quarters of the chip)
         if (h == 12) rfft2_mf<12, 4><<<grid, 256, 0, st>>>(x, c, xcs, tables, spec, scs);
         else if (h == 24) rfft2_mf<24, 4><<<grid, 256, 0, st>>>(x, c, xcs, tables, spec, scs);
-        else rfft2_mf<48, 8><<<grid, 512, 0, st>>>(x, c, xcs, tables, spec, scs);
+        else rfft2_mf<48, 4, 2><<<2 * grid, 256, 0, st>>>(x, c, xcs, tables, spec, scs);
         return check_launch("rfft2");
     }
     const size_t smem = (per * cg + fixed) * sizeof(float);
@@ -375,7 +381,7 @@ extern "C" int s2v_irfft2(const float *spec, int n, int h, int w, int c, int scs
         const unsigned grid = n * (c / FCG);
         if (h == 12) irfft2_mf<12, 4><<<grid, 256, 0, st>>>(spec, c, scs, tables, res, rcs, y, ycs);
         else if (h == 24) irfft2_mf<24, 4><<<grid, 256, 0, st>>>(spec, c, scs, tables, res, rcs, y, ycs);
-        else irfft2_mf<48, 8><<<grid, 512, 0, st>>>(spec, c, scs, tables, res, rcs, y, ycs);
+        else irfft2_mf<48, 4, 2><<<2 * grid, 256, 0, st>>>(spec, c, scs, tables, res, rcs, y, ycs);
         return check_launch("irfft2");
     }
     const size_t smem = (per * cg + fixed) * sizeof(float);
