@@ -158,26 +158,36 @@ __global__ __launch_bounds__(256, 1) void conv_igemm(ConvArgs a) {
 }
 
 // Split-K fold: one thread per 4 consecutive output channels (16-byte partial-sum loads) when
-// cout % 4 == 0, else per channel; the epilogue is the kernels' own.
-__global__ void splitk_reduce(ConvArgs a, int batch) {
+// cout % 4 == 0, else per channel; the epilogue is the kernels' own (one 16-byte store when ``vec``).
+// 32-bit index math when the fold has < 2^31 items (the 64-bit divisions cost more VALU than the
+// fold's arithmetic).
+__device__ void store_epilogue4(const ConvArgs &a, int bidx, int m, int n, f4 v, bool vec, bool nt);
+
+__global__ void splitk_reduce(ConvArgs a, int batch, int vec) {
     const int cv = (a.cout & 3) == 0 ? 4 : 1;
     const int nq = a.cout / cv;
     const long long total = (long long)batch * a.M * nq;
     const long long slab = (long long)a.M * a.cout;
+    const bool small = total < (1LL << 31);
     for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
          idx += (long long)gridDim.x * blockDim.x) {
-        const int q = (int)(idx % nq);
-        const long long bm = idx / nq;
-        const int m = (int)(bm % a.M);
-        const int bidx = (int)(bm / a.M);
+        int q, m, bidx;
+        if (small) {
+            const unsigned u = (unsigned)idx, bm = u / (unsigned)nq;
+            q = (int)(u - bm * (unsigned)nq);
+            bidx = (int)(bm / (unsigned)a.M);
+            m = (int)(bm - (unsigned)bidx * (unsigned)a.M);
+        } else {
+            q = (int)(idx % nq);
+            const long long bm = idx / nq;
+            m = (int)(bm % a.M);
+            bidx = (int)(bm / a.M);
+        }
         const float *src = a.ws + (long long)bidx * a.splits * slab + (long long)m * a.cout + q * cv;
         if (cv == 4) {
             f4 s = *(const f4 *)src;
             for (int sp = 1; sp < a.splits; ++sp) s += *(const f4 *)(src + sp * slab);
-            store_epilogue(a, bidx, m, 4 * q + 0, s.x);
-            store_epilogue(a, bidx, m, 4 * q + 1, s.y);
-            store_epilogue(a, bidx, m, 4 * q + 2, s.z);
-            store_epilogue(a, bidx, m, 4 * q + 3, s.w);
+            store_epilogue4(a, bidx, m, 4 * q, s, vec != 0, false);
         } else {
             float s = src[0];
             for (int sp = 1; sp < a.splits; ++sp) s += src[sp * slab];
@@ -189,7 +199,7 @@ __global__ void splitk_reduce(ConvArgs a, int batch) {
 // Epilogue of 4 consecutive output channels [n, n + 4) of row m as one 16-byte store (host
 // guarantees 16-byte aligned rows: ycs, res_cs % 4 == 0; n % 4 == 0); per-element otherwise.
 __device__ __forceinline__ void store_epilogue4(const ConvArgs &a, int bidx, int m, int n, f4 v, bool vec,
-                                                bool nt = false) {
+                                                bool nt) {
     const Epi &e = a.epi;
     if (!vec || e.nc_scale || (e.res && !e.res_simple) || a.y_step > 1) {
         store_epilogue(a, bidx, m, n + 0, v.x);
@@ -835,6 +845,13 @@ struct Plan {
     int splits, tps, ktiles;
 };
 
+// 16-byte epilogue stores are possible (store_epilogue4's vec): aligned rows and per-channel vectors
+static int epi_vec4(const s2v_conv_params *p) {
+    return p->cout % 4 == 0 && p->ycs % 4 == 0 && ((uintptr_t)p->y % 16) == 0 && p->y_bs % 4 == 0 &&
+           (!p->res || (p->res_cs % 4 == 0 && ((uintptr_t)p->res % 16) == 0 && p->res_bs % 4 == 0)) &&
+           (!p->scale || ((uintptr_t)p->scale % 16) == 0) && (!p->shift || ((uintptr_t)p->shift % 16) == 0);
+}
+
 static bool use_direct(const s2v_conv_params *p) { return p->cout <= 4 && !p->b_kn; }
 
 static bool vec4_input(const s2v_conv_params *p) {
@@ -1290,9 +1307,7 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
         const long long groups = (long long)batch * M / px;
         const unsigned grid = cdiv(groups, (256 / tppx) * iters);
         const size_t lds = (size_t)K * p->cout * sizeof(float);
-        const int vec = p->ycs % 4 == 0 && ((uintptr_t)p->y % 16) == 0 && p->y_bs % 4 == 0 &&
-                        (!p->res || (p->res_cs % 4 == 0 && ((uintptr_t)p->res % 16) == 0 && p->res_bs % 4 == 0)) &&
-                        (!p->scale || ((uintptr_t)p->scale % 16) == 0) && (!p->shift || ((uintptr_t)p->shift % 16) == 0);
+        const int vec = epi_vec4(p);
         const int kt = p->cin == 4 && p->kh == p->kw && (p->kh == 1 || p->kh == 3) ? p->kh * p->kw : 0;
         if (kt == 9 && qpt == 1) conv_smallk4<1, 9><<<grid, 256, lds, s>>>(a, batch, tppx, iters, vec);
         else if (kt == 9) conv_smallk4<2, 9><<<grid, 256, lds, s>>>(a, batch, tppx, iters, vec);
@@ -1318,7 +1333,7 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
         }
         rc = check_launch("conv_halo_small");
         if (rc || pl.splits <= 1) return rc;
-        splitk_reduce<<<cdiv((long long)M * p->cout, 256), 256, 0, s>>>(a, 1);
+        splitk_reduce<<<cdiv((long long)M * p->cout, 256), 256, 0, s>>>(a, 1, epi_vec4(p));
         return check_launch("splitk_reduce");
     }
     if (pl.tile < 0) {
@@ -1378,6 +1393,6 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
     const long long total = (long long)batch * M * (p->cout % 4 == 0 ? p->cout / 4 : p->cout);
     unsigned blocks = cdiv(total, 256);
     if (blocks > 65535u * 4u) blocks = 65535u * 4u;
-    splitk_reduce<<<blocks, 256, 0, s>>>(a, batch);
+    splitk_reduce<<<blocks, 256, 0, s>>>(a, batch, epi_vec4(p));
     return check_launch("splitk_reduce");
 }
