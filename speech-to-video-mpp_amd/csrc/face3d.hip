@@ -154,6 +154,133 @@ __global__ __launch_bounds__(256) void pil_resize_crop_kernel(const unsigned cha
     }
 }
 
+// R output rows per block (ow <= 256): the column taps are computed once per block, and the
+// horizontal pass of every input row the R rows need is computed once into LDS (uint8, as
+// Pillow's intermediate image) instead of once per (output row, vertical tap).  A block whose rows
+// need more than PIL_RMAX input rows (a > ~4x vertical downscale) runs the rows one by one.
+constexpr int PIL_R = 4, PIL_RMAX = 40;
+
+__device__ __forceinline__ void pil_hrow(const unsigned char *row, int X, bool need_h, int x0, int nx, const int *k,
+                                         int hv[3]) {
+    if (!need_h) {
+        const unsigned char *p = row + X * 3;
+        hv[0] = p[0];
+        hv[1] = p[1];
+        hv[2] = p[2];
+        return;
+    }
+    int s0 = 1 << (PIL_PREC - 1), s1 = s0, s2 = s0;
+    for (int u = 0; u < nx; ++u) {
+        const unsigned char *p = row + (x0 + u) * 3;
+        const int kk = k[u * 256];
+        s0 += p[0] * kk;
+        s1 += p[1] * kk;
+        s2 += p[2] * kk;
+    }
+    hv[0] = pil_clip8(s0);
+    hv[1] = pil_clip8(s1);
+    hv[2] = pil_clip8(s2);
+}
+
+__global__ __launch_bounds__(256) void pil_resize_crop_rows(const unsigned char *__restrict__ x, int h0, int w0,
+                                                            long long xis, const int *__restrict__ params,
+                                                            int filter, float *__restrict__ y, int oh, int ow,
+                                                            int ycs) {
+    __shared__ int ky[PIL_R][PIL_KMAX];
+    __shared__ int yb[PIL_R][3];                 // first row, row count, ok
+    __shared__ int rng[2];                       // first input row, input row count
+    __shared__ int kx[PIL_KMAX * 256];
+    __shared__ unsigned char hb[PIL_RMAX * 256 * 3];
+    const int j0 = blockIdx.x * PIL_R, b = blockIdx.y, tid = threadIdx.x;
+    const int W = params[4 * b + 0], H = params[4 * b + 1], left = params[4 * b + 2], up = params[4 * b + 3];
+    const unsigned char *img = x + b * xis;
+    const bool need_v = H != h0, need_h = W != w0;
+    if (tid < PIL_R) {
+        const int Y = up + j0 + tid;
+        yb[tid][1] = 0;
+        yb[tid][2] = 1;
+        if (j0 + tid < oh && Y >= 0 && Y < H && W > 0 && H > 0) {
+            if (need_v) {
+                if (!pil_coeffs(filter, h0, H, Y, &yb[tid][0], &yb[tid][1], ky[tid], 1)) yb[tid][2] = 0;
+            } else {
+                yb[tid][0] = Y;
+                yb[tid][1] = 1;
+            }
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int lo = 1 << 30, hi = -1;
+        for (int t = 0; t < PIL_R; ++t)
+            if (yb[t][1] > 0) {
+                lo = min(lo, yb[t][0]);
+                hi = max(hi, yb[t][0] + yb[t][1]);
+            }
+        rng[0] = lo;
+        rng[1] = hi > lo ? hi - lo : 0;
+    }
+    // the column's taps (kept in LDS, column-major per thread)
+    const int i = tid, X = left + i;
+    const bool col = i < ow && X >= 0 && X < W;
+    int x0 = X, nx = 1;
+    bool xok = true;
+    if (col && need_h) xok = pil_coeffs(filter, w0, W, X, &x0, &nx, kx + tid, 256);
+    __syncthreads();
+    const int rlo = rng[0], nr = rng[1];
+    const bool shared_rows = nr <= PIL_RMAX;
+    if (shared_rows && col && xok) {
+        for (int r = 0; r < nr; ++r) {
+            int hv[3];
+            pil_hrow(img + (long long)(rlo + r) * w0 * 3, X, need_h, x0, nx, kx + tid, hv);
+            unsigned char *d = hb + (r * 256 + i) * 3;
+            d[0] = (unsigned char)hv[0];
+            d[1] = (unsigned char)hv[1];
+            d[2] = (unsigned char)hv[2];
+        }
+    }
+    if (i >= ow) return;                          // no barrier follows
+    for (int t = 0; t < PIL_R; ++t) {
+        const int j = j0 + t;
+        if (j >= oh) break;
+        float *o = y + (((long long)b * oh + j) * ow + i) * ycs;
+        const int ny = yb[t][1];
+        if (ny == 0 || !col) {
+            for (int c = 0; c < ycs; ++c) o[c] = 0.f;
+            continue;
+        }
+        if (!xok || !yb[t][2]) {                  // more taps than PIL_KMAX: loud NaN
+            for (int c = 0; c < ycs; ++c) o[c] = __builtin_nanf("");
+            continue;
+        }
+        const int y0 = yb[t][0];
+        int acc[3] = {1 << (PIL_PREC - 1), 1 << (PIL_PREC - 1), 1 << (PIL_PREC - 1)};
+        int v[3] = {0, 0, 0};
+        for (int k = 0; k < ny; ++k) {
+            int hv[3];
+            if (shared_rows) {
+                const unsigned char *s = hb + ((y0 + k - rlo) * 256 + i) * 3;
+                hv[0] = s[0];
+                hv[1] = s[1];
+                hv[2] = s[2];
+            } else {
+                pil_hrow(img + (long long)(y0 + k) * w0 * 3, X, need_h, x0, nx, kx + tid, hv);
+            }
+            if (need_v) {
+                const int kk = ky[t][k];
+                acc[0] += hv[0] * kk;
+                acc[1] += hv[1] * kk;
+                acc[2] += hv[2] * kk;
+            } else {
+                v[0] = hv[0];
+                v[1] = hv[1];
+                v[2] = hv[2];
+            }
+        }
+        for (int c = 0; c < 3; ++c) o[c] = (float)((double)(need_v ? pil_clip8(acc[c]) : v[c]) / 255.0);
+        for (int c = 3; c < ycs; ++c) o[c] = 0.f;
+    }
+}
+
 // y[b][c] = mean over the hw pixels of x[b][p][c] (fp64 sum, one rounding)
 __global__ __launch_bounds__(256) void spatial_mean_kernel(const float *__restrict__ x, int n, int hw, int c,
                                                            float *__restrict__ y) {
@@ -178,8 +305,12 @@ extern "C" int s2v_pil_resize_crop(const unsigned char *x, int n, int h0, int w0
     S2V_REQUIRE(ycs >= 3 && xis >= (long long)h0 * w0 * 3, "pil_resize_crop: pitch ycs %d / frame stride %lld", ycs,
                 xis);
     S2V_REQUIRE(oh <= 65535 && n <= 65535, "pil_resize_crop: grid too large");
-    pil_resize_crop_kernel<<<dim3(oh, n), 256, 0, (hipStream_t)stream>>>(x, h0, w0, xis, params, filter, y, oh, ow,
-                                                                        ycs);
+    if (ow <= 256)
+        pil_resize_crop_rows<<<dim3(cdiv(oh, PIL_R), n), 256, 0, (hipStream_t)stream>>>(x, h0, w0, xis, params,
+                                                                                       filter, y, oh, ow, ycs);
+    else
+        pil_resize_crop_kernel<<<dim3(oh, n), 256, 0, (hipStream_t)stream>>>(x, h0, w0, xis, params, filter, y, oh,
+                                                                            ow, ycs);
     return check_launch("pil_resize_crop");
 }
 

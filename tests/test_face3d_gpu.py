@@ -123,3 +123,17 @@ def test_resize_crop_rejects_bad_inputs():
     params = torch.tensor([[100, 100, 0, 0]], dtype=torch.int32, device=DEV)
     assert lib.s2v_pil_resize_crop(fr.data_ptr(), 1, 240, 240, 240 * 240 * 3, params.data_ptr(), 1, out.ptr, 8, 8,
                                    4, ctx.stream) != 0                    # filter 1 (NEAREST) unsupported
+
+
+@pytest.mark.parametrize("box,oh,ow", [((500, 380, -20, 10), 50, 300),     # > 256 columns: row-per-block kernel
+                                       ((61, 23, 3, -2), 30, 64),          # 7.8x vertical downscale: per-row fallback
+                                       ((240, 180, 5, 7), 33, 200)])       # no resample at all (copy + crop)
+def test_resize_crop_kernel_paths_vs_oracle(box, oh, ow):
+    from s2v_amd import face3d, ops
+    from s2v_amd.ops import NHWC
+    frames = face3d_frames(2)
+    out = NHWC.empty(2, oh, ow, 4, DEV)
+    face3d.resize_crop(ops.Ctx(DEV), torch.from_numpy(frames).to(DEV), [box, box], out)
+    got = out.t.cpu().numpy()
+    for i in range(2):
+        assert np.array_equal(_u8(got[i, ..., :3]), O3.pil_resize_crop(frames[i], box, oh, ow)), (box, i)
