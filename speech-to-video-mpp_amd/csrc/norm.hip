@@ -415,6 +415,15 @@ static int in_chunks_v(int n, long long hw, int c) {
     return (int)k;
 }
 
+// pixel chunks of the apply pass: at least the stats chunks, up to >= 1024 blocks with >= 16 pixels
+// each (the apply pass has no partials to keep small, and one block per CU left it latency-bound)
+static int in_apply_chunks(int n, long long hw, int c, int kv) {
+    const long long cq = (c + 255) / 256;
+    long long k = kv;
+    while ((long long)n * cq * k < 1024 && k * 2 * 16 <= hw && k < 256) k *= 2;
+    return (int)k;
+}
+
 // ------------------------------------------------------------------ token LayerNorm
 __global__ __launch_bounds__(256) void row_ln(const float *__restrict__ x, int rows, int dim, int xld,
                                               const float *__restrict__ w, const float *__restrict__ b, float eps,
@@ -573,8 +582,9 @@ extern "C" int s2v_instnorm_adain(const float *x, int n, int h, int w, int c, in
         in_stats_v<<<dim3(kv, cq, n), 256, 0, s>>>(x, hw, c, xcs, kv, (double *)ws);
         int rc = check_launch("in_stats");
         if (rc) return rc;
-        in_apply_v<<<dim3(kv, cq, n), 256, 0, s>>>(x, hw, c, xcs, gamma, beta, gb_ns, eps, act, alpha, res, res_cs,
-                                                    y, ycs, (const double *)ws, kv, kv);
+        const int ka = in_apply_chunks(n, hw, c, kv);
+        in_apply_v<<<dim3(ka, cq, n), 256, 0, s>>>(x, hw, c, xcs, gamma, beta, gb_ns, eps, act, alpha, res, res_cs,
+                                                    y, ycs, (const double *)ws, kv, ka);
         return check_launch("in_apply");
     }
     const unsigned cg = cdiv(c, 64);
@@ -609,8 +619,9 @@ extern "C" int s2v_instnorm_adain_pad(const float *x, int n, int h, int w, int c
     in_stats_v<<<dim3(kv, cq, n), 256, 0, s>>>(x, hw, c, xcs, kv, (double *)ws);
     int rc = check_launch("in_stats");
     if (rc) return rc;
-    in_apply_v<<<dim3(kv, cq, n), 256, 0, s>>>(x, hw, c, xcs, gamma, beta, gb_ns, eps, act, alpha, res, res_cs, y, ycs,
-                                                (const double *)ws, kv, kv, w, yp, ypcs);
+    const int ka = in_apply_chunks(n, hw, c, kv);
+    in_apply_v<<<dim3(ka, cq, n), 256, 0, s>>>(x, hw, c, xcs, gamma, beta, gb_ns, eps, act, alpha, res, res_cs, y, ycs,
+                                                (const double *)ws, kv, ka, w, yp, ypcs);
     return check_launch("in_apply");
 }
 
