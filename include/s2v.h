@@ -143,9 +143,12 @@ int s2v_conv2d_plan(const s2v_conv_params *p, int *out10);
  *                             s2v_conv2d_ws_bytes) and folds them with the epilogue;
  *   S2V_TUNE_GLDS_TILE        force an LDS-DMA tile config (-1 = planner, env S2V_GLDS_TILE);
  *   S2V_TUNE_SMALLK_TILE      1: split-precision convs with K <= 128 on large M take one N tile over
- *                             cout (default, env S2V_SMALLK_TILE); 0: the throughput model.
+ *                             cout (default, env S2V_SMALLK_TILE); 0: the throughput model;
+ *   S2V_TUNE_X3_RATE_512      the planner's sustained rate (TFLOP/s) of the 512x128 split-precision
+ *                             tile (0 = the built-in table, env S2V_X3_RATE_512; A/B tuning).
  * Sets ``value``, returns the previous one in *old_value (may be NULL). */
-enum { S2V_TUNE_HALO_MIN_BLOCKS = 0, S2V_TUNE_GLDS_TILE = 1, S2V_TUNE_SMALLK_TILE = 2, S2V_TUNE_COUNT = 3 };
+enum { S2V_TUNE_HALO_MIN_BLOCKS = 0, S2V_TUNE_GLDS_TILE = 1, S2V_TUNE_SMALLK_TILE = 2, S2V_TUNE_X3_RATE_512 = 3,
+       S2V_TUNE_COUNT = 4 };
 int s2v_tune(int key, long long value, long long *old_value);
 
 /* Split packed fp32 weights [rows][kpad] (kpad % 32 == 0) into the layout of ``prec``

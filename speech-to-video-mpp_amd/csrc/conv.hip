@@ -775,6 +775,8 @@ static long long tune_value(int key) {
         g_tune[S2V_TUNE_GLDS_TILE] = e ? atoll(e) : -1;
         e = getenv("S2V_SMALLK_TILE");
         g_tune[S2V_TUNE_SMALLK_TILE] = e ? atoll(e) : 1;
+        e = getenv("S2V_X3_RATE_512");
+        g_tune[S2V_TUNE_X3_RATE_512] = e ? atoll(e) : 0;
         g_tune_init = true;
     }
     return g_tune[key];
@@ -969,7 +971,9 @@ static Plan make_plan_x3(const s2v_conv_params *p, int M, Plan pl) {
             if (s > 1 && (p->force_splits > 0 || s > pl.ktiles / 4)) break;
             if (p->force_splits > 0) s = p->force_splits;
             const int tps = (pl.ktiles + s - 1) / s;
-            const double t_block = 2.0 * c.t.bm * c.t.bn * 32.0 * tps / (c.tflops * 1e12 / slots);
+            const long long r512 = (c.t.bm == 512) ? tune_value(S2V_TUNE_X3_RATE_512) : 0;
+            const double rate = r512 > 0 ? (double)r512 : c.tflops;
+            const double t_block = 2.0 * c.t.bm * c.t.bn * 32.0 * tps / (rate * 1e12 / slots);
             double t = std::ceil((double)(tiles * s) / slots) * t_block;
             if (s > 1) t += 4e-6 + (double)batch * M * p->cout * 4.0 * (s + 1) / 4e12;
             if (t < best * 0.97) {   // prefer the earlier (larger) tile / fewer splits on near ties
