@@ -90,6 +90,12 @@ __device__ __forceinline__ void split4(const f4 &v, u32x2 &hi, u32x2 &lo) {
 // the same LDS reads per MFMA cycle; on MI355X the 16x16x32 loop holds a higher clock under load
 // (MI355X_MICROARCH.md, DVFS give-back item 7): 256x256 f16x3 372 -> 389 TFLOP/s, 128x128 291 -> 309
 // (tools/conv_micro.py, 16x200x200x256 3x3).
+// Waves raise their issue priority over the MFMA block of a K-slice: always in the 4-wave tiles
+// (measured on MI355X: 16x12^2x1024 -> 256, 128x64 tile, 74 -> 68 us), X3_PRIO=1 also in the 8-wave
+// tiles (no change there: their two waves per SIMD already run the phases staggered)
+#ifndef X3_PRIO
+#define X3_PRIO 0
+#endif
 #ifndef X3_MFMA16
 #define X3_MFMA16 1
 #endif
@@ -426,6 +432,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3(ConvArgs a) {
     const int hs16 = ((lane >> 4) ^ swz(l16)) << 4, ls16 = hs16 ^ 64;
     // multiply ``nv`` (<= KS) slices of one stage
     auto compute = [&](const char *st, int nv) {
+        if constexpr (X3_PRIO || NW == 4) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int u = 0; u < KS; ++u) {
             if (u >= nv) break;
@@ -479,6 +486,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3(ConvArgs a) {
                     }
             }
         }
+        if constexpr (X3_PRIO || NW == 4) __builtin_amdgcn_s_setprio(0);
     };
 
     const int n = kt1 - kt0;
