@@ -100,11 +100,15 @@ class NHWC:
 
 class Workspace:
     """Grow-only scratch buffer shared by the ops of one stream (split-K partials, norm stats).
-    Grows only outside graph capture; a capture that needs more raises."""
+    Grows only outside graph capture; a capture that needs more raises.  A replaced buffer is kept
+    alive: HIP graphs captured earlier hold its address (an eager call of another shape — a ragged
+    last batch — may grow the workspace after a capture; freeing the old one would leave those
+    graphs writing into memory the allocator hands out again)."""
 
     def __init__(self, device):
         self.device = device
         self.buf = torch.empty(0, dtype=torch.uint8, device=device)
+        self._retired = []
 
     def get(self, nbytes: int):
         if nbytes <= 0:
@@ -112,6 +116,8 @@ class Workspace:
         if self.buf.numel() < nbytes:
             if torch.device(self.device).type == "cuda" and torch.cuda.is_current_stream_capturing():
                 raise _lib.S2VError("workspace must be sized by an eager run before graph capture")
+            if self.buf.numel() > 0:
+                self._retired.append(self.buf)
             self.buf = torch.empty(int(nbytes * 1.25) + 256, dtype=torch.uint8, device=self.device)
         return self.buf.data_ptr(), self.buf.numel()
 

@@ -117,3 +117,19 @@ def test_run_sharded_world1_rccl(nets_pair):
     coeffs = torch.from_numpy(P.dnet_coefficients(semantic[:n], expression)).to(DEV)
     direct = pipe.run(chunks, src[:n].to(DEV), coeffs, 0, n)
     assert full.shape == direct.shape and torch.equal(full.cpu(), direct.cpu())
+
+
+def test_graph_replay_after_an_eager_ragged_batch(nets_pair):
+    """A second run() replays the graph captured in the first after the ragged tail ran eagerly
+    (which may grow the op workspaces: the graph must keep its own buffers, ops.Workspace)."""
+    from s2v_amd import audio, pipeline as P
+    dnet, enet = nets_pair
+    wav, semantic, expression, src = _clip(21, 3)
+    chunks = audio.mel_chunks(audio.melspectrogram(torch.from_numpy(wav).to(DEV)))
+    n = min(chunks.shape[0], 21)
+    coeffs = torch.from_numpy(P.dnet_coefficients(semantic[:n], expression)).to(DEV)
+    pipe = P.LipSyncPipeline(dnet, enet, DEV, batch=8)                       # 2 graph batches + 5 eager
+    one = pipe.run(chunks, src[:n].to(DEV), coeffs, 0, n)
+    again = pipe.run(chunks, src[:n].to(DEV), coeffs, 0, n)
+    d = (one.cpu().int() - again.cpu().int()).abs().flatten(1).max(1).values.tolist()
+    assert torch.equal(one.cpu(), again.cpu()), d
