@@ -99,7 +99,8 @@ def make_inputs(batch, size, device, seed):
 
 def live_roofline(forward, workload="lipsync"):
     """One un-graphed ``forward()`` with every conv/GEMM launch bracketed by HIP events on its
-    stream; per kernel symbol: sum of algorithmic FLOPs / sum of durations."""
+    stream; per kernel symbol: sum of algorithmic FLOPs / sum of durations.  The dominant symbol's
+    durations are then re-measured with each launch repeated back to back (second pass)."""
     from s2v_amd import ops
     recs = []
 
@@ -145,6 +146,40 @@ def live_roofline(forward, workload="lipsync"):
             tf = v["flops"] / max(v["ms"], 1e-9) / 1e9
             print(f"  {v['ms']:9.3f} ms  {v['launches']:4d} launches  {tf:7.2f} TF/s  {k}", file=sys.stderr)
     d = per[dom]
+    # second pass for the dominant symbol: each of its launches repeated REPS times back to back
+    # between one event pair (a single short launch between two events also times the event
+    # overhead: LNet's ~20 us 64x64 tiles read ~36 us that way); launches that accumulate into
+    # their own output (res == y) run once
+    REPS = 5
+    rep = {"ms": 0.0, "n": 0}
+
+    def hook2(ctx, p, flops, launch):
+        if ops.conv_symbol(ctx, p) != dom:
+            launch()
+            return
+        reps = 1 if (p.res is not None and p.res == p.y) else REPS
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            launch()
+        e.record()
+        rep_recs.append((s, e, reps))
+
+    rep_recs = []
+    _lnet.BRANCHES = _enet.OVERLAP = False
+    ops.CONV_HOOK = hook2
+    try:
+        with torch.no_grad():
+            forward()
+        torch.cuda.synchronize()
+    finally:
+        ops.CONV_HOOK = None
+        _lnet.BRANCHES, _enet.OVERLAP = saved
+    for s, e, reps in rep_recs:
+        rep["ms"] += s.elapsed_time(e) / reps
+        rep["n"] += 1
+    if rep["n"] == d["launches"] and rep["ms"] > 0:
+        d = dict(d, ms=rep["ms"])
     achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12
     peak = X3_PEAK_TFLOPS if "conv_igemm_x3" in dom else FP32_MFMA_PEAK_TFLOPS
     total_ms = sum(v["ms"] for v in per.values())
