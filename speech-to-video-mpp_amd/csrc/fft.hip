@@ -156,7 +156,7 @@ __global__ __launch_bounds__(256) void irfft2_kernel(const float *__restrict__ s
 // VALU register-blocked form this replaces (one thread per output row, 1.4M serial fmas per
 // block), the waves of a block (4, or 8 at 48x48) share every pass.
 typedef float mf16 __attribute__((ext_vector_type(16)));
-constexpr int FCG = 4;   // channels per block (2 at 48x48: twice the blocks, a third of the LDS per block)
+constexpr int FCG = 4;   // channels per block (the kernels take it as a template parameter)
 
 __device__ __forceinline__ int mf_row(int r, int lh) { return (r & 3) + 8 * (r >> 2) + 4 * lh; }
 
@@ -350,11 +350,11 @@ extern "C" int s2v_rfft2(const float *x, int n, int h, int w, int c, int xcs, co
     hipStream_t st = (hipStream_t)stream;
     if (c % FCG == 0 && aligned && h == w && (h == 12 || h == 24 || h == 48)) {
         const unsigned grid = n * (c / FCG);
-        // 48x48: 2 channels per block (16 x 48 channels -> 384 blocks; 4 channels gave 192 blocks of
-        // 104 KB LDS, one per CU, three quarters of the chip)
+        // 48x48: 8 waves per block (one block per CU by LDS).  2 channels per block (twice the blocks,
+        // 4 waves) measured slower on MI355X: rfft 29.7 -> 35.7 us, irfft 34.6 -> 40.5 us (r02)
         if (h == 12) rfft2_mf<12, 4><<<grid, 256, 0, st>>>(x, c, xcs, tables, spec, scs);
         else if (h == 24) rfft2_mf<24, 4><<<grid, 256, 0, st>>>(x, c, xcs, tables, spec, scs);
-        else rfft2_mf<48, 4, 2><<<2 * grid, 256, 0, st>>>(x, c, xcs, tables, spec, scs);
+        else rfft2_mf<48, 8><<<grid, 512, 0, st>>>(x, c, xcs, tables, spec, scs);
         return check_launch("rfft2");
     }
     const size_t smem = (per * cg + fixed) * sizeof(float);
@@ -381,7 +381,7 @@ extern "C" int s2v_irfft2(const float *spec, int n, int h, int w, int c, int scs
         const unsigned grid = n * (c / FCG);
         if (h == 12) irfft2_mf<12, 4><<<grid, 256, 0, st>>>(spec, c, scs, tables, res, rcs, y, ycs);
         else if (h == 24) irfft2_mf<24, 4><<<grid, 256, 0, st>>>(spec, c, scs, tables, res, rcs, y, ycs);
-        else irfft2_mf<48, 4, 2><<<2 * grid, 256, 0, st>>>(spec, c, scs, tables, res, rcs, y, ycs);
+        else irfft2_mf<48, 8><<<grid, 512, 0, st>>>(spec, c, scs, tables, res, rcs, y, ycs);
         return check_launch("irfft2");
     }
     const size_t smem = (per * cg + fixed) * sizeof(float);
