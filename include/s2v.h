@@ -145,10 +145,13 @@ int s2v_conv2d_plan(const s2v_conv_params *p, int *out10);
  *   S2V_TUNE_SMALLK_TILE      1: split-precision convs with K <= 128 on large M take one N tile over
  *                             cout (default, env S2V_SMALLK_TILE); 0: the throughput model;
  *   S2V_TUNE_X3_RATE_512      the planner's sustained rate (TFLOP/s) of the 512x128 split-precision
- *                             tile (0 = the built-in table, env S2V_X3_RATE_512; A/B tuning).
+ *                             tile (0 = the built-in table, env S2V_X3_RATE_512; A/B tuning);
+ *   S2V_TUNE_IN_FUSED         1 (env S2V_IN_FUSED): InstanceNorm / ADAIN on planes of <= 256 pixels
+ *                             with >= 64 (plane, 256-channel group) blocks runs as one launch; default 0
+ *                             (measured in-process, tools/ab_tune.py: LNet 10.59 -> 10.95 ms with it).
  * Sets ``value``, returns the previous one in *old_value (may be NULL). */
 enum { S2V_TUNE_HALO_MIN_BLOCKS = 0, S2V_TUNE_GLDS_TILE = 1, S2V_TUNE_SMALLK_TILE = 2, S2V_TUNE_X3_RATE_512 = 3,
-       S2V_TUNE_COUNT = 4 };
+       S2V_TUNE_IN_FUSED = 4, S2V_TUNE_COUNT = 5 };
 int s2v_tune(int key, long long value, long long *old_value);
 
 /* Split packed fp32 weights [rows][kpad] (kpad % 32 == 0) into the layout of ``prec``

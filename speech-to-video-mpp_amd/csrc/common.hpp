@@ -12,6 +12,7 @@ namespace s2v {
 void set_error(const char *fmt, ...);
 int check_launch(const char *what);
 int device_cus();
+long long tune_get(int key);   // s2v_tune knobs (conv.hip)
 
 #define S2V_REQUIRE(cond, ...)            \
     do {                                  \

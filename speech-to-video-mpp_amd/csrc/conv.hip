@@ -777,10 +777,14 @@ static long long tune_value(int key) {
         g_tune[S2V_TUNE_SMALLK_TILE] = e ? atoll(e) : 1;
         e = getenv("S2V_X3_RATE_512");
         g_tune[S2V_TUNE_X3_RATE_512] = e ? atoll(e) : 0;
+        e = getenv("S2V_IN_FUSED");
+        g_tune[S2V_TUNE_IN_FUSED] = e ? atoll(e) : 0;
         g_tune_init = true;
     }
     return g_tune[key];
 }
+
+long long tune_get(int key) { return tune_value(key); }
 
 static int halo_ks(const s2v_conv_params *p) {
     const int batch = p->batch > 0 ? p->batch : 1;

@@ -322,7 +322,7 @@ __global__ __launch_bounds__(256) void in_apply_v(const float *__restrict__ x, i
     __shared__ float coef[64][8];
     {
         double s[4] = {0.0, 0.0, 0.0, 0.0}, q[4] = {0.0, 0.0, 0.0, 0.0};
-        if (live) {
+        if (live && part) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const long long o = ((long long)n * c + cc + j) * chunks * 2;
@@ -330,6 +330,16 @@ __global__ __launch_bounds__(256) void in_apply_v(const float *__restrict__ x, i
                     s[j] += part[o + 2 * i];
                     q[j] += part[o + 2 * i + 1];
                 }
+            }
+        } else if (live) {
+            // fused form (part == NULL, one block per plane and channel group): the moments of
+            // the whole plane straight from x, then the apply below re-reads it (from L2)
+            const float *xs = x + (long long)n * hw * xcs + cc;
+            for (int p = ph; p < hw; p += nph) {
+                const float4 v = *(const float4 *)(xs + (long long)p * xcs);
+                const double a = v.x, b = v.y, d = v.z, e = v.w;
+                s[0] += a; s[1] += b; s[2] += d; s[3] += e;
+                q[0] += a * a; q[1] += b * b; q[2] += d * d; q[3] += e * e;
             }
         }
 #pragma unroll
@@ -422,6 +432,13 @@ static int in_apply_chunks(int n, long long hw, int c, int kv) {
     long long k = kv;
     while ((long long)n * cq * k < 1024 && k * 2 * 16 <= hw && k < 256) k *= 2;
     return (int)k;
+}
+
+// one launch (moments + apply in one block per plane and channel group) for small planes with
+// enough planes to fill the chip (LNet's 12^2 level: 16 x 4 blocks of 144 pixels); opt-in
+// (S2V_TUNE_IN_FUSED): 64 blocks per launch lose more than the saved launch (LNet +3 %, r02)
+static bool in_fused(int n, int hw, unsigned cq) {
+    return tune_get(S2V_TUNE_IN_FUSED) != 0 && hw <= 256 && (long long)n * cq >= 64;
 }
 
 // ------------------------------------------------------------------ token LayerNorm
@@ -579,6 +596,11 @@ extern "C" int s2v_instnorm_adain(const float *x, int n, int h, int w, int c, in
         }
         const int qb = c / 4 < 64 ? c / 4 : 64;
         const unsigned cq = cdiv(c, 4 * qb);
+        if (in_fused(n, hw, cq)) {
+            in_apply_v<<<dim3(1, cq, n), 256, 0, s>>>(x, hw, c, xcs, gamma, beta, gb_ns, eps, act, alpha, res, res_cs,
+                                                       y, ycs, nullptr, 1, 1);
+            return check_launch("in_apply");
+        }
         in_stats_v<<<dim3(kv, cq, n), 256, 0, s>>>(x, hw, c, xcs, kv, (double *)ws);
         int rc = check_launch("in_stats");
         if (rc) return rc;
@@ -616,6 +638,11 @@ extern "C" int s2v_instnorm_adain_pad(const float *x, int n, int h, int w, int c
     hipStream_t s = (hipStream_t)stream;
     const int qb = c / 4 < 64 ? c / 4 : 64;
     const unsigned cq = cdiv(c, 4 * qb);
+    if (in_fused(n, hw, cq)) {
+        in_apply_v<<<dim3(1, cq, n), 256, 0, s>>>(x, hw, c, xcs, gamma, beta, gb_ns, eps, act, alpha, res, res_cs, y,
+                                                   ycs, nullptr, 1, 1, w, yp, ypcs);
+        return check_launch("in_apply");
+    }
     in_stats_v<<<dim3(kv, cq, n), 256, 0, s>>>(x, hw, c, xcs, kv, (double *)ws);
     int rc = check_launch("in_stats");
     if (rc) return rc;

@@ -475,7 +475,7 @@ def split_act(ctx: Ctx, x: NHWC, out: NHWC | None = None) -> NHWC:
     return out
 
 
-TUNE_HALO_MIN_BLOCKS, TUNE_GLDS_TILE, TUNE_SMALLK_TILE, TUNE_X3_RATE_512 = 0, 1, 2, 3
+TUNE_HALO_MIN_BLOCKS, TUNE_GLDS_TILE, TUNE_SMALLK_TILE, TUNE_X3_RATE_512, TUNE_IN_FUSED = 0, 1, 2, 3, 4
 
 
 def tune(ctx: Ctx, key: int, value: int) -> int:

@@ -622,3 +622,29 @@ def test_resblock_skip_as_strided_conv(ctx, prec):
     ref = F.conv2d(F.interpolate(x, scale_factor=0.5, mode="bilinear", align_corners=False), wt)
     bound = F.conv2d(F.avg_pool2d(x.abs(), 2), wt.abs())
     assert ((to_nchw(y) - ref).abs() <= REL[prec] * (bound + 1) + 1e-6).all()
+
+
+def test_instnorm_fused_small_planes(ctx):
+    """12^2 planes, 16 x 1024 channels: one-launch InstanceNorm (S2V_TUNE_IN_FUSED) against the
+    two-pass form and torch, with the residual and the reflect-padded second output."""
+    n, c, h, w = 16, 1024, 12, 12
+    x = rnd(n, c, h, w, seed=31) * 2 - 0.5
+    g, bt = rnd(n, c, seed=32), rnd(n, c, seed=33)
+    gb = torch.cat([g, bt], 1).float().to(DEV)
+    res = rnd(n, c, h, w, seed=34)
+    outs = {}
+    for fused in (1, 0):
+        prev = ops.tune(ctx, ops.TUNE_IN_FUSED, fused)
+        try:
+            y = NHWC.empty(n, h, w, c, DEV)
+            yp = NHWC.empty(n, h + 2, w + 2, c, DEV)
+            ops.instnorm(ctx, nhwc(x.float()), y, gb.data_ptr(), gb.data_ptr() + 4 * c, 2 * c, act=ops.ACT_LRELU,
+                         alpha=0.01, res=nhwc(res.float()), pad_out=yp)
+            outs[fused] = (y.t.clone(), yp.t.clone())
+        finally:
+            ops.tune(ctx, ops.TUNE_IN_FUSED, prev)
+    ref = F.leaky_relu(F.instance_norm(x, eps=1e-5) * (1 + g[:, :, None, None]) + bt[:, :, None, None], 0.01) + res
+    y1, p1 = outs[1]
+    assert (y1.permute(0, 3, 1, 2).cpu() - ref).abs().max() < 2e-5
+    assert (y1 - outs[0][0]).abs().max() < 1e-5
+    assert torch.equal(p1, F.pad(y1.permute(0, 3, 1, 2), (1, 1, 1, 1), mode="reflect").permute(0, 2, 3, 1))
