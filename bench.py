@@ -4,7 +4,10 @@
 Workload (one "step"): ENet(+LNet) forward — models/ENet.py:82-139 — on one batch of B=16
 synthetic 256x256 face crops + 16 mel windows [1,80,16] (inference.py:393-399 batching,
 LNet_batch_size 16), weights from the portable synthetic checkpoint (s2v_amd.synth), inputs
-resident in HBM.  The whole forward is one HIP-graph replay.
+resident in HBM.  The whole forward is one HIP-graph replay; with ``--lanes L`` (default 2) the steps
+alternate between L captured lanes (runtime.LaneRunner: separate buffers, workspaces and streams,
+shared read-only weights), so batch k+1's latency-bound LNet head overlaps batch k's MFMA-bound
+StyleConv tail.  Every step still runs the whole forward of its own batch.
 
 Multi-GPU: one process per GPU.  Under torchrun (the driver's N > 1 launch) the ranks come from the
 environment; ``python bench.py --gpus N`` without it spawns N fresh worker processes itself (before
@@ -33,7 +36,7 @@ Other workloads (not the headline metric):
   --workload clip       one step = the 1000-frame clip of configs[3] through pipeline.run_sharded: broadcast
                         of wav / semantic / expression, mel + windows, coefficient windows, DNet -> ENet ->
                         uint8 on each rank's contiguous frame range (HIP-graph replay per 16-frame batch),
-                        all-gather of the uint8 frames to rank 0;
+                        gather of the uint8 frames to rank 0;
   --workload selftest   (tests only, --device cpu) the launcher / timing / JSON path on the gloo backend.
 """
 from __future__ import annotations
@@ -75,6 +78,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=0, help="0 = the workload's default (16, or 4 for enhance)")
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--lanes", type=int, default=2,
+                    help="execution lanes: consecutive steps replay captured graphs on this many lanes, each on its "
+                         "own stream (runtime.LaneRunner); 1 = every step on one stream")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -112,7 +118,7 @@ def live_roofline(forward, workload="lipsync"):
         launch()
         e.record()
         recs.append((sym, flops, splits, s, e, (p.n, p.h, p.w, p.cin, p.oh, p.ow, p.cout, p.kh, p.kw,
-                                                bool(p.in_scale), bool(p.nc_scale), bool(p.pix_add), bool(p.res))))
+                                                p.in_scale, p.nc_scale, p.pix_add, p.res)))
 
     # per-kernel durations are measured with the side-stream branches serialised (engine.lnet
     # BRANCHES, engine.enet OVERLAP), so concurrent kernels do not inflate each other's time
@@ -157,7 +163,7 @@ def live_roofline(forward, workload="lipsync"):
         if ops.conv_symbol(ctx, p) != dom:
             launch()
             return
-        reps = 1 if (p.res is not None and p.res == p.y) else REPS
+        reps = 1 if p.res_is_y else REPS
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
         for _ in range(reps):
@@ -203,6 +209,82 @@ def live_roofline(forward, workload="lipsync"):
         "conv_family": {"achieved": round(total_flops / (total_ms * 1e-3) / 1e12, 2),
                         "ms_per_step": round(total_ms, 3), "symbols": len(per)},
     }
+
+
+class Stamper:
+    """In-kernel launch timer of one kernel symbol in captured, replayed steps (ops.STAMP /
+    s2v_conv_params.stamps): per lane a replay counter (bumped by the first kernel of every replay)
+    and a [reps, launches, 2] buffer of (first block start, last block end) device real-time clock
+    values (s_memrealtime, 100 MHz) per launch of the symbol in that replay."""
+
+    CLOCK_HZ = 100e6
+
+    def __init__(self, kernel, launches, reps, device):
+        self.kernel, self.stride, self.reps, self.device = kernel, max(1, launches), reps, device
+        self.lanes = {}
+        self.cur = None
+
+    def begin(self, lane):
+        """Start of one forward of ``lane`` (eager warm-up or capture): bump its replay counter
+        (captured as the graph's first kernel) and restart the launch numbering."""
+        from s2v_amd import ops
+        if lane not in self.lanes:
+            buf = torch.zeros((self.reps, self.stride, 2), dtype=torch.int64, device=self.device)
+            self.lanes[lane] = {"buf": buf, "ctr": torch.zeros(1, dtype=torch.int64, device=self.device), "n": 0}
+        L = self.lanes[lane]
+        L["n"] = 0
+        self.cur = L
+        ops.S2V.counter_add_(L["ctr"], 1)
+
+    def __call__(self, info, flops):
+        from s2v_amd import ops
+        if self.cur is None or ops.plan_symbol(info.plan) != self.kernel:
+            return None
+        L = self.cur
+        slot = L["n"]
+        L["n"] += 1
+        if slot >= self.stride:
+            return None
+        return L["buf"], L["ctr"], [slot, self.stride, self.reps]
+
+    def arm(self):
+        torch.cuda.synchronize()
+        for L in self.lanes.values():
+            L["buf"][..., 0] = -1              # uint64 max: atomic min start
+            L["buf"][..., 1] = 0
+            L["c0"] = int(L["ctr"].item())
+
+    def durations_us(self):
+        """Per-launch durations (us) of every stamped launch of the timed replays."""
+        torch.cuda.synchronize()
+        out = []
+        for L in self.lanes.values():
+            c1 = int(L["ctr"].item())
+            buf = L["buf"].cpu()
+            for r in range(L["c0"] + 1, c1 + 1):
+                for s0, s1 in buf[r % self.reps].tolist():
+                    if s0 != -1 and s1 > 0:
+                        out.append((s1 - s0) / self.CLOCK_HZ * 1e6)
+        return out
+
+
+def replay_roofline(pre, stamper):
+    """roofline of the dominant kernel from the timed (graph-replayed, overlapped) launches."""
+    d = stamper.durations_us() if stamper is not None else []
+    r = dict(pre)
+    iso = {"avg_launch_us": pre["avg_launch_us"], "frac": pre["frac"], "achieved": pre["achieved"],
+           "how": "un-graphed pass, side branches serialised, each launch repeated back to back between HIP events"}
+    if not d:
+        r["timing"] = "isolated (no stamped launches in the timed run)"
+        return r
+    avg = sum(d) / len(d)
+    ach = pre["flops_per_launch"] / (avg * 1e-6) / 1e12
+    r.update(achieved=round(ach, 2), frac=round(ach / pre["peak"], 4), avg_launch_us=round(avg, 2),
+             timed_launches=len(d),
+             timing="in-kernel clock stamps (s_memrealtime, first block start to last block end) of every launch "
+                    "of this kernel in the timed, graph-replayed steps",
+             isolated=iso)
+    return r
 
 
 def host_threads():
@@ -278,6 +360,7 @@ class LipSync(Workload):
         self.size = args.size
         self.inputs = make_inputs(self.batch, args.size, dev, 1000 + rank)
         self.fn = lambda m, f, g: self.model(m, f, g)  # noqa: E731
+        self.fn_lane = lambda lane, m, f, g: self.model(m, f, g, lane=lane)  # noqa: E731
         self.config = {"workload": f"ENet(+LNet) forward, B={self.batch} synthetic {args.size}x{args.size} crops "
                                    f"+ [1,80,16] mel windows -> 384x384 (models/ENet.py:82-139)",
                        "crop": args.size}
@@ -310,14 +393,16 @@ class LNetOnly(Workload):
         self.size = args.size
         mel, face, _ = make_inputs(self.batch, args.size, dev, 5000 + rank)
         self.inputs = [mel, face]
-        self.x96 = torch.empty((self.batch, 6, 96, 96), device=dev)
+        self.x96 = [torch.empty((self.batch, 6, 96, 96), device=dev) for _ in range(max(1, args.lanes))]
         ctx = ops.Ctx(dev)
 
-        def step(m, f):
+        def step(lane, m, f):
             # F.interpolate(face, (96, 96), mode='bilinear') (ENet.py:104) on the device, then LNet
-            ops.resize(ctx, f.data_ptr(), tuple(f.shape), f.stride(), self.x96.data_ptr(), (96, 96), self.x96.stride())
-            return self.model(m, self.x96)
-        self.fn = step
+            x = self.x96[lane]
+            ops.resize(ctx, f, 0, tuple(f.shape), f.stride(), x, 0, (96, 96), x.stride())
+            return self.model(m, x, lane=lane)
+        self.fn = lambda m, f: step(0, m, f)  # noqa: E731
+        self.fn_lane = step
         self.config = {"workload": f"LNet forward, B={self.batch} synthetic {args.size}x{args.size} 6-channel crops "
                                    "(lower half of the masked half zeroed) bilinear-resized to 96x96 + [1,80,16] mel "
                                    "windows (models/LNet.py:122-139)", "crop": args.size}
@@ -374,8 +459,9 @@ class Pipeline(Workload):
         b = self.batch
         self.inputs = [chunks[:b].contiguous(), torch.rand((b, 3, 256, 256), generator=g, device=dev) * 2 - 1,
                        torch.from_numpy(coeffs[:b]).to(dev)]
-        self.out = torch.empty((b, 3, 384, 384), dtype=torch.uint8, device=dev)
-        self.fn = lambda m, s, c: self.pipe.run_batch(m, s, c, self.out)  # noqa: E731
+        self.outs = [torch.empty((b, 3, 384, 384), dtype=torch.uint8, device=dev) for _ in range(max(1, args.lanes))]
+        self.fn = lambda m, s, c: self.pipe.run_batch(m, s, c, self.outs[0])  # noqa: E731
+        self.fn_lane = lambda lane, m, s, c: self.pipe.run_batch(m, s, c, self.outs[lane], lane=lane)  # noqa: E731
         self.config = {"workload": f"DNet -> uint8 ref -> ENet(+LNet) -> uint8, B={b} frames per step "
                                    "(inference.py:259-288, facing.py:176-191), 256x256 DNet/ENet crops",
                        "host_precompute": self.host}
@@ -628,7 +714,7 @@ class Clip(Pipeline):
     """BASELINE configs[3] (configs[2] at N = 1): the 1000-frame clip sharded over the ranks by
     pipeline.run_sharded — RCCL broadcast of the per-clip host data, device mel + windows, host
     coefficient windows, DNet -> ENet(+LNet) -> uint8 per rank (graph replay per 16-frame batch),
-    all-gather of the uint8 frames to rank 0.  Total work per step is fixed (strong scaling)."""
+    gather of the uint8 frames to rank 0.  Total work per step is fixed (strong scaling)."""
     metric = "full-clip lip-sync frames/sec (1000-frame clip sharded over the GPUs, DNet->LNet->ENet->uint8)"
     graphable = False
     scaling = "strong"
@@ -638,6 +724,7 @@ class Clip(Pipeline):
         from s2v_amd import pipeline
         super().__init__(args, dev, rank, world)
         self.pipe.graph = not args.no_graph
+        self.pipe.lanes = max(1, args.lanes)
         n = args.frames
         rng = np.random.default_rng(0)
         t = np.arange(n * 640) / 16000.0                      # 40 s of 16 kHz audio per 1000 frames at 25 fps
@@ -655,7 +742,7 @@ class Clip(Pipeline):
         self.result = None
         self.config = {"workload": f"run_sharded over a {n}-frame clip (40 ms of 16 kHz audio per frame): broadcast "
                                    "wav/semantic/expression, mel + 16-column windows, coefficient windows, "
-                                   "DNet -> uint8 ref -> ENet(+LNet) -> uint8 384x384 per rank, all-gather to rank 0 "
+                                   "DNet -> uint8 ref -> ENet(+LNet) -> uint8 384x384 per rank, gather to rank 0 "
                                    "(inference.py:204-288, facing.py:176-191)", "clip_frames": n}
 
     def units_per_step(self, world):
@@ -727,7 +814,7 @@ def worker(args):
         else:
             dist.init_process_group("gloo")
         world_seen = dist.get_world_size()
-    from s2v_amd.runtime import GraphRunner
+    from s2v_amd.runtime import GraphRunner, LaneRunner
 
     from s2v_amd import ops
     wl = WORKLOADS[args.workload](args, dev, rank, world)
@@ -738,7 +825,22 @@ def worker(args):
         if cuda:
             torch.cuda.synchronize()
 
-    def timed(prec):
+    def capture(fn_lane, stamper):
+        """The step as captured lanes (or one graph); with ``stamper`` every launch of the dominant
+        kernel records its in-kernel clock stamps (ops.STAMP) into the stamper's per-lane buffers."""
+        def wrap(lane, *x):
+            if stamper is not None:
+                stamper.begin(lane)
+            return fn_lane(lane, *x)
+        ops.STAMP = stamper
+        try:
+            if args.lanes > 1 and hasattr(wl, "fn_lane"):
+                return LaneRunner(wrap, list(wl.inputs), lanes=args.lanes, warmup=1)
+            return GraphRunner(lambda *x: wrap(0, *x), list(wl.inputs), warmup=1)
+        finally:
+            ops.STAMP = None
+
+    def timed(prec, stamper=None):
         """Capture (or not) the step in conv arithmetic ``prec``, warm up, time args.steps steps
         between barriers; returns the max over ranks of the elapsed seconds."""
         ops.set_precision(prec)
@@ -751,10 +853,13 @@ def worker(args):
             for _ in range(max(1, args.warmup)):
                 step()
         else:
-            runner = GraphRunner(wl.fn, list(wl.inputs), warmup=1)
+            fn_lane = wl.fn_lane if hasattr(wl, "fn_lane") else (lambda lane, *x: wl.fn(*x))
+            runner = capture(fn_lane, stamper)
             step = runner.replay
-            for _ in range(args.warmup):
+            for _ in range(max(args.warmup, args.lanes)):
                 step()
+        if stamper is not None:
+            stamper.arm()                      # counters read and stamp slots cleared before the timed region
         barrier()
         t0 = time.perf_counter()
         for _ in range(args.steps):
@@ -767,24 +872,39 @@ def worker(args):
             el = float(t.item())
         return el
 
-    elapsed = timed(args.precision)
+    # roofline pre-pass (rank 0, un-graphed, launches serialised): the dominant kernel symbol, its
+    # algorithmic FLOPs per launch and its isolated duration; the timed run below then stamps that
+    # kernel's launches in-kernel, so the reported duration is the one of the benchmarked,
+    # graph-replayed, overlapped launches (what rocprofv3 --kernel-trace sees for the same command)
+    pre, stamper = None, None
+    if rank == 0 and not args.no_roofline and cuda and wl.graphable:
+        ops.set_precision(args.precision)
+        pre = live_roofline(wl.forward, args.workload)
+        if not args.no_graph:
+            stamper = Stamper(pre["kernel"], pre["launches"], args.warmup + args.steps + 2 * args.lanes + 4, dev)
+    elapsed = timed(args.precision, stamper)
     units = wl.units_per_step(world) * args.steps
     value = units / elapsed
     config = dict(wl.config)
     config.update({"global_batch": wl.units_per_step(world), "batch_per_gpu": wl.batch,
                    "parallelism": f"frame-shard x{world} (no data-path collective)", "graph": not args.no_graph,
+                   "lanes": args.lanes if (wl.graphable and not args.no_graph and hasattr(wl, "fn_lane")) else 1,
                    "world_size_seen": world_seen,
                    "achieved_tflops_algorithmic": round(value * wl.gflop_per_unit / 1e3, 2),
                    "gflop_per_unit": wl.gflop_per_unit})
     if args.workload == "clip":
-        config["parallelism"] = (f"frame-shard x{world}: RCCL broadcast of the clip inputs + all-gather of the "
-                                 "uint8 frames inside the step" if world > 1 else "single GPU")
+        config["parallelism"] = (f"frame-shard x{world}: RCCL broadcast of the clip inputs + gather of the uint8 "
+                                 "frames to rank 0 inside the step" if world > 1 else "single GPU")
     result = {
         "metric": wl.metric, "value": round(value, 3), "unit": wl.unit, "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
         "scaling": wl.scaling, "vs_baseline": None, "dtype": "f32", "data": "synthetic", "config": config,
     }
     config["conv_arith"] = ARITH[args.precision]
+    if pre is not None:
+        result["roofline"] = replay_roofline(pre, stamper)
+    elif rank == 0 and not args.no_roofline and cuda:
+        result["roofline"] = live_roofline(wl.forward, args.workload)
     if world == 1 and not args.no_alt and cuda and wl.graphable:
         result["alt_precision"] = {}
         for other in ARITH:
@@ -794,8 +914,6 @@ def worker(args):
             result["alt_precision"][other] = {"value": round(units / el, 3),
                                               "ms_per_step": round(1e3 * el / args.steps, 3)}
         ops.set_precision(args.precision)
-    if rank == 0 and not args.no_roofline and cuda:
-        result["roofline"] = live_roofline(wl.forward, args.workload)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and cuda:
         result["cpu_baseline"] = wl.cpu(args.cpu_threads or host_threads(), args.cpu_seconds)
     if rank == 0:

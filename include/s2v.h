@@ -121,6 +121,16 @@ typedef struct s2v_conv_params {
      * LDS-DMA (conv_glds_x3).  Needs prec BF16X3 / F16X3, a direct zero-padded conv with cin % 32 == 0,
      * <= 32 taps, packed weights, no in_scale / pre_act, xcs % 4 == 0 and a 16-byte aligned x. */
     int x_split;
+    /* optional launch timer of the implicit-GEMM kernels (bench.py's roofline of graph-replayed,
+     * overlapped launches): with ``stamps`` set, the launch records the device real-time clock
+     * (s_memrealtime, 100 MHz) of its first block's start (atomic min) and its last block's end
+     * (atomic max) into stamps[2 s], stamps[2 s + 1] with slot s = (*stamp_ctr % stamp_reps) *
+     * stamp_stride + stamp_slot — stamp_ctr a device replay counter read when the kernel runs, so a
+     * captured graph records every replay in its own slot.  The caller initialises the pairs to
+     * (UINT64_MAX, 0). */
+    unsigned long long *stamps;
+    const unsigned long long *stamp_ctr;
+    int stamp_slot, stamp_stride, stamp_reps;
 } s2v_conv_params;
 
 enum { S2V_PREC_F32 = 0, S2V_PREC_BF16X3 = 1, S2V_PREC_F16X3 = 2 };
@@ -134,7 +144,7 @@ size_t s2v_conv2d_ws_bytes(const s2v_conv_params *p);
  * conv_igemm_x3<BM,BN,WAVES_M,NW,KS,PF,AVEC,B_KN,prec-1> (prec 1 / 2) instance, or
  * {0, CO, TPP, LW, 0, 1, 0, 0, 0, 0} for conv_small_cpar<CO,TPP,LW> (conv_direct_small<CO> when
  * TPP == 0), or {0, cout, -QPT, PX, 0, 1, ...} for conv_smallk<QPT,PX>.  force_tile: 0 = planner,
- * 1..6 (f32) / 1..8 (split precisions) a fixed tile of the selected precision's table (tests / tuning). */
+ * 1..6 (f32) / 1..11 (split precisions) a fixed tile of the selected precision's table (tests / tuning). */
 int s2v_conv2d_plan(const s2v_conv_params *p, int *out10);
 /* Planner knobs (tests / tuning; process-wide, not thread-safe against concurrent planning):
  *   S2V_TUNE_HALO_MIN_BLOCKS  the halo-tiled small-Cout kernel needs at least this many 8x128 tiles
@@ -424,6 +434,10 @@ int s2v_u8_to_gan(const unsigned char *x, int n, int h, int w, float *y, s2v_str
 int s2v_gan_to_u8(const float *x, int n, int h, int w, unsigned char *y, s2v_stream_t stream);
 /* y = x / 255. as float64 (mask_sharp, face_enhancement.py:137). */
 int s2v_u8_div255_f64(const unsigned char *x, long long n, double *y, s2v_stream_t stream);
+/* mask_sharp of FaceEnhancement.process after mask_postprocess mutated it: parse / 255. with the
+ * ``border``-pixel frame zeroed (face_enhancement.py:84-85 on the array of :144).  x: uint8 [h, w],
+ * y: fp64 [h, w]. */
+int s2v_u8_div255_f64_border(const unsigned char *x, int h, int w, int border, double *y, s2v_stream_t stream);
 /* Final blend of FaceEnhancement.process on uint8 HWC frames (3 channels): mask_sharp == NULL:
  * convertScaleAbs(base * (1 - full_mask) + full_img * full_mask) (use_sr, :175-176); else
  * img = that (base = ori_img), then convertScaleAbs(ori * (1 - mask_sharp) + img * mask_sharp) with

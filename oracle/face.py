@@ -384,9 +384,12 @@ def gaussian_blur(img, ksize, sigma):
 
 
 def mask_postprocess(mask, thres=26):
-    """face_enhancement.py:83-88 on mask_sharp = parse / 255. (float64): zero a thres-pixel border,
-    two 101x101 sigma-11 Gaussian blurs in float64, astype float32."""
-    mask = np.array(mask, dtype=np.float64)
+    """face_enhancement.py:83-88 on mask_sharp = parse / 255. (float64): zero a thres-pixel border
+    IN PLACE (the caller's mask_sharp keeps the zeroed border, as the reference's does: :144-150 go
+    on to resize and warp that same array), then two 101x101 sigma-11 Gaussian blurs in float64,
+    astype float32."""
+    if not (isinstance(mask, np.ndarray) and mask.dtype == np.float64):
+        mask = np.array(mask, dtype=np.float64)
     mask[:thres, :] = 0
     mask[-thres:, :] = 0
     mask[:, :thres] = 0

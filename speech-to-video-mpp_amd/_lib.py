@@ -46,6 +46,8 @@ class ConvParams(ctypes.Structure):
         ("wt_scale", _c_float),
         ("out_pool", _c_int),
         ("x_split", _c_int),
+        ("stamps", _vp), ("stamp_ctr", _vp), ("stamp_slot", _c_int), ("stamp_stride", _c_int),
+        ("stamp_reps", _c_int),
     ]
 
 
@@ -127,6 +129,7 @@ _SIGS = {
     "s2v_u8_to_gan": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _vp]),
     "s2v_gan_to_u8": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _vp]),
     "s2v_u8_div255_f64": (_c_int, [_vp, _c_ll, _vp, _vp]),
+    "s2v_u8_div255_f64_border": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _vp]),
     "s2v_face_blend": (_c_int, [_vp, _vp, _vp, _vp, _vp, _c_ll, _vp]),
     "s2v_pil_resize_crop": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_ll, _vp, _c_int, _vp, _c_int, _c_int, _c_int,
                                      _vp]),

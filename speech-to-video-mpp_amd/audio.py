@@ -13,7 +13,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from . import _lib
+from . import _lib, ops
 from .ops import Ctx
 
 SR, N_FFT, HOP, N_MELS, FMIN, FMAX = 16000, 800, 200, 80, 55.0, 7600.0
@@ -76,10 +76,7 @@ def melspectrogram(wav: torch.Tensor, pad_mode: str = "constant") -> torch.Tenso
     n = wav.numel()
     frames = 1 + n // HOP
     out = torch.empty((N_MELS, frames), device=wav.device)
-    ctx = _ctx(wav.device)
-    _lib.check(ctx.lib.s2v_melspectrogram(wav.data_ptr(), n, tables(wav.device).data_ptr(),
-                                          int(pad_mode == "reflect"), out.data_ptr(), frames, ctx.stream),
-               "s2v_melspectrogram")
+    ops.S2V.melspectrogram_(wav, tables(wav.device), pad_mode == "reflect", out)
     return out
 
 
@@ -101,8 +98,5 @@ def mel_chunks(mel: torch.Tensor, fps: float = 25.0, step: int = 16) -> torch.Te
     st = chunk_starts(T, fps, step)
     starts = torch.tensor(st, dtype=torch.int32).to(mel.device)
     out = torch.empty((len(st), 1, N_MELS, step), device=mel.device)
-    ctx = _ctx(mel.device)
-    mel = mel.contiguous()
-    _lib.check(ctx.lib.s2v_mel_chunks(mel.data_ptr(), T, starts.data_ptr(), len(st), step,
-                                      out.data_ptr(), ctx.stream), "s2v_mel_chunks")
+    ops.S2V.mel_chunks_(mel.contiguous(), starts, step, out)
     return out

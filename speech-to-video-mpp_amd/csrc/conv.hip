@@ -60,6 +60,7 @@ __global__ __launch_bounds__(256, 1) void conv_igemm(ConvArgs a) {
     constexpr int BR = BN / 32;
     constexpr int STAGE = (BM + BN) * LDK;
     static_assert(TM >= 1 && TN >= 1 && WTM % 32 == 0 && WTN % 32 == 0, "tile");
+    launch_stamp(a, false);
 
     __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
 
@@ -155,6 +156,7 @@ __global__ __launch_bounds__(256, 1) void conv_igemm(ConvArgs a) {
     // ---- epilogue (shared with the split-bf16 kernel, conv_impl.hpp)
     static_assert(BM * (BN + 4) <= 2 * STAGE, "C tile must fit in the staging LDS");
     epilogue_tile<BM, BN, WAVES_M, TM, TN>(a, acc, smem, tid, m0, n0, bz, bidx);
+    launch_stamp(a, true);
 }
 
 // Split-K fold: one thread per 4 consecutive output channels (16-byte partial-sum loads) when
@@ -840,7 +842,9 @@ struct X3Cfg {
 static const X3Cfg kX3Tiles[] = {
     {{256, 256, 2, 8, 1, 1}, 400.f, 1}, {{128, 128, 2, 8, 1, 1}, 330.f, 2}, {{64, 128, 2, 8, 1, 1}, 260.f, 3},
     {{128, 64, 2, 4, 1, 1}, 290.f, 3},  {{64, 64, 2, 4, 1, 1}, 265.f, 4},   {{128, 32, 4, 4, 1, 1}, 235.f, 4},
-    {{256, 128, 4, 8, 1, 1}, 335.f, 1}, {{256, 64, 8, 8, 1, 1}, 300.f, 2},  {{512, 128, 4, 8, 1, 1}, 330.f, 1}};
+    {{256, 128, 4, 8, 1, 1}, 335.f, 1}, {{256, 64, 8, 8, 1, 1}, 300.f, 2},  {{512, 128, 4, 8, 1, 1}, 330.f, 1},
+    // two K-slice groups in flight (PF 2) for the 4-wave tiles: forced-only (tflops 0) until measured
+    {{128, 64, 2, 4, 1, 2}, 0.f, 3},    {{64, 64, 2, 4, 1, 2}, 0.f, 4},     {{128, 32, 4, 4, 1, 2}, 0.f, 4}};
 constexpr int kNumX3 = sizeof(kX3Tiles) / sizeof(kX3Tiles[0]);
 
 static const TileCfg &tile_cfg(const s2v_conv_params *p, int tile);
@@ -961,10 +965,11 @@ static Plan make_plan_x3(const s2v_conv_params *p, int M, Plan pl) {
         }
     }
     double best = 1e30;
-    int bt = kNumX3 - 1, bs = 1;
+    int bt = 8, bs = 1;                                      // 512x128: the planner's fallback
     const int am = a_mode(p);
     for (int i = 0; i < kNumX3; ++i) {
         const X3Cfg &c = kX3Tiles[i];
+        if (c.tflops <= 0.f) continue;                          // forced-only configurations
         if (p->b_kn && c.t.nw != 4) continue;
         if (c.t.bm >= 256 && c.t.bn >= 128 && am != 0 && am != 3) continue;   // generic gathers spill there
         if (c.t.bm == 256 && c.t.bn == 64 && am != 0) continue;   // measured slower than 128x64 on per-row gathers
@@ -1090,6 +1095,9 @@ static Plan make_plan(const s2v_conv_params *p_in, int M, int K) {
 
 static int validate(const s2v_conv_params *p, int &M, int &K) {
     S2V_REQUIRE(p && p->x && p->y, "conv2d: null pointer");
+    S2V_REQUIRE(!p->stamps || (p->stamp_ctr && p->stamp_reps > 0 && p->stamp_slot >= 0 &&
+                               p->stamp_slot < p->stamp_stride),
+                "conv2d: launch stamps need stamp_ctr, stamp_reps > 0 and 0 <= stamp_slot < stamp_stride");
     S2V_REQUIRE(p->prec == S2V_PREC_F32 || p->prec == S2V_PREC_BF16X3 || p->prec == S2V_PREC_F16X3,
                 "conv2d: bad prec %d", p->prec);
     {
@@ -1187,6 +1195,8 @@ static ConvArgs make_args(const s2v_conv_params *p, int M, int K, const Plan &pl
     a.cnt = nullptr;
     a.acc_scale = ((p->x_split || tiled_x3(p)) && !p->b_kn && p->wt_scale > 0.f) ? 1.f / p->wt_scale : 1.f;
     a.pool = p->out_pool != 0;
+    a.stamps = p->stamps; a.stamp_ctr = p->stamp_ctr; a.stamp_slot = p->stamp_slot;
+    a.stamp_stride = p->stamp_stride; a.stamp_reps = p->stamp_reps > 0 ? p->stamp_reps : 1;
     return a;
 }
 

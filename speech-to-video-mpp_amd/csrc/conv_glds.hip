@@ -64,6 +64,7 @@ __global__ __launch_bounds__(512, 1) void conv_glds_x3(ConvArgs a) {
     static_assert(NST == 2 || NST == 3, "stages");
 
     __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+    launch_stamp(a, false);
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
@@ -207,7 +208,7 @@ __global__ __launch_bounds__(512, 1) void conv_glds_x3(ConvArgs a) {
                 for (int r = 0; r < 4; ++r)
                     Cs[(r0 + 4 * (lane >> 4) + r) * LDC + wn * WTN + j * 16 + l16] = acc4[i][j][r] * a.acc_scale;
         }
-    });
+    });    launch_stamp(a, true);
 }
 
 // fp32 NHWC [pixels][xcs] -> split layout (same pitch): per 32-channel block 32 hi halves then 32 lo

@@ -39,7 +39,24 @@ struct ConvArgs {
     unsigned x_bytes, w_bytes;   // buffer-load extents of one batch slab of x / of the weights (AMODE 4)
     int pool;               // 2x2 average-pooled output: M runs over 2x2 output quads (quad-major),
                             // the epilogue writes act(v) averaged over each quad to pixel m / 4
+    unsigned long long *stamps;            // launch timer (s2v_conv_params.stamps), or null
+    const unsigned long long *stamp_ctr;
+    int stamp_slot, stamp_stride, stamp_reps;
 };
+
+// Launch timer: block start (atomic min) / end (atomic max) of the device real-time clock into the
+// slot of the current replay.  One lane per block; vector-memory 64-bit atomics.
+__device__ __forceinline__ void launch_stamp(const ConvArgs &a, bool end) {
+    if (a.stamps == nullptr) return;
+    if (threadIdx.x == 0) {
+        const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+        const unsigned long long r = __hip_atomic_load(a.stamp_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned long long *p = a.stamps + 2 * ((long long)(r % (unsigned long long)a.stamp_reps) * a.stamp_stride +
+                                                a.stamp_slot);
+        if (end) atomicMax(p + 1, t);
+        else atomicMin(p, t);
+    }
+}
 
 // Element offset of output row m (flattened n, oy, ox) for channel 0.
 __device__ __forceinline__ long long out_row(const ConvArgs &a, long long m) {

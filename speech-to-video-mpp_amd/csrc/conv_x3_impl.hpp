@@ -275,6 +275,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3(ConvArgs a) {
     constexpr int BKR = BKN ? BN / 32 : 1;                    // b_kn loader rows (256 threads)
 
     __shared__ __attribute__((aligned(16))) char smem[SMEM];
+    launch_stamp(a, false);
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
@@ -559,6 +560,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3(ConvArgs a) {
     } else {
         epilogue_tile<BM, BN, WAVES_M, TM, TN, NW, CH>(a, acc, (float *)smem, tid, m0, n0, bz, bidx);
     }
+    launch_stamp(a, true);
 }
 
 template <int BM, int BN, int WM, int NW, int KS, int PF, int ELT>
@@ -595,7 +597,10 @@ void launch_conv_x3(int cfg, const ConvArgs &a, int amode, bool bkn, dim3 grid, 
         case 5: launch_x3<128, 32, 4, 4, 1, 1, ELT>(a, amode, bkn, grid, s); break;
         case 6: launch_x3<256, 128, 4, 8, 1, 1, ELT>(a, amode, bkn, grid, s); break;
         case 7: launch_x3<256, 64, 8, 8, 1, 1, ELT>(a, amode, bkn, grid, s); break;
-        default: launch_x3<512, 128, 4, 8, 1, 1, ELT>(a, amode, bkn, grid, s); break;  // 8: N = 128 layers
+        case 8: launch_x3<512, 128, 4, 8, 1, 1, ELT>(a, amode, bkn, grid, s); break;   // N = 128 layers
+        case 9: launch_x3<128, 64, 2, 4, 1, 2, ELT>(a, amode, bkn, grid, s); break;
+        case 10: launch_x3<64, 64, 2, 4, 1, 2, ELT>(a, amode, bkn, grid, s); break;
+        default: launch_x3<128, 32, 4, 4, 1, 2, ELT>(a, amode, bkn, grid, s); break;
     }
 }
 

@@ -379,6 +379,18 @@ __global__ __launch_bounds__(256) void u8_div255_f64_kernel(const unsigned char 
         y[e] = (double)x[e] / 255.0;
 }
 
+// mask_sharp = parse / 255. after FaceEnhancement.mask_postprocess zeroed its border in place
+// (face_enhancement.py:84-85, :144-145): pixels within ``border`` of an edge are 0
+__global__ __launch_bounds__(256) void u8_div255_f64_border_kernel(const unsigned char *__restrict__ x, int h, int w,
+                                                                   int border, double *__restrict__ y) {
+    const long long n = (long long)h * w;
+    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
+        const int r = (int)(e / w), c = (int)(e - (long long)r * w);
+        const bool in = r >= border && r < h - border && c >= border && c < w - border;
+        y[e] = in ? (double)x[e] / 255.0 : 0.0;
+    }
+}
+
 __device__ __forceinline__ unsigned char cvt_abs_u8(float v) {
     return (unsigned char)min(max(__float2int_rn(fabsf(v)), 0), 255);
 }
@@ -581,6 +593,13 @@ extern "C" int s2v_u8_div255_f64(const unsigned char *x, long long n, double *y,
     S2V_REQUIRE(x && y && n > 0, "u8_div255_f64: bad args");
     u8_div255_f64_kernel<<<grid_1d(n), 256, 0, (hipStream_t)stream>>>(x, n, y);
     return check_launch("u8_div255_f64");
+}
+
+extern "C" int s2v_u8_div255_f64_border(const unsigned char *x, int h, int w, int border, double *y,
+                                        s2v_stream_t stream) {
+    S2V_REQUIRE(x && y && h > 0 && w > 0 && border >= 0, "u8_div255_f64_border: bad args");
+    u8_div255_f64_border_kernel<<<grid_1d((long long)h * w), 256, 0, (hipStream_t)stream>>>(x, h, w, border, y);
+    return check_launch("u8_div255_f64_border");
 }
 
 extern "C" int s2v_face_blend(const unsigned char *base, const float *full_mask, const unsigned char *full_img,

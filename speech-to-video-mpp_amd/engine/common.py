@@ -74,13 +74,12 @@ class AdainBank:
         b = z.n
         hid = NHWC.empty(b, 1, 1, self.layer1.cout, self.device)
         ops.conv2d(ctx, z, self.layer1, hid, act=ops.ACT_RELU)
-        out = torch.empty((b, self.total), device=self.device, dtype=torch.float32)
+        out = ops.empty((b, self.total), self.device)
         ops.adain_params(ctx, hid.t.view(b, -1), self.NH, self.w2t, self.b2, self.seg, out)
-        self.params = out
         return out
 
-    def gamma_beta(self, gid):
-        """(gamma_ptr, beta_ptr, row_stride) of a group in the last ``run`` output."""
+    def gamma_beta(self, gid, params):
+        """(gamma, beta): [B, ct] row views of a group in ``params`` (a ``run`` output; the bank
+        itself keeps no per-forward state, so lanes can share it)."""
         off, ct = self.groups[gid]
-        base = self.params.data_ptr()
-        return base + 4 * off, base + 4 * (off + ct), self.total
+        return params[:, off: off + ct], params[:, off + ct: off + 2 * ct]

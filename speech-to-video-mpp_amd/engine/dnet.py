@@ -69,11 +69,12 @@ class DNetEngine:
     def _adain(self, sd, p, c):
         return self.bank.add_group(sd, [(p, c)])
 
-    def _norm_act(self, ctx, x: NHWC, gid, out: NHWC | None = None, act=ops.ACT_LRELU, res=None):
+    def _norm_act(self, ctx, ap, x: NHWC, gid, out: NHWC | None = None, act=ops.ACT_LRELU, res=None):
+        """ADAIN ``gid`` (gamma / beta from the bank output ``ap``) + act (+ res)."""
         if out is None:
             out = NHWC.empty(x.n, x.h, x.w, x.c, self.device)
-        g, b, ns = self.bank.gamma_beta(gid)
-        ops.instnorm(ctx, x, out, g, b, ns, act=act, alpha=LRELU, res=res)
+        g, b = self.bank.gamma_beta(gid, ap)
+        ops.instnorm(ctx, x, out, g, b, act=act, alpha=LRELU, res=res)
         return out
 
     def _conv(self, ctx, x: NHWC, cw: ConvW, out: NHWC | None = None, **kw):
@@ -88,8 +89,8 @@ class DNetEngine:
         dev = self.device
         b, c, L = coeff.shape
         x = NHWC.empty(b, 1, L, c, dev)
-        ops.resize(ctx, coeff.data_ptr(), (b, c, 1, L), (coeff.stride(0), coeff.stride(1), 0, coeff.stride(2)),
-                   x.ptr, (1, L), ops.nhwc_strides(x))
+        ops.resize(ctx, coeff, 0, (b, c, 1, L), (coeff.stride(0), coeff.stride(1), 0, coeff.stride(2)),
+                   x.t, x.coff, (1, L), ops.nhwc_strides(x))
         out = self._conv(ctx, x, self.map_first)
         for cw in self.map_enc:
             # y = conv(lrelu(out)) + out[:, :, 3:-3]
@@ -103,7 +104,7 @@ class DNetEngine:
         dev = self.device
         b, _, H, W = img.shape
         desc = self.mapping(ctx, coeff)
-        self.bank.run(ctx, desc)
+        ap = self.bank.run(ctx, desc)                   # every ADAIN's gamma / beta (descriptor-conditioned)
         # ---- WarpingNet hourglass (base_blocks.py:308-365)
         src = NHWC.empty(b, H, W, 3, dev)
         ops.nchw_to_nhwc(ctx, img, src)
@@ -116,20 +117,20 @@ class DNetEngine:
             cats[k] = NHWC.empty(b, hh, ww, dd["c1"].cout + enc_c[k], dev)
         x = self._conv(ctx, src, self.input_layer)
         for i, e in enumerate(self.enc):
-            t = self._norm_act(ctx, x, e["n0"])
+            t = self._norm_act(ctx, ap, x, e["n0"])
             t = self._conv(ctx, t, e["c0"])
-            t = self._norm_act(ctx, t, e["n1"], out=t)
+            t = self._norm_act(ctx, ap, t, e["n1"], out=t)
             lvl = i + 1
             dst = cats[lvl].slice(cats[lvl].c - enc_c[lvl], enc_c[lvl]) if lvl in cats else None
             x = self._conv(ctx, t, e["c1"], out=dst)
         cur = x                                          # 256 @ H/32
         for k, d in zip((4, 3, 2), self.dec):
-            xs_in = self._norm_act(ctx, cur, d["ns"])
+            xs_in = self._norm_act(ctx, ap, cur, d["ns"])
             out = cats[k].slice(0, d["c1"].cout)
             self._conv(ctx, xs_in, d["cs"], out=out)      # x_s = conv_s(actvn(norm_s(x)))
-            t = self._norm_act(ctx, cur, d["n0"])
+            t = self._norm_act(ctx, ap, cur, d["n0"])
             t = self._conv(ctx, t, d["c0"])
-            t = self._norm_act(ctx, t, d["n1"], out=t)
+            t = self._norm_act(ctx, ap, t, d["n1"], out=t)
             self._conv(ctx, t, d["c1"], out=out, res=out)  # x_s + dx
             cur = cats[k]
         hg = cur                                         # 256 @ H/4
@@ -159,7 +160,7 @@ class DNetEngine:
         for lv in self.e_dec:
             for c2, gid in lv["res"]:
                 t = self._conv(ctx, out, c2)
-                self._norm_act(ctx, t, gid, out=out, act=ops.ACT_NONE, res=out)   # norm2(conv2(x)) + x
+                self._norm_act(ctx, ap, t, gid, out=out, act=ops.ACT_NONE, res=out)   # norm2(conv2(x)) + x
             up = lv["up"](ctx, out)
             lv["jump"](ctx, skips.pop(), out=up, res=up)
             out = up

@@ -88,15 +88,11 @@ class ENetEngine:
         self.mod = ConvW(torch.cat(ws, 0), torch.cat(bs, 0), dev)
         self.mod_offs = offs
         self.noise_seed = 0x5EED
-        self.noise_ctr = ops.NoiseCounter()
 
-    def _side(self):
-        """(stream, Ctx) for the style encoder branch, made once (CUDA devices only)."""
-        if getattr(self, "_side_branch", None) is None:
-            if self.device.type != "cuda":
-                return None
-            self._side_branch = (torch.cuda.Stream(self.device), ops.Ctx(self.device))
-        return self._side_branch
+    def _side(self, ctx):
+        """(stream, Ctx) of the calling lane for the style encoder branch (CUDA devices only)."""
+        side = ctx.streams(("enet", id(self)), 1)
+        return None if side is None else side[0]
 
     def style_code(self, ctx, ref: torch.Tensor):
         """ref: NCHW [B,3,H,W] device tensor -> style [B,1,1,512] (ENet.py:94-101)."""
@@ -126,12 +122,12 @@ class ENetEngine:
         dev = self.device
         b = audio.shape[0]
         svec = NHWC.empty(b, 1, 1, self.mod.cout, dev)
-        side = self._side() if OVERLAP else None
+        side = self._side(ctx) if OVERLAP else None
         if side is not None:
             sst, sctx = side
             cur_st = torch.cuda.current_stream(dev)
             sst.wait_stream(cur_st)
-            with torch.cuda.stream(sst):
+            with ops.side_stream(sst, ctx.keep):
                 style = self.style_code(sctx, face[:, 3:])
                 ops.conv2d(sctx, style, self.mod, svec)
         else:
@@ -155,7 +151,7 @@ class ENetEngine:
         skip = cur               # RGB + a finite pad channel: the x2 skip upsample takes the float4 path
         ctr = None
         if noises is None and any(L.noise_w for L in self.layers):
-            ctr = self.noise_ctr.bump(ctx)             # one draw per forward, also under graph replay
+            ctr = ctx.noise(id(self)).bump(ctx)        # one draw per forward, also under graph replay
         for st in range(2):
             for li in range(2):
                 L = self.layers[3 * st + li]

@@ -69,7 +69,6 @@ class GFPGANEngine:
         self.noise_bufs = [sd[f"{d}noises.noise{i}"].float().reshape(-1).to(dev) for i in range(2 * nd + 1)]
         self._noise_cache = {}
         self.noise_seed = 0x6F9A
-        self.noise_ctr = ops.NoiseCounter()
 
     def _stored_noise(self, b):
         """Stored noise buffers [1,1,H,W] broadcast over the batch (randomize_noise=False)."""
@@ -158,7 +157,7 @@ class GFPGANEngine:
         if noises is not None:
             noise = [None if t is None else t.reshape(b, -1).contiguous() for t in noises]
         elif randomize_noise:
-            ctr = self.noise_ctr.bump(ctx)                 # fresh draws per call, also under graph replay
+            ctr = ctx.noise(id(self)).bump(ctx)            # fresh draws per call, also under graph replay
             noise = []
             for j in range(nl):
                 r = 2 ** ((j + 5) // 2)

@@ -180,26 +180,29 @@ class FFCLama:
             branches.run(ctx, lambda c: ops.conv2d(c, xr, self.conv_to_l, y.slice(0, cl)), l2g, spectral)
         ops.conv2d(ctx, u, self.st2, yg, res=yg)
 
-    def norm(self, ctx, bank: AdainBank, y: NHWC, out: NHWC, res: NHWC | None = None, pad_out: NHWC | None = None):
-        g, bt, ns = bank.gamma_beta(self.gid)
-        ops.instnorm(ctx, y, out, g, bt, ns, act=ops.ACT_LRELU, alpha=LRELU_FFC, res=res, pad_out=pad_out)
+    def norm(self, ctx, bank: AdainBank, params, y: NHWC, out: NHWC, res: NHWC | None = None,
+             pad_out: NHWC | None = None):
+        g, bt = bank.gamma_beta(self.gid, params)
+        ops.instnorm(ctx, y, out, g, bt, act=ops.ACT_LRELU, alpha=LRELU_FFC, res=res, pad_out=pad_out)
 
 
 class Branches:
     """Fork / join of independent work on side HIP streams (captured into the same graph when the
-    caller is capturing: the side streams fork from and join back into the calling stream).  Each
-    branch has its own Ctx, so split-K workspaces never alias across concurrent launches."""
+    caller is capturing: the side streams fork from and join back into the calling stream).  The
+    streams and their Ctx objects belong to the calling lane (``ops.Ctx.streams``), so split-K
+    workspaces never alias across concurrent launches or across lanes."""
 
-    def __init__(self, device, n=2):
+    def __init__(self, device, side):
         self.device = torch.device(device)
-        self.side = [(torch.cuda.Stream(self.device), ops.Ctx(self.device)) for _ in range(n)]
+        self.side = side
 
     def run(self, ctx, main, *others):
         cur = torch.cuda.current_stream(self.device)
         for st, _ in self.side[: len(others)]:
             st.wait_stream(cur)
+        keep = ctx.keep                          # side-branch tensors: calling-stream memory (ops.side_stream)
         for (st, c), fn in zip(self.side, others):
-            with torch.cuda.stream(st):
+            with ops.side_stream(st, keep):
                 fn(c)
         main(ctx)
         for st, _ in self.side[: len(others)]:
@@ -252,12 +255,9 @@ class LNetEngine:
             c = L.conv.cout
         return n, h, w, c
 
-    def _branches(self):
-        if getattr(self, "_br", None) is None:
-            if self.device.type != "cuda":
-                return None
-            self._br = Branches(self.device)
-        return self._br
+    def _branches(self, ctx):
+        side = ctx.streams(("lnet", id(self)), 2)
+        return None if side is None else Branches(self.device, side)
 
     def forward(self, ctx, audio: torch.Tensor, face6: NHWC, out: NHWC, logits: NHWC | None = None,
                 pad_rgb: bool = False):
@@ -296,9 +296,9 @@ class LNetEngine:
                 y = NHWC.empty(b, oh2, ow2, cw.cout, dev)
                 ops.conv2d(cx, x, cw, y, act=ops.ACT_RELU, res=x if res else None)
                 x = y
-            self.bank.run(cx, x)
+            st["adain"] = self.bank.run(cx, x)
 
-        br = self._branches() if BRANCHES else None
+        br = self._branches(ctx) if BRANCHES else None
         if br is None:
             masked(ctx)
             reference(ctx)
@@ -306,6 +306,7 @@ class LNetEngine:
         else:
             br.run(ctx, masked, reference, audio_enc)
         self.ca2(ctx, st["xm2"], cat.slice(c, c), cat.slice(0, c))
+        ap = st["adain"]                                        # ADAIN gamma / beta of every FFC
         # ---- decoder (LNet.py:67-77)
         cur = cat
         for lv in self.levels:
@@ -321,9 +322,9 @@ class LNetEngine:
             nblk = len(lv["blocks"])
             for bi, (l1, l2) in enumerate(lv["blocks"]):
                 l1.pre_norm(ctx, cur, ya, br, xpad=pc if bi > 0 else None)
-                l1.norm(ctx, self.bank, ya, ya, pad_out=pa)
+                l1.norm(ctx, self.bank, ap, ya, ya, pad_out=pa)
                 l2.pre_norm(ctx, ya, yb, br, xpad=pa)
-                l2.norm(ctx, self.bank, yb, cur, res=cur,        # FFCResnetBlock: id + conv2(conv1(x))
+                l2.norm(ctx, self.bank, ap, yb, cur, res=cur,    # FFCResnetBlock: id + conv2(conv1(x))
                         pad_out=pc if bi + 1 < nblk else None)
             up = lv["up"](ctx, cur)
             skip = skips.pop()

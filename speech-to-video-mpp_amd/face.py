@@ -231,7 +231,10 @@ def gaussian_blur(x: torch.Tensor, ksize, sigma, *, out_dtype=None, zero_border=
     return y
 
 
-def mask_postprocess(mask_u8: torch.Tensor, thres=26) -> torch.Tensor:
+MASK_BORDER = 26          # FaceEnhancement.mask_postprocess(mask, thres=26) (face_enhancement.py:83)
+
+
+def mask_postprocess(mask_u8: torch.Tensor, thres=MASK_BORDER) -> torch.Tensor:
     """FaceEnhancement.mask_postprocess (face_enhancement.py:83-88) of mask_sharp = parse / 255.:
     border zeroing + /255 fused into the first blur's row pass, two 101-tap sigma-11 blurs in fp64,
     astype(float32) fused into the second's column pass."""
@@ -466,9 +469,12 @@ class FaceEnhancement:
             if tmp_mask.shape[0] != S:
                 tmp_mask = post.resize_linear(tmp_mask, (S, S))
             if need_sharp:
+                # mask_sharp = parse / 255. as mask_postprocess left it: the reference zeroes its
+                # 26-pixel border IN PLACE (face_enhancement.py:84-85 on the array of :144) before it
+                # is resized and warped (:149-150)
                 ms = torch.empty(m8.shape, dtype=torch.float64, device=dev)
-                check(ctx.lib.s2v_u8_div255_f64(m8.data_ptr(), m8.numel(), ms.data_ptr(), ctx.stream),
-                      "s2v_u8_div255_f64")
+                check(ctx.lib.s2v_u8_div255_f64_border(m8.data_ptr(), m8.shape[0], m8.shape[1], MASK_BORDER,
+                                                       ms.data_ptr(), ctx.stream), "s2v_u8_div255_f64_border")
                 if ms.shape[0] != ef.shape[0]:
                     ms = post.resize_linear(ms, (ef.shape[1], ef.shape[0]))
                 mask_sharp = warp_affine(ms, tfm_inv, (width, height))

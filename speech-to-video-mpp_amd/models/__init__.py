@@ -31,20 +31,36 @@ def _need_cuda(*ts):
 
 
 class _EngineMixin:
+    """Device engines of a module: the folded / packed weights (one engine per device, read-only
+    after it is built) and one ``ops.Ctx`` per *lane* — the mutable device state of a forward
+    (workspace, side streams, noise counters).  Forwards on different lanes of one module can run
+    concurrently (e.g. two captured graphs replayed on two streams); forwards on one lane must not
+    overlap.  Copies of a module (copy.copy / deepcopy / pickle) get fresh engines: an engine and its
+    lanes are never shared between two modules."""
     _engine_cls = None
     _prefix = ""
 
-    def _engine(self, device):
+    def _engine(self, device, lane: int = 0):
         cache = self.__dict__.setdefault("_s2v_engines", {})
         key = str(device)
         if key not in cache:
             sd = {k: v.detach().to("cpu") for k, v in self.state_dict().items()}
-            cache[key] = (self._build_engine(sd, device), ops.Ctx(device))
-        return cache[key]
+            cache[key] = (self._build_engine(sd, device), {})
+        eng, lanes = cache[key]
+        if lane not in lanes:
+            lanes[lane] = ops.Ctx(device)
+        ctx = lanes[lane]
+        ctx.keep.clear()        # a new forward on this lane: the previous one's side branches have been joined
+        return eng, ctx
 
     def refresh(self):
         self.__dict__.pop("_s2v_engines", None)
         return self
+
+    def __getstate__(self):
+        state = dict(self.__dict__)
+        state.pop("_s2v_engines", None)
+        return state
 
     def load_state_dict(self, state_dict, strict=True, assign=False):
         self.refresh()
@@ -59,14 +75,15 @@ class LNet(_EngineMixin, arch.LNetParams):
         return LNetEngine(sd, device)
 
     @torch.no_grad()
-    def forward(self, audio_sequences, face_sequences):
+    def forward(self, audio_sequences, face_sequences, *, lane: int = 0):
+        """``lane`` (keyword-only, not in the reference): the execution lane (see _EngineMixin)."""
         _need_cuda(audio_sequences, face_sequences)
         b = audio_sequences.size(0)
         five = face_sequences.dim() > 4
         if five:
             audio_sequences = _fold5(audio_sequences, 1)
             face_sequences = _fold5(face_sequences, 2)
-        eng, ctx = self._engine(face_sequences.device)
+        eng, ctx = self._engine(face_sequences.device, lane)
         n, _, h, w = face_sequences.shape
         dev = face_sequences.device
         x6 = NHWC.empty(n, h, w, 6, dev)
@@ -91,7 +108,8 @@ class ENet(_EngineMixin, arch.ENetParams):
         return ENetEngine(sd, device)
 
     @torch.no_grad()
-    def forward(self, audio_sequences, face_sequences, gt_sequences, noises=None):
+    def forward(self, audio_sequences, face_sequences, gt_sequences, noises=None, *, lane: int = 0):
+        """``lane`` (keyword-only, not in the reference): the execution lane (see _EngineMixin)."""
         _need_cuda(audio_sequences, face_sequences, gt_sequences)
         b = audio_sequences.size(0)
         five = face_sequences.dim() > 4
@@ -99,7 +117,7 @@ class ENet(_EngineMixin, arch.ENetParams):
             audio_sequences = _fold5(audio_sequences, 1)
             face_sequences = _fold5(face_sequences, 2)
             gt_sequences = _fold5(gt_sequences, 2)
-        eng, ctx = self._engine(face_sequences.device)
+        eng, ctx = self._engine(face_sequences.device, lane)
         n = face_sequences.shape[0]
         dev = face_sequences.device
         out = torch.empty((n, 3, 384, 384), device=dev)
@@ -109,8 +127,7 @@ class ENet(_EngineMixin, arch.ENetParams):
             out = torch.stack(torch.split(out, b, 0), 2)
             # F.interpolate(low_res_img, outputs.size()[3:]) (default mode 'nearest', ENet.py:134)
             up = torch.empty((n, 3) + tuple(out.shape[3:]), device=dev)
-            ops.resize(ctx, low.data_ptr(), tuple(low.shape), low.stride(), up.data_ptr(), tuple(out.shape[3:]),
-                       up.stride(), mode=1)
+            ops.resize(ctx, low, 0, tuple(low.shape), low.stride(), up, 0, tuple(out.shape[3:]), up.stride(), mode=1)
             low = torch.stack(torch.split(up, b, 0), 2)
         return out, low
 
@@ -123,9 +140,10 @@ class DNet(_EngineMixin, arch.DNetParams):
         return DNetEngine(sd, device)
 
     @torch.no_grad()
-    def forward(self, input_image, driving_source, stage=None):
+    def forward(self, input_image, driving_source, stage=None, *, lane: int = 0):
+        """``lane`` (keyword-only, not in the reference): the execution lane (see _EngineMixin)."""
         _need_cuda(input_image, driving_source)
-        eng, ctx = self._engine(input_image.device)
+        eng, ctx = self._engine(input_image.device, lane)
         return eng.forward(ctx, input_image.float(), driving_source.float(), stage=stage)
 
 

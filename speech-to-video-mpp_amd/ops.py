@@ -1,21 +1,26 @@
-"""Tensor-level wrappers over the C ABI (libs2v.so).
+"""Tensor-level model-path ops: every kernel launch of the LNet / ENet / DNet / GFPGAN / GPEN
+engines is a dispatch of a ``torch.ops.s2v`` custom op (csrc/torch_launch.cpp: TORCH_LIBRARY(s2v),
+HIP kernel key), which validates the views and calls the C ABI of libs2v.so on the current HIP
+stream.  torch.profiler therefore attributes the model path to ``s2v::*`` ops, like the reference's
+aten ops under torch.no_grad() (inference.py:266), and a hipGraph capture records just the kernels.
 
-PyTorch is used only as the device allocator and stream provider: every op here hands raw
-device pointers + sizes to a HIP kernel in libs2v.  Inputs must be CUDA (HIP) fp32 tensors; a
-CPU tensor raises (there is no CPU path in the product).
+PyTorch is used only as the dispatcher, device allocator and stream provider.  Inputs must be HIP
+fp32 tensors; a CPU tensor raises (there is no CPU path in the product).
 
 Layout: activations are NHWC tensors [N, H, W, Ctot]; an ``NHWC`` view selects a channel slice
 [coff, coff + c) of one, which is how the reference's torch.cat / split / narrow disappear.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import math
 import os
+import threading
 
 import torch
 
-from . import _lib
+from . import _lib, torch_ops
 from ._lib import (ACT_GELU_TANH, ACT_LRELU, ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_TANH,  # noqa: F401
                    IN_DIRECT, IN_NEAREST_UP2, IN_TRANSPOSED, PAD_REFLECT, PAD_ZERO, PREC_BF16X3, PREC_F16X3, PREC_F32,
                    check)
@@ -58,9 +63,75 @@ def set_precision(name: str) -> str:
 def prec_code() -> int:
     return _PRECISIONS[PRECISION]
 
-# Optional per-launch observer (bench.py's live roofline): called as hook(ctx, params, flops, launch)
-# where launch() performs the conv; the hook may bracket it with events.
+# Optional per-launch observer (bench.py's live roofline): called as hook(ctx, info, flops, launch)
+# where info is the launch's ConvLaunch (kernel plan + shape) and launch() performs the conv; the
+# hook may bracket it with events.
 CONV_HOOK = None
+# Optional launch timer (bench.py's roofline of the benchmarked, graph-replayed launches): called as
+# STAMP(info, flops) for every conv launch (info: ConvLaunch); returns None or (stamps, stamp_ctr,
+# [slot, stride, reps]) for the kernel's in-launch clock stamps (s2v_conv_params.stamps).
+STAMP = None
+_NOSTAMP = (None, None, [0, 1, 1])
+
+
+class _Dispatch:
+    """``torch.ops.s2v`` (libs2v_torch.so, loaded on first use).  tests/test_engine_dryrun.py swaps
+    in a schema-checking stand-in to walk the engines' host plans on a machine without a GPU."""
+
+    def __getattr__(self, name):
+        return getattr(torch_ops.load(), name)
+
+
+S2V = _Dispatch()
+
+
+class ConvLaunch:
+    """What one conv launch runs: ``plan`` = s2v_conv2d_plan's ten ints (kernel instance, split-K
+    factor) plus the problem shape, for conv_symbol() / conv_splits() and the roofline hooks."""
+    __slots__ = ("plan", "n", "h", "w", "cin", "oh", "ow", "cout", "kh", "kw", "in_scale", "nc_scale", "pix_add", "res",
+                 "res_is_y")
+
+    def __init__(self, plan, **kw):
+        self.plan = list(plan)
+        for k in self.__slots__[1:]:
+            setattr(self, k, kw.get(k, 0))
+
+
+_SIDE = threading.local()
+
+
+@contextlib.contextmanager
+def side_stream(stream, keep: list):
+    """Run a forward's side branch on ``stream``: kernels launch there, but every tensor the branch
+    allocates through ``empty`` / ``NHWC.empty`` comes from the *calling* stream and is appended to
+    ``keep`` (alive until the caller drops the list, after the branch has been joined back).
+
+    Why: the caching allocator puts an allocation made during a hipGraph capture into the graph's
+    private pool only when its stream is recognised as capturing; a side stream forked into the
+    capture is not reliably recognised on ROCm, so its tensors came from the global pool, went back
+    there when the branch returned and were handed to the next forward or graph that allocated on
+    that (pooled, recycled) stream — two graphs writing one buffer: the round-2 cross-engine
+    corruption (tests/test_lanes_gpu.py).  Allocated on the capture stream they are graph-owned;
+    kept alive to the join they are never reused while the branch still reads them."""
+    prev = getattr(_SIDE, "v", None)
+    _SIDE.v = (torch.cuda.current_stream(), keep)
+    try:
+        with torch.cuda.stream(stream):
+            yield
+    finally:
+        _SIDE.v = prev
+
+
+def empty(shape, device, dtype=torch.float32) -> torch.Tensor:
+    """torch.empty for forward activations (side branches allocate from the calling stream)."""
+    side = getattr(_SIDE, "v", None)
+    if side is None:
+        return torch.empty(shape, device=device, dtype=dtype)
+    main, keep = side
+    with torch.cuda.stream(main):
+        t = torch.empty(shape, device=device, dtype=dtype)
+    keep.append(t)
+    return t
 
 
 def _require_cuda(t: torch.Tensor, what: str):
@@ -70,19 +141,24 @@ def _require_cuda(t: torch.Tensor, what: str):
 
 
 class NHWC:
-    """Channel-slice view of a contiguous [N, H, W, Ctot] fp32 device tensor.  ``split``: the
-    tensor holds the split-fp32 layout of the current precision (s2v_split_act; only convolutions
-    with x_split read it)."""
+    """Channel-slice view of a contiguous [N, H, W, Ctot] fp32 device tensor.  ``split``: 0, or the
+    precision code (PREC_BF16X3 / PREC_F16X3) whose split-fp32 layout the tensor holds
+    (s2v_split_act; only convolutions with x_split read it, and only in that same precision)."""
     __slots__ = ("t", "n", "h", "w", "cs", "coff", "c", "split")
 
-    def __init__(self, t: torch.Tensor, coff: int = 0, c: int | None = None, split: bool = False):
+    def __init__(self, t: torch.Tensor, coff: int = 0, c: int | None = None, split: int = 0):
         assert t.dim() == 4 and t.is_contiguous(), "NHWC view needs a contiguous 4-D tensor"
         _require_cuda(t, "NHWC")
+        n_, h_, w_, c_ = t.shape
+        canon = (h_ * w_ * c_, w_ * c_, c_, 1)
+        if t.stride() != canon:       # contiguous with size-1 dims of arbitrary stride: canonical view
+            t = t.as_strided(t.shape, canon)
         self.t = t
         self.n, self.h, self.w, self.cs = t.shape
         self.coff = coff
         self.c = self.cs - coff if c is None else c
-        self.split = split
+        self.split = int(split)
+        assert self.split in (0, PREC_BF16X3, PREC_F16X3), "split: 0 or a split precision code"
         assert 0 <= coff and coff + self.c <= self.cs
         assert not split or (coff % 32 == 0 and self.c % 32 == 0), "split views cover whole 32-channel blocks"
 
@@ -90,12 +166,17 @@ class NHWC:
     def ptr(self) -> int:
         return self.t.data_ptr() + F32 * self.coff
 
+    @property
+    def v(self) -> torch.Tensor:
+        """The view as a torch tensor [N, H, W, c] (a channel slice of ``t``)."""
+        return self.t if (self.coff == 0 and self.c == self.cs) else self.t[..., self.coff: self.coff + self.c]
+
     def slice(self, coff: int, c: int) -> "NHWC":
         return NHWC(self.t, self.coff + coff, c, self.split)
 
     @staticmethod
     def empty(n, h, w, c, device) -> "NHWC":
-        return NHWC(torch.empty((n, h, w, c), device=device, dtype=torch.float32))
+        return NHWC(empty((n, h, w, c), device))
 
 
 class Workspace:
@@ -121,9 +202,28 @@ class Workspace:
             self.buf = torch.empty(int(nbytes * 1.25) + 256, dtype=torch.uint8, device=self.device)
         return self.buf.data_ptr(), self.buf.numel()
 
+    def tensor(self):
+        """The current buffer (uint8; None while empty) for the ops' ``Tensor? ws`` argument."""
+        return self.buf if self.buf.numel() else None
+
+
+def _with_ws(ctx, launch):
+    """Run ``launch(ws)`` (an s2v op returning the workspace bytes it still needs, 0 = launched);
+    grow the context's workspace once when it is short."""
+    need = launch(ctx.ws.tensor())
+    if need:
+        ctx.ws.get(need)
+        need = launch(ctx.ws.tensor())
+        if need:
+            raise _lib.S2VError(f"workspace of {ctx.ws.buf.numel()} bytes, the launch needs {need}")
+
 
 class Ctx:
-    """Execution context: device, stream handle, workspace."""
+    """Execution context = one *lane*: device, workspace, and every piece of mutable device state a
+    forward needs besides its activations — the side streams (each with its own Ctx, so split-K
+    workspaces never alias across concurrent launches) and the noise draw counters.  Engines keep
+    only read-only weights, so two Ctx objects can run forwards of the same engine concurrently
+    (two captured graphs replayed on two streams): nothing either graph writes is shared."""
 
     N_COUNTERS = 1 << 18
 
@@ -132,6 +232,25 @@ class Ctx:
         self.ws = Workspace(self.device)
         self.lib = _lib.load()
         self._counters = None
+        self._streams = {}
+        self._noise = {}
+        self.keep = []          # the current forward's side-branch tensors (side_stream), dropped per forward
+
+    def streams(self, key, n):
+        """``n`` (stream, Ctx) pairs for the side branches of engine ``key`` (made once, CUDA
+        devices only; None on other devices)."""
+        if self.device.type != "cuda":
+            return None
+        if key not in self._streams:
+            self._streams[key] = [(torch.cuda.Stream(self.device), Ctx(self.device)) for _ in range(n)]
+        assert len(self._streams[key]) >= n
+        return self._streams[key][:n]
+
+    def noise(self, key) -> "NoiseCounter":
+        """The noise draw counter of engine ``key`` in this lane."""
+        if key not in self._noise:
+            self._noise[key] = NoiseCounter()
+        return self._noise[key]
 
     def counters(self):
         """Zeroed split-K tile counters (s2v_conv_params.tile_counters), made once per context
@@ -225,8 +344,7 @@ class ConvW:
             if self.wt.is_cuda and torch.cuda.is_current_stream_capturing():
                 raise _lib.S2VError("split weights must be built by an eager run before graph capture")
             out = torch.empty(self.wt.shape, dtype=torch.float32, device=self.wt.device)
-            check(ctx.lib.s2v_split_weights(self.wt.data_ptr(), self.npad, self.kpad, prec, self.split_scale(prec),
-                                            out.data_ptr(), ctx.stream), "s2v_split_weights")
+            S2V.split_weights_(self.wt, out, prec, self.split_scale(prec))
             self._split[prec] = out
         return self._split[prec]
 
@@ -269,9 +387,10 @@ def _ptr(t):
 def conv2d(ctx: Ctx, x: NHWC, cw: ConvW, y: NHWC, *, act=ACT_NONE, alpha=0.0, res: NHWC | None = None,
            res_after=False, res_offset=(0, 0), nc_scale=None, in_scale=None, pre_act=ACT_NONE, pre_alpha=0.0,
            pix_add=None, pix_w=0.0, scale=None, shift=None, force_tile=0, force_splits=0, pool=False):
-    """Fused conv (see s2v_conv_params).  nc_scale / in_scale: [N, C] device tensors.  A transposed
-    ConvW with a polyphase plan (``cw.poly``) runs as one stride-1 conv per output parity class.
-    ``pool``: y is the 2x2 average pool of the activated conv output (half the conv's size)."""
+    """Fused conv (s2v_conv_params, dispatched as ``s2v::conv2d_``).  nc_scale / in_scale: [N, C]
+    device tensors.  A transposed ConvW with a polyphase plan (``cw.poly``) runs as one stride-1 conv
+    per output parity class, each writing every second pixel of y.  ``pool``: y is the 2x2 average
+    pool of the activated conv output (half the conv's size)."""
     if getattr(cw, "poly", None) is not None:
         assert pix_add is None, "polyphase transposed conv: no pix_add epilogue"
         assert res is None or (res.t.data_ptr() == y.t.data_ptr() and res.coff == y.coff and not res_after), \
@@ -279,160 +398,121 @@ def conv2d(ctx: Ctx, x: NHWC, cw: ConvW, y: NHWC, *, act=ACT_NONE, alpha=0.0, re
         oh, ow = cw.out_hw(x.h, x.w)
         assert (y.n, y.h, y.w, y.c) == (x.n, oh, ow, cw.cout), "conv_transpose: output view mismatch"
         for (ry, rx), sub, _ in cw.poly:
-            ch, cwid = (oh - ry + 1) // 2, (ow - rx + 1) // 2
-            if ch <= 0 or cwid <= 0:
+            if (oh - ry + 1) // 2 <= 0 or (ow - rx + 1) // 2 <= 0:
                 continue
-            base = NHWC.__new__(NHWC)
-            base.t, base.n, base.h, base.w, base.cs, base.c = y.t, y.n, ch, cwid, y.cs, y.c
-            base.split = False
-            base.coff = y.coff + (ry * y.w + rx) * y.cs
-            _conv(ctx, x, sub, base, (ch, cwid), (2, y.h, y.w), act, alpha, None if res is None else base, False,
-                  (0, 0), nc_scale, in_scale, pre_act, pre_alpha, None, 0.0, scale, shift, force_tile, force_splits)
+            yc = y.t[:, ry::2, rx::2, y.coff: y.coff + y.c]          # one output parity class
+            _conv(ctx, x, sub, yc, 2, act, alpha, yc if res is not None else None, False, (0, 0), nc_scale,
+                  in_scale, pre_act, pre_alpha, None, 0.0, scale, shift, force_tile, force_splits)
         return y
     oh, ow = cw.out_hw(x.h, x.w)
     assert x.c == cw.cin, f"conv: input has {x.c} channels, weights expect {cw.cin}"
     f = 2 if pool else 1
     assert (y.n, y.h * f, y.w * f, y.c) == (x.n, oh, ow, cw.cout), \
         f"conv: output view {(y.n, y.h, y.w, y.c)} != {(x.n, oh // f, ow // f, cw.cout)}"
-    return _conv(ctx, x, cw, y, (oh, ow), None, act, alpha, res, res_after, res_offset, nc_scale, in_scale, pre_act,
-                 pre_alpha, pix_add, pix_w, scale, shift, force_tile, force_splits, pool=pool)
+    _conv(ctx, x, cw, y.v, 1, act, alpha, None if res is None else res.v, res_after, res_offset, nc_scale, in_scale,
+          pre_act, pre_alpha, pix_add, pix_w, scale, shift, force_tile, force_splits, pool=pool)
+    return y
 
 
-def _conv(ctx, x, cw, y, ohw, out_view, act, alpha, res, res_after, res_offset, nc_scale, in_scale, pre_act,
-          pre_alpha, pix_add, pix_w, scale, shift, force_tile, force_splits, per_sample_wt=None, pool=False):
-    oh, ow = ohw
-    p = _lib.ConvParams()
-    p.x, p.n, p.h, p.w, p.cin, p.xcs = x.ptr, x.n, x.h, x.w, x.c, x.cs
-    p.in_mode, p.pad_mode, p.pre_act, p.pre_alpha = cw.in_mode, cw.pad_mode, pre_act, pre_alpha
-    if in_scale is not None:
-        p.in_scale, p.in_scale_ns = in_scale.data_ptr(), in_scale.stride(0)
-    p.kh, p.kw, p.sh, p.sw, p.ph, p.pw, p.dh, p.dw = cw.kh, cw.kw, cw.sh, cw.sw, cw.ph, cw.pw, cw.dh, cw.dw
-    p.wt, p.kpad, p.npad, p.cout = cw.wt.data_ptr(), cw.kpad, cw.npad, cw.cout
-    p.prec = prec_code()
-    p.y, p.oh, p.ow, p.ycs = y.ptr, oh, ow, y.cs
+def _conv_flops(x, cw, yv, pool):
+    """Algorithmic FLOPs (2 MAC) of one launch; a transposed conv counts only its real taps."""
+    oh, ow = (yv.shape[1], yv.shape[2])
+    if pool:
+        oh, ow = 2 * oh, 2 * ow
+    pix = x.n * x.h * x.w if cw.in_mode == IN_TRANSPOSED else x.n * oh * ow
+    return 2.0 * pix * cw.kh * cw.kw * cw.cin * cw.cout
+
+
+def _conv(ctx, x, cw, yv, out_step, act, alpha, resv, res_after, res_offset, nc_scale, in_scale, pre_act, pre_alpha,
+          pix_add, pix_w, scale, shift, force_tile, force_splits, pool=False):
+    """One ``s2v::conv2d_`` launch: x an NHWC view, yv / resv torch views (out_step 2: a strided
+    parity-class view of a wider tensor)."""
+    prec = prec_code()
+    x_split = int(getattr(x, "split", 0))
+    if x_split and x_split != prec:
+        raise _lib.S2VError(f"conv: the input holds the split layout of precision code {x_split}, but the conv runs "
+                            f"in {PRECISION!r} (code {prec}); split it again with split_act after set_precision")
+    wsplit = cw.wt_x3(ctx, prec) if prec != PREC_F32 else None
+    wscale = cw.split_scale(prec)
+    counters = _counters(ctx)
     sc = cw.scale if scale is None else scale
     sh = cw.shift if shift is None else shift
-    p.scale, p.shift = _ptr(sc), _ptr(sh)
-    if nc_scale is not None:
-        p.nc_scale, p.nc_scale_ns = nc_scale.data_ptr(), nc_scale.stride(0)
-    if pix_add is not None:
-        p.pix_add, p.pix_w = pix_add.data_ptr(), pix_w
-    if res is not None:
-        p.res, p.res_cs, p.res_h, p.res_w = res.ptr, res.cs, res.h, res.w
-        p.res_oy, p.res_ox = res_offset
-        p.res_after_act = int(res_after)
-    p.act, p.alpha = act, alpha
-    p.batch = 1
-    p.force_tile, p.force_splits = force_tile, force_splits
-    p.out_pool = int(pool)
-    p.x_split = int(getattr(x, "split", False))
-    if p.x_split:
-        assert p.prec != PREC_F32, "split-layout inputs need a split precision (f16x3 / bf16x3)"
-    if out_view is not None:
-        p.out_step, p.out_full_h, p.out_full_w = out_view
-    if per_sample_wt is not None:        # batch mode: one image per batch entry, its own weights
-        assert in_scale is None and nc_scale is None and out_view is None
-        p.n, p.batch = 1, x.n
-        p.w_bs = cw.npad * cw.kpad
-        p.x_bs, p.y_bs = x.h * x.w * x.cs, y.h * y.w * y.cs
-        if res is not None:
-            p.res_bs = res.h * res.w * res.cs
-    use_x3 = False
-    if p.prec != PREC_F32:
-        p.wt_x3 = p.wt                   # placeholder: the plan query only checks it is set
-        use_x3 = bool(_plan(ctx, p)[6]) and not p.b_kn
-        p.wt_x3 = None
-    if per_sample_wt is not None:
-        wb, wscale = per_sample_wt(p.prec if use_x3 else PREC_F32)   # as the kernel reads them
-        if use_x3:
-            p.wt, p.wt_x3, p.wt_scale = None, wb.data_ptr(), wscale
-        else:
-            p.wt = wb.data_ptr()
-    elif use_x3:                         # implicit-GEMM path: pre-split packed weights
-        p.wt_x3 = cw.wt_x3(ctx, p.prec).data_ptr()
-        p.wt_scale = cw.split_scale(p.prec)
-    need = ctx.lib.s2v_conv2d_ws_bytes(ctypes.byref(p))
-    p.ws, p.ws_bytes = ctx.ws.get(need)
-    _set_counters(ctx, p, need)
-    if CONV_HOOK is not None:
-        # algorithmic MACs: a transposed conv only counts real (non-inserted-zero) taps
-        taps = cw.kh * cw.kw
-        pix = x.n * x.h * x.w if cw.in_mode == IN_TRANSPOSED else x.n * oh * ow
-        flops = 2.0 * pix * taps * cw.cin * cw.cout
-        CONV_HOOK(ctx, p, flops, lambda: check(ctx.lib.s2v_conv2d(ctypes.byref(p), ctx.stream), "s2v_conv2d"))
-        return y
-    check(ctx.lib.s2v_conv2d(ctypes.byref(p), ctx.stream), "s2v_conv2d")
-    return y
+
+    def launch(ws, dry=False, st=_NOSTAMP):
+        return S2V.conv2d_(x.v, yv, cw.wt, wsplit, wscale, cw.cout, [cw.kh, cw.kw], [cw.sh, cw.sw], [cw.ph, cw.pw],
+                           [cw.dh, cw.dw], cw.in_mode, cw.pad_mode, prec, sc, sh, in_scale, nc_scale, pre_act, pre_alpha,
+                           pix_add, pix_w, resv, list(res_offset), res_after, act, alpha, out_step, pool, x_split != 0,
+                           ws, counters, force_tile, force_splits, st[0], st[1], st[2], dry)
+    _run_conv(ctx, launch, x, cw, yv, pool, in_scale, nc_scale, pix_add, resv)
+
+
+def _run_conv(ctx, launch, x, cw, yv, pool, in_scale=None, nc_scale=None, pix_add=None, resv=None):
+    st = _NOSTAMP
+
+    def go():
+        _with_ws(ctx, lambda ws: launch(ws, False, st)[0])
+    if CONV_HOOK is None and STAMP is None:
+        go()
+        return
+    plan = launch(ctx.ws.tensor(), True)[1:]
+    oh, ow = yv.shape[1] * (2 if pool else 1), yv.shape[2] * (2 if pool else 1)
+    info = ConvLaunch(plan, n=x.n, h=x.h, w=x.w, cin=x.c, oh=oh, ow=ow, cout=cw.cout, kh=cw.kh, kw=cw.kw,
+                      in_scale=in_scale is not None, nc_scale=nc_scale is not None, pix_add=pix_add is not None,
+                      res=resv is not None, res_is_y=resv is not None and resv.data_ptr() == yv.data_ptr())
+    flops = _conv_flops(x, cw, yv, pool)
+    if STAMP is not None:
+        st = STAMP(info, flops) or _NOSTAMP
+    if CONV_HOOK is None:
+        go()
+    else:
+        CONV_HOOK(ctx, info, flops, go)
 
 
 def modulated_conv2d(ctx: Ctx, x: NHWC, cw: ConvW, y: NHWC, s: torch.Tensor, d: torch.Tensor | None = None, *,
                      act=ACT_NONE, alpha=0.0, res: NHWC | None = None, res_after=False, pix_add=None, pix_w=0.0,
                      shift=None, force_splits=0):
-    """StyleGAN2 modulated conv with per-sample weights W * s[b, c] (* d[b, o]) built by
-    s2v_modulate_weights, then one batched conv (no prologue / epilogue scaling in the GEMM).
-    s: [B, cin] (row stride s.stride(0)); d: [B, cout] demodulation or None."""
+    """StyleGAN2 modulated conv with per-sample weights W * s[b, c] (* d[b, o]) written by the
+    ``s2v::modulated_conv2d_`` op in the form its planned kernel reads (split layout with a 2^11 f16
+    pre-scale when demodulated, or fp32), then one batched conv (no prologue / epilogue scaling in
+    the GEMM).  s: [B, cin] (row stride s.stride(0)); d: [B, cout] demodulation or None."""
     oh, ow = cw.out_hw(x.h, x.w)
-    assert cw.in_mode != IN_TRANSPOSED and cw.poly is None, "modulated_conv2d: direct / up2 convs only"
+    assert cw.in_mode != IN_TRANSPOSED and cw.poly is None and (cw.sh, cw.sw, cw.dh, cw.dw) == (1, 1, 1, 1), \
+        "modulated_conv2d: direct stride-1 convs only"
     assert x.c == cw.cin and (y.n, y.h, y.w, y.c) == (x.n, oh, ow, cw.cout)
-    b = x.n
+    wbuf = torch.empty((x.n, cw.npad, cw.kpad), device=cw.wt.device)
+    yv, resv = y.v, None if res is None else res.v
+    prec = prec_code()
+    x_split = int(getattr(x, "split", 0))
+    if x_split and x_split != prec:
+        raise _lib.S2VError(f"modulated conv: the input holds the split layout of precision code {x_split}, but the "
+                            f"conv runs in {PRECISION!r} (code {prec})")
+    sh = cw.shift if shift is None else shift            # the layer bias (epilogue shift) unless overridden
 
-    def weights(prec):
-        # the split implicit GEMM reads split weights; the VALU kernels (small K / Cout) fp32.
-        # Demodulated rows have |w * s * d| <= post (ENet / GFPGAN / GPEN: sqrt 2), so f16 halves
-        # take a fixed 2^11 pre-scale (room up to |w| < 32); without demodulation the range is open
-        # and the weights go unscaled (f16 subnormal halves keep an absolute error <= 2^-25).
-        wb = torch.empty((b, cw.npad, cw.kpad), device=cw.wt.device)
-        dp, dns = (None, 0) if d is None else (d.data_ptr(), d.stride(0))
-        if prec == PREC_F32:
-            check(ctx.lib.s2v_modulate_weights(cw.wt.data_ptr(), cw.npad, cw.kpad, cw.K, cw.cin, cw.cout, s.data_ptr(),
-                                               s.stride(0), dp, dns, b, wb.data_ptr(), ctx.stream),
-                  "s2v_modulate_weights")
-            return wb, 1.0
-        scale = 2048.0 if (prec == PREC_F16X3 and d is not None) else 1.0
-        check(ctx.lib.s2v_modulate_weights_split(cw.wt.data_ptr(), cw.npad, cw.kpad, cw.K, cw.cin, cw.cout,
-                                                 s.data_ptr(), s.stride(0), dp, dns, b, prec, scale, wb.data_ptr(),
-                                                 ctx.stream), "s2v_modulate_weights_split")
-        return wb, scale
-    return _conv(ctx, x, cw, y, (oh, ow), None, act, alpha, res, res_after, (0, 0), None, None, ACT_NONE, 0.0,
-                 pix_add, pix_w, None, shift, 0, force_splits, per_sample_wt=weights)
+    def launch(ws, dry=False, st=_NOSTAMP):
+        return S2V.modulated_conv2d_(x.v, yv, cw.wt, s, d, wbuf, cw.cout, [cw.kh, cw.kw], [cw.ph, cw.pw], prec,
+                                     x_split != 0, cw.scale, sh, pix_add, pix_w, resv, res_after, act, alpha, ws,
+                                     force_splits, st[0], st[1], st[2], dry)
+    _run_conv(ctx, launch, x, cw, yv, False, pix_add=pix_add, resv=resv)
+    return y
 
 
 def gemm_kn(ctx: Ctx, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, batch: int, a_bs: int, b_bs: int,
             out_bs: int, res: torch.Tensor | None = None, res_bs: int = 0, act=ACT_NONE, alpha=0.0,
             force_tile=0, force_splits=0):
     """Batched out[z] = a[z] @ b[z] (+res[z]) with a [M, K] row-major (K contiguous, lda = K),
-    b [K, N] row-major (ldb = N), out [M, N] (ldc = N).  Used for the FourierUnit DFT products."""
-    M, K = a.shape[-2], a.shape[-1]
-    N = b.shape[-1]
-    p = _lib.ConvParams()
-    p.x, p.n, p.h, p.w, p.cin, p.xcs = a.data_ptr(), 1, 1, M, K, K
-    p.kh = p.kw = p.sh = p.sw = p.dh = p.dw = 1
-    p.wt, p.cout, p.b_kn, p.ldb = b.data_ptr(), N, 1, N
-    p.prec = prec_code()
-    p.y, p.oh, p.ow, p.ycs = out.data_ptr(), 1, M, N
-    if res is not None:
-        p.res, p.res_cs, p.res_h, p.res_w = res.data_ptr(), N, 1, M
-        p.res_bs = res_bs
-    p.act, p.alpha = act, alpha
-    p.batch, p.x_bs, p.w_bs, p.y_bs = batch, a_bs, b_bs, out_bs
-    p.force_tile, p.force_splits = force_tile, force_splits
-    need = ctx.lib.s2v_conv2d_ws_bytes(ctypes.byref(p))
-    p.ws, p.ws_bytes = ctx.ws.get(need)
-    _set_counters(ctx, p, need)
-    if CONV_HOOK is not None:   # DFT products: executed work, not reference-algorithmic FLOPs
-        CONV_HOOK(ctx, p, 0.0, lambda: check(ctx.lib.s2v_conv2d(ctypes.byref(p), ctx.stream), "s2v_conv2d(gemm)"))
-        return out
-    check(ctx.lib.s2v_conv2d(ctypes.byref(p), ctx.stream), "s2v_conv2d(gemm)")
+    b [K, N] row-major (ldb = N), out [M, N] (ldc = N) (``s2v::gemm_kn_``)."""
+    prec = prec_code()
+    _with_ws(ctx, lambda ws: S2V.gemm_kn_(a, b, out, batch, a_bs, b_bs, out_bs, res, res_bs, act, alpha, prec, ws,
+                                          force_tile, force_splits, False)[0])
     return out
 
 
-def _set_counters(ctx: Ctx, p, ws_need):
-    """Split-K launches fold their partial sums in-launch when the context has tile counters."""
-    if ws_need and USE_TILE_COUNTERS:
-        c = getattr(ctx, "counters", None)
-        t = c() if callable(c) else None
-        if t is not None:
-            p.tile_counters, p.n_counters = t.data_ptr(), t.numel()
+def _counters(ctx: Ctx):
+    """Split-K tile counters of the opt-in in-launch fold (S2V_SPLITK_FOLD=1), else None."""
+    if not USE_TILE_COUNTERS:
+        return None
+    c = getattr(ctx, "counters", None)
+    return c() if callable(c) else None
 
 
 def _plan(ctx: Ctx, p):
@@ -441,9 +521,9 @@ def _plan(ctx: Ctx, p):
     return list(out)
 
 
-def conv_symbol(ctx: Ctx, p) -> str:
-    """Kernel symbol (as rocprofv3 reports it, demangled) the launch of ``p`` runs."""
-    bm, bn, wm, avec, bkn, splits, x3, nw, ks, pf = _plan(ctx, p)
+def plan_symbol(plan) -> str:
+    """Kernel symbol (as rocprofv3 reports it, demangled) of a launch plan (s2v_conv2d_plan's ten ints)."""
+    bm, bn, wm, avec, bkn, splits, x3, nw, ks, pf = plan
     if avec == 5:
         return f"void s2v::conv_glds_x3<{bm}, {bn}, {wm}, {ks}, {x3 - 1}>(s2v::ConvArgs)"
     if bm == 0:
@@ -462,16 +542,21 @@ def conv_symbol(ctx: Ctx, p) -> str:
     return f"void s2v::conv_igemm<{bm}, {bn}, {wm}, {avec}, {bkn}>(s2v::ConvArgs)"
 
 
+def conv_symbol(ctx: Ctx, p) -> str:
+    """Kernel symbol the launch ``p`` runs (a ConvLaunch from CONV_HOOK, or raw s2v_conv_params)."""
+    return plan_symbol(p.plan if isinstance(p, ConvLaunch) else _plan(ctx, p))
+
+
 def split_act(ctx: Ctx, x: NHWC, out: NHWC | None = None) -> NHWC:
-    """fp32 activations -> the split layout of the current precision (s2v_split_act), the input
-    form of the LDS-DMA convolutions.  ``out``: a whole contiguous tensor of x's shape."""
+    """fp32 activations -> the split layout of the current precision (``s2v::split_act_``), the
+    input form of the LDS-DMA convolutions.  ``out``: a whole contiguous tensor of x's shape."""
     prec = prec_code()
     assert prec != PREC_F32, "split_act needs a split precision (f16x3 / bf16x3)"
     if out is None:
         out = NHWC.empty(x.n, x.h, x.w, x.c, x.t.device)
     assert (out.n, out.h, out.w, out.c) == (x.n, x.h, x.w, x.c) and out.coff == 0
-    check(ctx.lib.s2v_split_act(x.ptr, x.n * x.h * x.w, x.c, x.cs, prec, out.ptr, out.cs, ctx.stream), "s2v_split_act")
-    out.split = True
+    S2V.split_act_(x.v, out.v, prec)
+    out.split = prec
     return out
 
 
@@ -479,59 +564,43 @@ TUNE_HALO_MIN_BLOCKS, TUNE_GLDS_TILE, TUNE_SMALLK_TILE, TUNE_X3_RATE_512, TUNE_I
 
 
 def tune(ctx: Ctx, key: int, value: int) -> int:
-    """Set a planner knob (s2v_tune); returns the previous value."""
+    """Set a planner knob (s2v_tune, host-only); returns the previous value."""
     old = ctypes.c_longlong(0)
     check(ctx.lib.s2v_tune(key, value, ctypes.byref(old)), "s2v_tune")
     return old.value
 
 
 def conv_splits(ctx: Ctx, p) -> int:
-    return _plan(ctx, p)[5]
+    return (p.plan if isinstance(p, ConvLaunch) else _plan(ctx, p))[5]
 
 
 def layernorm2d(ctx: Ctx, x: NHWC, weight, bias, y: NHWC, *, act=ACT_LRELU, alpha=0.1, pool=False,
                 res: NHWC | None = None, eps=1e-5):
-    need = ctx.lib.s2v_layernorm2d_ws_bytes(x.n, x.h, x.w, x.c)
-    ws, nb = ctx.ws.get(need)
-    check(ctx.lib.s2v_layernorm2d(x.ptr, x.n, x.h, x.w, x.c, x.cs, weight.data_ptr(), bias.data_ptr(), eps, act, alpha,
-                                  int(pool), None if res is None else res.ptr, 0 if res is None else res.cs,
-                                  y.ptr, y.cs, ws, nb, ctx.stream), "s2v_layernorm2d")
+    rv = None if res is None else res.v
+    _with_ws(ctx, lambda ws: S2V.layernorm2d_(x.v, weight, bias, eps, act, alpha, pool, rv, y.v, ws))
     return y
 
 
-def instnorm(ctx: Ctx, x: NHWC, y: NHWC, gamma=None, beta=None, gb_ns=0, *, act=ACT_NONE, alpha=0.0,
+def instnorm(ctx: Ctx, x: NHWC, y: NHWC, gamma=None, beta=None, *, act=ACT_NONE, alpha=0.0,
              res: NHWC | None = None, eps=1e-5, pad_out: NHWC | None = None):
-    """gamma/beta: raw device pointers (ints) or None; gb_ns = per-sample row stride.  ``pad_out``
+    """InstanceNorm2d (+ ADAIN: gamma / beta [N, C] row views) + act (+ res).  ``pad_out``
     ([n, h+2, w+2, c] view) also receives F.pad(y, (1, 1, 1, 1), 'reflect')."""
-    need = ctx.lib.s2v_instnorm_ws_bytes(x.n, x.h, x.w, x.c)
-    ws, nb = ctx.ws.get(need)
-    rp, rcs = (None, 0) if res is None else (res.ptr, res.cs)
     if pad_out is not None:
         assert (pad_out.n, pad_out.h, pad_out.w, pad_out.c) == (x.n, x.h + 2, x.w + 2, x.c)
-        check(ctx.lib.s2v_instnorm_adain_pad(x.ptr, x.n, x.h, x.w, x.c, x.cs, gamma, beta, gb_ns, eps, act, alpha,
-                                             rp, rcs, y.ptr, y.cs, pad_out.ptr, pad_out.cs, ws, nb, ctx.stream),
-              "s2v_instnorm_adain_pad")
-        return y
-    check(ctx.lib.s2v_instnorm_adain(x.ptr, x.n, x.h, x.w, x.c, x.cs, gamma, beta, gb_ns, eps, act, alpha,
-                                     rp, rcs, y.ptr, y.cs, ws, nb, ctx.stream), "s2v_instnorm_adain")
+    rv, pv = None if res is None else res.v, None if pad_out is None else pad_out.v
+    _with_ws(ctx, lambda ws: S2V.instnorm_(x.v, gamma, beta, eps, act, alpha, rv, y.v, pv, ws))
     return y
 
 
 def adain_params(ctx: Ctx, hid: torch.Tensor, nhidden: int, w2t: torch.Tensor, bias: torch.Tensor, seg: torch.Tensor,
                  out: torch.Tensor):
-    batch, total = out.shape
-    check(ctx.lib.s2v_adain_params(hid.data_ptr(), batch, hid.stride(0), nhidden, w2t.data_ptr(), bias.data_ptr(),
-                                   seg.data_ptr(), total, out.data_ptr(), out.stride(0), ctx.stream),
-          "s2v_adain_params")
+    S2V.adain_params_(hid, nhidden, w2t, bias, seg, out)
     return out
 
 
 def modconv_demod(ctx: Ctx, s: torch.Tensor, wsq: torch.Tensor, out: torch.Tensor, *, eps=1e-8, post=1.0):
     """s: [B, cin] view (row stride s.stride(0)), wsq: [cout, cin], out: [B, cout]."""
-    batch, cin = s.shape
-    cout = wsq.shape[0]
-    check(ctx.lib.s2v_modconv_demod(s.data_ptr(), batch, s.stride(0), cin, wsq.data_ptr(), cout, eps, post,
-                                    out.data_ptr(), out.stride(0), ctx.stream), "s2v_modconv_demod")
+    S2V.modconv_demod_(s, wsq, out, eps, post)
     return out
 
 
@@ -542,17 +611,18 @@ def torch_bilinear_scale(in_size: int, out_size: int, scale_factor=None) -> floa
     return float(torch.tensor(in_size, dtype=torch.float32) / out_size)
 
 
-def resize(ctx: Ctx, x_ptr: int, x_shape, x_strides, y_ptr: int, y_hw, y_strides, *, scale_factor=None,
-           mode=0):
-    """x_shape = (n, c, ih, iw); strides (sn, sc, sy, sx) in elements, for input and output."""
+def resize(ctx: Ctx, x: torch.Tensor, x_off: int, x_shape, x_strides, y: torch.Tensor, y_off: int, y_hw, y_strides, *,
+           scale_factor=None, mode=0):
+    """F.interpolate between strided views (``s2v::resize_``): the view of x starts ``x_off``
+    elements into x's data with x_shape = (n, c, ih, iw) and strides (sn, sc, sy, sx) in elements
+    (any sign); the same for y with its (oh, ow).  mode 0 bilinear, 1 nearest."""
     n, c, ih, iw = x_shape
     oh, ow = y_hw
     sh = torch_bilinear_scale(ih, oh, scale_factor) if mode == 0 else (
         float(torch.tensor(1.0 / scale_factor, dtype=torch.float32)) if scale_factor else ih / oh)
     sw = torch_bilinear_scale(iw, ow, scale_factor) if mode == 0 else (
         float(torch.tensor(1.0 / scale_factor, dtype=torch.float32)) if scale_factor else iw / ow)
-    check(ctx.lib.s2v_resize(x_ptr, n, c, ih, iw, *x_strides, y_ptr, oh, ow, *y_strides, sh, sw, mode, ctx.stream),
-          "s2v_resize")
+    S2V.resize_(x, x_off, [n, c, ih, iw], list(x_strides), y, y_off, [n, c, oh, ow], list(y_strides), sh, sw, mode)
 
 
 def nhwc_strides(v: NHWC):
@@ -560,7 +630,7 @@ def nhwc_strides(v: NHWC):
 
 
 def resize_nhwc(ctx: Ctx, x: NHWC, y: NHWC, scale_factor=None, mode=0):
-    resize(ctx, x.ptr, (x.n, x.c, x.h, x.w), nhwc_strides(x), y.ptr, (y.h, y.w), nhwc_strides(y),
+    resize(ctx, x.t, x.coff, (x.n, x.c, x.h, x.w), nhwc_strides(x), y.t, y.coff, (y.h, y.w), nhwc_strides(y),
            scale_factor=scale_factor, mode=mode)
     return y
 
@@ -568,31 +638,25 @@ def resize_nhwc(ctx: Ctx, x: NHWC, y: NHWC, scale_factor=None, mode=0):
 def nchw_to_nhwc(ctx: Ctx, x: torch.Tensor, y: NHWC, size=None):
     """NCHW device tensor (any strides) -> NHWC view, optionally bilinear-resized to y's size."""
     _require_cuda(x, "nchw_to_nhwc")
-    n, c, h, w = x.shape
-    sn, sc, sy, sx = x.stride()
-    resize(ctx, x.data_ptr(), (n, c, h, w), (sn, sc, sy, sx), y.ptr, (y.h, y.w), nhwc_strides(y))
+    resize(ctx, x, 0, tuple(x.shape), x.stride(), y.t, y.coff, (y.h, y.w), nhwc_strides(y))
     return y
 
 
 def nhwc_to_nchw(ctx: Ctx, x: NHWC, out: torch.Tensor, crop=(0, 0)):
     """NHWC view (optionally cropped by (top, left) to out's H, W) -> contiguous NCHW tensor."""
     n, c, oh, ow = out.shape
-    base = x.ptr + F32 * (crop[0] * x.w + crop[1]) * x.cs
-    resize(ctx, base, (n, c, oh, ow), nhwc_strides(x), out.data_ptr(), (oh, ow), out.stride())
+    off = x.coff + (crop[0] * x.w + crop[1]) * x.cs
+    resize(ctx, x.t, off, (n, c, oh, ow), nhwc_strides(x), out, 0, (oh, ow), out.stride())
     return out
 
 
 def pad_reflect(ctx: Ctx, x: NHWC, y: NHWC, pads):
-    pt, pb, pl, pr = pads
-    check(ctx.lib.s2v_pad_reflect(x.ptr, x.n, x.h, x.w, x.c, x.cs, pt, pb, pl, pr, y.ptr, y.cs, ctx.stream),
-          "s2v_pad_reflect")
+    S2V.pad_reflect_(x.v, y.v, list(pads))
     return y
 
 
 def row_layernorm(ctx: Ctx, x: torch.Tensor, weight, bias, y: torch.Tensor, eps=1e-5):
-    rows, dim = x.shape
-    check(ctx.lib.s2v_row_layernorm(x.data_ptr(), rows, dim, x.stride(0), weight.data_ptr(), bias.data_ptr(), eps,
-                                    y.data_ptr(), y.stride(0), ctx.stream), "s2v_row_layernorm")
+    S2V.row_layernorm_(x, weight, bias, eps, y)
     return y
 
 
@@ -600,23 +664,18 @@ def attention(ctx: Ctx, q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: 
               tokens, dim_head=64, scale=None):
     """q, k, v, out: [batch*tokens, *] row views (row stride = stride(0)); head h = cols [64h, 64h+64)."""
     scale = dim_head ** -0.5 if scale is None else scale
-    check(ctx.lib.s2v_attention(q.data_ptr(), k.data_ptr(), v.data_ptr(), batch, heads, tokens, dim_head,
-                                q.stride(0), k.stride(0), v.stride(0), tokens * q.stride(0), tokens * k.stride(0),
-                                tokens * v.stride(0), scale, out.data_ptr(), out.stride(0), tokens * out.stride(0),
-                                ctx.stream), "s2v_attention")
+    S2V.attention_(q, k, v, out, batch, heads, tokens, dim_head, scale)
     return out
 
 
 def flow_warp(ctx: Ctx, flow: NHWC, src: torch.Tensor, y: NHWC):
     """flow: NHWC view with >= 2 channels (x, y); src: NCHW-strided device tensor."""
-    n, c, h, w = src.shape
-    check(ctx.lib.s2v_flow_warp(flow.ptr, flow.n, flow.h, flow.w, flow.cs, src.data_ptr(), c, h, w, *src.stride(),
-                                y.ptr, y.cs, ctx.stream), "s2v_flow_warp")
+    S2V.flow_warp_(flow.v, src, y.v)
     return y
 
 
 def fill(ctx: Ctx, t: torch.Tensor, value: float = 0.0):
-    check(ctx.lib.s2v_fill(t.data_ptr(), t.numel(), value, ctx.stream), "s2v_fill")
+    S2V.fill_value_(t, value)
     return t
 
 
@@ -628,17 +687,17 @@ def pad_cin(w: torch.Tensor, cin: int) -> torch.Tensor:
     return torch.cat([w, z], 1)
 
 
+def _i64(v: int) -> int:
+    """A 64-bit pattern as the signed int64 a torch op schema carries."""
+    v &= 2 ** 64 - 1
+    return v - 2 ** 64 if v >= 2 ** 63 else v
+
+
 def gaussian_noise(ctx: Ctx, out: torch.Tensor, seed: int, offset: int = 0, ctr: torch.Tensor | None = None,
                    shift: int = 40):
     """N(0,1) into ``out``; with a device counter ``ctr`` (int64 [1]) the stream offset advances by
     ctr << shift, read when the kernel runs (fresh draws on every graph replay)."""
-    if ctr is None:
-        check(ctx.lib.s2v_gaussian_noise(out.data_ptr(), out.numel(), seed & (2 ** 64 - 1), offset & (2 ** 64 - 1),
-                                         ctx.stream), "s2v_gaussian_noise")
-    else:
-        check(ctx.lib.s2v_gaussian_noise_ctr(out.data_ptr(), out.numel(), seed & (2 ** 64 - 1),
-                                             offset & (2 ** 64 - 1), ctr.data_ptr(), shift, ctx.stream),
-              "s2v_gaussian_noise_ctr")
+    S2V.gaussian_noise_(out, _i64(seed), _i64(offset), ctr, shift)
     return out
 
 
@@ -655,7 +714,7 @@ class NoiseCounter:
             if ctx.device.type == "cuda" and torch.cuda.is_current_stream_capturing():
                 raise _lib.S2VError("noise counter must be created by an eager run before graph capture")
             self.t = torch.zeros(1, dtype=torch.int64, device=ctx.device)
-        check(ctx.lib.s2v_counter_add(self.t.data_ptr(), 1, ctx.stream), "s2v_counter_add")
+        S2V.counter_add_(self.t, 1)
         return self.t
 
 
@@ -693,9 +752,7 @@ def fir2d(ctx: Ctx, x: NHWC, kernel: torch.Tensor, y: NHWC, *, up=1, down=1, pad
     """upfirdn2d on NHWC views (pad0 = (pad_y0, pad_x0); the far pads follow from y's size)
     with y = post * act(gain * fir + bias[c])."""
     assert x.n == y.n and x.c == y.c, "fir2d: batch / channel mismatch"
-    kh, kw = kernel.shape
-    check(ctx.lib.s2v_fir2d(x.ptr, x.n, x.h, x.w, x.c, x.cs, kernel.data_ptr(), kh, kw, up, down, pad0[0], pad0[1],
-                            y.ptr, y.h, y.w, y.cs, gain, _ptr(bias), act, alpha, post, ctx.stream), "s2v_fir2d")
+    S2V.fir2d_(x.v, kernel, y.v, up, down, pad0[0], pad0[1], gain, bias, act, alpha, post)
     return y
 
 
@@ -705,9 +762,7 @@ def eltwise(ctx: Ctx, x: NHWC, y: NHWC, *, a=1.0, mul: NHWC | None = None, add: 
     assert (x.n, x.h, x.w, x.c) == (y.n, y.h, y.w, y.c)
     for v in (mul, add):
         assert v is None or (v.n, v.h, v.w, v.c) == (x.n, x.h, x.w, x.c)
-    check(ctx.lib.s2v_eltwise(x.ptr, x.cs, None if mul is None else mul.ptr, 0 if mul is None else mul.cs,
-                              None if add is None else add.ptr, 0 if add is None else add.cs, _ptr(bias),
-                              x.n * x.h * x.w, x.c, a, act, alpha, post, y.ptr, y.cs, ctx.stream), "s2v_eltwise")
+    S2V.eltwise_(x.v, None if mul is None else mul.v, None if add is None else add.v, bias, a, act, alpha, post, y.v)
     return y
 
 
@@ -739,14 +794,11 @@ def fft_tables(h: int, w: int, device):
 
 def rfft2(ctx: Ctx, x: NHWC, tables: torch.Tensor, spec: torch.Tensor):
     """x NHWC [n,h,w,C] -> spec [n, h*(w//2+1), 2C] (channel = part*C + c), rfftn ortho."""
-    check(ctx.lib.s2v_rfft2(x.ptr, x.n, x.h, x.w, x.c, x.cs, tables.data_ptr(), spec.data_ptr(), spec.shape[-1],
-                            ctx.stream), "s2v_rfft2")
+    S2V.rfft2_(x.v, tables, spec)
     return spec
 
 
 def irfft2(ctx: Ctx, spec: torch.Tensor, tables: torch.Tensor, y: NHWC, res: NHWC | None = None):
     """spec [n, F, >=2C] -> y NHWC = irfftn(spec, s=(h, w), ortho) (+ res)."""
-    check(ctx.lib.s2v_irfft2(spec.data_ptr(), y.n, y.h, y.w, y.c, spec.shape[-1], tables.data_ptr(),
-                             None if res is None else res.ptr, 0 if res is None else res.cs, y.ptr, y.cs, ctx.stream),
-          "s2v_irfft2")
+    S2V.irfft2_(spec, tables, None if res is None else res.v, y.v)
     return y

@@ -18,7 +18,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from . import _lib, audio
+from . import audio, ops
 from .ops import Ctx
 
 
@@ -71,32 +71,35 @@ def shard_range(n: int, rank: int, world: int):
 
 # ----------------------------------------------------------------------------- device path
 class LipSyncPipeline:
-    """mel windows + DNet source frames + coefficient windows -> uint8 [n, 3, 384, 384] frames."""
+    """mel windows + DNet source frames + coefficient windows -> uint8 [n, 3, 384, 384] frames.
 
-    def __init__(self, dnet, enet, device="cuda", batch: int = 16, graph: bool = True):
+    Full batches replay captured HIP graphs on ``lanes`` execution lanes (runtime.LaneRunner):
+    batch k runs on lane k % lanes, on that lane's stream, so one batch's latency-bound LNet chain
+    overlaps the previous batch's MFMA-bound StyleConv decoder.  Each lane has its own workspaces,
+    side streams and noise counters (the models' per-lane ops.Ctx) and its own graph buffers."""
+
+    def __init__(self, dnet, enet, device="cuda", batch: int = 16, graph: bool = True, lanes: int = 2):
         self.dnet, self.enet = dnet, enet
         self.device = torch.device(device)
         self.batch = batch
         self.ctx = Ctx(self.device)
-        self.graph = graph          # full batches of ``run`` replay one captured HIP graph
+        self.graph = graph          # full batches of ``run`` replay captured HIP graphs
+        self.lanes = lanes
         self._runner = None
 
     @torch.no_grad()
-    def run_batch(self, mel: torch.Tensor, src: torch.Tensor, coeff: torch.Tensor, out_u8: torch.Tensor):
+    def run_batch(self, mel: torch.Tensor, src: torch.Tensor, coeff: torch.Tensor, out_u8: torch.Tensor,
+                  lane: int = 0):
         """mel [b,1,80,16], src [b,3,256,256] in [-1,1] (DNet input, trans_image layout), coeff
         [b,73,26] -> out_u8 [b,3,384,384] (RGB, NCHW)."""
         b, _, h, w = src.shape
-        fake = self.dnet(src, coeff)["fake_image"]
+        fake = self.dnet(src, coeff, lane=lane)["fake_image"]
         ref_u8 = torch.empty((b, 3, h, w), dtype=torch.uint8, device=self.device)
         face6 = torch.empty((b, 6, h, w), device=self.device)
         gt = torch.empty((b, 3, h, w), device=self.device)
-        src = src.contiguous()
-        _lib.check(self.ctx.lib.s2v_lipsync_inputs(src.data_ptr(), fake.data_ptr(), b, h, w,
-                                                   ref_u8.data_ptr(), face6.data_ptr(), gt.data_ptr(),
-                                                   self.ctx.stream), "s2v_lipsync_inputs")
-        pred, _ = self.enet(mel, face6, gt)
-        _lib.check(self.ctx.lib.s2v_to_u8(pred.data_ptr(), pred.numel(), 0.0, 1.0, 255.0, 0.0, out_u8.data_ptr(),
-                                          self.ctx.stream), "s2v_to_u8")
+        ops.S2V.lipsync_inputs_(src.contiguous(), fake, ref_u8, face6, gt)
+        pred, _ = self.enet(mel, face6, gt, lane=lane)
+        ops.S2V.to_u8_(pred, out_u8, 0.0, 1.0, 255.0, 0.0)             # inference.py:267, :288
         return out_u8
 
     @torch.no_grad()
@@ -110,23 +113,32 @@ class LipSyncPipeline:
             raise ValueError(f"frames [{start}, {stop}) need {n} src frames / coefficient windows and "
                              f"mel windows up to {stop} (got {src.shape[0]}, {coeffs.shape[0]}, {mel_chunks.shape[0]})")
         out = torch.empty((n, 3, 384, 384), dtype=torch.uint8, device=self.device)
+        runner = None
         for b0 in range(0, n, self.batch):
             b1 = min(n, b0 + self.batch)
             m, s, c = mel_chunks[start + b0: start + b1], src[b0:b1], coeffs[b0:b1]
             if self.graph and b1 - b0 == self.batch:
-                out[b0:b1].copy_(self._graph_runner(m, s, c)(m, s, c))
+                runner = self._graph_runner(m, s, c)
+                dst = out[b0:b1]
+                runner(m, s, c, out_fn=lambda o, d=dst: d.copy_(o))
+                out.record_stream(runner.streams[(runner.k - 1) % runner.lanes])
             else:
+                if runner is not None:
+                    runner.join()                 # the eager batch uses lane 0's workspaces
                 self.run_batch(m, s, c, out[b0:b1])
+        if runner is not None:
+            runner.join()
         return out
 
     def _graph_runner(self, m, s, c):
-        """One captured run_batch for full batches (~2,000 launches -> one graph replay); inputs are
-        copied into its static buffers, the uint8 frames read from its static output."""
+        """Captured run_batch per lane for full batches (~2,000 launches -> one graph replay each);
+        inputs are copied into a lane's static buffers, its uint8 frames read from its static output."""
         if self._runner is None:
-            from .runtime import GraphRunner
-            buf = torch.empty((self.batch, 3, 384, 384), dtype=torch.uint8, device=self.device)
-            self._runner = GraphRunner(lambda mm, ss, cc: self.run_batch(mm, ss, cc, buf),
-                                       [m.contiguous(), s.contiguous(), c.contiguous()], warmup=1)
+            from .runtime import LaneRunner
+            bufs = [torch.empty((self.batch, 3, 384, 384), dtype=torch.uint8, device=self.device)
+                    for _ in range(self.lanes)]
+            self._runner = LaneRunner(lambda lane, mm, ss, cc: self.run_batch(mm, ss, cc, bufs[lane], lane=lane),
+                                      [m.contiguous(), s.contiguous(), c.contiguous()], lanes=self.lanes, warmup=1)
         return self._runner
 
 
@@ -154,29 +166,34 @@ def broadcast_tensor(t: torch.Tensor | None, shape, dtype, device, src: int = 0)
 
 def gather_frames(local: torch.Tensor, n_total: int, dst: int = 0):
     """Gather contiguous frame shards (shard_range layout) to ``dst``; returns [n_total, ...] on
-    dst, None elsewhere.  Uses all_gather_into_tensor on equal, padded shards."""
+    dst, None elsewhere (a gather to rank 0, not an all-gather).
+
+    Only ``dst`` allocates the whole clip: it copies its own shard into place and posts one
+    point-to-point receive per peer straight into that peer's frame range of the output (no padding,
+    no concatenation); every other rank sends its shard once and receives nothing.  Over RCCL the
+    receives run concurrently on dst's xGMI links (each peer's ~55 MB of a 1000-frame clip on its own
+    link); gloo carries the same calls on the CPU."""
     import torch.distributed as dist
     rank, world = _dist()
     if world == 1:
         return local
-    per = (n_total + world - 1) // world
-    pad = torch.zeros((per,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-    pad[: local.shape[0]] = local
-    full = torch.empty((per * world,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-    if local.dtype == torch.uint8 and local.device.type == "cpu":
-        # gloo has no uint8 all_gather_into_tensor: gather as a list
-        parts = [torch.empty_like(pad) for _ in range(world)]
-        dist.all_gather(parts, pad)
-        full = torch.cat(parts, 0)
-    else:
-        dist.all_gather_into_tensor(full, pad)
+    s, e = shard_range(n_total, rank, world)
+    if local.shape[0] != e - s:
+        raise ValueError(f"gather_frames: rank {rank} holds {local.shape[0]} frames, its range [{s}, {e}) has {e - s}")
     if rank != dst:
+        if e > s:
+            dist.send(local.contiguous(), dst)
         return None
-    pieces = []
+    out = torch.empty((n_total,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    out[s:e].copy_(local)
+    ops = []
     for r in range(world):
-        s, e = shard_range(n_total, r, world)
-        pieces.append(full[r * per: r * per + (e - s)])
-    return torch.cat(pieces, 0)
+        rs, re_ = shard_range(n_total, r, world)
+        if r != dst and re_ > rs:
+            ops.append(dist.P2POp(dist.irecv, out[rs:re_], r))
+    for w in dist.batch_isend_irecv(ops) if ops else []:
+        w.wait()
+    return out
 
 
 def run_sharded(pipeline: LipSyncPipeline, wav, semantic, expression, src_provider, fps: float = 25.0,

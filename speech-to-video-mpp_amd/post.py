@@ -185,7 +185,7 @@ class FaceParse:
         x4 = NHWC.empty(b, self.size, self.size, 4, self.device)
         ops.fill(ctx, x4.t)
         sn, sc, sy, sx = imt.stride()                           # flip(1): channel 2 first, stride -sc
-        ops.resize(ctx, imt.data_ptr() + 4 * 2 * sc, (b, 3, h, w), (sn, -sc, sy, sx), x4.ptr,
+        ops.resize(ctx, imt, 2 * sc, (b, 3, h, w), (sn, -sc, sy, sx), x4.t, 0,
                    (self.size, self.size), ops.nhwc_strides(x4.slice(0, 3)), mode=1)
         ops.eltwise(ctx, x4.slice(0, 3), x4.slice(0, 3), a=2.0, bias=torch.full((3,), -1.0, device=self.device))
         m = parse_mask(eng.mask_logits(ctx, x4), self.MASK_COLORMAP)

@@ -12,8 +12,9 @@ Drop-ins for the reference's only native FFI (GPEN's JIT-built pybind11 extensio
 
 plus the module-level ``fused_leaky_relu`` / ``upfirdn2d`` with the device-branch semantics of
 op/fused_act.py:92-96 and op/upfirdn2d.py:149-157 (forward / inference only, like the engines),
-and the model-path ops ``torch.ops.s2v.{conv2d_nhwc, layernorm2d, instnorm_adain, attention, rfft2,
-irfft2, resize_bilinear, flow_warp, mel_spectrogram}``.
+the functional model-path ops ``torch.ops.s2v.{conv2d_nhwc, layernorm2d, instnorm_adain, attention,
+rfft2, irfft2, resize_bilinear, flow_warp, mel_spectrogram}``, and the in-place launch ops
+(LAUNCH_OPS) through which the engines dispatch every kernel of the model forwards.
 """
 from __future__ import annotations
 
@@ -27,6 +28,12 @@ from . import _lib
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libs2v_torch.so")
 OPS = ("fused_bias_act", "upfirdn2d", "conv2d_nhwc", "layernorm2d", "instnorm_adain", "attention", "rfft2", "irfft2",
        "resize_bilinear", "flow_warp", "mel_spectrogram")
+# the launch ops every kernel of the model forwards is dispatched through (csrc/torch_launch.cpp,
+# called by s2v_amd.ops): in-place on caller-owned views, capturable
+LAUNCH_OPS = ("conv2d_", "modulated_conv2d_", "gemm_kn_", "split_weights_", "split_act_", "layernorm2d_", "instnorm_",
+              "adain_params_", "modconv_demod_", "row_layernorm_", "attention_", "resize_", "pad_reflect_",
+              "flow_warp_", "fill_value_", "gaussian_noise_", "counter_add_", "rfft2_", "irfft2_", "eltwise_", "fir2d_",
+              "lipsync_inputs_", "to_u8_", "mel_chunks_", "melspectrogram_")
 _lock = threading.Lock()
 _loaded = False
 

@@ -149,3 +149,21 @@ def test_glds_512x128_tile(ctx, sprec, case):
         test_glds_conv_matches_x3_kernel(ctx, sprec, case)
     finally:
         ops.tune(ctx, ops.TUNE_GLDS_TILE, prev)
+
+
+def test_split_input_of_another_precision_raises(ctx, sprec):
+    """A tensor split in one precision is not read as the other's halves (bf16 vs f16 layout)."""
+    x = NHWC.empty(1, 8, 8, 32, DEV)
+    xs = ops.split_act(ctx, x)
+    other = "f16x3" if sprec == "bf16x3" else "bf16x3"
+    y = NHWC.empty(1, 8, 8, 32, DEV)
+    cw = ConvW(torch.randn(32, 32, 3, 3), None, DEV, padding=1)
+    prev = ops.set_precision(other)
+    try:
+        with pytest.raises(ops._lib.S2VError, match="split layout"):
+            ops.conv2d(ctx, xs, cw, y)
+        ops.set_precision("f32")
+        with pytest.raises(ops._lib.S2VError, match="split layout"):
+            ops.conv2d(ctx, xs, cw, y)
+    finally:
+        ops.set_precision(prev)

@@ -1,7 +1,9 @@
-"""Dry run of every engine's host plan on CPU: the libs2v entry points are replaced by no-ops
-that only validate their argument counts, so the shape / view / slice bookkeeping of each
-forward (every NHWC assertion in ops.py) runs without a GPU.  Nothing is computed — numerics are
-the gpu-marked tests' job; this catches plumbing errors before a GPU box is spent on them."""
+"""Dry run of every engine's host plan on CPU: the ``torch.ops.s2v`` launch ops and the libs2v
+entry points are replaced by no-ops that validate their arguments against the registered op
+schemas (count, tensor-ness, int lists) / the C ABI's argument counts, so the shape / view / slice
+bookkeeping of each forward (every NHWC assertion in ops.py) runs without a GPU.  Nothing is
+computed — numerics are the gpu-marked tests' job; this catches plumbing errors before a GPU box is
+spent on them."""
 import ctypes
 
 import pytest
@@ -28,13 +30,42 @@ class _NoLib:
         return fn
 
 
+class _NoOps:
+    """Stand-in for torch.ops.s2v: each call is checked against the real op's schema."""
+
+    def __init__(self, calls):
+        from s2v_amd import torch_ops
+        self.ns = torch_ops.load()
+        self.calls = calls
+
+    def __getattr__(self, name):
+        schema = getattr(self.ns, name).default._schema
+        args = schema.arguments
+
+        def fn(*a):
+            assert len(a) == len(args), f"{name}: {len(a)} args, schema has {len(args)}"
+            for v, arg in zip(a, args):
+                t = str(arg.type)
+                if t == "Tensor":
+                    assert isinstance(v, torch.Tensor), f"{name}.{arg.name}: tensor expected, got {type(v)}"
+                elif t == "Optional[Tensor]":
+                    assert v is None or isinstance(v, torch.Tensor), f"{name}.{arg.name}: tensor or None"
+                elif t.startswith("List[int]"):
+                    assert isinstance(v, (list, tuple)) and all(isinstance(i, int) for i in v), f"{name}.{arg.name}"
+                elif t == "int":
+                    assert isinstance(v, int), f"{name}.{arg.name}: int expected, got {type(v)}"
+            self.calls[name] = self.calls.get(name, 0) + 1
+            ret = str(schema.returns[0].type) if schema.returns else ""
+            return [0] * 11 if ret.startswith("List") else 0 if ret == "int" else None
+        return fn
+
+
 @pytest.fixture
 def dry(monkeypatch):
     lib = _NoLib()
+    monkeypatch.setattr(ops, "S2V", _NoOps(lib.calls))
     monkeypatch.setattr(ops, "_require_cuda", lambda t, what: None)
-    monkeypatch.setattr(ops.Ctx, "__init__", lambda self, device: (setattr(self, "device", torch.device(device)),
-                                                                   setattr(self, "ws", ops.Workspace(device)),
-                                                                   setattr(self, "lib", lib))[0])
+    monkeypatch.setattr(ops._lib, "load", lambda: lib)
     monkeypatch.setattr(ops.Ctx, "stream", property(lambda self: ctypes.c_void_p(0)))
     return lib
 
@@ -47,7 +78,7 @@ def test_gfpgan_plan(dry):
     for rn in (True, False):
         _, rgbs = eng.forward(ops.Ctx("cpu"), x, out, return_rgb=True, randomize_noise=rn)
     assert [r.shape[-1] for r in rgbs] == [8, 16, 32, 64, 128, 256, 512]
-    assert dry.calls["s2v_conv2d"] > 120 and dry.calls["s2v_eltwise"] == 2 * 14
+    assert dry.calls.get("modulated_conv2d_", 0) + dry.calls["conv2d_"] > 120 and dry.calls["eltwise_"] == 2 * 14
 
 
 def test_gpen_plan(dry):
@@ -55,7 +86,7 @@ def test_gpen_plan(dry):
     eng = GPENEngine(synth_sd("gpen"), "cpu")
     x = torch.zeros(2, 3, 512, 512)
     eng.forward(ops.Ctx("cpu"), x, torch.empty_like(x))
-    assert dry.calls["s2v_fir2d"] == 7 + 7 + 7 and dry.calls["s2v_eltwise"] == 15
+    assert dry.calls["fir2d_"] == 7 + 7 + 7 and dry.calls["eltwise_"] == 15
 
 
 def test_lipsync_engines_plan(dry):
@@ -79,4 +110,4 @@ def test_parsenet_plan(dry):
     x = torch.zeros(2, 3, 512, 512)
     eng.forward(ops.Ctx("cpu"), x, torch.empty(2, 19, 512, 512), torch.empty(2, 3, 512, 512))
     # encoder conv + 4 down blocks (3 convs) + 10 body blocks (2) + 4 up blocks (3) + 2 heads
-    assert dry.calls["s2v_conv2d"] == 1 + 12 + 20 + 12 + 2 and dry.calls["s2v_eltwise"] == 1
+    assert dry.calls["conv2d_"] == 1 + 12 + 20 + 12 + 2 and dry.calls["eltwise_"] == 1

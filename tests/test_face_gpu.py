@@ -88,6 +88,27 @@ def test_mask_postprocess_and_blur_bit_exact():
     assert np.array_equal(got, OF.gaussian_blur(x32, 31, 4.0))
 
 
+def test_mask_sharp_keeps_the_zeroed_border():
+    """face_enhancement.py:144-150: mask_postprocess zeroes a 26-px border of mask_sharp in place
+    before mask_sharp is resized and warped; the device's mask_sharp (s2v_u8_div255_f64_border) must
+    carry that border too, for a parse mask that reaches the crop edge."""
+    from s2v_amd import _lib, face
+    g = np.random.default_rng(7)
+    m = np.zeros((512, 512), np.uint8)
+    m[g.random((512, 512)) < 0.5] = 255
+    m[:, :3] = 255                                    # face region touching every crop edge
+    m[-2:, :] = 255
+    exp = m / 255.
+    OF.mask_postprocess(exp)                          # mutates exp like the reference's mask_sharp
+    assert exp[:26].max() == 0 and exp[:, -26:].max() == 0 and exp[26:-26, 26:-26].max() == 1.0
+    src = torch.from_numpy(m).to(DEV)
+    got = torch.empty((512, 512), dtype=torch.float64, device=DEV)
+    lib = _lib.load()
+    _lib.check(lib.s2v_u8_div255_f64_border(src.data_ptr(), 512, 512, face.MASK_BORDER, got.data_ptr(),
+                                            torch.cuda.current_stream().cuda_stream), "div255_border")
+    assert np.array_equal(got.cpu().numpy(), exp)
+
+
 def test_filter2d_and_gan_conversions_bit_exact():
     from s2v_amd import face
     img = rng_u8(4, (33, 47, 3))

@@ -155,3 +155,13 @@ def test_face_entry_points_reject_bad_arguments():
     assert b"level 2" in lib.s2v_last_error()
     assert lib.s2v_gaussian_blur(p(img), 0, 8, 8, 0, p(M), 4, p(out), 1, 2, p(out), 1 << 20, None) == -1   # even ksize
     assert lib.s2v_maxpool2d_nhwc(p(cand), 1, 8, 8, 6, 3, 2, 1, p(cand), 4, 4, None) == -1                 # c % 4
+
+
+def test_mask_postprocess_mutates_mask_sharp_in_place():
+    """face_enhancement.py:83-85: mask[:thres] = 0 ... act on the caller's mask_sharp array, which
+    the reference then resizes and warps (:144-150); the restatement must do the same."""
+    ms = np.ones((80, 80))
+    out = face.mask_postprocess(ms, thres=26)
+    assert out.dtype == np.float32
+    assert ms[:26].max() == 0 and ms[-26:].max() == 0 and ms[:, :26].max() == 0 and ms[:, -26:].max() == 0
+    assert ms[26:-26, 26:-26].min() == 1.0

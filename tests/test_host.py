@@ -273,8 +273,12 @@ def test_torch_custom_ops_registered_hip_only():
     the GPEN drop-ins, and a CPU tensor raises (no CPU kernel, no fallback)."""
     from s2v_amd import torch_ops
     ns = torch_ops.load()
-    for name in torch_ops.OPS:
+    for name in torch_ops.OPS + torch_ops.LAUNCH_OPS:
         assert hasattr(ns, name), name
+    for name in torch_ops.LAUNCH_OPS:           # launch ops mutate caller-owned outputs
+        assert "(a!)" in str(getattr(ns, name).default._schema), name
+    with pytest.raises(NotImplementedError):
+        ns.fill_value_(torch.zeros(4), 1.0)
     assert str(ns.fused_bias_act.default._schema) == (
         "s2v::fused_bias_act(Tensor input, Tensor bias, Tensor refer, int act, int grad, float alpha, "
         "float scale) -> Tensor")

@@ -88,8 +88,6 @@ def test_lnet_intermediates(prec, lnet, golden):
     eng.forward(ctx, torch.from_numpy(mel).to(DEV), x6, out, logits=logits)
     lg = logits.t.permute(0, 3, 1, 2).cpu()
     within(lg, g["logits"], TOL[prec]["logits"], "logits")
-    z = eng.bank  # audio feature is the bank's input; compare via the stored params' source
-    assert z.params.shape == (2, z.total)
 
 
 def test_lnet_5d_input_fold(lnet):

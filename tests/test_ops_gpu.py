@@ -354,7 +354,7 @@ def test_instnorm_adain(ctx, c):
         gb = torch.cat([g, bt], 1).float().to(DEV)
         res = rnd(2, c, h, w, seed=20)
         y = NHWC.empty(2, h, w, c, DEV)
-        ops.instnorm(ctx, nhwc(x.float()), y, gb.data_ptr(), gb.data_ptr() + 4 * c, 2 * c, act=ops.ACT_LRELU,
+        ops.instnorm(ctx, nhwc(x.float()), y, gb[:, :c], gb[:, c:], act=ops.ACT_LRELU,
                      alpha=0.01, res=nhwc(res.float()))
         ref = F.leaky_relu(F.instance_norm(x, eps=1e-5) * (1 + g[:, :, None, None]) + bt[:, :, None, None], 0.01) + res
         assert (to_nchw(y) - ref).abs().max() < 2e-5
@@ -363,7 +363,7 @@ def test_instnorm_adain(ctx, c):
             # values as y, laid out as F.pad(y, (1, 1, 1, 1), 'reflect'); y itself unchanged
             y2 = NHWC.empty(2, h, w, c, DEV)
             yp = NHWC(torch.full((2, h + 2, w + 2, c), float("nan"), device=DEV))
-            ops.instnorm(ctx, nhwc(x.float()), y2, gb.data_ptr(), gb.data_ptr() + 4 * c, 2 * c, act=ops.ACT_LRELU,
+            ops.instnorm(ctx, nhwc(x.float()), y2, gb[:, :c], gb[:, c:], act=ops.ACT_LRELU,
                          alpha=0.01, res=nhwc(res.float()), pad_out=yp)
             assert torch.equal(y2.t, y.t)
             exp = F.pad(y.t.permute(0, 3, 1, 2), (1, 1, 1, 1), mode="reflect").permute(0, 2, 3, 1)
@@ -638,7 +638,7 @@ def test_instnorm_fused_small_planes(ctx):
         try:
             y = NHWC.empty(n, h, w, c, DEV)
             yp = NHWC.empty(n, h + 2, w + 2, c, DEV)
-            ops.instnorm(ctx, nhwc(x.float()), y, gb.data_ptr(), gb.data_ptr() + 4 * c, 2 * c, act=ops.ACT_LRELU,
+            ops.instnorm(ctx, nhwc(x.float()), y, gb[:, :c], gb[:, c:], act=ops.ACT_LRELU,
                          alpha=0.01, res=nhwc(res.float()), pad_out=yp)
             outs[fused] = (y.t.clone(), yp.t.clone())
         finally:

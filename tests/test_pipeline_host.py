@@ -79,14 +79,23 @@ def _worker(rank, world, port, n, q):
         # per-frame stand-in for the device path: frame i -> constant (i % 251)
         local = torch.stack([torch.full((3, 4, 4), i % 251, dtype=torch.uint8) for i in range(s, e)]) \
             if e > s else torch.zeros((0, 3, 4, 4), dtype=torch.uint8)
+        if rank != 0:
+            # the gather is rank-0 only: no other rank receives or allocates the clip
+            def refuse(*a, **k):
+                raise AssertionError(f"rank {rank} must not receive frames")
+            dist.recv = dist.irecv = dist.all_gather = dist.all_gather_into_tensor = refuse
         full = P.gather_frames(local, n)
         if rank == 0:
+            ref = torch.stack([torch.full((3, 4, 4), i % 251, dtype=torch.uint8) for i in range(n)])
+            assert full.shape == (n, 3, 4, 4) and torch.equal(full, ref)      # == the world-1 result
             q.put([int(full[i, 0, 0, 0]) for i in range(n)])
+        else:
+            assert full is None
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n", [7, 16])
+@pytest.mark.parametrize("n", [7, 16, 1])
 def test_broadcast_and_gather_world2_gloo(n):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--cout", type=int, default=128)
     ap.add_argument("--k", type=int, default=3)
     ap.add_argument("--stride", type=int, default=1)
+    ap.add_argument("--pad", type=int, default=-1, help="padding (default k // 2)")
     ap.add_argument("--up2", action="store_true", help="nearest-x2 upsampled input (IN_NEAREST_UP2)")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--sweep", action="store_true")
@@ -40,7 +41,7 @@ def main():
     dev = torch.device("cuda")
     ctx = ops.Ctx(dev)
     w = torch.randn(a.cout, a.cin, a.k, a.k) / math.sqrt(a.cin * a.k * a.k)
-    cw = ConvW(w, torch.randn(a.cout), dev, stride=a.stride, padding=a.k // 2,
+    cw = ConvW(w, torch.randn(a.cout), dev, stride=a.stride, padding=a.k // 2 if a.pad < 0 else a.pad,
                in_mode=ops.IN_NEAREST_UP2 if a.up2 else ops.IN_DIRECT)
     x = NHWC(torch.randn(a.n, a.h, a.w, a.cin, device=dev))
     oh, ow = cw.out_hw(a.h, a.w)
