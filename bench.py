@@ -4,7 +4,7 @@
 Workload (one "step"): ENet(+LNet) forward — models/ENet.py:82-139 — on one batch of B=16
 synthetic 256x256 face crops + 16 mel windows [1,80,16] (inference.py:393-399 batching,
 LNet_batch_size 16), weights from the portable synthetic checkpoint (s2v_amd.synth), inputs
-resident in HBM.  The whole forward is one HIP-graph replay; with ``--lanes L`` (default 2) the steps
+resident in HBM.  The whole forward is one HIP-graph replay; with ``--lanes L`` (default 1) the steps
 alternate between L captured lanes (runtime.LaneRunner: separate buffers, workspaces and streams,
 shared read-only weights), so batch k+1's latency-bound LNet head overlaps batch k's MFMA-bound
 StyleConv tail.  Every step still runs the whole forward of its own batch.
@@ -78,7 +78,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=0, help="0 = the workload's default (16, or 4 for enhance)")
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--lanes", type=int, default=2,
+    ap.add_argument("--lanes", type=int, default=1,
                     help="execution lanes: consecutive steps replay captured graphs on this many lanes, each on its "
                          "own stream (runtime.LaneRunner); 1 = every step on one stream")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -883,6 +883,8 @@ def worker(args):
         if not args.no_graph:
             stamper = Stamper(pre["kernel"], pre["launches"], args.warmup + args.steps + 2 * args.lanes + 4, dev)
     elapsed = timed(args.precision, stamper)
+    if cuda:
+        ops.check_all_ranges(args.workload)     # f16x3 range guard: raises if a timed launch overflowed
     units = wl.units_per_step(world) * args.steps
     value = units / elapsed
     config = dict(wl.config)

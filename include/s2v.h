@@ -131,6 +131,14 @@ typedef struct s2v_conv_params {
     unsigned long long *stamps;
     const unsigned long long *stamp_ctr;
     int stamp_slot, stamp_stride, stamp_reps;
+    /* activation range of the split precisions (f16x3: f16 halves cover |v| < 65504, lo halves lose
+     * precision below 2^-3): the implicit-GEMM x3 kernels multiply the A operand by ``x_scale`` (a
+     * power of two, 0 means 1; the epilogue divides it out exactly) before splitting it, and when
+     * ``nonfinite`` is set, a launch whose accumulators hold a non-finite value sets *nonfinite = 1
+     * (a range overflow is never silent).  The host picks x_scale per layer from the input's max |v|
+     * (s2v_amax). */
+    float x_scale;
+    int *nonfinite;
 } s2v_conv_params;
 
 enum { S2V_PREC_F32 = 0, S2V_PREC_BF16X3 = 1, S2V_PREC_F16X3 = 2 };
@@ -163,6 +171,10 @@ int s2v_conv2d_plan(const s2v_conv_params *p, int *out10);
 enum { S2V_TUNE_HALO_MIN_BLOCKS = 0, S2V_TUNE_GLDS_TILE = 1, S2V_TUNE_SMALLK_TILE = 2, S2V_TUNE_X3_RATE_512 = 3,
        S2V_TUNE_IN_FUSED = 4, S2V_TUNE_COUNT = 5 };
 int s2v_tune(int key, long long value, long long *old_value);
+
+/* max |x| over an NHWC view (pixels x c at pitch xcs) -> *out (fp32 bits; NaN propagates as the
+ * largest value).  *out must be 0 before the launch (the kernel folds with an atomic max). */
+int s2v_amax(const float *x, long long pixels, int c, int xcs, float *out, s2v_stream_t stream);
 
 /* Split packed fp32 weights [rows][kpad] (kpad % 32 == 0) into the layout of ``prec``
  * (S2V_PREC_BF16X3 / S2V_PREC_F16X3): [rows][kpad/32][hi 32 | lo 32] 16-bit (same byte size),
@@ -320,7 +332,8 @@ int s2v_counter_add(unsigned long long *ctr, unsigned long long inc, s2v_stream_
 /* Full-clip pipeline glue.  DNet fake [n,3,h,w] in [-1,1] -> uint8 reference frames
  * (preprocessing/facing.py:190-191) and the ENet inputs built from them and the original crops src
  * (inference.py:393-399): face6 = [masked original | ref] / 255 (rows >= h/2 of the original zeroed),
- * gt = ref / 255.  All NCHW. */
+ * gt = ref / 255.  All NCHW.  fake NULL: ref_u8 is an input (the references a Step-5 enhancer replaced,
+ * inference.py:234-238) and only face6 / gt are written. */
 int s2v_lipsync_inputs(const float *src, const float *fake, int n, int h, int w, unsigned char *ref_u8,
                        float *face6, float *gt, s2v_stream_t stream);
 /* y = uint8((clamp(x, lo, hi) + offset) * scale) with truncation (inference.py:267, :288). */

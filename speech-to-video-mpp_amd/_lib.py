@@ -48,6 +48,7 @@ class ConvParams(ctypes.Structure):
         ("x_split", _c_int),
         ("stamps", _vp), ("stamp_ctr", _vp), ("stamp_slot", _c_int), ("stamp_stride", _c_int),
         ("stamp_reps", _c_int),
+        ("x_scale", _c_float), ("nonfinite", _vp),
     ]
 
 
@@ -89,6 +90,7 @@ _SIGS = {
     "s2v_irfft2": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_int, _vp, _c_int, _vp]),
     "s2v_split_weights": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_float, _vp, _vp]),
     "s2v_split_act": (_c_int, [_vp, _c_ll, _c_int, _c_int, _c_int, _vp, _c_int, _vp]),
+    "s2v_amax": (_c_int, [_vp, _c_ll, _c_int, _c_int, _vp, _vp]),
     "s2v_split_weights_x3": (_c_int, [_vp, _c_int, _c_int, _vp, _vp]),
     "s2v_modulate_weights_split": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp, _c_int,
                                             _c_int, _c_int, _c_float, _vp, _vp]),

@@ -1095,6 +1095,13 @@ static Plan make_plan(const s2v_conv_params *p_in, int M, int K) {
 
 static int validate(const s2v_conv_params *p, int &M, int &K) {
     S2V_REQUIRE(p && p->x && p->y, "conv2d: null pointer");
+    {
+        int e;
+        S2V_REQUIRE(p->x_scale == 0.f || (p->x_scale > 0.f && std::frexp(p->x_scale, &e) == 0.5f),
+                    "conv2d: x_scale must be 0 or a positive power of two, got %g", p->x_scale);
+        S2V_REQUIRE(!p->x_split || p->x_scale == 0.f || p->x_scale == 1.f,
+                    "conv2d: split-layout inputs carry no x_scale (split them already scaled)");
+    }
     S2V_REQUIRE(!p->stamps || (p->stamp_ctr && p->stamp_reps > 0 && p->stamp_slot >= 0 &&
                                p->stamp_slot < p->stamp_stride),
                 "conv2d: launch stamps need stamp_ctr, stamp_reps > 0 and 0 <= stamp_slot < stamp_stride");
@@ -1197,6 +1204,12 @@ static ConvArgs make_args(const s2v_conv_params *p, int M, int K, const Plan &pl
     a.pool = p->out_pool != 0;
     a.stamps = p->stamps; a.stamp_ctr = p->stamp_ctr; a.stamp_slot = p->stamp_slot;
     a.stamp_stride = p->stamp_stride; a.stamp_reps = p->stamp_reps > 0 ? p->stamp_reps : 1;
+    a.x_scale = 1.f;
+    a.nonfinite = p->nonfinite;
+    if (tiled_x3(p) && !p->b_kn && !p->x_split && p->x_scale > 0.f && p->x_scale != 1.f) {
+        a.x_scale = p->x_scale;
+        a.acc_scale /= p->x_scale;
+    }
     return a;
 }
 

@@ -42,6 +42,8 @@ struct ConvArgs {
     unsigned long long *stamps;            // launch timer (s2v_conv_params.stamps), or null
     const unsigned long long *stamp_ctr;
     int stamp_slot, stamp_stride, stamp_reps;
+    float x_scale;          // split-precision A operand pre-scale (power of two; 1 = none)
+    int *nonfinite;         // set to 1 when an accumulator is non-finite (or null)
 };
 
 // Launch timer: block start (atomic min) / end (atomic max) of the device real-time clock into the

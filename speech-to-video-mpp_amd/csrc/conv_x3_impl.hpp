@@ -418,8 +418,12 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3(ConvArgs a) {
                         prologue4<AR8, AMODE>(a, R, j, rc[p][u] + 4, ra[p][u][2 * j + 1]);
                     }
                 }
-                store_a8_x3<AR8, NT, ELT>(sb, tid, ra[p][u]);
             }
+            if (a.x_scale != 1.f) {            // activation range pre-scale (exact: a power of two)
+#pragma unroll
+                for (int j = 0; j < AR; ++j) ra[p][u][j] *= a.x_scale;
+            }
+            if constexpr (A8) store_a8_x3<AR8, NT, ELT>(sb, tid, ra[p][u]);
             else store_a_x3<AR, RS, ELT>(sb, tid, ra[p][u]);
             if constexpr (BKN) store_b_kn_x3<BN, BKR, ELT>(sb + BM * 128, tid, rbk[p][u]);
             else store_b_x3<BR, RS>(sb + BM * 128, tid, rbp[p][u]);
@@ -544,6 +548,16 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3(ConvArgs a) {
     }
     if constexpr (M16) {
         // stage the 16x16 accumulators (col = lane & 15, row = 4 (lane >> 4) + r) chunk by chunk
+        if (a.nonfinite) {                     // range guard: any non-finite accumulator flags the launch
+            bool bad = false;
+#pragma unroll
+            for (int i = 0; i < TM16; ++i)
+#pragma unroll
+                for (int j = 0; j < TN16; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) bad |= !__builtin_isfinite(acc4[i][j][r]);
+            if (bad) __hip_atomic_store(a.nonfinite, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         epilogue_tile_fn<BM, BN, NW, CH>(a, (float *)smem, tid, m0, n0, bz, bidx, [&](float *Cs, int c0) {
             constexpr int LDC = BN + 4;
 #pragma unroll

@@ -550,7 +550,7 @@ __global__ __launch_bounds__(256) void gaussian_kernel(float *__restrict__ y, lo
 // truncation like numpy's float->uint8 cast) and the ENet inputs built from it (inference.py:
 // 393-399: lower half of the original crop zeroed, [masked | ref] / 255; gt = ref).
 __global__ __launch_bounds__(256) void lipsync_inputs_kernel(const float *__restrict__ src, const float *__restrict__ fake,
-                                                            int n, int h, int w, unsigned char *__restrict__ ref_u8,
+                                                            int n, int h, int w, unsigned char *ref_u8,
                                                             float *__restrict__ face6, float *__restrict__ gt) {
     const long long plane = (long long)h * w;
     const long long total = (long long)n * 3 * plane;
@@ -559,9 +559,14 @@ __global__ __launch_bounds__(256) void lipsync_inputs_kernel(const float *__rest
         const int c = (int)((e / plane) % 3);
         const int b = (int)(e / (3 * plane));
         const int y = (int)(p / w);
-        float f = fminf(fmaxf(fake[e], -1.f), 1.f);
-        const unsigned char q = (unsigned char)((f + 1.f) * 0.5f * 255.f);
-        ref_u8[e] = q;
+        unsigned char q;
+        if (fake) {
+            const float f = fminf(fmaxf(fake[e], -1.f), 1.f);
+            q = (unsigned char)((f + 1.f) * 0.5f * 255.f);
+            ref_u8[e] = q;
+        } else {
+            q = ref_u8[e];                     // references given (enhanced by a Step-5 hook)
+        }
         const float r = (float)q / 255.f;
         // original crop as uint8 then /255 (the reference reads frames as uint8)
         float s = fminf(fmaxf(src[e], -1.f), 1.f);
@@ -629,6 +634,26 @@ __global__ __launch_bounds__(256) void eltwise4_kernel(const float *__restrict__
 
 __global__ __launch_bounds__(256) void fill_kernel(float *__restrict__ y, long long n, float v) {
     for (long long e = blockIdx.x * 256LL + threadIdx.x; e < n; e += (long long)gridDim.x * 256) y[e] = v;
+}
+
+// max |x| of an NHWC view (the split precisions' per-layer activation range, conv x_scale): a wave
+// max per block, one atomic max on the fp32 bits (non-negative floats order as unsigned ints; a NaN
+// has the largest bits, so it propagates)
+__global__ __launch_bounds__(256) void amax_kernel(const float *__restrict__ x, long long pixels, int c, int xcs,
+                                                   unsigned *__restrict__ out) {
+    const long long total = pixels * c;
+    unsigned mb = 0;
+    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+        const long long p = e / c;
+        const unsigned b = __float_as_uint(fabsf(x[p * xcs + (e - p * c)]));
+        mb = b > mb ? b : mb;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned t = __shfl_xor(mb, o);
+        mb = t > mb ? t : mb;
+    }
+    if ((threadIdx.x & 63) == 0 && mb) atomicMax(out, mb);
 }
 
 // Per-sample StyleGAN2 weights (base_blocks.py:487-495 / stylegan2_clean_arch.py:66-80 /
@@ -841,7 +866,7 @@ extern "C" int s2v_counter_add(unsigned long long *ctr, unsigned long long inc, 
 
 extern "C" int s2v_lipsync_inputs(const float *src, const float *fake, int n, int h, int w, unsigned char *ref_u8,
                                   float *face6, float *gt, s2v_stream_t stream) {
-    S2V_REQUIRE(src && fake && ref_u8 && face6 && gt && n > 0 && h > 1 && w > 0, "lipsync_inputs: bad args");
+    S2V_REQUIRE(src && ref_u8 && face6 && gt && n > 0 && h > 1 && w > 0, "lipsync_inputs: bad args");
     lipsync_inputs_kernel<<<grid_for((long long)n * 3 * h * w), 256, 0, (hipStream_t)stream>>>(src, fake, n, h, w,
                                                                                                ref_u8, face6, gt);
     return check_launch("lipsync_inputs");
@@ -880,6 +905,13 @@ extern "C" int s2v_fill(float *y, long long n, float value, s2v_stream_t stream)
     if (n == 0) return 0;
     fill_kernel<<<grid_for(n), 256, 0, (hipStream_t)stream>>>(y, n, value);
     return check_launch("fill");
+}
+
+extern "C" int s2v_amax(const float *x, long long pixels, int c, int xcs, float *out, s2v_stream_t stream) {
+    S2V_REQUIRE(x && out && pixels >= 0 && c > 0 && xcs >= c, "amax: bad args");
+    if (pixels == 0) return 0;
+    amax_kernel<<<grid_for(pixels * c), 256, 0, (hipStream_t)stream>>>(x, pixels, c, xcs, (unsigned *)out);
+    return check_launch("amax");
 }
 
 extern "C" int s2v_modulate_weights(const float *wt, int npad, int kpad, int K, int cin, int cout, const float *s,

@@ -129,6 +129,15 @@ void set_stamps(s2v_conv_params &p, const OptT &stamps, const OptT &ctr, at::Int
     p.stamp_slot = (int)pos[0]; p.stamp_stride = (int)pos[1]; p.stamp_reps = (int)pos[2];
 }
 
+// split-precision activation range (s2v_conv_params.x_scale / nonfinite): int32 [1] flag
+void set_range(s2v_conv_params &p, double x_scale, const OptT &nonfinite, const at::Device &dev) {
+    p.x_scale = (float)x_scale;
+    if (!has(nonfinite)) return;
+    same_dev(*nonfinite, dev, "conv nonfinite");
+    TORCH_CHECK(nonfinite->scalar_type() == at::kInt && nonfinite->numel() >= 1, "conv nonfinite: int32 [1]");
+    p.nonfinite = nonfinite->data_ptr<int>();
+}
+
 std::vector<int64_t> plan_list(const s2v_conv_params &p, int64_t need) {
     int pl[10] = {0};
     check(s2v_conv2d_plan(&p, pl), "s2v_conv2d_plan");
@@ -157,7 +166,10 @@ void conv_common(s2v_conv_params &p, const Tensor &x, const Tensor &y, int64_t c
     p.in_mode = (int)in_mode; p.pad_mode = (int)pad_mode;
     p.kh = (int)kernel[0]; p.kw = (int)kernel[1]; p.sh = (int)stride[0]; p.sw = (int)stride[1];
     p.ph = (int)padding[0]; p.pw = (int)padding[1]; p.dh = (int)dilation[0]; p.dw = (int)dilation[1];
-    TORCH_CHECK(p.kh > 0 && p.kw > 0 && p.sh > 0 && p.sw > 0 && p.dh > 0 && p.dw > 0 && p.ph >= 0 && p.pw >= 0,
+    // (negative padding: the polyphase sub-convolutions of a transposed conv, whose parity classes start
+    // inside the input)
+    TORCH_CHECK(p.kh > 0 && p.kw > 0 && p.sh > 0 && p.sw > 0 && p.dh > 0 && p.dw > 0 &&
+                    (out_step > 1 || (p.ph >= 0 && p.pw >= 0)),
                 "conv: bad kernel geometry");
     p.cout = (int)cout;
     p.y = yv.p; p.ycs = yv.cs;
@@ -221,7 +233,8 @@ std::vector<int64_t> conv2d_(const Tensor &x, const Tensor &y, const Tensor &wt,
                              double pix_w, const OptT &res, at::IntArrayRef res_offset, bool res_after_act,
                              int64_t act, double alpha, int64_t out_step, bool out_pool, bool x_split, const OptT &ws,
                              const OptT &tile_counters, int64_t force_tile, int64_t force_splits, const OptT &stamps,
-                             const OptT &stamp_ctr, at::IntArrayRef stamp_pos, bool dry) {
+                             const OptT &stamp_ctr, at::IntArrayRef stamp_pos, double x_scale, const OptT &nonfinite,
+                             bool dry) {
     const c10::DeviceGuard guard(x.device());
     const at::Device dev = x.device();
     s2v_conv_params p{};
@@ -263,6 +276,7 @@ std::vector<int64_t> conv2d_(const Tensor &x, const Tensor &y, const Tensor &wt,
         p.tile_counters = tile_counters->data_ptr<int>(); p.n_counters = (int)tile_counters->numel();
     }
     set_stamps(p, stamps, stamp_ctr, stamp_pos, dev);
+    set_range(p, x_scale, nonfinite, dev);
     const size_t need = s2v_conv2d_ws_bytes(&p);
     const Ws w = workspace(ws, dev);
     if (dry || w.bytes < need) return plan_list(p, (int64_t)need);
@@ -278,16 +292,18 @@ std::vector<int64_t> conv2d_(const Tensor &x, const Tensor &y, const Tensor &wt,
 // pre-scale when demodulated, or fp32), then one batched conv.  Returns as conv2d_.
 std::vector<int64_t> modulated_conv2d_(const Tensor &x, const Tensor &y, const Tensor &wt, const Tensor &s,
                                        const OptT &d, const Tensor &wbuf, int64_t cout, at::IntArrayRef kernel,
-                                       at::IntArrayRef padding, int64_t prec, bool x_split, const OptT &scale,
+                                       at::IntArrayRef padding, int64_t in_mode, int64_t prec, bool x_split,
+                                       const OptT &scale,
                                        const OptT &shift, const OptT &pix_add,
                                        double pix_w, const OptT &res, bool res_after_act, int64_t act, double alpha,
                                        const OptT &ws, int64_t force_splits, const OptT &stamps, const OptT &stamp_ctr,
-                                       at::IntArrayRef stamp_pos, bool dry) {
+                                       at::IntArrayRef stamp_pos, double x_scale, const OptT &nonfinite, bool dry) {
     const c10::DeviceGuard guard(x.device());
     const at::Device dev = x.device();
     s2v_conv_params p{};
     const int64_t one[2] = {1, 1}, zero[2] = {0, 0};
-    conv_common(p, x, y, cout, kernel, at::IntArrayRef(one, 2), padding, at::IntArrayRef(one, 2), S2V_IN_DIRECT,
+    TORCH_CHECK(in_mode == S2V_IN_DIRECT || in_mode == S2V_IN_NEAREST_UP2, "modconv: direct or nearest-x2 input");
+    conv_common(p, x, y, cout, kernel, at::IntArrayRef(one, 2), padding, at::IntArrayRef(one, 2), in_mode,
                 S2V_PAD_ZERO, scale, shift, pix_add, pix_w, res, at::IntArrayRef(zero, 2), res_after_act, act, alpha, 1,
                 false, x_split, true, prec, 0, force_splits);
     f32(wt, dev, "modconv wt");
@@ -317,6 +333,7 @@ std::vector<int64_t> modulated_conv2d_(const Tensor &x, const Tensor &y, const T
         p.wt = nullptr; p.wt_x3 = wbuf.data_ptr(); p.wt_scale = wscale;
     }
     set_stamps(p, stamps, stamp_ctr, stamp_pos, dev);
+    set_range(p, x_scale, nonfinite, dev);
     const size_t need = s2v_conv2d_ws_bytes(&p);
     const Ws w = workspace(ws, dev);
     if (dry || w.bytes < need) return plan_list(p, (int64_t)need);
@@ -370,6 +387,16 @@ std::vector<int64_t> gemm_kn_(const Tensor &a, const Tensor &b, const Tensor &ou
     auto o = plan_list(p, 0);
     check(s2v_conv2d(&p, stream()), "s2v_conv2d(gemm)");
     return o;
+}
+
+// max |x| of an NHWC view into out (float32 [1], zeroed here first)
+void amax_(const Tensor &x, const Tensor &out) {
+    const c10::DeviceGuard guard(x.device());
+    const NV xv = nhwc(x, x.device(), "amax x");
+    f32(out, x.device(), "amax out");
+    TORCH_CHECK(out.numel() >= 1 && out.is_contiguous(), "amax out: float32 [1]");
+    check(s2v_fill(out.data_ptr<float>(), 1, 0.f, stream()), "s2v_fill");
+    check(s2v_amax(xv.p, (long long)xv.n * xv.h * xv.w, xv.c, xv.cs, out.data_ptr<float>(), stream()), "s2v_amax");
 }
 
 void split_weights_(const Tensor &w, const Tensor &out, int64_t prec, double scale) {
@@ -679,23 +706,27 @@ void fir2d_(const Tensor &x, const Tensor &kernel, const Tensor &y, int64_t up, 
 }
 
 // ------------------------------------------------------------------------------------------ pipeline glue
-void lipsync_inputs_(const Tensor &src, const Tensor &fake, const Tensor &ref_u8, const Tensor &face6,
+// fake None: ref_u8 holds the references (an enhancer replaced them) and only face6 / gt are built
+void lipsync_inputs_(const Tensor &src, const OptT &fake, const Tensor &ref_u8, const Tensor &face6,
                      const Tensor &gt) {
     const c10::DeviceGuard guard(src.device());
     const at::Device dev = src.device();
-    f32(src, dev, "lipsync src"); f32(fake, dev, "lipsync fake"); f32(face6, dev, "lipsync face6");
+    f32(src, dev, "lipsync src"); f32(face6, dev, "lipsync face6");
     f32(gt, dev, "lipsync gt");
     same_dev(ref_u8, dev, "lipsync ref_u8");
     TORCH_CHECK(src.dim() == 4 && src.size(1) == 3 && src.is_contiguous(), "lipsync: src [N, 3, H, W] contiguous");
     const int64_t n = src.size(0), h = src.size(2), w = src.size(3);
-    TORCH_CHECK(fake.is_contiguous() && fake.sizes() == src.sizes(), "lipsync: fake like src");
+    if (has(fake)) {
+        f32(*fake, dev, "lipsync fake");
+        TORCH_CHECK(fake->is_contiguous() && fake->sizes() == src.sizes(), "lipsync: fake like src");
+    }
     TORCH_CHECK(ref_u8.scalar_type() == at::kByte && ref_u8.is_contiguous() && ref_u8.sizes() == src.sizes(),
                 "lipsync: ref_u8 uint8 like src");
     TORCH_CHECK(face6.is_contiguous() && face6.dim() == 4 && face6.size(0) == n && face6.size(1) == 6 &&
                     face6.size(2) == h && face6.size(3) == w,
                 "lipsync: face6 [N, 6, H, W]");
     TORCH_CHECK(gt.is_contiguous() && gt.sizes() == src.sizes(), "lipsync: gt like src");
-    check(s2v_lipsync_inputs(src.data_ptr<float>(), fake.data_ptr<float>(), (int)n, (int)h, (int)w,
+    check(s2v_lipsync_inputs(src.data_ptr<float>(), has(fake) ? fake->data_ptr<float>() : nullptr, (int)n, (int)h, (int)w,
                              ref_u8.data_ptr<uint8_t>(), face6.data_ptr<float>(), gt.data_ptr<float>(), stream()),
           "s2v_lipsync_inputs");
 }
@@ -749,12 +780,15 @@ TORCH_LIBRARY_FRAGMENT(s2v, m) {
           "Tensor? shift, Tensor? in_scale, Tensor? nc_scale, int pre_act, float pre_alpha, Tensor? pix_add, "
           "float pix_w, Tensor? res, int[2] res_offset, bool res_after_act, int act, float alpha, int out_step, "
           "bool out_pool, bool x_split, Tensor? ws, Tensor? tile_counters, int force_tile, int force_splits, "
-          "Tensor(s!)? stamps, Tensor? stamp_ctr, int[3] stamp_pos, bool dry) -> int[]");
+          "Tensor(s!)? stamps, Tensor? stamp_ctr, int[3] stamp_pos, float x_scale, Tensor(f!)? nonfinite, "
+          "bool dry) -> int[]");
     m.def("modulated_conv2d_(Tensor x, Tensor(a!) y, Tensor wt, Tensor s, Tensor? d, Tensor(b!) wbuf, int cout, "
-          "int[2] kernel, int[2] padding, int prec, bool x_split, Tensor? scale, Tensor? shift, Tensor? pix_add, "
+          "int[2] kernel, int[2] padding, int in_mode, int prec, bool x_split, Tensor? scale, Tensor? shift, "
+          "Tensor? pix_add, "
           "float pix_w, Tensor? res, "
           "bool res_after_act, int act, float alpha, Tensor? ws, int force_splits, Tensor(s!)? stamps, Tensor? stamp_ctr, "
-          "int[3] stamp_pos, bool dry) -> int[]");
+          "int[3] stamp_pos, float x_scale, Tensor(f!)? nonfinite, bool dry) -> int[]");
+    m.def("amax_(Tensor x, Tensor(a!) out) -> ()");
     m.def("gemm_kn_(Tensor a, Tensor b, Tensor(a!) out, int batch, int a_bs, int b_bs, int out_bs, Tensor? res, "
           "int res_bs, int act, float alpha, int prec, Tensor? ws, int force_tile, int force_splits, bool dry) -> int[]");
     m.def("split_weights_(Tensor w, Tensor(a!) out, int prec, float scale) -> ()");
@@ -781,7 +815,7 @@ TORCH_LIBRARY_FRAGMENT(s2v, m) {
           "Tensor(a!) y) -> ()");
     m.def("fir2d_(Tensor x, Tensor kernel, Tensor(a!) y, int up, int down, int pad_y0, int pad_x0, float gain, "
           "Tensor? bias, int act, float alpha, float post) -> ()");
-    m.def("lipsync_inputs_(Tensor src, Tensor fake, Tensor(a!) ref_u8, Tensor(b!) face6, Tensor(c!) gt) -> ()");
+    m.def("lipsync_inputs_(Tensor src, Tensor? fake, Tensor(a!) ref_u8, Tensor(b!) face6, Tensor(c!) gt) -> ()");
     m.def("to_u8_(Tensor x, Tensor(a!) y, float lo, float hi, float scale, float offset) -> ()");
     m.def("mel_chunks_(Tensor mel, Tensor starts, int step, Tensor(a!) out) -> ()");
     m.def("melspectrogram_(Tensor wav, Tensor tables, bool pad_reflect, Tensor(a!) out) -> ()");
@@ -792,6 +826,7 @@ TORCH_LIBRARY_IMPL(s2v, CUDA, m) {
     m.impl("modulated_conv2d_", &modulated_conv2d_);
     m.impl("gemm_kn_", &gemm_kn_);
     m.impl("split_weights_", &split_weights_);
+    m.impl("amax_", &amax_);
     m.impl("split_act_", &split_act_);
     m.impl("layernorm2d_", &layernorm2d_);
     m.impl("instnorm_", &instnorm_);

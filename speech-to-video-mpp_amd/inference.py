@@ -12,12 +12,18 @@ Steps (reference file:line in brackets):
     image (no cv2 / ffmpeg), so the frames are synthetic uint8 BGR frames of that size (SURVEY.md
     §8d allows this), or an .npy [N,H,W,3] uint8 array given as --face;
   * frames truncated to the number of mel windows [inference.py:219-221];
-  * the face box: face detection + 3DMM cropping (preprocessing/facing.py) is outside the built
-    scope (SURVEY.md §8f(4)); the box is the centred square of --box_frac of the short side;
-  * DNet stabilisation of the box crop (trans_image: 256x256, [-1, 1], facing.py:177-191) with
-    semantic coefficient windows (synthetic 3DMM coefficients: the regressor is out of scope),
-    then ENet(LNet) on [masked crop, reference] batches of LNet_batch_size, clamp(0, 1) * 255
-    [inference.py:259-267, :393-399] (s2v_amd.pipeline.LipSyncPipeline);
+  * the face box: the centred square of --box_frac of the short side (the reference finds it with
+    dlib / FAN landmarks, which need packages and weights this image lacks: DESIGN.md §7);
+  * 3DMM coefficients: with --checkpoints holding face3d's epoch_20.pth, the built extractor
+    (s2v_amd.face3d.Face3DExtractor: align_img + ReconNetWrapper('resnet50'), facing.py:100-130)
+    regresses them from the frames with the box-derived 5 landmarks; otherwise they are synthetic;
+  * DNet stabilisation of the box crop (trans_image: 256x256, [-1, 1], facing.py:177-191) with the
+    coefficient windows, then ENet(LNet) on [masked crop, reference] batches of LNet_batch_size,
+    clamp(0, 1) * 255 [inference.py:259-267, :393-399] (s2v_amd.pipeline.LipSyncPipeline);
+  * --ref_enhance: Step 5, ``ref_enhancer.process(img, img, face_enhance=False)`` with
+    FaceEnhancement(in_size 512, use_sr False) on every stabilised reference before ENet
+    [inference.py:224-238] (needs real RetinaFace / ParseNet weights: synthetic ones detect no face,
+    and the reference raises on a frame without one);
   * each 384x384 prediction resized into the box and pasted into its frame [inference.py:287-291];
   * --enhance: FaceEnhancement (SR x2, RetinaFace, GPEN-2048, parse-mask paste) on each pasted frame
     against the 2x frame [inference.py:228-231, :317-328]; needs real checkpoints (synthetic
@@ -174,9 +180,62 @@ def _frames(face: str, max_frames: int):
         f"synthetic {info['width']}x{info['height']} (no decoder; {info['frames']} frames in the file)"
 
 
+# face3d's 5-point 3D reference when BFM/similarity_Lm3D_all.mat is absent (stated stand-in, the
+# layout of lm3d_from_68: eyes, nose tip, mouth corners)
+LM3D_STANDIN = np.array([[-0.31, 0.29, 0.41], [0.31, 0.29, 0.41], [0.0, 0.0, 0.65], [-0.25, -0.36, 0.44],
+                         [0.25, -0.36, 0.44]])
+
+
+def _semantic(frames_bgr: torch.Tensor, ckpt_dir, dev):
+    """facing.py:100-130 face_3dmm_extraction on the frames: ReconNetWrapper('resnet50') from
+    face3d_pretrain_epoch_20.pth (synthetic weights without it), the reference's no-landmark path
+    (all -1 landmarks -> lm3d positions, facing.py:110-116) since FAN is absent -> [n, 262]."""
+    from . import face3d, models, synth
+    from .models.face3d_arch import ReconNetWrapperParams
+    path = os.path.join(ckpt_dir or "", "face3d_pretrain_epoch_20.pth")
+    if ckpt_dir and os.path.exists(path):
+        net = models.load_face3d_net(path, dev)
+        kind = "checkpoint"
+    else:
+        net = models.ReconNetWrapper()
+        net.load_state_dict(synth.synth_torch_state_dict(ReconNetWrapperParams(), **synth.RETINA_SYNTH))
+        net = net.eval()
+        kind = "synthetic"
+    bfm = os.path.join(ckpt_dir or "", "BFM")
+    lm3d = face3d.load_lm3d(bfm) if os.path.exists(os.path.join(bfm, "similarity_Lm3D_all.mat")) else LM3D_STANDIN
+    n = frames_bgr.shape[0]
+    rgb = frames_bgr[..., [2, 1, 0]].contiguous()                               # facing.py reads RGB PIL frames
+    ext = face3d.Face3DExtractor(net, lm3d, dev)
+    return ext.face_3dmm_extraction(rgb, np.full((n, 68, 2), -1.0, np.float32)), kind
+
+
+def _ref_enhancer(ckpt_dir, dev):
+    """inference.py:224-226: FaceEnhancement(in_size=512, channel_multiplier=2, narrow=1, sr_scale=4,
+    model='GPEN-BFR-512', use_sr=False) as a hook on the stabilised uint8 RGB references."""
+    from . import face as faces
+    enh = faces.FaceEnhancement(base_dir=ckpt_dir or "checkpoints", in_size=512, channel_multiplier=2, narrow=1,
+                                sr_scale=4, model="GPEN-BFR-512", use_sr=False, device=dev)
+    return reference_hook(enh)
+
+
+def reference_hook(enh):
+    """Step 5 (inference.py:234-238) as a LipSyncPipeline ref hook: each uint8 RGB [3, h, w] reference
+    -> BGR HWC -> ``enh.process_device(img, img, face_enhance=False, possion_blending=False)`` -> back."""
+    def hook(ref_u8: torch.Tensor) -> torch.Tensor:
+        out = torch.empty_like(ref_u8)
+        for i in range(ref_u8.shape[0]):
+            bgr = ref_u8[i].flip(0).permute(1, 2, 0).contiguous()
+            img = enh.process_device(bgr, bgr, face_enhance=False, possion_blending=False)[0]
+            out[i] = img.permute(2, 0, 1).flip(0)
+        return out
+    return hook
+
+
 def run(face: str, audio_path: str, max_frames: int = 8, batch: int = 16, box_frac: float = 0.6,
-        ckpt_dir: str | None = None, enhance: bool = False, device: str = "cuda"):
-    """-> dict(frames uint8 [n,H,W,3] device, preds uint8 [n,3,384,384], meta)."""
+        ckpt_dir: str | None = None, enhance: bool = False, device: str = "cuda", ref_enhance: bool = False,
+        ref_hook=None):
+    """-> dict(frames uint8 [n,H,W,3] device, preds uint8 [n,3,384,384], meta).  ``ref_enhance``:
+    Step 5 with FaceEnhancement-512 (``ref_hook``: any callable on uint8 [b,3,h,w] references)."""
     from . import audio, pipeline, post, synth
     dev = torch.device(device)
     t0 = time.time()
@@ -199,10 +258,12 @@ def run(face: str, audio_path: str, max_frames: int = 8, batch: int = 16, box_fr
     ctx = post._ctx(dev)
     from ._lib import check
     check(ctx.lib.s2v_u8_to_gan(crops.data_ptr(), n, 256, 256, src.data_ptr(), ctx.stream), "s2v_u8_to_gan")
-    semantic = synth.hash_array("inference.semantic", (n, 262), -1.0, 1.0)
-    expression = synth.hash_array("inference.expression", (64,), -1.0, 1.0)
+    semantic, skind = _semantic(frames, ckpt_dir, dev)                             # facing.py:100-130
+    expression = synth.hash_array("inference.expression", (64,), -1.0, 1.0)        # expression.mat is absent
     coeffs = torch.from_numpy(pipeline.dnet_coefficients(semantic, expression, False, 0, n)).to(dev)
-    pipe = pipeline.LipSyncPipeline(dnet, enet, device=dev, batch=batch, graph=False)
+    if ref_enhance and ref_hook is None:
+        ref_hook = _ref_enhancer(ckpt_dir, dev)
+    pipe = pipeline.LipSyncPipeline(dnet, enet, device=dev, batch=batch, graph=False, ref_hook=ref_hook)
     preds = pipe.run(chunks[:n], src, coeffs)                                       # [n,3,384,384] uint8
     out = frames.clone()
     hwc = preds.permute(0, 2, 3, 1).contiguous()
@@ -221,7 +282,8 @@ def run(face: str, audio_path: str, max_frames: int = 8, batch: int = 16, box_fr
     torch.cuda.synchronize(dev)
     meta = {"frames": n, "frame_hw": [int(H), int(W)], "fps": fps, "video": src_kind, "weights": wkind,
             "mel_cols": int(mel.shape[1]), "mel_windows": int(chunks.shape[0]), "wav_samples_16k": int(len(wav)),
-            "box": [y1, y2, x1, x2], "seconds": round(time.time() - t0, 3)}
+            "box": [y1, y2, x1, x2], "semantic": skind, "ref_enhance": ref_hook is not None,
+            "seconds": round(time.time() - t0, 3)}
     return {"frames": out, "preds": preds, "enhanced": enhanced, "meta": meta}
 
 
@@ -235,8 +297,10 @@ def main(argv=None):
     ap.add_argument("--box_frac", type=float, default=0.6)
     ap.add_argument("--checkpoints", default=None)
     ap.add_argument("--enhance", action="store_true")
+    ap.add_argument("--ref_enhance", action="store_true", help="Step 5: FaceEnhancement-512 on the references")
     a = ap.parse_args(argv)
-    r = run(a.face, a.audio, a.max_frames, a.LNet_batch_size, a.box_frac, a.checkpoints, a.enhance)
+    r = run(a.face, a.audio, a.max_frames, a.LNet_batch_size, a.box_frac, a.checkpoints, a.enhance,
+            ref_enhance=a.ref_enhance)
     os.makedirs(os.path.dirname(os.path.abspath(a.outfile)), exist_ok=True)
     arrays = {"frames": r["frames"].cpu().numpy(), "preds": r["preds"].cpu().numpy()}
     if r["enhanced"] is not None:

@@ -17,6 +17,7 @@ import ctypes
 import math
 import os
 import threading
+import weakref
 
 import torch
 
@@ -41,6 +42,27 @@ SPLIT_PRECISIONS = ("f16x3", "bf16x3")
 PRECISION = os.environ.get("S2V_PRECISION", "f16x3")
 if PRECISION not in _PRECISIONS:
     raise ValueError(f"S2V_PRECISION must be one of {sorted(_PRECISIONS)}, got {PRECISION!r}")
+
+
+# f16x3 activation range guard.  The f16 halves of a split operand cover |v| < 65504, and a lo half
+# becomes an f16 subnormal (absolute spacing 2^-24) once |v| < 2^-3.  Weights are pre-scaled by a
+# power of two at packing (ConvW.split_scale); activations get a per-layer power-of-two pre-scale
+# (s2v_conv_params.x_scale) chosen from the layer input's max |v| on its first eager run (``s2v::amax_``):
+# a layer whose max lies outside [X_LO, X_HI) is scaled so that it lands in [2^13, 2^14).  Every
+# f16x3 launch also carries the lane's non-finite flag: an input that still overflows (a later
+# batch far outside the calibrated range) sets it, and check_range() raises — never silent.
+# S2V_RANGE_GUARD=0 turns both off.
+RANGE_GUARD = os.environ.get("S2V_RANGE_GUARD", "1") == "1"
+X_LO, X_HI = 2.0 ** -3, 2.0 ** 14
+
+
+def x_scale_for(amax: float) -> float:
+    """Power-of-two activation pre-scale for a layer whose input max |v| is ``amax``."""
+    if not (amax > 0.0) or math.isinf(amax):
+        return 1.0
+    if X_LO <= amax < X_HI:
+        return 1.0
+    return float(2.0 ** (13 - math.floor(math.log2(amax))))
 
 
 # in-launch split-K fold (s2v_conv_params.tile_counters), opt-in with S2V_SPLITK_FOLD=1.  It gives
@@ -226,6 +248,7 @@ class Ctx:
     (two captured graphs replayed on two streams): nothing either graph writes is shared."""
 
     N_COUNTERS = 1 << 18
+    ALL = weakref.WeakSet()          # every context (check_all_ranges)
 
     def __init__(self, device):
         self.device = torch.device(device)
@@ -235,6 +258,31 @@ class Ctx:
         self._streams = {}
         self._noise = {}
         self.keep = []          # the current forward's side-branch tensors (side_stream), dropped per forward
+        self.parent = None      # side-branch contexts share their lane's range flag
+        self._flag = None
+        Ctx.ALL.add(self)
+
+    def range_flag(self):
+        """The lane's non-finite flag (int32 [1], made eagerly on first use; None off-device)."""
+        if self.parent is not None:
+            return self.parent.range_flag()
+        if self._flag is None:
+            if self.device.type != "cuda" or torch.cuda.is_current_stream_capturing():
+                return None
+            self._flag = torch.zeros(1, dtype=torch.int32, device=self.device)
+        return self._flag
+
+    def check_range(self, what="s2v"):
+        """Raise if a split-precision conv of this lane produced a non-finite value since the last
+        check (activation range outside the calibrated pre-scale); resets the flag."""
+        f = self._flag
+        if f is None:
+            return
+        if int(f.item()):
+            f.zero_()
+            raise _lib.S2VError(f"{what}: a split-precision (f16x3) conv produced non-finite values: an activation "
+                                "left the range calibrated on the first forward.  Re-calibrate (model.refresh()) "
+                                "or run S2V_PRECISION=bf16x3 (fp32 exponent range)")
 
     def streams(self, key, n):
         """``n`` (stream, Ctx) pairs for the side branches of engine ``key`` (made once, CUDA
@@ -243,6 +291,8 @@ class Ctx:
             return None
         if key not in self._streams:
             self._streams[key] = [(torch.cuda.Stream(self.device), Ctx(self.device)) for _ in range(n)]
+            for _, c in self._streams[key]:
+                c.parent = self
         assert len(self._streams[key]) >= n
         return self._streams[key][:n]
 
@@ -434,6 +484,7 @@ def _conv(ctx, x, cw, yv, out_step, act, alpha, resv, res_after, res_offset, nc_
                             f"in {PRECISION!r} (code {prec}); split it again with split_act after set_precision")
     wsplit = cw.wt_x3(ctx, prec) if prec != PREC_F32 else None
     wscale = cw.split_scale(prec)
+    xscale, flag = _range(ctx, cw, x, prec)
     counters = _counters(ctx)
     sc = cw.scale if scale is None else scale
     sh = cw.shift if shift is None else shift
@@ -442,8 +493,33 @@ def _conv(ctx, x, cw, yv, out_step, act, alpha, resv, res_after, res_offset, nc_
         return S2V.conv2d_(x.v, yv, cw.wt, wsplit, wscale, cw.cout, [cw.kh, cw.kw], [cw.sh, cw.sw], [cw.ph, cw.pw],
                            [cw.dh, cw.dw], cw.in_mode, cw.pad_mode, prec, sc, sh, in_scale, nc_scale, pre_act, pre_alpha,
                            pix_add, pix_w, resv, list(res_offset), res_after, act, alpha, out_step, pool, x_split != 0,
-                           ws, counters, force_tile, force_splits, st[0], st[1], st[2], dry)
+                           ws, counters, force_tile, force_splits, st[0], st[1], st[2], xscale, flag, dry)
     _run_conv(ctx, launch, x, cw, yv, pool, in_scale, nc_scale, pix_add, resv)
+
+
+def check_all_ranges(what="s2v"):
+    """Ctx.check_range over every live context (raises on the first flagged lane)."""
+    for c in list(Ctx.ALL):
+        c.check_range(what)
+
+
+def _range(ctx, cw, x, prec):
+    """(x_scale, flag) of an f16x3 launch: the layer's calibrated activation pre-scale (measured on
+    its first eager call, ``s2v::amax_``) and the lane's non-finite flag."""
+    if prec != PREC_F16X3 or not RANGE_GUARD or int(getattr(x, "split", 0)):
+        return 1.0, None
+    scales = cw.__dict__.setdefault("_xscale", {})
+    s = scales.get(prec)
+    if s is None:
+        if x.t.is_cuda and torch.cuda.is_current_stream_capturing():
+            raise _lib.S2VError("activation ranges must be calibrated by an eager run before graph capture")
+        m = torch.zeros(1, device=x.t.device)
+        S2V.amax_(x.v, m)
+        amax = float(m.item())
+        s = x_scale_for(amax)
+        scales[prec] = s
+        cw.x_amax = amax
+    return s, ctx.range_flag()
 
 
 def _run_conv(ctx, launch, x, cw, yv, pool, in_scale=None, nc_scale=None, pix_add=None, resv=None):
@@ -487,11 +563,13 @@ def modulated_conv2d(ctx: Ctx, x: NHWC, cw: ConvW, y: NHWC, s: torch.Tensor, d: 
         raise _lib.S2VError(f"modulated conv: the input holds the split layout of precision code {x_split}, but the "
                             f"conv runs in {PRECISION!r} (code {prec})")
     sh = cw.shift if shift is None else shift            # the layer bias (epilogue shift) unless overridden
+    xscale, flag = _range(ctx, cw, x, prec)
 
     def launch(ws, dry=False, st=_NOSTAMP):
-        return S2V.modulated_conv2d_(x.v, yv, cw.wt, s, d, wbuf, cw.cout, [cw.kh, cw.kw], [cw.ph, cw.pw], prec,
+        return S2V.modulated_conv2d_(x.v, yv, cw.wt, s, d, wbuf, cw.cout, [cw.kh, cw.kw], [cw.ph, cw.pw], cw.in_mode,
+                                     prec,
                                      x_split != 0, cw.scale, sh, pix_add, pix_w, resv, res_after, act, alpha, ws,
-                                     force_splits, st[0], st[1], st[2], dry)
+                                     force_splits, st[0], st[1], st[2], xscale, flag, dry)
     _run_conv(ctx, launch, x, cw, yv, False, pix_add=pix_add, resv=resv)
     return y
 

@@ -78,13 +78,15 @@ class LipSyncPipeline:
     overlaps the previous batch's MFMA-bound StyleConv decoder.  Each lane has its own workspaces,
     side streams and noise counters (the models' per-lane ops.Ctx) and its own graph buffers."""
 
-    def __init__(self, dnet, enet, device="cuda", batch: int = 16, graph: bool = True, lanes: int = 2):
+    def __init__(self, dnet, enet, device="cuda", batch: int = 16, graph: bool = True, lanes: int = 1,
+                 ref_hook=None):
         self.dnet, self.enet = dnet, enet
         self.device = torch.device(device)
         self.batch = batch
         self.ctx = Ctx(self.device)
         self.graph = graph          # full batches of ``run`` replay captured HIP graphs
         self.lanes = lanes
+        self.ref_hook = ref_hook    # Step 5 (inference.py:234-238) on the uint8 references; eager batches only
         self._runner = None
 
     @torch.no_grad()
@@ -98,6 +100,9 @@ class LipSyncPipeline:
         face6 = torch.empty((b, 6, h, w), device=self.device)
         gt = torch.empty((b, 3, h, w), device=self.device)
         ops.S2V.lipsync_inputs_(src.contiguous(), fake, ref_u8, face6, gt)
+        if self.ref_hook is not None:                 # the enhanced references replace ref / 255 (datagen)
+            ref_u8 = self.ref_hook(ref_u8).contiguous()
+            ops.S2V.lipsync_inputs_(src.contiguous(), None, ref_u8, face6, gt)
         pred, _ = self.enet(mel, face6, gt, lane=lane)
         ops.S2V.to_u8_(pred, out_u8, 0.0, 1.0, 255.0, 0.0)             # inference.py:267, :288
         return out_u8
@@ -117,7 +122,7 @@ class LipSyncPipeline:
         for b0 in range(0, n, self.batch):
             b1 = min(n, b0 + self.batch)
             m, s, c = mel_chunks[start + b0: start + b1], src[b0:b1], coeffs[b0:b1]
-            if self.graph and b1 - b0 == self.batch:
+            if self.graph and b1 - b0 == self.batch and self.ref_hook is None:
                 runner = self._graph_runner(m, s, c)
                 dst = out[b0:b1]
                 runner(m, s, c, out_fn=lambda o, d=dst: d.copy_(o))
@@ -128,6 +133,10 @@ class LipSyncPipeline:
                 self.run_batch(m, s, c, out[b0:b1])
         if runner is not None:
             runner.join()
+        for m in (self.dnet, self.enet):          # f16x3 range guard: never a silent overflow
+            for _, lanes in m.__dict__.get("_s2v_engines", {}).values():
+                for c in lanes.values():
+                    c.check_range(type(m).__name__)
         return out
 
     def _graph_runner(self, m, s, c):

@@ -40,3 +40,20 @@ def test_runner_cli_writes_npz(tmp_path):
     assert inference.main(["--face", str(mp4), "--audio", str(wav), "--outfile", str(out), "--max_frames", "8"]) == 0
     z = np.load(out)
     assert z["frames"].shape == (8, 180, 200, 3) and z["preds"].shape == (8, 3, 384, 384)
+
+
+def test_runner_reference_hook_and_semantic(tmp_path):
+    """Step 5 wiring (inference.py:234-238): an identity reference hook gives the frames of the run
+    without it; the 3DMM coefficients come from the built extractor (facing.py:100-130)."""
+    from s2v_amd import inference
+    mp4 = write_mp4_header(tmp_path / "v.mp4", 200, 180, 12, 12800, 6144)
+    wav = write_wav(tmp_path / "a.wav", rate=16000, channels=1, seconds=0.5)
+    a = inference.run(str(mp4), str(wav), max_frames=5, batch=4)
+    calls = []
+
+    def ident(ref):
+        calls.append(tuple(ref.shape))
+        return ref.clone()
+    b = inference.run(str(mp4), str(wav), max_frames=5, batch=4, ref_hook=ident)
+    assert calls == [(4, 3, 256, 256), (1, 3, 256, 256)] and b["meta"]["ref_enhance"]
+    assert torch.equal(a["preds"], b["preds"]) and a["meta"]["semantic"] == "synthetic"

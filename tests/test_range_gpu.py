@@ -1,0 +1,83 @@
+"""f16x3 activation range guard (ops.RANGE_GUARD).
+
+f16 halves cover |v| < 65504 and a lo half turns subnormal below 2^-3: a layer whose input leaves
+that range gets a calibrated power-of-two pre-scale (s2v_conv_params.x_scale), and an input that
+still overflows later sets the lane's non-finite flag (check_range raises)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+import s2v_import  # noqa: F401
+from s2v_amd import _lib, ops
+from s2v_amd.ops import NHWC, ConvW
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+REL = 3e-6          # f16x3 per-product bound (as tests/test_conv_glds_gpu.py), relative to |x| * |w|
+
+
+@pytest.fixture
+def f16x3():
+    prev = ops.set_precision("f16x3")
+    yield
+    ops.set_precision(prev)
+
+
+def _case(seed, cin=64, cout=96, h=13, w=11):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.rand(2, cin, h, w, generator=g, dtype=torch.float64) * 2 - 1
+    wt = torch.randn(cout, cin, 3, 3, generator=g, dtype=torch.float64) / math.sqrt(cin * 9)
+    return x, wt
+
+
+@pytest.mark.parametrize("mag", [6e4, 1e5, 1e-6, 3.0])
+def test_conv_inputs_outside_the_f16_range(f16x3, mag):
+    x, wt = _case(1)
+    x = x * mag
+    ctx = ops.Ctx(DEV)
+    cw = ConvW(wt.float(), None, DEV, padding=1)
+    xv = NHWC(x.permute(0, 2, 3, 1).float().contiguous().to(DEV))
+    y = NHWC.empty(2, 13, 11, 96, DEV)
+    ops.conv2d(ctx, xv, cw, y)
+    ctx.check_range()                                    # no overflow with the calibrated pre-scale
+    got = y.t.permute(0, 3, 1, 2).double().cpu()
+    ref = F.conv2d(x.float().double(), wt.float().double(), None, 1, 1)
+    bound = F.conv2d(x.float().double().abs(), wt.float().double().abs(), None, 1, 1)
+    assert torch.isfinite(got).all()
+    assert ((got - ref).abs() <= REL * bound + 1e-30).all(), float(((got - ref).abs() / (bound + 1e-30)).max())
+    expect = ops.x_scale_for(float(x.float().abs().max()))
+    assert cw._xscale[ops.PREC_F16X3] == expect and (expect != 1.0) == (mag != 3.0)
+
+
+def test_overflow_after_calibration_is_flagged(f16x3):
+    x, wt = _case(2)
+    ctx = ops.Ctx(DEV)
+    cw = ConvW(wt.float(), None, DEV, padding=1)
+    y = NHWC.empty(2, 13, 11, 96, DEV)
+    small = NHWC((x * 10).permute(0, 2, 3, 1).float().contiguous().to(DEV))
+    ops.conv2d(ctx, small, cw, y)                        # calibrates: no pre-scale needed
+    ctx.check_range()
+    big = NHWC((x * 1e6).permute(0, 2, 3, 1).float().contiguous().to(DEV))
+    ops.conv2d(ctx, big, cw, y)                          # far outside the calibrated range
+    with pytest.raises(_lib.S2VError, match="non-finite"):
+        ctx.check_range()
+    ctx.check_range()                                    # the flag was reset
+
+
+def test_modulated_conv_range(f16x3):
+    x, wt = _case(3, cin=32, cout=64)
+    x = x * 2e5
+    ctx = ops.Ctx(DEV)
+    cw = ConvW(wt.float(), None, DEV, padding=1)
+    xv = NHWC(x.permute(0, 2, 3, 1).float().contiguous().to(DEV))
+    y = NHWC.empty(2, 13, 11, 64, DEV)
+    s = torch.full((2, 32), 0.5, device=DEV)
+    d = torch.full((2, 64), 2.0, device=DEV)
+    ops.modulated_conv2d(ctx, xv, cw, y, s, d)
+    ctx.check_range()
+    got = y.t.permute(0, 3, 1, 2).double().cpu()
+    ref = F.conv2d(x.float().double(), wt.float().double(), None, 1, 1)      # 0.5 * 2.0 = 1
+    bound = F.conv2d(x.float().double().abs(), wt.float().double().abs(), None, 1, 1)
+    assert torch.isfinite(got).all() and ((got - ref).abs() <= 2 * REL * bound).all()
