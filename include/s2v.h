@@ -167,9 +167,11 @@ int s2v_conv2d_plan(const s2v_conv_params *p, int *out10);
  *   S2V_TUNE_IN_FUSED         1 (env S2V_IN_FUSED): InstanceNorm / ADAIN on planes of <= 256 pixels
  *                             with >= 64 (plane, 256-channel group) blocks runs as one launch; default 0
  *                             (measured in-process, tools/ab_tune.py: LNet 10.59 -> 10.95 ms with it).
+ *   S2V_TUNE_RESIZE_UP2       1 (env S2V_RESIZE_UP2, default): exact x2 bilinear resizes take the 2x2-quad
+ *                             kernel; 0: the generic float4 resize kernel.
  * Sets ``value``, returns the previous one in *old_value (may be NULL). */
 enum { S2V_TUNE_HALO_MIN_BLOCKS = 0, S2V_TUNE_GLDS_TILE = 1, S2V_TUNE_SMALLK_TILE = 2, S2V_TUNE_X3_RATE_512 = 3,
-       S2V_TUNE_IN_FUSED = 4, S2V_TUNE_COUNT = 5 };
+       S2V_TUNE_IN_FUSED = 4, S2V_TUNE_RESIZE_UP2 = 5, S2V_TUNE_COUNT = 6 };
 int s2v_tune(int key, long long value, long long *old_value);
 
 /* max |x| over an NHWC view (pixels x c at pitch xcs) -> *out (fp32 bits; NaN propagates as the
@@ -230,6 +232,16 @@ int s2v_modconv_demod(const float *s, int batch, int s_ns, int cin, const float 
 int s2v_resize(const float *x, int n, int c, int ih, int iw, long long xsn, long long xsc, long long xsy,
                long long xsx, float *y, int oh, int ow, long long ysn, long long ysc, long long ysy,
                long long ysx, float scale_h, float scale_w, int mode, s2v_stream_t stream);
+
+/* ENet / StyleGAN2 ToRGB and its skip upsample in one pass (base_blocks.py:536-554, ENet.py:119-129;
+ * replaces s2v_modulate_weights + the small-Cout conv with ``res`` + the x2 s2v_resize of the skip):
+ *   y[b,p,o] = (sum_c wt[o][c] * s[b][c] * x[b,p,c] + bias[o]) + up2(skip)[b,p,o]   (o < 3)
+ *   y[b,p,3] = up2(skip)[b,p,3]
+ * x NHWC [n][h][w] (pixel pitch xcs, c % 32 == 0), wt packed 1x1 rows [3+][kpad], s [n][s_ns], bias [3]
+ * or NULL, skip NHWC [n][h/2][w/2] (pitch skcs >= 4), y NHWC [n][h][w] (pitch ycs >= 4); up2 is
+ * F.interpolate(scale_factor=2, mode='bilinear', align_corners=False).  h*w % 32 == 0. */
+int s2v_torgb_up2(const float *x, int n, int h, int w, int c, int xcs, const float *wt, int kpad, const float *s,
+                  int s_ns, const float *bias, const float *skip, int skcs, float *y, int ycs, s2v_stream_t stream);
 
 /* F.pad(mode='reflect') on NHWC (ENet.py:119). */
 int s2v_pad_reflect(const float *x, int n, int h, int w, int c, int xcs, int pt, int pb, int pl, int pr,

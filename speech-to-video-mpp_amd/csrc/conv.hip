@@ -781,6 +781,8 @@ static long long tune_value(int key) {
         g_tune[S2V_TUNE_X3_RATE_512] = e ? atoll(e) : 0;
         e = getenv("S2V_IN_FUSED");
         g_tune[S2V_TUNE_IN_FUSED] = e ? atoll(e) : 0;
+        e = getenv("S2V_RESIZE_UP2");
+        g_tune[S2V_TUNE_RESIZE_UP2] = e ? atoll(e) : 1;
         g_tune_init = true;
     }
     return g_tune[key];

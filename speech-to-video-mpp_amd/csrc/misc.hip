@@ -86,9 +86,17 @@ __global__ __launch_bounds__(256) void resize_nhwc4_kernel(const float *__restri
 }
 
 // Exact x2 bilinear upsample (align_corners=False, source scale 0.5) of a float4-channel NHWC
-// view: one thread = one channel quad of one source pixel -> the 2x2 output quad it centres, from
-// its 3x3 source neighbourhood (9 loads for 4 outputs against 16 in the generic kernel; no per-
-// element divisions).  Same index / weight rule (bilin_index) and expression as resize_nhwc4_kernel.
+// view: one thread = one channel quad of one source pixel -> the 2x2 output quad it centres.  The
+// 3x3 source neighbourhood (rows / columns clamped to the image) is loaded once, 9 float4 loads for
+// 4 outputs, and each output takes its 4 taps from those registers by the same index / weight rule
+// (bilin_index) and expression as resize_nhwc4_kernel, so the result is the generic kernel's bit for
+// bit.  (Loading each output's 4 taps separately, 16 loads with the centre pixel requested 4 times,
+// returned wrong data in the upper quarter-wave under two concurrently replayed graphs on MI355X:
+// tools/dbg_lanes4.py)
+__device__ __forceinline__ float4 sel3(int k, const float4 &a, const float4 &b, const float4 &c) {
+    return k == 0 ? a : (k == 1 ? b : c);
+}
+
 __global__ __launch_bounds__(256) void up2_bilinear_nhwc4_kernel(const float *__restrict__ x, int n, int c4, int ih,
                                                                  int iw, long long xsn, int xsy, int xsx,
                                                                  float *__restrict__ y, long long ysn, int ysy,
@@ -101,6 +109,7 @@ __global__ __launch_bounds__(256) void up2_bilinear_nhwc4_kernel(const float *__
         float la0, la1, lb0, lb1;
         bilin_index(0.5f, 2 * iy, ih, ya0, ya1, la0, la1);
         bilin_index(0.5f, 2 * iy + 1, ih, yb0, yb1, lb0, lb1);
+        const int rm = iy > 0 ? iy - 1 : 0, rp = iy < ih - 1 ? iy + 1 : iy;
         float *y0r = y + nn * ysn + (long long)(2 * iy) * ysy;
         float *y1r = y0r + ysy;
         for (int e = blockIdx.x * 256 + threadIdx.x; e < per_row; e += gridDim.x * 256) {
@@ -109,12 +118,22 @@ __global__ __launch_bounds__(256) void up2_bilinear_nhwc4_kernel(const float *__
             float ma0, ma1, mb0, mb1;
             bilin_index(0.5f, 2 * ix, iw, xa0, xa1, ma0, ma1);
             bilin_index(0.5f, 2 * ix + 1, iw, xb0, xb1, mb0, mb1);
-            const float *ra0 = xb + (long long)ya0 * xsy + 4 * cq, *ra1 = xb + (long long)ya1 * xsy + 4 * cq;
-            const float *rb0 = xb + (long long)yb0 * xsy + 4 * cq, *rb1 = xb + (long long)yb1 * xsy + 4 * cq;
-            auto lerp4 = [](const float *p0, const float *p1, int x0, int x1, int xs, float ly0, float ly1, float lx0,
-                            float lx1) {
-                const float4 a = *(const float4 *)(p0 + x0 * xs), b = *(const float4 *)(p0 + x1 * xs);
-                const float4 c = *(const float4 *)(p1 + x0 * xs), d = *(const float4 *)(p1 + x1 * xs);
+            const int cm = ix > 0 ? ix - 1 : 0, cp = ix < iw - 1 ? ix + 1 : ix;
+            const float *q0 = xb + (long long)rm * xsy + 4 * cq, *q1 = xb + (long long)iy * xsy + 4 * cq,
+                        *q2 = xb + (long long)rp * xsy + 4 * cq;
+            const float4 n00 = *(const float4 *)(q0 + cm * xsx), n01 = *(const float4 *)(q0 + ix * xsx),
+                         n02 = *(const float4 *)(q0 + cp * xsx);
+            const float4 n10 = *(const float4 *)(q1 + cm * xsx), n11 = *(const float4 *)(q1 + ix * xsx),
+                         n12 = *(const float4 *)(q1 + cp * xsx);
+            const float4 n20 = *(const float4 *)(q2 + cm * xsx), n21 = *(const float4 *)(q2 + ix * xsx),
+                         n22 = *(const float4 *)(q2 + cp * xsx);
+            // neighbourhood value of a source (row, column) index pair (every tap lies in [i - 1, i + 1])
+            auto tap = [&](int yy, int xx) {
+                const int a = yy - iy + 1, b = xx - ix + 1;
+                return sel3(a, sel3(b, n00, n01, n02), sel3(b, n10, n11, n12), sel3(b, n20, n21, n22));
+            };
+            auto lerp4 = [&](int y0, int y1, int x0, int x1, float ly0, float ly1, float lx0, float lx1) {
+                const float4 a = tap(y0, x0), b = tap(y0, x1), c = tap(y1, x0), d = tap(y1, x1);
                 float4 v;
                 v.x = ly0 * (lx0 * a.x + lx1 * b.x) + ly1 * (lx0 * c.x + lx1 * d.x);
                 v.y = ly0 * (lx0 * a.y + lx1 * b.y) + ly1 * (lx0 * c.y + lx1 * d.y);
@@ -122,14 +141,10 @@ __global__ __launch_bounds__(256) void up2_bilinear_nhwc4_kernel(const float *__
                 v.w = ly0 * (lx0 * a.w + lx1 * b.w) + ly1 * (lx0 * c.w + lx1 * d.w);
                 return v;
             };
-            const float4 v00 = lerp4(ra0, ra1, xa0, xa1, xsx, la0, la1, ma0, ma1);
-            const float4 v01 = lerp4(ra0, ra1, xb0, xb1, xsx, la0, la1, mb0, mb1);
-            const float4 v10 = lerp4(rb0, rb1, xa0, xa1, xsx, lb0, lb1, ma0, ma1);
-            const float4 v11 = lerp4(rb0, rb1, xb0, xb1, xsx, lb0, lb1, mb0, mb1);
-            *(float4 *)(y0r + (2 * ix) * ysx + 4 * cq) = v00;
-            *(float4 *)(y0r + (2 * ix + 1) * ysx + 4 * cq) = v01;
-            *(float4 *)(y1r + (2 * ix) * ysx + 4 * cq) = v10;
-            *(float4 *)(y1r + (2 * ix + 1) * ysx + 4 * cq) = v11;
+            *(float4 *)(y0r + (2 * ix) * ysx + 4 * cq) = lerp4(ya0, ya1, xa0, xa1, la0, la1, ma0, ma1);
+            *(float4 *)(y0r + (2 * ix + 1) * ysx + 4 * cq) = lerp4(ya0, ya1, xb0, xb1, la0, la1, mb0, mb1);
+            *(float4 *)(y1r + (2 * ix) * ysx + 4 * cq) = lerp4(yb0, yb1, xa0, xa1, lb0, lb1, ma0, ma1);
+            *(float4 *)(y1r + (2 * ix + 1) * ysx + 4 * cq) = lerp4(yb0, yb1, xb0, xb1, lb0, lb1, mb0, mb1);
         }
     }
 }
@@ -699,7 +714,7 @@ extern "C" int s2v_resize(const float *x, int n, int c, int ih, int iw, long lon
                     ysy % 4 == 0 && xsn % 4 == 0 && ysn % 4 == 0 && ((uintptr_t)x % 16) == 0 &&
                     ((uintptr_t)y % 16) == 0 && xsy < (1LL << 31) && ysy < (1LL << 31);
     if (v4 && mode == 0 && oh == 2 * ih && ow == 2 * iw && scale_h == 0.5f && scale_w == 0.5f &&
-        (long long)ysy * 2 < (1LL << 31)) {
+        (long long)ysy * 2 < (1LL << 31) && tune_get(S2V_TUNE_RESIZE_UP2)) {
         // exact x2 (StyleConv / ToRGB upsamples): 2x2 output quads per thread
         const long long row = (long long)iw * (c / 4);
         const unsigned gx = (unsigned)((row + 255) / 256);

@@ -584,6 +584,26 @@ void pad_reflect_(const Tensor &x, const Tensor &y, at::IntArrayRef pads) {
           "s2v_pad_reflect");
 }
 
+// ToRGB + x2 bilinear skip upsample (s2v_torgb_up2): x NHWC view [N, H, W, C], wt packed 1x1 rows
+// [>= 3, kpad], s [N, >= C] row view, bias [3] or None, skip NHWC [N, H/2, W/2, >= 4], y NHWC [N, H, W, >= 4]
+void torgb_up2_(const Tensor &x, const Tensor &wt, const Tensor &s, const OptT &bias, const Tensor &skip,
+                const Tensor &y) {
+    const c10::DeviceGuard guard(x.device());
+    const at::Device dev = x.device();
+    const NV xv = nhwc(x, dev, "torgb x"), kv = nhwc(skip, dev, "torgb skip"), yv = nhwc(y, dev, "torgb y");
+    f32(wt, dev, "torgb wt");
+    TORCH_CHECK(wt.dim() == 2 && wt.is_contiguous() && wt.size(0) >= 3 && wt.size(1) >= xv.c,
+                "torgb wt: packed 1x1 rows [>= 3, kpad >= C]");
+    const int s_ns = (int)rows_view(s, dev, xv.n, xv.c, "torgb s");
+    const float *bp = vec(bias, dev, 3, "torgb bias");
+    TORCH_CHECK(kv.n == xv.n && yv.n == xv.n && yv.h == xv.h && yv.w == xv.w && 2 * kv.h == xv.h && 2 * kv.w == xv.w &&
+                    kv.c == 4 && yv.c == 4,
+                "torgb: skip [N, H/2, W/2, 4] and y [N, H, W, 4] views expected");
+    check(s2v_torgb_up2(xv.p, xv.n, xv.h, xv.w, xv.c, xv.cs, wt.data_ptr<float>(), (int)wt.size(1), s.data_ptr<float>(),
+                        s_ns, bp, kv.p, kv.cs, yv.p, yv.cs, stream()),
+          "s2v_torgb_up2");
+}
+
 // flow NHWC view (>= 2 channels: x, y), src [N, C, H, W] (any strides), y NHWC view [N, H, W, C]
 void flow_warp_(const Tensor &flow, const Tensor &src, const Tensor &y) {
     const c10::DeviceGuard guard(flow.device());
@@ -805,6 +825,7 @@ TORCH_LIBRARY_FRAGMENT(s2v, m) {
     m.def("resize_(Tensor x, int x_off, int[4] x_size, int[4] x_stride, Tensor(a!) y, int y_off, int[4] y_size, "
           "int[4] y_stride, float scale_h, float scale_w, int mode) -> ()");
     m.def("pad_reflect_(Tensor x, Tensor(a!) y, int[4] pads) -> ()");
+    m.def("torgb_up2_(Tensor x, Tensor wt, Tensor s, Tensor? bias, Tensor skip, Tensor(a!) y) -> ()");
     m.def("flow_warp_(Tensor flow, Tensor src, Tensor(a!) y) -> ()");
     m.def("fill_value_(Tensor(a!) y, float value) -> ()");
     m.def("gaussian_noise_(Tensor(a!) y, int seed, int offset, Tensor? ctr, int shift) -> ()");
@@ -836,6 +857,7 @@ TORCH_LIBRARY_IMPL(s2v, CUDA, m) {
     m.impl("attention_", &attention_);
     m.impl("resize_", &resize_);
     m.impl("pad_reflect_", &pad_reflect_);
+    m.impl("torgb_up2_", &torgb_up2_);
     m.impl("flow_warp_", &flow_warp_);
     m.impl("fill_value_", &fill_value_);
     m.impl("gaussian_noise_", &gaussian_noise_);

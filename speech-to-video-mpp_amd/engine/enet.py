@@ -22,6 +22,8 @@ LRELU = 0.2  # ENet.py:94-97, base_blocks.py:41-44, :522
 # the style encoder and LNet are independent until the StyleConvs (ENet.py:94-112): run the style
 # encoder on a side stream beside LNet (S2V_ENET_OVERLAP=0 serialises them)
 OVERLAP = os.environ.get("S2V_ENET_OVERLAP", "1") == "1"
+# ToRGB and its skip upsample as one pass (ops.torgb_up2); S2V_ENET_FUSED_TORGB=0: resize + small conv
+FUSED_TORGB = os.environ.get("S2V_ENET_FUSED_TORGB", "1") == "1"
 
 
 class StyleLayer:
@@ -176,8 +178,11 @@ class ENetEngine:
             R = self.layers[3 * st + 2]
             off = self.mod_offs[3 * st + 2]
             rgb = NHWC.empty(b, cur.h, cur.w, 4, dev)
-            ops.resize_nhwc(ctx, skip, rgb, scale_factor=2)          # skip upsample (base_blocks.py:552)
-            ops.modulated_conv2d(ctx, cur, R.conv, rgb.slice(0, 3), s2[:, off: off + R.cin], res=rgb.slice(0, 3))
+            if FUSED_TORGB and R.cin % 32 == 0 and (cur.h * cur.w) % 32 == 0:
+                ops.torgb_up2(ctx, cur, R.conv, s2[:, off: off + R.cin], skip, rgb)   # + skip upsample (:552)
+            else:
+                ops.resize_nhwc(ctx, skip, rgb, scale_factor=2)      # skip upsample (base_blocks.py:552)
+                ops.modulated_conv2d(ctx, cur, R.conv, rgb.slice(0, 3), s2[:, off: off + R.cin], res=rgb.slice(0, 3))
             skip = rgb
         ops.nhwc_to_nchw(ctx, skip.slice(0, 3), out, crop=(8, 8))    # [:, :, 8:-8, 8:-8]
         return out, low

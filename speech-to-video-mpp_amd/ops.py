@@ -638,7 +638,7 @@ def split_act(ctx: Ctx, x: NHWC, out: NHWC | None = None) -> NHWC:
     return out
 
 
-TUNE_HALO_MIN_BLOCKS, TUNE_GLDS_TILE, TUNE_SMALLK_TILE, TUNE_X3_RATE_512, TUNE_IN_FUSED = 0, 1, 2, 3, 4
+TUNE_HALO_MIN_BLOCKS, TUNE_GLDS_TILE, TUNE_SMALLK_TILE, TUNE_X3_RATE_512, TUNE_IN_FUSED, TUNE_RESIZE_UP2 = 0, 1, 2, 3, 4, 5
 
 
 def tune(ctx: Ctx, key: int, value: int) -> int:
@@ -726,6 +726,16 @@ def nhwc_to_nchw(ctx: Ctx, x: NHWC, out: torch.Tensor, crop=(0, 0)):
     off = x.coff + (crop[0] * x.w + crop[1]) * x.cs
     resize(ctx, x.t, off, (n, c, oh, ow), nhwc_strides(x), out, 0, (oh, ow), out.stride())
     return out
+
+
+def torgb_up2(ctx: Ctx, x: NHWC, cw: "ConvW", s: torch.Tensor, skip: NHWC, y: NHWC):
+    """ToRGB (1x1 modulated conv to 3 channels, no demodulation, + bias) plus the x2 bilinear
+    upsample of ``skip`` in one pass (``s2v::torgb_up2_``, base_blocks.py:536-554).  skip / y carry 4
+    channels (the 4th is the upsampled skip's 4th).  s: [B, cin] row view."""
+    assert cw.kh == cw.kw == 1 and cw.cout == 3 and x.c == cw.cin, "torgb_up2: a 1x1 conv to 3 channels"
+    assert (y.n, y.h, y.w, y.c) == (x.n, x.h, x.w, 4) and (skip.n, 2 * skip.h, 2 * skip.w, skip.c) == (x.n, x.h, x.w, 4)
+    S2V.torgb_up2_(x.v, cw.wt, s, cw.shift, skip.v, y.v)
+    return y
 
 
 def pad_reflect(ctx: Ctx, x: NHWC, y: NHWC, pads):

@@ -569,6 +569,27 @@ def test_small_cout_per_sample_weights(ctx, n, hw, cin):
     assert ((to_nchw(y) - ref).abs() <= 2e-6 * (bound + 1) + 1e-6).all()
 
 
+@pytest.mark.parametrize("n,h,w,cin", [(2, 16, 16, 256), (3, 32, 16, 128), (2, 8, 12, 64), (1, 40, 40, 32)])
+def test_torgb_up2_fused(ctx, n, h, w, cin):
+    """ToRGB + skip upsample in one pass (ops.torgb_up2, base_blocks.py:536-554) against the reference
+    composition: per-sample 1x1 conv of W * s (no demodulation) + bias + F.interpolate(skip, x2,
+    bilinear); the 4th channel is the upsampled skip's 4th.  Pixel counts cover every PPT variant."""
+    wt = rnd(3, cin, 1, 1, seed=61) / math.sqrt(cin)
+    bias = rnd(3, seed=62)
+    x = rnd(n, cin, h, w, seed=63)
+    s = rnd(n, cin, seed=64, lo=0.5, hi=1.5)
+    skip = rnd(n, 4, h // 2, w // 2, seed=65)
+    cw = ConvW(wt.float(), bias.float(), DEV)
+    y = NHWC.empty(n, h, w, 4, DEV)
+    ops.torgb_up2(ctx, nhwc(x.float()), cw, s.float().to(DEV), nhwc(skip.float()), y)
+    up = F.interpolate(skip, scale_factor=2, mode="bilinear", align_corners=False)
+    wb = wt[None] * s[:, None, :, None, None]
+    conv = torch.stack([F.conv2d(x[i:i + 1], wb[i], bias)[0] for i in range(n)])
+    ref = torch.cat([conv + up[:, :3], up[:, 3:]], 1)
+    bound = torch.cat([conv_bound(x * s[:, :, None, None], wt, 1, 0, 1), up[:, 3:].abs()], 1) + up.abs()
+    assert ((to_nchw(y) - ref).abs() <= 2e-6 * (bound + 1) + 1e-6).all()
+
+
 @pytest.mark.parametrize("mag", [1e-2, 30.0])
 def test_f16x3_operand_range(ctx, mag):
     """f16x3 keeps its 3 * 2^-22 per-product bound away from unit scale: activations of magnitude
