@@ -836,6 +836,8 @@ static const TileCfg kTiles[] = {
 // split-fp32 (S2V_PREC_BF16X3 / F16X3) configurations, conv_x3_impl.hpp launch_conv_x3, with the sustained
 // throughput each reaches on a full chip (TFLOP/s fp32-equivalent, MI355X, tools/conv_micro.py r01)
 // and resident blocks per CU (LDS / waves) for the planner's cost model
+// (512x128: 360, set end to end on MI355X r03 — lipsync 29.11 -> 28.35 ms, its 400^2 N = 128 StyleConvs;
+// 420 also displaces the 256x256 tile on N = 256 layers: 28.80 ms)
 struct X3Cfg {
     TileCfg t;
     float tflops;
@@ -844,7 +846,7 @@ struct X3Cfg {
 static const X3Cfg kX3Tiles[] = {
     {{256, 256, 2, 8, 1, 1}, 400.f, 1}, {{128, 128, 2, 8, 1, 1}, 330.f, 2}, {{64, 128, 2, 8, 1, 1}, 260.f, 3},
     {{128, 64, 2, 4, 1, 1}, 290.f, 3},  {{64, 64, 2, 4, 1, 1}, 265.f, 4},   {{128, 32, 4, 4, 1, 1}, 235.f, 4},
-    {{256, 128, 4, 8, 1, 1}, 335.f, 1}, {{256, 64, 8, 8, 1, 1}, 300.f, 2},  {{512, 128, 4, 8, 1, 1}, 330.f, 1},
+    {{256, 128, 4, 8, 1, 1}, 335.f, 1}, {{256, 64, 8, 8, 1, 1}, 300.f, 2},  {{512, 128, 4, 8, 1, 1}, 360.f, 1},
     // two K-slice groups in flight (PF 2) for the 4-wave tiles: forced-only (tflops 0) until measured
     {{128, 64, 2, 4, 1, 2}, 0.f, 3},    {{64, 64, 2, 4, 1, 2}, 0.f, 4},     {{128, 32, 4, 4, 1, 2}, 0.f, 4}};
 constexpr int kNumX3 = sizeof(kX3Tiles) / sizeof(kX3Tiles[0]);

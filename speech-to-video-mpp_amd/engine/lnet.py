@@ -22,6 +22,9 @@ BRANCHES = os.environ.get("S2V_LNET_BRANCHES", "1") == "1"
 PREPAD = os.environ.get("S2V_LNET_PREPAD", "1") == "1"
 # with PREPAD: the InstanceNorm that ends an FFC writes the next FFC's reflect-padded input itself
 FUSED_PAD = os.environ.get("S2V_LNET_FUSED_PAD", "1") == "1"
+# split-K factor forced on the FourierUnit chain's 1x1 convs (st1, fu, st2); 0 = the planner's choice.  1 (no
+# split-K, no reduce launch on the branch): LNet B=16 11.97 -> 11.69 ms on MI355X (r03), lipsync unchanged
+SPEC_SPLITS = int(os.environ.get("S2V_LNET_SPEC_SPLITS", "1"))
 
 AUDIO_CFG = [  # LNet.py:102-120: (stride, padding, residual)
     (1, 1, False), (1, 1, True), (1, 1, True), ((3, 1), 1, False), (1, 1, True), (1, 1, True),
@@ -167,9 +170,10 @@ class FFCLama:
             ops.conv2d(c, xr.slice(0, cl), self.conv_l2g, yg)
 
         def spectral(c):
-            ops.conv2d(c, x.slice(cl, cg), self.st1, t1, act=ops.ACT_RELU)
+            ops.conv2d(c, x.slice(cl, cg), self.st1, t1, act=ops.ACT_RELU, force_splits=SPEC_SPLITS)
             ops.rfft2(c, t1, self.fft, spec)                             # rfftn ortho (ffc.py:99-104)
-            ops.conv2d(c, NHWC(spec.view(b, self.F, 1, 2 * cc)), self.fu, spec2, act=ops.ACT_RELU)
+            ops.conv2d(c, NHWC(spec.view(b, self.F, 1, 2 * cc)), self.fu, spec2, act=ops.ACT_RELU,
+                       force_splits=SPEC_SPLITS)
             ops.irfft2(c, spec2.t.view(b, self.F, 2 * cc), self.fft, u, res=t1)   # irfftn + x (ffc.py:120-126, :158)
 
         if branches is None:
@@ -178,7 +182,7 @@ class FFCLama:
             spectral(ctx)
         else:
             branches.run(ctx, lambda c: ops.conv2d(c, xr, self.conv_to_l, y.slice(0, cl)), l2g, spectral)
-        ops.conv2d(ctx, u, self.st2, yg, res=yg)
+        ops.conv2d(ctx, u, self.st2, yg, res=yg, force_splits=SPEC_SPLITS)
 
     def norm(self, ctx, bank: AdainBank, params, y: NHWC, out: NHWC, res: NHWC | None = None,
              pad_out: NHWC | None = None):

@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Phase timeline of graph-replayed ENet(+LNet) steps from a rocprofv3 --kernel-trace database.
+
+A step starts at its ``fill_kernel`` (the style encoder's input, first kernel of ENet.forward) and
+its StyleConv tail at the first ``modulate_weights`` kernel after it.  Per phase: wall time, busy
+time (union of kernel intervals) and the summed kernel time (> busy when kernels overlap), plus the
+top kernels of each phase.  Usage: timeline.py run_results.db [--steps N]"""
+import sqlite3
+import sys
+from collections import defaultdict
+
+
+def load(path):
+    db = sqlite3.connect(path)
+    cols = [r[1] for r in db.execute("pragma table_info(kernels)")]
+    s = "start" if "start" in cols else "start_ns"
+    e = "end" if "end" in cols else "end_ns"
+    return [(n, a, b) for n, a, b in db.execute(f"select name, {s}, {e} from kernels order by {s}")]
+
+
+def busy(iv):
+    tot, cur_a, cur_b = 0, None, None
+    for a, b in sorted(iv):
+        if cur_b is None or a > cur_b:
+            if cur_b is not None:
+                tot += cur_b - cur_a
+            cur_a, cur_b = a, b
+        else:
+            cur_b = max(cur_b, b)
+    if cur_b is not None:
+        tot += cur_b - cur_a
+    return tot
+
+
+def main():
+    path = sys.argv[1]
+    nsteps = int(sys.argv[sys.argv.index("--steps") + 1]) if "--steps" in sys.argv else 3
+    ks = load(path)
+    starts = [i for i, (n, a, b) in enumerate(ks) if n.startswith("s2v::fill_kernel")]
+    if len(starts) < 2:
+        print("no step markers (fill_kernel) found")
+        return
+    for si in range(max(0, len(starts) - 1 - nsteps), len(starts) - 1):
+        i0, i2 = starts[si], starts[si + 1]
+        step = ks[i0:i2]
+        t0, t2 = step[0][1], ks[i2][1]
+        i1 = next((i for i, (n, a, b) in enumerate(step) if "modulate_weights" in n), None)
+        t1 = step[i1][1] if i1 is not None else t2
+        print(f"step {si}: {(t2 - t0) / 1e3:8.1f} us, {len(step)} kernels")
+        for name, lo, hi in (("encoder+LNet", t0, t1), ("StyleConv tail", t1, t2)):
+            iv = [(max(a, lo), min(b, hi)) for n, a, b in step if b > lo and a < hi]
+            per = defaultdict(float)
+            for n, a, b in step:
+                if b > lo and a < hi:
+                    per[n.split("(")[0][:70]] += (min(b, hi) - max(a, lo)) / 1e3
+            tot = sum(b - a for a, b in iv)
+            print(f"  {name:15s} wall {(hi - lo) / 1e3:8.1f} us  busy {busy(iv) / 1e3:8.1f}  kernel-sum {tot / 1e3:8.1f}  "
+                  f"kernels {len(iv)}")
+            for n, t in sorted(per.items(), key=lambda kv: -kv[1])[:8]:
+                print(f"      {t:8.1f} us  {n}")
+
+
+if __name__ == "__main__" and "--lnet" not in sys.argv:
+    main()
+
+
+def lnet_levels(path):
+    """LNet forward: wall time per decoder level (first rfft2 .. last irfft2 of that size) of the last
+    forward in the trace, with busy time and kernel count, and the encoder part before the decoder."""
+    ks = load(path)
+    hs = (12, 24, 48)
+    last = {h: max(i for i, (n, a, b) in enumerate(ks) if n.startswith(f"void s2v::irfft2_mf<{h},")) for h in hs}
+    first = {}
+    for h in hs:
+        # the last forward's first rfft of this size: walk back 18 rffts from the end
+        idx = [i for i, (n, a, b) in enumerate(ks) if n.startswith(f"void s2v::rfft2_mf<{h},") and i <= last[h]]
+        first[h] = idx[-18]
+    for h in hs:
+        seg = [(a, b) for n, a, b in ks[first[h]: last[h] + 1]]
+        lo, hi = ks[first[h]][1], max(b for a, b in seg)
+        print(f"level {h:2d}x{h:<2d}: wall {(hi - lo) / 1e3:8.1f} us  busy {busy(seg) / 1e3:8.1f}  "
+              f"kernels {len(seg)}  per FFC {(hi - lo) / 18e3:6.1f} us")
+
+
+if __name__ == "__main__" and "--lnet" in sys.argv:
+    lnet_levels(sys.argv[1])
