@@ -164,14 +164,18 @@ int s2v_conv2d_plan(const s2v_conv_params *p, int *out10);
  *                             cout (default, env S2V_SMALLK_TILE); 0: the throughput model;
  *   S2V_TUNE_X3_RATE_512      the planner's sustained rate (TFLOP/s) of the 512x128 split-precision
  *                             tile (0 = the built-in table, env S2V_X3_RATE_512; A/B tuning);
- *   S2V_TUNE_IN_FUSED         1 (env S2V_IN_FUSED): InstanceNorm / ADAIN on planes of <= 256 pixels
- *                             with >= 64 (plane, 256-channel group) blocks runs as one launch; default 0
- *                             (measured in-process, tools/ab_tune.py: LNet 10.59 -> 10.95 ms with it).
+ *   S2V_TUNE_IN_FUSED         max plane pixels (env S2V_IN_FUSED, default 576) of the one-launch InstanceNorm /
+ *                             ADAIN (moments + apply per plane and 16-32-channel group, >= 512 blocks where
+ *                             possible); 0: always stats + apply launches.  576 (LNet 12^2 and 24^2): LNet
+ *                             B=16 11.65 -> 11.43 ms, lipsync 28.5 -> 28.0 ms on MI355X (r03).
  *   S2V_TUNE_RESIZE_UP2       1 (env S2V_RESIZE_UP2, default): exact x2 bilinear resizes take the 2x2-quad
  *                             kernel; 0: the generic float4 resize kernel.
+ *   S2V_TUNE_FFT_X3           1 (env S2V_FFT_X3): the 12 / 24 / 48 square FourierUnit transforms on
+ *                             split-fp32 f16 MFMAs; 0 (default): the exact-fp32 MFMA kernels (the x3 forms
+ *                             measured slower: 48x48 rfft 30 -> 38 us, irfft 35 -> 43 us, r03).
  * Sets ``value``, returns the previous one in *old_value (may be NULL). */
 enum { S2V_TUNE_HALO_MIN_BLOCKS = 0, S2V_TUNE_GLDS_TILE = 1, S2V_TUNE_SMALLK_TILE = 2, S2V_TUNE_X3_RATE_512 = 3,
-       S2V_TUNE_IN_FUSED = 4, S2V_TUNE_RESIZE_UP2 = 5, S2V_TUNE_COUNT = 6 };
+       S2V_TUNE_IN_FUSED = 4, S2V_TUNE_RESIZE_UP2 = 5, S2V_TUNE_FFT_X3 = 6, S2V_TUNE_COUNT = 7 };
 int s2v_tune(int key, long long value, long long *old_value);
 
 /* max |x| over an NHWC view (pixels x c at pitch xcs) -> *out (fp32 bits; NaN propagates as the

@@ -780,9 +780,11 @@ static long long tune_value(int key) {
         e = getenv("S2V_X3_RATE_512");
         g_tune[S2V_TUNE_X3_RATE_512] = e ? atoll(e) : 0;
         e = getenv("S2V_IN_FUSED");
-        g_tune[S2V_TUNE_IN_FUSED] = e ? atoll(e) : 0;
+        g_tune[S2V_TUNE_IN_FUSED] = e ? atoll(e) : 576;   // max plane pixels of the one-launch InstanceNorm
         e = getenv("S2V_RESIZE_UP2");
         g_tune[S2V_TUNE_RESIZE_UP2] = e ? atoll(e) : 1;
+        e = getenv("S2V_FFT_X3");
+        g_tune[S2V_TUNE_FFT_X3] = e ? atoll(e) : 0;
         g_tune_init = true;
     }
     return g_tune[key];

@@ -312,8 +312,8 @@ __global__ __launch_bounds__(256) void in_apply_v(const float *__restrict__ x, i
                                                   int gb_ns, float eps, int act, float alpha, const float *res,
                                                   int res_cs, float *y, int ycs, const double *__restrict__ part,
                                                   int chunks, int achunks, int w = 0, float *yp = nullptr,
-                                                  int ypcs = 0) {
-    const int qb = in_quads(c), nph = 256 / qb;
+                                                  int ypcs = 0, int qbo = 0) {
+    const int qb = qbo > 0 ? qbo : in_quads(c), nph = 256 / qb;
     const int q4 = threadIdx.x % qb, ph = threadIdx.x / qb;
     const int cc = (blockIdx.y * qb + q4) * 4;
     const int n = blockIdx.z;
@@ -335,6 +335,7 @@ __global__ __launch_bounds__(256) void in_apply_v(const float *__restrict__ x, i
             // fused form (part == NULL, one block per plane and channel group): the moments of
             // the whole plane straight from x, then the apply below re-reads it (from L2)
             const float *xs = x + (long long)n * hw * xcs + cc;
+#pragma unroll 4
             for (int p = ph; p < hw; p += nph) {
                 const float4 v = *(const float4 *)(xs + (long long)p * xcs);
                 const double a = v.x, b = v.y, d = v.z, e = v.w;
@@ -434,11 +435,16 @@ static int in_apply_chunks(int n, long long hw, int c, int kv) {
     return (int)k;
 }
 
-// one launch (moments + apply in one block per plane and channel group) for small planes with
-// enough planes to fill the chip (LNet's 12^2 level: 16 x 4 blocks of 144 pixels); opt-in
-// (S2V_TUNE_IN_FUSED): 64 blocks per launch lose more than the saved launch (LNet +3 %, r02)
-static bool in_fused(int n, int hw, unsigned cq) {
-    return tune_get(S2V_TUNE_IN_FUSED) != 0 && hw <= 256 && (long long)n * cq >= 64;
+// One launch (moments + apply in one block per plane and channel group) for planes of at most
+// S2V_TUNE_IN_FUSED pixels (0: never), the channel group narrowed to 16 - 32 channels so the launch
+// has >= 512 blocks where it can (LNet 12^2: 16 x 1024 channels -> 512 blocks of 32 channels; 24^2:
+// 256 blocks of 16): the stats pass, its launch and the dependency gap before the apply go away.
+// (r02's form, one block per 256 channels — 64 blocks at 12^2 — measured slower than two launches.)
+static int in_fused_qb(int n, int hw, int c) {
+    if (hw > tune_get(S2V_TUNE_IN_FUSED)) return 0;
+    int qb = c / 4 < 64 ? c / 4 : 64;
+    while (qb > 4 && (long long)n * cdiv(c, 4 * qb) < 512) qb /= 2;
+    return qb;
 }
 
 // ------------------------------------------------------------------ token LayerNorm
@@ -596,9 +602,10 @@ extern "C" int s2v_instnorm_adain(const float *x, int n, int h, int w, int c, in
         }
         const int qb = c / 4 < 64 ? c / 4 : 64;
         const unsigned cq = cdiv(c, 4 * qb);
-        if (in_fused(n, hw, cq)) {
-            in_apply_v<<<dim3(1, cq, n), 256, 0, s>>>(x, hw, c, xcs, gamma, beta, gb_ns, eps, act, alpha, res, res_cs,
-                                                       y, ycs, nullptr, 1, 1);
+        if (const int qf = in_fused_qb(n, hw, c)) {
+            in_apply_v<<<dim3(1, cdiv(c, 4 * qf), n), 256, 0, s>>>(x, hw, c, xcs, gamma, beta, gb_ns, eps, act, alpha,
+                                                                   res, res_cs, y, ycs, nullptr, 1, 1, 0, nullptr, 0,
+                                                                   qf);
             return check_launch("in_apply");
         }
         in_stats_v<<<dim3(kv, cq, n), 256, 0, s>>>(x, hw, c, xcs, kv, (double *)ws);
@@ -638,9 +645,9 @@ extern "C" int s2v_instnorm_adain_pad(const float *x, int n, int h, int w, int c
     hipStream_t s = (hipStream_t)stream;
     const int qb = c / 4 < 64 ? c / 4 : 64;
     const unsigned cq = cdiv(c, 4 * qb);
-    if (in_fused(n, hw, cq)) {
-        in_apply_v<<<dim3(1, cq, n), 256, 0, s>>>(x, hw, c, xcs, gamma, beta, gb_ns, eps, act, alpha, res, res_cs, y,
-                                                   ycs, nullptr, 1, 1, w, yp, ypcs);
+    if (const int qf = in_fused_qb(n, hw, c)) {
+        in_apply_v<<<dim3(1, cdiv(c, 4 * qf), n), 256, 0, s>>>(x, hw, c, xcs, gamma, beta, gb_ns, eps, act, alpha, res,
+                                                               res_cs, y, ycs, nullptr, 1, 1, w, yp, ypcs, qf);
         return check_launch("in_apply");
     }
     in_stats_v<<<dim3(kv, cq, n), 256, 0, s>>>(x, hw, c, xcs, kv, (double *)ws);

@@ -645,17 +645,18 @@ def test_resblock_skip_as_strided_conv(ctx, prec):
     assert ((to_nchw(y) - ref).abs() <= REL[prec] * (bound + 1) + 1e-6).all()
 
 
-def test_instnorm_fused_small_planes(ctx):
-    """12^2 planes, 16 x 1024 channels: one-launch InstanceNorm (S2V_TUNE_IN_FUSED) against the
-    two-pass form and torch, with the residual and the reflect-padded second output."""
-    n, c, h, w = 16, 1024, 12, 12
+@pytest.mark.parametrize("n,c,h,w", [(16, 1024, 12, 12), (16, 256, 24, 24), (3, 40, 10, 9)])
+def test_instnorm_fused_small_planes(ctx, n, c, h, w):
+    """LNet's 12^2 / 24^2 planes (and a ragged one): one-launch InstanceNorm (S2V_TUNE_IN_FUSED = max
+    plane pixels, narrow channel groups) against the two-pass form and torch, with the residual and
+    the reflect-padded second output."""
     x = rnd(n, c, h, w, seed=31) * 2 - 0.5
     g, bt = rnd(n, c, seed=32), rnd(n, c, seed=33)
     gb = torch.cat([g, bt], 1).float().to(DEV)
     res = rnd(n, c, h, w, seed=34)
     outs = {}
     for fused in (1, 0):
-        prev = ops.tune(ctx, ops.TUNE_IN_FUSED, fused)
+        prev = ops.tune(ctx, ops.TUNE_IN_FUSED, h * w if fused else 0)
         try:
             y = NHWC.empty(n, h, w, c, DEV)
             yp = NHWC.empty(n, h + 2, w + 2, c, DEV)
