@@ -25,6 +25,9 @@ FUSED_PAD = os.environ.get("S2V_LNET_FUSED_PAD", "1") == "1"
 # split-K factor forced on the FourierUnit chain's 1x1 convs (st1, fu, st2); 0 = the planner's choice.  1 (no
 # split-K, no reduce launch on the branch): LNet B=16 11.97 -> 11.69 ms on MI355X (r03), lipsync unchanged
 SPEC_SPLITS = int(os.environ.get("S2V_LNET_SPEC_SPLITS", "1"))
+# encoder branches: calling stream first, then the two side streams (m = masked face, r = reference
+# face, a = audio encoder + ADAIN heads)
+ENC_ORDER = os.environ.get("S2V_LNET_ENC_ORDER", "mra")
 
 AUDIO_CFG = [  # LNet.py:102-120: (stride, padding, residual)
     (1, 1, False), (1, 1, True), (1, 1, True), ((3, 1), 1, False), (1, 1, True), (1, 1, True),
@@ -308,7 +311,8 @@ class LNetEngine:
             reference(ctx)
             audio_enc(ctx)
         else:
-            br.run(ctx, masked, reference, audio_enc)
+            fns = dict(m=masked, r=reference, a=audio_enc)
+            br.run(ctx, *(fns[k] for k in ENC_ORDER))
         self.ca2(ctx, st["xm2"], cat.slice(c, c), cat.slice(0, c))
         ap = st["adain"]                                        # ADAIN gamma / beta of every FFC
         # ---- decoder (LNet.py:67-77)
