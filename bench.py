@@ -193,7 +193,7 @@ def live_roofline(forward, workload="lipsync"):
     # HBM bytes per launch of the same symbol from the PMC passes of this workload (tools/gpu_profile.sh:
     # separate FETCH_SIZE / WRITE_SIZE runs of this bench command; the newest round's file wins)
     traffic, traffic_src = None, None
-    for rnd in ("r02", "r01"):
+    for rnd in ("r03", "r02", "r01"):
         pmc = os.path.join(ROOT, "profiles", f"pmc_{rnd}_{workload}.json")
         if os.path.exists(pmc):
             with open(pmc) as f:
