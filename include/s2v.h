@@ -55,7 +55,8 @@ enum {
 enum { S2V_PAD_ZERO = 0, S2V_PAD_REFLECT = 1 };
 
 /*
- * Fused convolution / GEMM (implicit GEMM on v_mfma_f32_32x32x2_f32, exact fp32).
+ * Fused convolution / GEMM: implicit GEMM on the MFMA, in the arithmetic ``prec`` selects (below;
+ * default S2V_PREC_F16X3: split-fp32 operands on v_mfma_f32_16x16x32_f16, fp32 accumulate).
  *   out[n, oy, ox, o] = epilogue( sum_{ky,kx,c} A(n, oy, ox, ky, kx, c) * W[o][(ky*kw + kx)*cin + c] )
  * A = prologue(x) addressed per ``in_mode`` / ``pad_mode``; prologue = act(x * in_scale[n, c]).
  * Epilogue order:  v = acc * scale[o] * nc_scale[n, o] + shift[o] + pix_w * pix_add[n, oy, ox]
