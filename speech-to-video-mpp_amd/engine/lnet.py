@@ -28,6 +28,9 @@ SPEC_SPLITS = int(os.environ.get("S2V_LNET_SPEC_SPLITS", "1"))
 # encoder branches: calling stream first, then the two side streams (m = masked face, r = reference
 # face, a = audio encoder + ADAIN heads)
 ENC_ORDER = os.environ.get("S2V_LNET_ENC_ORDER", "mra")
+# split-K forced on the FFC's conv_to_l / l2g at the 12^2 level (0 = the planner's choice)
+C2L_SPLITS = int(os.environ.get("S2V_LNET_C2L_SPLITS", "0"))
+L2G_SPLITS = int(os.environ.get("S2V_LNET_L2G_SPLITS", "0"))
 
 AUDIO_CFG = [  # LNet.py:102-120: (stride, padding, residual)
     (1, 1, False), (1, 1, True), (1, 1, True), ((3, 1), 1, False), (1, 1, True), (1, 1, True),
@@ -169,8 +172,12 @@ class FFCLama:
             xr = NHWC.empty(b, self.h + 2, self.w + 2, x.c, dev)
             ops.pad_reflect(ctx, x, xr, (1, 1, 1, 1))
 
+        small = self.h <= 12
+        fs_l2g = L2G_SPLITS if small else 0
+        fs_c2l = C2L_SPLITS if small else 0
+
         def l2g(c):
-            ops.conv2d(c, xr.slice(0, cl), self.conv_l2g, yg)
+            ops.conv2d(c, xr.slice(0, cl), self.conv_l2g, yg, force_splits=fs_l2g)
 
         def spectral(c):
             ops.conv2d(c, x.slice(cl, cg), self.st1, t1, act=ops.ACT_RELU, force_splits=SPEC_SPLITS)
@@ -180,11 +187,12 @@ class FFCLama:
             ops.irfft2(c, spec2.t.view(b, self.F, 2 * cc), self.fft, u, res=t1)   # irfftn + x (ffc.py:120-126, :158)
 
         if branches is None:
-            ops.conv2d(ctx, xr, self.conv_to_l, y.slice(0, cl))
+            ops.conv2d(ctx, xr, self.conv_to_l, y.slice(0, cl), force_splits=fs_c2l)
             l2g(ctx)
             spectral(ctx)
         else:
-            branches.run(ctx, lambda c: ops.conv2d(c, xr, self.conv_to_l, y.slice(0, cl)), l2g, spectral)
+            branches.run(ctx, lambda c: ops.conv2d(c, xr, self.conv_to_l, y.slice(0, cl), force_splits=fs_c2l), l2g,
+                         spectral)
         ops.conv2d(ctx, u, self.st2, yg, res=yg, force_splits=SPEC_SPLITS)
 
     def norm(self, ctx, bank: AdainBank, params, y: NHWC, out: NHWC, res: NHWC | None = None,
