@@ -140,6 +140,12 @@ typedef struct s2v_conv_params {
      * (s2v_amax). */
     float x_scale;
     int *nonfinite;
+    /* Depth-to-space output (the polyphase x2-bilinear-upsample StyleConv, ENet.py:119-129 via
+     * base_blocks.py:487-533): with d2s_cout > 0 (requires out_step == 2, cout == 4 * d2s_cout, no
+     * res / pool) output column n = cls * d2s_cout + o of conv pixel (n_, oy, ox) goes to
+     * y + ((n_*out_full_h + 2*oy + cls/2)*out_full_w + 2*ox + cls%2)*ycs + o, and pix_add is read
+     * at that full-resolution pixel ([N, out_full_h, out_full_w]). */
+    int d2s_cout;
 } s2v_conv_params;
 
 enum { S2V_PREC_F32 = 0, S2V_PREC_BF16X3 = 1, S2V_PREC_F16X3 = 2 };

@@ -49,6 +49,7 @@ class ConvParams(ctypes.Structure):
         ("stamps", _vp), ("stamp_ctr", _vp), ("stamp_slot", _c_int), ("stamp_stride", _c_int),
         ("stamp_reps", _c_int),
         ("x_scale", _c_float), ("nonfinite", _vp),
+        ("d2s_cout", _c_int),
     ]
 
 

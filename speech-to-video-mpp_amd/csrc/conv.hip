@@ -212,7 +212,7 @@ __device__ __forceinline__ void store_epilogue4(const ConvArgs &a, int bidx, int
     }
     if (e.scale) v *= *(const f4 *)(e.scale + n);
     if (e.shift) v += *(const f4 *)(e.shift + n);
-    if (e.pix_add) v += e.pix_w * e.pix_add[(long long)bidx * a.oh * a.ow * a.n + m];
+    if (e.pix_add) v += e.pix_w * e.pix_add[pix_index(a, bidx, m, n)];
     f4 r = {0.f, 0.f, 0.f, 0.f};
     if (e.res) {
         r = *(const f4 *)(e.res + (long long)bidx * a.res_bs + (long long)m * e.res_cs + n);
@@ -1146,7 +1146,8 @@ static int validate(const s2v_conv_params *p, int &M, int &K) {
                 "conv2d: bad shape n=%d h=%d w=%d cin=%d cout=%d oh=%d ow=%d", p->n, p->h, p->w, p->cin,
                 p->cout, p->oh, p->ow);
     S2V_REQUIRE(p->kh > 0 && p->kw > 0 && p->sh > 0 && p->sw > 0 && p->dh > 0 && p->dw > 0, "conv2d: bad kernel");
-    S2V_REQUIRE(p->xcs >= p->cin && p->ycs >= p->cout, "conv2d: channel stride smaller than channels");
+    S2V_REQUIRE(p->xcs >= p->cin && p->ycs >= (p->d2s_cout > 0 ? p->d2s_cout : p->cout),
+                "conv2d: channel stride smaller than channels");
     S2V_REQUIRE(p->in_mode >= 0 && p->in_mode <= 2, "conv2d: bad in_mode %d", p->in_mode);
     S2V_REQUIRE(!(p->pad_mode == S2V_PAD_REFLECT && p->in_mode == S2V_IN_TRANSPOSED),
                 "conv2d: reflect padding only with direct or nearest-x2 input");
@@ -1176,8 +1177,11 @@ static int validate(const s2v_conv_params *p, int &M, int &K) {
         S2V_REQUIRE(p->x_split || (!(use_direct(p) && !p->force_tile) && !is_smallk(p)),
                     "conv2d: out_pool needs the implicit-GEMM path");
     }
+    if (p->d2s_cout > 0)
+        S2V_REQUIRE(p->out_step == 2 && p->cout == 4 * p->d2s_cout && !p->res && !p->out_pool && !p->nc_scale,
+                    "conv2d: depth-to-space output needs out_step 2, cout == 4 * d2s_cout, no res / pool / nc_scale");
     if (p->out_step > 1) {
-        S2V_REQUIRE(!p->pix_add, "conv2d: strided output cannot take pix_add");
+        S2V_REQUIRE(!p->pix_add || p->d2s_cout > 0, "conv2d: strided output cannot take pix_add");
         S2V_REQUIRE(!p->res || (p->res == p->y && p->res_cs == p->ycs && p->res_oy == 0 && p->res_ox == 0),
                     "conv2d: strided output only takes an in-place residual (res == y)");
         S2V_REQUIRE(p->cout > 4 || p->x_split, "conv2d: strided output needs the implicit-GEMM path (cout > 4)");
@@ -1205,6 +1209,7 @@ static ConvArgs make_args(const s2v_conv_params *p, int M, int K, const Plan &pl
     a.x_bs = p->x_bs; a.w_bs = p->w_bs; a.y_bs = p->y_bs; a.res_bs = p->res_bs;
     a.M = M; a.K = K; a.ktiles = pl.ktiles; a.splits = pl.splits; a.tps = pl.tps; a.ws = p->ws;
     a.y_step = p->out_step > 1 ? p->out_step : 1; a.y_h = p->out_full_h; a.y_w = p->out_full_w;
+    a.d2s_c = p->d2s_cout > 0 ? p->d2s_cout : 0;
     a.cnt = nullptr;
     a.acc_scale = ((p->x_split || tiled_x3(p)) && !p->b_kn && p->wt_scale > 0.f) ? 1.f / p->wt_scale : 1.f;
     a.pool = p->out_pool != 0;

@@ -34,6 +34,7 @@ struct ConvArgs {
     int M, K, ktiles, splits, tps;
     float *ws;
     int y_step, y_h, y_w;   // strided (polyphase) output, y_step > 1
+    int d2s_c;              // depth-to-space output (s2v_conv_params.d2s_cout), 0 = off
     int *cnt;               // split-K tile counters (in-launch fold), or null
     float acc_scale;        // accumulator factor before the epilogue (1 / the split weights' pre-scale)
     unsigned x_bytes, w_bytes;   // buffer-load extents of one batch slab of x / of the weights (AMODE 4)
@@ -70,6 +71,25 @@ __device__ __forceinline__ long long out_row(const ConvArgs &a, long long m) {
     return ((img * a.y_h + (long long)oy * a.y_step) * a.y_w + (long long)ox * a.y_step) * a.ycs;
 }
 
+// Element offset of output column n relative to out_row(): n, or under depth-to-space
+// (a.d2s_c > 0) the output channel n % d2s_c at the parity-class pixel cls = n / d2s_c
+__device__ __forceinline__ long long out_col(const ConvArgs &a, int n) {
+    if (a.d2s_c <= 0) return n;
+    const int cls = n / a.d2s_c;
+    return ((long long)(cls >> 1) * a.y_w + (cls & 1)) * a.ycs + (n - cls * a.d2s_c);
+}
+
+// pix_add element of output row m (conv pixel) and column n
+__device__ __forceinline__ long long pix_index(const ConvArgs &a, int bidx, int m, int n) {
+    if (a.d2s_c <= 0) return (long long)bidx * a.oh * a.ow * a.n + m;
+    const int hw = a.oh * a.ow;
+    const int img = m / hw, rem = m - img * hw;
+    const int oy = rem / a.ow, ox = rem - (rem / a.ow) * a.ow;
+    const int cls = n / a.d2s_c;
+    return (long long)bidx * a.y_h * a.y_w * a.n + ((long long)img * a.y_h + 2 * oy + (cls >> 1)) * a.y_w + 2 * ox +
+           (cls & 1);
+}
+
 __device__ __forceinline__ void store_epilogue(const ConvArgs &a, int bidx, int m, int n, float v) {
     const Epi &e = a.epi;
     const int hw = a.oh * a.ow;
@@ -83,7 +103,7 @@ __device__ __forceinline__ void store_epilogue(const ConvArgs &a, int bidx, int 
     if (e.scale) v *= e.scale[n];
     if (e.nc_scale) v *= e.nc_scale[(long long)img * e.nc_ns + n];
     if (e.shift) v += e.shift[n];
-    if (e.pix_add) v += e.pix_w * e.pix_add[(long long)bidx * hw * a.n + m];
+    if (e.pix_add) v += e.pix_w * e.pix_add[pix_index(a, bidx, m, n)];
     float r = 0.f;
     if (e.res) {
         long long off = a.y_step > 1 ? out_row(a, m)     // in-place residual on a strided output
@@ -95,7 +115,7 @@ __device__ __forceinline__ void store_epilogue(const ConvArgs &a, int bidx, int 
     }
     v = apply_act(v, e.act, e.alpha);
     if (e.res && e.res_after) v += r;
-    a.y[(long long)bidx * a.y_bs + out_row(a, m) + n] = v;
+    a.y[(long long)bidx * a.y_bs + out_row(a, m) + out_col(a, n)] = v;
 }
 
 // Map an output pixel + filter tap to an input pixel; false -> zero padding.
@@ -391,7 +411,7 @@ __device__ __forceinline__ void epilogue_tile_fn(const ConvArgs &a, float *Cs, i
             for (int rr = tid / TPR; rr < clim; rr += RSTEP)
                 w[(long long)(m0 + c0 + rr) * a.cout + n] = Cs[rr * LDC + cn];
         } else if (simple) {
-            float *__restrict__ yb = a.y + (long long)bidx * a.y_bs + n;
+            float *__restrict__ yb = a.y + (long long)bidx * a.y_bs + out_col(a, n);
             const float *rsrc = e.res ? e.res + (long long)bidx * a.res_bs + n : nullptr;
             int rr0 = tid / TPR;
             if (rsrc && a.y_step <= 1) {

@@ -297,15 +297,39 @@ std::vector<int64_t> modulated_conv2d_(const Tensor &x, const Tensor &y, const T
                                        const OptT &shift, const OptT &pix_add,
                                        double pix_w, const OptT &res, bool res_after_act, int64_t act, double alpha,
                                        const OptT &ws, int64_t force_splits, const OptT &stamps, const OptT &stamp_ctr,
-                                       at::IntArrayRef stamp_pos, double x_scale, const OptT &nonfinite, bool dry) {
+                                       at::IntArrayRef stamp_pos, double x_scale, const OptT &nonfinite, bool dry,
+                                       int64_t d2s) {
     const c10::DeviceGuard guard(x.device());
     const at::Device dev = x.device();
     s2v_conv_params p{};
     const int64_t one[2] = {1, 1}, zero[2] = {0, 0};
     TORCH_CHECK(in_mode == S2V_IN_DIRECT || in_mode == S2V_IN_NEAREST_UP2, "modconv: direct or nearest-x2 input");
-    conv_common(p, x, y, cout, kernel, at::IntArrayRef(one, 2), padding, at::IntArrayRef(one, 2), in_mode,
-                S2V_PAD_ZERO, scale, shift, pix_add, pix_w, res, at::IntArrayRef(zero, 2), res_after_act, act, alpha, 1,
-                false, x_split, true, prec, 0, force_splits);
+    if (d2s) {
+        // depth-to-space (polyphase x2 upsample): y is the full [N, 2H, 2W, cout / 4] output; the conv
+        // runs on x's grid with its 4 parity classes as 4 blocks of cout / 4 output columns
+        TORCH_CHECK(cout % 4 == 0 && in_mode == S2V_IN_DIRECT && !has(res) && y.dim() == 4 &&
+                        y.size(3) == cout / 4 && y.size(1) % 2 == 0 && y.size(2) % 2 == 0,
+                    "modconv d2s: y [N, 2H, 2W, cout / 4], direct input, no res");
+        const Tensor yc = y.slice(1, 0, y.size(1), 2).slice(2, 0, y.size(2), 2);   // parity class (0, 0)
+        conv_common(p, x, yc, cout / 4, kernel, at::IntArrayRef(one, 2), padding, at::IntArrayRef(one, 2), in_mode,
+                    S2V_PAD_ZERO, scale, shift, c10::nullopt, 0.0, res, at::IntArrayRef(zero, 2), false, act, alpha, 2,
+                    false, x_split, true, prec, 0, force_splits);
+        p.cout = (int)cout;
+        p.d2s_cout = (int)(cout / 4);
+        TORCH_CHECK(!p.scale || (scale->numel() >= cout), "modconv d2s: scale needs cout entries");
+        TORCH_CHECK(!p.shift || (shift->numel() >= cout), "modconv d2s: shift needs cout entries");
+        if (has(pix_add)) {
+            f32(*pix_add, dev, "modconv pix_add");
+            TORCH_CHECK(pix_add->is_contiguous() && pix_add->numel() == y.size(0) * y.size(1) * y.size(2),
+                        "modconv d2s pix_add: contiguous [N, 2H, 2W]");
+            p.pix_add = pix_add->data_ptr<float>();
+            p.pix_w = (float)pix_w;
+        }
+    } else {
+        conv_common(p, x, y, cout, kernel, at::IntArrayRef(one, 2), padding, at::IntArrayRef(one, 2), in_mode,
+                    S2V_PAD_ZERO, scale, shift, pix_add, pix_w, res, at::IntArrayRef(zero, 2), res_after_act, act, alpha,
+                    1, false, x_split, true, prec, 0, force_splits);
+    }
     f32(wt, dev, "modconv wt");
     TORCH_CHECK(wt.dim() == 2 && wt.is_contiguous() && wt.size(0) >= cout, "modconv wt: packed [npad, kpad]");
     const int npad = (int)wt.size(0), kpad = (int)wt.size(1), K = p.kh * p.kw * p.cin, B = p.batch;
@@ -807,7 +831,7 @@ TORCH_LIBRARY_FRAGMENT(s2v, m) {
           "Tensor? pix_add, "
           "float pix_w, Tensor? res, "
           "bool res_after_act, int act, float alpha, Tensor? ws, int force_splits, Tensor(s!)? stamps, Tensor? stamp_ctr, "
-          "int[3] stamp_pos, float x_scale, Tensor(f!)? nonfinite, bool dry) -> int[]");
+          "int[3] stamp_pos, float x_scale, Tensor(f!)? nonfinite, bool dry, int d2s=0) -> int[]");
     m.def("amax_(Tensor x, Tensor(a!) out) -> ()");
     m.def("gemm_kn_(Tensor a, Tensor b, Tensor(a!) out, int batch, int a_bs, int b_bs, int out_bs, Tensor? res, "
           "int res_bs, int act, float alpha, int prec, Tensor? ws, int force_tile, int force_splits, bool dry) -> int[]");

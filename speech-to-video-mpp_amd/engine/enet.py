@@ -24,6 +24,23 @@ LRELU = 0.2  # ENet.py:94-97, base_blocks.py:41-44, :522
 OVERLAP = os.environ.get("S2V_ENET_OVERLAP", "1") == "1"
 # ToRGB and its skip upsample as one pass (ops.torgb_up2); S2V_ENET_FUSED_TORGB=0: resize + small conv
 FUSED_TORGB = os.environ.get("S2V_ENET_FUSED_TORGB", "1") == "1"
+# x2-upsample StyleConvs on >= 32 channels as one polyphase conv over the un-upsampled input
+# (ops.modulated_conv2d d2s: the bilinear taps folded into 4 parity-class filters, written depth-to-space)
+# plus the four border lines recomputed exactly; S2V_ENET_POLY_UP=0: upsample pass + conv
+POLY_UP = os.environ.get("S2V_ENET_POLY_UP", "1") == "1"
+
+# x2 bilinear upsample (align_corners=False) followed by a 3-tap conv, per output parity r: weight of
+# input tap a (i-1, i, i+1) from conv tap p (-1, 0, 1), away from the image border
+_FOLD = (((0.75, 0.25, 0.0), (0.25, 0.75, 0.75), (0.0, 0.0, 0.25)),
+         ((0.25, 0.0, 0.0), (0.75, 0.75, 0.25), (0.0, 0.25, 0.75)))
+
+
+def fold_up2_conv3(w: torch.Tensor) -> torch.Tensor:
+    """[O, I, 3, 3] conv weights applied after a x2 bilinear upsample -> [4 O, I, 3, 3]: the 3x3 filters
+    of the four output parity classes (ry, rx) (class-major) over the un-upsampled input."""
+    f = torch.tensor(_FOLD, dtype=torch.float64)
+    wd = w.double()
+    return torch.cat([torch.einsum("ap,bq,oipq->oiab", f[ry], f[rx], wd) for ry in (0, 1) for rx in (0, 1)]).float()
 
 
 class StyleLayer:
@@ -47,6 +64,10 @@ class StyleLayer:
             self.mod_b = torch.cat([self.mod_b, torch.zeros(self.cin - self.mod_b.shape[0])])
         self.noise_w = None if is_rgb else float(sd[p + "weight"].float().reshape(-1)[0])
         self.device = device
+        self.conv4 = self.wsq4 = None
+        if upsample and self.k == 3 and self.cin % 32 == 0:
+            self.conv4 = ConvW(fold_up2_conv3(w), bias.repeat(4), device, padding=1)
+            self.wsq4 = self.wsq.repeat(4, 1).contiguous()
 
 
 class ENetEngine:
@@ -95,6 +116,47 @@ class ENetEngine:
         """(stream, Ctx) of the calling lane for the style encoder branch (CUDA devices only)."""
         side = ctx.streams(("enet", id(self)), 1)
         return None if side is None else side[0]
+
+    def _poly_styleconv(self, ctx, L, cur: NHWC, s, idx, noises, ctr):
+        """StyleConv(sample_mode='upsample') (base_blocks.py:500-533): F.interpolate(x, 2, bilinear) then
+        the modulated 3x3 conv + noise + bias + LeakyReLU, as one depth-to-space conv over ``cur`` with
+        the folded parity-class filters (L.conv4).  The fold assumes every upsampled row / column is an
+        interior one: the clamped edge rows of the upsample and the conv's zero padding break that on
+        the two outermost output lines of each side, so those are recomputed from 2-pixel strips of
+        ``cur`` the direct way (upsample + conv with L.conv; every tap they read is exact) and copied
+        in."""
+        dev, b = self.device, cur.n
+        h2, w2 = 2 * cur.h, 2 * cur.w
+        d4 = torch.empty((b, L.conv4.cout), device=dev)
+        ops.modconv_demod(ctx, s, L.wsq4, d4, eps=1e-8, post=math.sqrt(2.0))
+        d = d4[:, : L.cout]                                      # the class-0 block: the layer's own demod
+        noise = None
+        if L.noise_w:
+            if noises is not None and noises[idx] is not None:
+                noise = noises[idx].reshape(b, h2, w2).contiguous()
+            else:
+                noise = torch.empty((b, h2, w2), device=dev)
+                ops.gaussian_noise(ctx, noise, self.noise_seed, idx << 36, ctr=ctr, shift=40)
+        y = NHWC.empty(b, h2, w2, L.cout, dev)
+        kw = dict(act=ops.ACT_LRELU, alpha=LRELU, pix_w=L.noise_w or 0.0)
+        ops.modulated_conv2d(ctx, cur, L.conv4, y, s, d4, pix_add=noise, d2s=True, **kw)
+        c = cur.c
+        # (x strip, its noise, the strip output lines kept, where they go): each strip's x2 upsample is
+        # exact on the lines the kept outputs read (the clamped source row / column is the image's own)
+        strips = ((cur.t[:, 0:2], lambda t: t[:, 0:4], lambda t: t[:, 0:2], lambda t: t[:, 0:2]),
+                  (cur.t[:, cur.h - 2:], lambda t: t[:, h2 - 4:], lambda t: t[:, 2:4], lambda t: t[:, h2 - 2:]),
+                  (cur.t[:, :, 0:2], lambda t: t[:, :, 0:4], lambda t: t[:, :, 0:2], lambda t: t[:, :, 0:2]),
+                  (cur.t[:, :, cur.w - 2:], lambda t: t[:, :, w2 - 4:], lambda t: t[:, :, 2:4],
+                   lambda t: t[:, :, w2 - 2:]))
+        for xs_t, nsel, ssel, ysel in strips:
+            xs = NHWC(xs_t.contiguous())
+            up = NHWC.empty(b, 2 * xs.h, 2 * xs.w, c, dev)
+            ops.resize_nhwc(ctx, xs, up, scale_factor=2)
+            ys = NHWC.empty(b, up.h, up.w, L.cout, dev)
+            nz = None if noise is None else nsel(noise).contiguous()
+            ops.modulated_conv2d(ctx, up, L.conv, ys, s, d, pix_add=nz, **kw)
+            ysel(y.t).copy_(ssel(ys.t))
+        return y
 
     def style_code(self, ctx, ref: torch.Tensor):
         """ref: NCHW [B,3,H,W] device tensor -> style [B,1,1,512] (ENet.py:94-101)."""
@@ -158,6 +220,9 @@ class ENetEngine:
             for li in range(2):
                 L = self.layers[3 * st + li]
                 off = self.mod_offs[3 * st + li]
+                if POLY_UP and L.conv4 is not None:
+                    cur = self._poly_styleconv(ctx, L, cur, s2[:, off: off + L.cin], 2 * st + li, noises, ctr)
+                    continue
                 x = cur
                 if L.upsample:
                     x = NHWC.empty(b, 2 * cur.h, 2 * cur.w, cur.c, dev)

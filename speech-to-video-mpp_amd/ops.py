@@ -546,15 +546,21 @@ def _run_conv(ctx, launch, x, cw, yv, pool, in_scale=None, nc_scale=None, pix_ad
 
 def modulated_conv2d(ctx: Ctx, x: NHWC, cw: ConvW, y: NHWC, s: torch.Tensor, d: torch.Tensor | None = None, *,
                      act=ACT_NONE, alpha=0.0, res: NHWC | None = None, res_after=False, pix_add=None, pix_w=0.0,
-                     shift=None, force_splits=0):
+                     shift=None, force_splits=0, d2s=False):
     """StyleGAN2 modulated conv with per-sample weights W * s[b, c] (* d[b, o]) written by the
     ``s2v::modulated_conv2d_`` op in the form its planned kernel reads (split layout with a 2^11 f16
     pre-scale when demodulated, or fp32), then one batched conv (no prologue / epilogue scaling in
-    the GEMM).  s: [B, cin] (row stride s.stride(0)); d: [B, cout] demodulation or None."""
+    the GEMM).  s: [B, cin] (row stride s.stride(0)); d: [B, cout] demodulation or None.
+    ``d2s``: cw holds the 4 parity classes of a x2-upsampled conv (cout = 4 classes x c, class-major)
+    and y is the full [B, 2H, 2W, c] output (s2v_conv_params.d2s_cout); pix_add is then [B, 2H, 2W]."""
     oh, ow = cw.out_hw(x.h, x.w)
     assert cw.in_mode != IN_TRANSPOSED and cw.poly is None and (cw.sh, cw.sw, cw.dh, cw.dw) == (1, 1, 1, 1), \
         "modulated_conv2d: direct stride-1 convs only"
-    assert x.c == cw.cin and (y.n, y.h, y.w, y.c) == (x.n, oh, ow, cw.cout)
+    if d2s:
+        assert x.c == cw.cin and cw.cout % 4 == 0 and res is None and (y.n, y.h, y.w, y.c) == (x.n, 2 * oh, 2 * ow,
+                                                                                             cw.cout // 4)
+    else:
+        assert x.c == cw.cin and (y.n, y.h, y.w, y.c) == (x.n, oh, ow, cw.cout)
     wbuf = torch.empty((x.n, cw.npad, cw.kpad), device=cw.wt.device)
     yv, resv = y.v, None if res is None else res.v
     prec = prec_code()
@@ -569,8 +575,10 @@ def modulated_conv2d(ctx: Ctx, x: NHWC, cw: ConvW, y: NHWC, s: torch.Tensor, d: 
         return S2V.modulated_conv2d_(x.v, yv, cw.wt, s, d, wbuf, cw.cout, [cw.kh, cw.kw], [cw.ph, cw.pw], cw.in_mode,
                                      prec,
                                      x_split != 0, cw.scale, sh, pix_add, pix_w, resv, res_after, act, alpha, ws,
-                                     force_splits, st[0], st[1], st[2], xscale, flag, dry)
-    _run_conv(ctx, launch, x, cw, yv, False, pix_add=pix_add, resv=resv)
+                                     force_splits, st[0], st[1], st[2], xscale, flag, dry, int(d2s))
+    # roofline accounting on the conv's own grid (one parity class of y x all 4 x c columns = the
+    # upsampled conv's FLOPs)
+    _run_conv(ctx, launch, x, cw, yv[:, ::2, ::2, :] if d2s else yv, False, pix_add=pix_add, resv=resv)
     return y
 
 

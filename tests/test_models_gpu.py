@@ -135,6 +135,34 @@ def test_enet_batch16_vs_oracle(prec, enet):
     assert (out2 - out[8:10]).abs().max() < 2e-3
 
 
+def test_enet_polyphase_upsample_matches_upsample_pass():
+    """The 200^2 -> 400^2 StyleConv as a depth-to-space polyphase conv with exact border lines
+    (engine.enet.POLY_UP) against the upsample pass + conv, whole frames including every border
+    pixel, with explicit StyleConv noise at a non-zero weight on both paths."""
+    from s2v_amd.engine import enet as E
+    mel, face, gt = synth.lipsync_inputs("enet.poly", 2, 256)
+    args = [torch.from_numpy(a).to(DEV) for a in (mel, face, gt)]
+    g = torch.Generator(device=DEV).manual_seed(5)
+    noises = [torch.randn((2, 1, 100 * 2 ** (i // 2 + 1), 100 * 2 ** (i // 2 + 1)), generator=g, device=DEV)
+              for i in range(4)]
+    from s2v_amd import models
+    sd = {k: (torch.full_like(v, 0.05) if k.startswith("style_convs.") and k.endswith(".weight") and v.numel() == 1
+              else v) for k, v in synth_sd("enet").items()}
+    model = models.ENet()
+    model.load_state_dict(sd, strict=True)
+    model.eval()
+    outs = {}
+    for poly in (True, False):
+        prev = E.POLY_UP
+        E.POLY_UP = poly
+        try:
+            outs[poly] = model(*args, noises=noises)[0]
+        finally:
+            E.POLY_UP = prev
+    err = (outs[True] - outs[False]).abs()
+    assert err.max() < 2e-3 and err.mean() < 2e-5, (float(err.max()), float(err.mean()))
+
+
 def test_enet_5d_input_fold(enet):
     """ENet.forward folds [B, C, T, H, W] face / gt and [B, T, 1, 80, 16] audio into the batch and
     unfolds the outputs (ENet.py:87-91, :131-137)."""

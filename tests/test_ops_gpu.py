@@ -590,6 +590,33 @@ def test_torgb_up2_fused(ctx, n, h, w, cin):
     assert ((to_nchw(y) - ref).abs() <= 2e-6 * (bound + 1) + 1e-6).all()
 
 
+@pytest.mark.parametrize("n,cin,h,w,cout", [(2, 64, 9, 7, 32), (3, 32, 12, 16, 128)])
+def test_modulated_conv_d2s_polyphase(ctx, prec, n, cin, h, w, cout):
+    """x2-bilinear-upsample + modulated 3x3 conv as one depth-to-space conv over the un-upsampled
+    input with the four folded parity-class filters (engine.enet.fold_up2_conv3, s2v_conv_params
+    .d2s_cout) against the reference order (F.interpolate, then the per-sample conv + noise + bias +
+    LeakyReLU, base_blocks.py:500-533), away from the two outermost output lines of each side (the
+    engine recomputes those directly; tests/test_models_gpu.py covers the composed frame)."""
+    from s2v_amd.engine.enet import fold_up2_conv3
+    wt = rnd(cout, cin, 3, 3, seed=71) / math.sqrt(cin * 9)
+    bias = rnd(cout, seed=72)
+    x = rnd(n, cin, h, w, seed=73)
+    s = rnd(n, cin, seed=74, lo=0.5, hi=1.5)
+    d = rnd(n, cout, seed=75, lo=0.5, hi=1.5)
+    noise = rnd(n, 2 * h, 2 * w, seed=76)
+    cw4 = ConvW(fold_up2_conv3(wt.float()), bias.float().repeat(4), DEV, padding=1)
+    y = NHWC.empty(n, 2 * h, 2 * w, cout, DEV)
+    ops.modulated_conv2d(ctx, nhwc(x.float()), cw4, y, s.float().to(DEV), d.float().repeat(1, 4).to(DEV),
+                         act=ops.ACT_LRELU, alpha=0.2, pix_add=noise.float().to(DEV), pix_w=0.3, d2s=True)
+    up = F.interpolate(x, scale_factor=2, mode="bilinear", align_corners=False)
+    wb = wt[None] * s[:, None, :, None, None] * d[:, :, None, None, None]
+    conv = torch.stack([F.conv2d(up[i:i + 1], wb[i], bias, padding=1)[0] for i in range(n)])
+    ref = F.leaky_relu(conv + 0.3 * noise[:, None], 0.2)
+    bound = torch.stack([F.conv2d(up[i:i + 1].abs(), wb[i].abs(), padding=1)[0] for i in range(n)]) + 1
+    err = (to_nchw(y) - ref).abs()[:, :, 2:-2, 2:-2]
+    assert (err <= 4 * REL[prec] * bound[:, :, 2:-2, 2:-2] + 1e-6).all(), f"max err {err.max():.3e}"
+
+
 @pytest.mark.parametrize("mag", [1e-2, 30.0])
 def test_f16x3_operand_range(ctx, mag):
     """f16x3 keeps its 3 * 2^-22 per-product bound away from unit scale: activations of magnitude
