@@ -905,6 +905,12 @@ def worker(args):
     config["conv_arith"] = ARITH[args.precision]
     if pre is not None:
         result["roofline"] = replay_roofline(pre, stamper)
+        from s2v_amd.engine import enet as _enet
+        if args.workload in ("lipsync", "pipeline", "clip") and _enet.OVERLAP and _enet.STYLE_GRID:
+            result["roofline"]["grid_cap"] = (
+                f"the style encoder's launches of this kernel (beside LNet) run as {_enet.STYLE_GRID} persistent "
+                "blocks, half the CUs (S2V_ENET_STYLE_GRID): the replayed average is over launches that hold "
+                "half the chip by design; 'isolated' is the full-grid rate")
     elif rank == 0 and not args.no_roofline and cuda:
         result["roofline"] = live_roofline(wl.forward, args.workload)
     if world == 1 and not args.no_alt and cuda and wl.graphable:

@@ -785,6 +785,8 @@ static long long tune_value(int key) {
         g_tune[S2V_TUNE_RESIZE_UP2] = e ? atoll(e) : 1;
         e = getenv("S2V_FFT_X3");
         g_tune[S2V_TUNE_FFT_X3] = e ? atoll(e) : 0;
+        e = getenv("S2V_X3_GRID_CAP");
+        g_tune[S2V_TUNE_X3_GRID_CAP] = e ? atoll(e) : 0;
         g_tune_init = true;
     }
     return g_tune[key];
@@ -1418,6 +1420,13 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
         if (am == 4) {
             a.x_bytes = (unsigned)x_extent_bytes(p);
             a.w_bytes = (unsigned)((long long)p->npad * p->kpad * 4);
+        }
+        const long long cap = tune_value(S2V_TUNE_X3_GRID_CAP) & ~7LL;
+        if (cap > 0 && !a.cnt && (long long)grid.x * grid.y * grid.z > cap) {
+            a.vgrid_x = (int)grid.x;            // persistent blocks over the tile grid (s2v.h)
+            a.vgrid_y = (int)grid.y;
+            a.vgrid_z = (int)grid.z;
+            grid = dim3((unsigned)cap, 1, 1);
         }
         if (p->prec == S2V_PREC_BF16X3) launch_conv_x3<0>(pl.tile, a, am, bkn, grid, s);
         else launch_conv_x3<1>(pl.tile, a, am, bkn, grid, s);

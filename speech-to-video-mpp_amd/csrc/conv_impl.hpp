@@ -45,6 +45,8 @@ struct ConvArgs {
     int stamp_slot, stamp_stride, stamp_reps;
     float x_scale;          // split-precision A operand pre-scale (power of two; 1 = none)
     int *nonfinite;         // set to 1 when an accumulator is non-finite (or null)
+    int vgrid_x, vgrid_y, vgrid_z;   // x3 persistent launch: the tile grid gridDim.x blocks loop over
+                                     // (S2V_TUNE_X3_GRID_CAP); vgrid_x == 0: one block per tile
 };
 
 // Launch timer: block start (atomic min) / end (atomic max) of the device real-time clock into the

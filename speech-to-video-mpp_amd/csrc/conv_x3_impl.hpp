@@ -253,8 +253,9 @@ constexpr int x3_chunk(int bm, int bn, int smem) {
 // branches, no zero fills), the tap / channel-slice offset a wave-uniform scalar; the B rows as
 // loop-invariant offsets plus a scalar K offset.  The host picks it when the x slab and the weights
 // fit 2^31 bytes and the filter has <= 32 taps.
+// One output tile: L is its linear index in the (gx, gy, total / (gx gy)) tile grid.
 template <int BM, int BN, int WAVES_M, int NW, int KS, int PF, int AMODE_, int BKN, int ELT>
-__global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3(ConvArgs a) {
+__device__ __forceinline__ void conv_x3_tile(const ConvArgs &a, int L, int gx, int gy, int total) {
     constexpr bool BUF = AMODE_ == 4;
     constexpr int AMODE = BUF ? 0 : AMODE_;
     constexpr int NT = 64 * NW, RS = NT / 8;
@@ -275,16 +276,12 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3(ConvArgs a) {
     constexpr int BKR = BKN ? BN / 32 : 1;                    // b_kn loader rows (256 threads)
 
     __shared__ __attribute__((aligned(16))) char smem[SMEM];
-    launch_stamp(a, false);
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WAVES_N, wn = wave % WAVES_N;
     int mt, nt, bz;
-    {   // XCD-aware tile order (see conv.hip)
-        const int gx = gridDim.x, gy = gridDim.y;
-        const int total = gx * gy * gridDim.z;
-        const int L = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    {   // XCD-aware tile order (see conv.hip): L & 7 is the XCD of the block that runs tile L
         const int per = total >> 3, rem = total & 7;
         const int xcd = L & 7, idx = L >> 3;
         const int Lp = xcd < rem ? xcd * (per + 1) + idx : rem * (per + 1) + (xcd - rem) * per + idx;
@@ -573,6 +570,26 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3(ConvArgs a) {
         });
     } else {
         epilogue_tile<BM, BN, WAVES_M, TM, TN, NW, CH>(a, acc, (float *)smem, tid, m0, n0, bz, bidx);
+    }
+}
+
+// One block per tile, or (a.vgrid_x > 0, S2V_TUNE_X3_GRID_CAP) gridDim.x persistent blocks, block b
+// running tiles b, b + gridDim.x, ...: gridDim.x is a multiple of 8, so every tile of a block has
+// the block's XCD (b & 7) in the tile order's sense and the L2 locality of the one-block form.
+template <int BM, int BN, int WAVES_M, int NW, int KS, int PF, int AMODE_, int BKN, int ELT>
+__global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3(ConvArgs a) {
+    launch_stamp(a, false);
+    if (a.vgrid_x == 0) {
+        conv_x3_tile<BM, BN, WAVES_M, NW, KS, PF, AMODE_, BKN, ELT>(
+            a, blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), gridDim.x, gridDim.y,
+            gridDim.x * gridDim.y * gridDim.z);
+    } else {
+        const int total = a.vgrid_x * a.vgrid_y * a.vgrid_z;
+#pragma unroll 1
+        for (int L = blockIdx.x; L < total; L += gridDim.x) {
+            conv_x3_tile<BM, BN, WAVES_M, NW, KS, PF, AMODE_, BKN, ELT>(a, L, a.vgrid_x, a.vgrid_y, total);
+            __syncthreads();     // the epilogue's LDS reads end before the next tile's operand stores
+        }
     }
     launch_stamp(a, true);
 }

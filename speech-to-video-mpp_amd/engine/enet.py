@@ -28,6 +28,12 @@ FUSED_TORGB = os.environ.get("S2V_ENET_FUSED_TORGB", "1") == "1"
 # (ops.modulated_conv2d d2s: the bilinear taps folded into 4 parity-class filters, written depth-to-space)
 # plus the four border lines recomputed exactly; S2V_ENET_POLY_UP=0: upsample pass + conv
 POLY_UP = os.environ.get("S2V_ENET_POLY_UP", "1") == "1"
+# the style encoder's split-precision convs (launched beside LNet) as this many persistent blocks
+# (s2v.h S2V_TUNE_X3_GRID_CAP): the CUs they leave free take LNet's latency-bound kernels as soon as
+# they are launched instead of after the encoder's 100-200 us tiles drain; 0: one block per tile.
+# 128 (half the CUs; divides every encoder layer's tile count) on MI355X, lipsync B=16: 29.1 -> 26.1-26.5
+# ms (192: 28.5, 160: 27.1, 112: 28.9, 96: 31.4, 64: 38.9; r03)
+STYLE_GRID = int(os.environ.get("S2V_ENET_STYLE_GRID", "128"))
 
 # x2 bilinear upsample (align_corners=False) followed by a 3-tap conv, per output parity r: weight of
 # input tap a (i-1, i, i+1) from conv tap p (-1, 0, 1), away from the image border
@@ -191,9 +197,14 @@ class ENetEngine:
             sst, sctx = side
             cur_st = torch.cuda.current_stream(dev)
             sst.wait_stream(cur_st)
-            with ops.side_stream(sst, ctx.keep):
-                style = self.style_code(sctx, face[:, 3:])
-                ops.conv2d(sctx, style, self.mod, svec)
+            old = ops.tune(ctx, ops.TUNE_X3_GRID_CAP, STYLE_GRID) if STYLE_GRID else None
+            try:
+                with ops.side_stream(sst, ctx.keep):
+                    style = self.style_code(sctx, face[:, 3:])
+                    ops.conv2d(sctx, style, self.mod, svec)
+            finally:
+                if old is not None:
+                    ops.tune(ctx, ops.TUNE_X3_GRID_CAP, old)
         else:
             style = self.style_code(ctx, face[:, 3:])
             ops.conv2d(ctx, style, self.mod, svec)

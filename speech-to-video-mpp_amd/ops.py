@@ -646,8 +646,8 @@ def split_act(ctx: Ctx, x: NHWC, out: NHWC | None = None) -> NHWC:
     return out
 
 
-TUNE_HALO_MIN_BLOCKS, TUNE_GLDS_TILE, TUNE_SMALLK_TILE, TUNE_X3_RATE_512, TUNE_IN_FUSED, TUNE_RESIZE_UP2, TUNE_FFT_X3 = (
-    0, 1, 2, 3, 4, 5, 6)
+(TUNE_HALO_MIN_BLOCKS, TUNE_GLDS_TILE, TUNE_SMALLK_TILE, TUNE_X3_RATE_512, TUNE_IN_FUSED, TUNE_RESIZE_UP2,
+ TUNE_FFT_X3, TUNE_X3_GRID_CAP) = (0, 1, 2, 3, 4, 5, 6, 7)
 
 
 def tune(ctx: Ctx, key: int, value: int) -> int:

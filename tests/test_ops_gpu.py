@@ -697,3 +697,34 @@ def test_instnorm_fused_small_planes(ctx, n, c, h, w):
     assert (y1.permute(0, 3, 1, 2).cpu() - ref).abs().max() < 2e-5
     assert (y1 - outs[0][0]).abs().max() < 1e-5
     assert torch.equal(p1, F.pad(y1.permute(0, 3, 1, 2), (1, 1, 1, 1), mode="reflect").permute(0, 2, 3, 1))
+
+
+@pytest.mark.parametrize("tile,splits,cap", [(1, 0, 8), (1, 0, 24), (4, 0, 16), (4, 3, 40)])
+def test_conv_x3_grid_cap_bit_exact(ctx, tile, splits, cap):
+    """S2V_TUNE_X3_GRID_CAP: ``cap`` persistent blocks looping over the tile grid (more tiles than
+    blocks, a ragged last round) compute every tile exactly as the one-block-per-tile launch does —
+    same K order, same epilogue — so the outputs are bit-identical (with and without split-K);
+    both are checked against the fp64 reference at the f16x3 bound."""
+    n, cin, h, w, cout = 2, 64, 64, 64, 160
+    wt = rnd(cout, cin, 3, 3, seed=11) / math.sqrt(cin * 9)
+    bias = rnd(cout, seed=12)
+    cw = ConvW(wt.float(), bias.float(), DEV, padding=1)
+    x = rnd(n, cin, h, w, seed=13)
+    prev_p = ops.set_precision("f16x3")
+    try:
+        outs = []
+        for c in (0, cap):
+            prev = ops.tune(ctx, ops.TUNE_X3_GRID_CAP, c)
+            try:
+                y = NHWC.empty(n, h, w, cout, DEV)
+                ops.conv2d(ctx, nhwc(x.float()), cw, y, act=ops.ACT_LRELU, alpha=0.2, force_tile=tile,
+                           force_splits=splits)
+                outs.append(y)
+            finally:
+                ops.tune(ctx, ops.TUNE_X3_GRID_CAP, prev)
+    finally:
+        ops.set_precision(prev_p)
+    assert torch.equal(outs[0].t, outs[1].t)
+    ref = F.leaky_relu(F.conv2d(x, wt, bias, padding=1), 0.2)
+    lim = REL["f16x3"] * (conv_bound(x, wt, 1, 1, 1) + 1) + 1e-6
+    assert ((to_nchw(outs[1]) - ref).abs() <= lim).all()
