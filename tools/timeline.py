@@ -58,6 +58,14 @@ def main():
                   f"kernels {len(iv)}")
             for n, t in sorted(per.items(), key=lambda kv: -kv[1])[:8]:
                 print(f"      {t:8.1f} us  {n}")
+            if name == "encoder+LNet":
+                # the two branches' ends: LNet's last FourierUnit transform, the style encoder's last
+                # 256x256-tile conv (LNet has none)
+                fft = [b for n, a, b in step if "fft2" in n and a < hi]
+                big = [b for n, a, b in step if n.startswith("void s2v::conv_igemm_x3<256, 256") and a < hi]
+                if fft and big:
+                    print(f"    LNet last FFT ends {(max(fft) - lo) / 1e3:8.1f} us, style encoder's last 256x256 conv "
+                          f"ends {(max(big) - lo) / 1e3:8.1f} us")
 
 
 if __name__ == "__main__" and "--lnet" not in sys.argv:
