@@ -197,14 +197,9 @@ class ENetEngine:
             sst, sctx = side
             cur_st = torch.cuda.current_stream(dev)
             sst.wait_stream(cur_st)
-            old = ops.tune(ctx, ops.TUNE_X3_GRID_CAP, STYLE_GRID) if STYLE_GRID else None
-            try:
-                with ops.side_stream(sst, ctx.keep):
-                    style = self.style_code(sctx, face[:, 3:])
-                    ops.conv2d(sctx, style, self.mod, svec)
-            finally:
-                if old is not None:
-                    ops.tune(ctx, ops.TUNE_X3_GRID_CAP, old)
+            with ops.x3_grid_cap(ctx, STYLE_GRID), ops.side_stream(sst, ctx.keep):
+                style = self.style_code(sctx, face[:, 3:])
+                ops.conv2d(sctx, style, self.mod, svec)
         else:
             style = self.style_code(ctx, face[:, 3:])
             ops.conv2d(ctx, style, self.mod, svec)

@@ -657,6 +657,20 @@ def tune(ctx: Ctx, key: int, value: int) -> int:
     return old.value
 
 
+@contextlib.contextmanager
+def x3_grid_cap(ctx: Ctx, blocks: int):
+    """S2V_TUNE_X3_GRID_CAP = ``blocks`` for the launches issued (captured) inside the block: their
+    split-precision tiled convs run as that many persistent blocks (0: unchanged)."""
+    if not blocks:
+        yield
+        return
+    old = tune(ctx, TUNE_X3_GRID_CAP, blocks)
+    try:
+        yield
+    finally:
+        tune(ctx, TUNE_X3_GRID_CAP, old)
+
+
 def conv_splits(ctx: Ctx, p) -> int:
     return (p.plan if isinstance(p, ConvLaunch) else _plan(ctx, p))[5]
 
