@@ -185,10 +185,12 @@ int s2v_conv2d_plan(const s2v_conv_params *p, int *out10);
  *                             over the tiles of its XCD; the CUs they leave free serve a concurrently
  *                             replayed latency-bound graph branch.  0 (default, env S2V_X3_GRID_CAP): one
  *                             block per tile.  Read at launch (graph capture) time.
+ *   S2V_TUNE_PLAN_CUS         > 0: the conv planner sizes split-K and tiles for this many CUs instead of the
+ *                             device's (env S2V_PLAN_CUS; launches that share the chip by design).
  * Sets ``value``, returns the previous one in *old_value (may be NULL). */
 enum { S2V_TUNE_HALO_MIN_BLOCKS = 0, S2V_TUNE_GLDS_TILE = 1, S2V_TUNE_SMALLK_TILE = 2, S2V_TUNE_X3_RATE_512 = 3,
        S2V_TUNE_IN_FUSED = 4, S2V_TUNE_RESIZE_UP2 = 5, S2V_TUNE_FFT_X3 = 6, S2V_TUNE_X3_GRID_CAP = 7,
-       S2V_TUNE_COUNT = 8 };
+       S2V_TUNE_PLAN_CUS = 8, S2V_TUNE_COUNT = 9 };
 int s2v_tune(int key, long long value, long long *old_value);
 
 /* max |x| over an NHWC view (pixels x c at pitch xcs) -> *out (fp32 bits; NaN propagates as the

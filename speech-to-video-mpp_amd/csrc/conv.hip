@@ -787,9 +787,18 @@ static long long tune_value(int key) {
         g_tune[S2V_TUNE_FFT_X3] = e ? atoll(e) : 0;
         e = getenv("S2V_X3_GRID_CAP");
         g_tune[S2V_TUNE_X3_GRID_CAP] = e ? atoll(e) : 0;
+        e = getenv("S2V_PLAN_CUS");
+        g_tune[S2V_TUNE_PLAN_CUS] = e ? atoll(e) : 0;
         g_tune_init = true;
     }
     return g_tune[key];
+}
+
+// CUs the planner fills (split-K factors, tile choice): S2V_TUNE_PLAN_CUS, else the device's
+static int plan_cus() {
+    const long long t = tune_value(S2V_TUNE_PLAN_CUS);
+    if (t > 0) return (int)t;
+    return device_cus() > 0 ? device_cus() : 256;
 }
 
 long long tune_get(int key) { return tune_value(key); }
@@ -812,7 +821,7 @@ static int halo_ks(const s2v_conv_params *p) {
 // channel splits of the halo kernel: about three blocks per CU, at least 8 channels per split
 static int halo_splits(const s2v_conv_params *p, int &per) {
     const long long blocks = (long long)p->n * cdiv(p->ow, 128) * cdiv(p->oh, 8);
-    const int cus = device_cus() > 0 ? device_cus() : 256;
+    const int cus = plan_cus();
     const int quads = p->cin / 4;
     int s = blocks >= 3LL * cus ? 1 : (int)((3LL * cus + blocks - 1) / blocks);
     if (s > quads / 2) s = quads / 2;
@@ -944,7 +953,7 @@ static void finish_plan(Plan &pl, int splits) {
 // with t_block = one block's share of the tile's sustained full-chip rate (kX3Tiles).
 static Plan make_plan_x3(const s2v_conv_params *p, int M, Plan pl) {
     const int batch = p->batch > 0 ? p->batch : 1;
-    const int cus = device_cus() > 0 ? device_cus() : 256;
+    const int cus = plan_cus();
     if (p->force_tile > 0) {
         pl.tile = p->force_tile - 1;
         const TileCfg &t = kX3Tiles[pl.tile].t;
@@ -1027,7 +1036,7 @@ static int glds_cfg(const s2v_conv_params *p) {
 
 static Plan make_plan_glds(const s2v_conv_params *p, int M, Plan pl) {
     const int batch = p->batch > 0 ? p->batch : 1;
-    const int cus = device_cus() > 0 ? device_cus() : 256;
+    const int cus = plan_cus();
     pl.tile = glds_cfg(p);
     const GldsCfg &c = kGlds[pl.tile];
     const long long blocks = (long long)cdiv(M, c.bm) * cdiv(p->cout, c.bn) * batch;
@@ -1064,7 +1073,7 @@ static Plan make_plan(const s2v_conv_params *p_in, int M, int K) {
     }
     if (tiled_x3(p)) return make_plan_x3(p, M, pl);
     const int batch = p->batch > 0 ? p->batch : 1;
-    const long long target = 2LL * (device_cus() > 0 ? device_cus() : 256);
+    const long long target = 2LL * plan_cus();
     int cands[kNumTiles];
     int nc = 0;
     if (p->force_tile > 0) {

@@ -647,7 +647,7 @@ def split_act(ctx: Ctx, x: NHWC, out: NHWC | None = None) -> NHWC:
 
 
 (TUNE_HALO_MIN_BLOCKS, TUNE_GLDS_TILE, TUNE_SMALLK_TILE, TUNE_X3_RATE_512, TUNE_IN_FUSED, TUNE_RESIZE_UP2,
- TUNE_FFT_X3, TUNE_X3_GRID_CAP) = (0, 1, 2, 3, 4, 5, 6, 7)
+ TUNE_FFT_X3, TUNE_X3_GRID_CAP, TUNE_PLAN_CUS) = (0, 1, 2, 3, 4, 5, 6, 7, 8)
 
 
 def tune(ctx: Ctx, key: int, value: int) -> int:
@@ -655,6 +655,19 @@ def tune(ctx: Ctx, key: int, value: int) -> int:
     old = ctypes.c_longlong(0)
     check(ctx.lib.s2v_tune(key, value, ctypes.byref(old)), "s2v_tune")
     return old.value
+
+
+@contextlib.contextmanager
+def tuned(ctx: Ctx, key: int, value: int):
+    """s2v_tune ``key`` = ``value`` for the launches issued (captured) inside the block (0: unchanged)."""
+    if not value:
+        yield
+        return
+    old = tune(ctx, key, value)
+    try:
+        yield
+    finally:
+        tune(ctx, key, old)
 
 
 @contextlib.contextmanager
