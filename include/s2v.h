@@ -180,8 +180,9 @@ int s2v_conv2d_plan(const s2v_conv_params *p, int *out10);
  *   S2V_TUNE_FFT_X3           1 (env S2V_FFT_X3): the 12 / 24 / 48 square FourierUnit transforms on
  *                             split-fp32 f16 MFMAs; 0 (default): the exact-fp32 MFMA kernels (the x3 forms
  *                             measured slower: 48x48 rfft 30 -> 38 us, irfft 35 -> 43 us, r03).
- *   S2V_TUNE_X3_GRID_CAP      > 0 (a multiple of 8): split-precision tiled convs (no in-launch split-K fold)
- *                             with more tiles than this launch this many persistent blocks, each looping
+ *   S2V_TUNE_X3_GRID_CAP      > 0 (a multiple of 8): split-precision convs on the 256x256 buffer-load tile (no
+ *                             in-launch split-K fold) with more tiles than this launch this many persistent
+ *                             blocks, each looping
  *                             over the tiles of its XCD; the CUs they leave free serve a concurrently
  *                             replayed latency-bound graph branch.  0 (default, env S2V_X3_GRID_CAP): one
  *                             block per tile.  Read at launch (graph capture) time.

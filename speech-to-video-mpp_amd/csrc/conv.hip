@@ -1431,7 +1431,8 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
             a.w_bytes = (unsigned)((long long)p->npad * p->kpad * 4);
         }
         const long long cap = tune_value(S2V_TUNE_X3_GRID_CAP) & ~7LL;
-        if (cap > 0 && !a.cnt && (long long)grid.x * grid.y * grid.z > cap) {
+        // persistent form: the 256x256 buffer-load tile only (conv_x3_impl.hpp x3_has_persist)
+        if (cap > 0 && !a.cnt && pl.tile == 0 && am == 4 && !bkn && (long long)grid.x * grid.y * grid.z > cap) {
             a.vgrid_x = (int)grid.x;            // persistent blocks over the tile grid (s2v.h)
             a.vgrid_y = (int)grid.y;
             a.vgrid_z = (int)grid.z;

@@ -573,23 +573,29 @@ __device__ __forceinline__ void conv_x3_tile(const ConvArgs &a, int L, int gx, i
     }
 }
 
-// One block per tile, or (a.vgrid_x > 0, S2V_TUNE_X3_GRID_CAP) gridDim.x persistent blocks, block b
-// running tiles b, b + gridDim.x, ...: gridDim.x is a multiple of 8, so every tile of a block has
-// the block's XCD (b & 7) in the tile order's sense and the L2 locality of the one-block form.
+// One block per tile.
 template <int BM, int BN, int WAVES_M, int NW, int KS, int PF, int AMODE_, int BKN, int ELT>
 __global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3(ConvArgs a) {
     launch_stamp(a, false);
-    if (a.vgrid_x == 0) {
-        conv_x3_tile<BM, BN, WAVES_M, NW, KS, PF, AMODE_, BKN, ELT>(
-            a, blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), gridDim.x, gridDim.y,
-            gridDim.x * gridDim.y * gridDim.z);
-    } else {
-        const int total = a.vgrid_x * a.vgrid_y * a.vgrid_z;
+    conv_x3_tile<BM, BN, WAVES_M, NW, KS, PF, AMODE_, BKN, ELT>(
+        a, blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), gridDim.x, gridDim.y,
+        gridDim.x * gridDim.y * gridDim.z);
+    launch_stamp(a, true);
+}
+
+// Persistent form (S2V_TUNE_X3_GRID_CAP, a.vgrid_*): gridDim.x blocks, block b running tiles b,
+// b + gridDim.x, ...; gridDim.x is a multiple of 8, so every tile of a block has the block's XCD
+// (b & 7) in the tile order's sense.  A kernel of its own: folding the loop (or a branch to it) into
+// conv_igemm_x3 cost every one-block-per-tile launch 3-10 % (LNet 11.4 -> 11.9 ms, enhance 18.0 ->
+// 19.8 ms, MI355X A/B of the builds, r03).
+template <int BM, int BN, int WAVES_M, int NW, int KS, int PF, int AMODE_, int BKN, int ELT>
+__global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3_persist(ConvArgs a) {
+    launch_stamp(a, false);
+    const int total = a.vgrid_x * a.vgrid_y * a.vgrid_z;
 #pragma unroll 1
-        for (int L = blockIdx.x; L < total; L += gridDim.x) {
-            conv_x3_tile<BM, BN, WAVES_M, NW, KS, PF, AMODE_, BKN, ELT>(a, L, a.vgrid_x, a.vgrid_y, total);
-            __syncthreads();     // the epilogue's LDS reads end before the next tile's operand stores
-        }
+    for (int L = blockIdx.x; L < total; L += gridDim.x) {
+        conv_x3_tile<BM, BN, WAVES_M, NW, KS, PF, AMODE_, BKN, ELT>(a, L, a.vgrid_x, a.vgrid_y, total);
+        __syncthreads();     // the epilogue's LDS reads end before the next tile's operand stores
     }
     launch_stamp(a, true);
 }
@@ -617,8 +623,16 @@ static void launch_x3(const ConvArgs &a, int amode, bool bkn, dim3 grid, hipStre
 }
 
 // x3 kernel configurations (index = the host planner's tile id, conv.hip kX3Tiles)
+// the persistent form exists for the 256x256 tile with buffer-load A (the ENet style encoder's
+// layers; conv.hip only sets a.vgrid_* for that configuration)
+constexpr bool x3_has_persist(int cfg, int amode, bool bkn) { return cfg == 0 && amode == 4 && !bkn; }
+
 template <int ELT>
 void launch_conv_x3(int cfg, const ConvArgs &a, int amode, bool bkn, dim3 grid, hipStream_t s) {
+    if (a.vgrid_x > 0) {
+        if (x3_has_persist(cfg, amode, bkn)) conv_igemm_x3_persist<256, 256, 2, 8, 1, 1, 4, 0, ELT><<<grid, 512, 0, s>>>(a);
+        return;
+    }
     switch (cfg) {
         case 0: launch_x3<256, 256, 2, 8, 1, 1, ELT>(a, amode, bkn, grid, s); break;
         case 1: launch_x3<128, 128, 2, 8, 1, 1, ELT>(a, amode, bkn, grid, s); break;
