@@ -105,12 +105,12 @@ typedef struct s2v_conv_params {
      * kernel divides out of the accumulators exactly); a b_kn matrix is split on the fly. */
     int prec;
     const void *wt_x3;
-    /* optional in-launch split-K fold: >= grid tiles (batch x M-tiles x N-tiles) zero-initialised ints.
-     * When given, the last-arriving split block of each output tile sums the tile's partials in split
-     * order (the same sums as the separate reduce) and runs the epilogue; the counters are left zero.
-     * NULL / too short: a separate reduce kernel folds the workspace (faster on MI355X: the fold's
-     * agent-scope release / acquire per split block costs more than the extra launch). */
-    int *tile_counters; int n_counters;
+    /* persistent launch of the 256x256 buffer-load split-precision tile: when > 0 (a multiple of 8) and the
+     * launch has more tiles than this, it runs ``grid_cap`` blocks that each loop over the tiles of their
+     * XCD (conv_igemm_x3_persist); the CUs left free serve a concurrent latency-bound graph branch (the
+     * ENet style encoder beside LNet takes half the device's CUs).  0: one block per tile.  Other tiles
+     * ignore it; s2v_conv2d_plan reports the persistent blocks in out11[10]. */
+    int grid_cap;
     float wt_scale;
     /* 2x2 average-pooled output (ResBlock 'down': lrelu(conv1) then F.interpolate(x0.5, bilinear) ==
      * the mean of each 2x2 quad, base_blocks.py:40-49): y is [n][oh/2][ow/2] (pitch ycs) and holds
@@ -154,13 +154,15 @@ enum { S2V_PREC_F32 = 0, S2V_PREC_BF16X3 = 1, S2V_PREC_F16X3 = 2 };
  * ENet.py, DNet.py, base_blocks.py, ffc.py, transformer.py (inventory: SURVEY.md App. A). */
 int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream);
 size_t s2v_conv2d_ws_bytes(const s2v_conv_params *p);
-/* The launch plan s2v_conv2d would use: out10 = {BM, BN, WAVES_M, AVEC, B_KN, splits, prec, NW, KS, PF}
- * of the conv_igemm<BM,BN,WAVES_M,AVEC,B_KN> (prec 0) or
- * conv_igemm_x3<BM,BN,WAVES_M,NW,KS,PF,AVEC,B_KN,prec-1> (prec 1 / 2) instance, or
- * {0, CO, TPP, LW, 0, 1, 0, 0, 0, 0} for conv_small_cpar<CO,TPP,LW> (conv_direct_small<CO> when
- * TPP == 0), or {0, cout, -QPT, PX, 0, 1, ...} for conv_smallk<QPT,PX>.  force_tile: 0 = planner,
- * 1..6 (f32) / 1..11 (split precisions) a fixed tile of the selected precision's table (tests / tuning). */
-int s2v_conv2d_plan(const s2v_conv_params *p, int *out10);
+/* The launch plan s2v_conv2d would use: out11 = {BM, BN, WAVES_M, AVEC, B_KN, splits, prec, NW, KS, PF,
+ * PERSIST} of the conv_igemm<BM,BN,WAVES_M,AVEC,B_KN> (prec 0) or
+ * conv_igemm_x3<BM,BN,WAVES_M,NW,KS,PF,AVEC,B_KN,prec-1> (prec 1 / 2) instance — conv_igemm_x3_persist<...>
+ * with PERSIST (> 0) blocks under ``grid_cap``, conv_ring_x3<BM,BN,PF,prec-1> when AVEC == 6,
+ * conv_glds_x3<BM,BN,WAVES_M,KS,prec-1> when AVEC == 5 — or {0, CO, TPP, LW, 0, 1, 0, ...} for
+ * conv_small_cpar<CO,TPP,LW> (conv_direct_small<CO> when TPP == 0), or {0, cout, -QPT, PX, 0, 1, ...} for
+ * conv_smallk<QPT,PX>.  force_tile: 0 = planner, 1..6 (f32) / 1..18 (split precisions: 13..18 the LDS-DMA
+ * ring tiles) a fixed tile of the selected precision's table (tests / tuning). */
+int s2v_conv2d_plan(const s2v_conv_params *p, int *out11);
 /* Planner knobs (tests / tuning; process-wide, not thread-safe against concurrent planning):
  *   S2V_TUNE_HALO_MIN_BLOCKS  the halo-tiled small-Cout kernel needs at least this many 8x128 tiles
  *                             (default 0, env S2V_HALO_MIN_BLOCKS; fewer go channel-parallel).  Below
@@ -177,21 +179,9 @@ int s2v_conv2d_plan(const s2v_conv_params *p, int *out10);
  *                             B=16 11.65 -> 11.43 ms, lipsync 28.5 -> 28.0 ms on MI355X (r03).
  *   S2V_TUNE_RESIZE_UP2       1 (env S2V_RESIZE_UP2, default): exact x2 bilinear resizes take the 2x2-quad
  *                             kernel; 0: the generic float4 resize kernel.
- *   S2V_TUNE_FFT_X3           1 (env S2V_FFT_X3): the 12 / 24 / 48 square FourierUnit transforms on
- *                             split-fp32 f16 MFMAs; 0 (default): the exact-fp32 MFMA kernels (the x3 forms
- *                             measured slower: 48x48 rfft 30 -> 38 us, irfft 35 -> 43 us, r03).
- *   S2V_TUNE_X3_GRID_CAP      > 0 (a multiple of 8): split-precision convs on the 256x256 buffer-load tile (no
- *                             in-launch split-K fold) with more tiles than this launch this many persistent
- *                             blocks, each looping
- *                             over the tiles of its XCD; the CUs they leave free serve a concurrently
- *                             replayed latency-bound graph branch.  0 (default, env S2V_X3_GRID_CAP): one
- *                             block per tile.  Read at launch (graph capture) time.
- *   S2V_TUNE_PLAN_CUS         > 0: the conv planner sizes split-K and tiles for this many CUs instead of the
- *                             device's (env S2V_PLAN_CUS; launches that share the chip by design).
  * Sets ``value``, returns the previous one in *old_value (may be NULL). */
 enum { S2V_TUNE_HALO_MIN_BLOCKS = 0, S2V_TUNE_GLDS_TILE = 1, S2V_TUNE_SMALLK_TILE = 2, S2V_TUNE_X3_RATE_512 = 3,
-       S2V_TUNE_IN_FUSED = 4, S2V_TUNE_RESIZE_UP2 = 5, S2V_TUNE_FFT_X3 = 6, S2V_TUNE_X3_GRID_CAP = 7,
-       S2V_TUNE_PLAN_CUS = 8, S2V_TUNE_COUNT = 9 };
+       S2V_TUNE_IN_FUSED = 4, S2V_TUNE_RESIZE_UP2 = 5, S2V_TUNE_COUNT = 6 };
 int s2v_tune(int key, long long value, long long *old_value);
 
 /* max |x| over an NHWC view (pixels x c at pitch xcs) -> *out (fp32 bits; NaN propagates as the

@@ -10,9 +10,8 @@ import ctypes
 import os
 import threading
 
-# S2V_LIB names an alternative in-tree build (kernel-variant experiments, tools/); the default is
-# the package's libs2v.so
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), os.environ.get("S2V_LIB", "libs2v.so"))
+# the package's in-tree build (libs2v_torch.so, the model path's launch ops, links this same file)
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libs2v.so")
 
 ACT_NONE, ACT_RELU, ACT_LRELU, ACT_SIGMOID, ACT_TANH, ACT_GELU_TANH = range(6)
 IN_DIRECT, IN_NEAREST_UP2, IN_TRANSPOSED = range(3)
@@ -42,7 +41,7 @@ class ConvParams(ctypes.Structure):
         ("force_tile", _c_int), ("force_splits", _c_int),
         ("out_step", _c_int), ("out_full_h", _c_int), ("out_full_w", _c_int),
         ("prec", _c_int), ("wt_x3", _vp),
-        ("tile_counters", _vp), ("n_counters", _c_int),
+        ("grid_cap", _c_int),
         ("wt_scale", _c_float),
         ("out_pool", _c_int),
         ("x_split", _c_int),

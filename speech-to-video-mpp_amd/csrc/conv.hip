@@ -21,10 +21,12 @@
 
 namespace s2v {
 
-template <int ELT>   // 0 = bf16, 1 = f16 halves (conv_x3_impl.hpp; instances in conv_x3_{bf16,f16}.hip)
-void launch_conv_x3(int tile, const ConvArgs &a, int amode, bool bkn, dim3 grid, hipStream_t s);
+template <int ELT>   // 0 = bf16, 1 = f16 halves (conv_x3_impl.hpp; instances in conv_x3_{bf16,f16}.hip); 0 or an error
+int launch_conv_x3(int tile, const ConvArgs &a, int amode, bool bkn, dim3 grid, hipStream_t s);
 template <int ELT>   // LDS-DMA kernels on split-layout inputs (conv_glds.hip): cfg 0 = 256x256, 1 = 256x128
 void launch_conv_glds(int cfg, const ConvArgs &a, dim3 grid, hipStream_t s);
+template <int ELT>   // LDS-DMA ring kernels on fp32 inputs (conv_ring.hip), cfg = X3Cfg::ring - 1
+void launch_conv_ring(int cfg, const ConvArgs &a, dim3 grid, hipStream_t s);
 
 template <int BM, int BN, int AR, int BR, int BKN>
 __device__ __forceinline__ void store_ab(float *As, float *Bs, int tid, const f4 (&ra)[AR],
@@ -783,23 +785,13 @@ static long long tune_value(int key) {
         g_tune[S2V_TUNE_IN_FUSED] = e ? atoll(e) : 576;   // max plane pixels of the one-launch InstanceNorm
         e = getenv("S2V_RESIZE_UP2");
         g_tune[S2V_TUNE_RESIZE_UP2] = e ? atoll(e) : 1;
-        e = getenv("S2V_FFT_X3");
-        g_tune[S2V_TUNE_FFT_X3] = e ? atoll(e) : 0;
-        e = getenv("S2V_X3_GRID_CAP");
-        g_tune[S2V_TUNE_X3_GRID_CAP] = e ? atoll(e) : 0;
-        e = getenv("S2V_PLAN_CUS");
-        g_tune[S2V_TUNE_PLAN_CUS] = e ? atoll(e) : 0;
         g_tune_init = true;
     }
     return g_tune[key];
 }
 
-// CUs the planner fills (split-K factors, tile choice): S2V_TUNE_PLAN_CUS, else the device's
-static int plan_cus() {
-    const long long t = tune_value(S2V_TUNE_PLAN_CUS);
-    if (t > 0) return (int)t;
-    return device_cus() > 0 ? device_cus() : 256;
-}
+// CUs the planner fills (split-K factors, tile choice): the device's
+static int plan_cus() { return device_cus() > 0 ? device_cus() : 256; }
 
 long long tune_get(int key) { return tune_value(key); }
 
@@ -851,17 +843,23 @@ static const TileCfg kTiles[] = {
 // and resident blocks per CU (LDS / waves) for the planner's cost model
 // (512x128: 360, set end to end on MI355X r03 — lipsync 29.11 -> 28.35 ms, its 400^2 N = 128 StyleConvs;
 // 420 also displaces the 256x256 tile on N = 256 layers: 28.80 ms)
+// ring > 0: the LDS-DMA ring kernel conv_ring_x3<BM, BN, NST = pf> (conv_ring.hip launch_conv_ring cfg
+// ring - 1; 4 waves stacked along M), for AMODE-0 convolutions without a prologue
 struct X3Cfg {
     TileCfg t;
     float tflops;
     int bpc;
+    int ring;
 };
 static const X3Cfg kX3Tiles[] = {
-    {{256, 256, 2, 8, 1, 1}, 400.f, 1}, {{128, 128, 2, 8, 1, 1}, 330.f, 2}, {{64, 128, 2, 8, 1, 1}, 260.f, 3},
-    {{128, 64, 2, 4, 1, 1}, 290.f, 3},  {{64, 64, 2, 4, 1, 1}, 265.f, 4},   {{128, 32, 4, 4, 1, 1}, 235.f, 4},
-    {{256, 128, 4, 8, 1, 1}, 335.f, 1}, {{256, 64, 8, 8, 1, 1}, 300.f, 2},  {{512, 128, 4, 8, 1, 1}, 360.f, 1},
+    {{256, 256, 2, 8, 1, 1}, 400.f, 1, 0}, {{128, 128, 2, 8, 1, 1}, 330.f, 2, 0}, {{64, 128, 2, 8, 1, 1}, 260.f, 3, 0},
+    {{128, 64, 2, 4, 1, 1}, 290.f, 3, 0},  {{64, 64, 2, 4, 1, 1}, 265.f, 4, 0},   {{128, 32, 4, 4, 1, 1}, 235.f, 4, 0},
+    {{256, 128, 4, 8, 1, 1}, 335.f, 1, 0}, {{256, 64, 8, 8, 1, 1}, 300.f, 2, 0},  {{512, 128, 4, 8, 1, 1}, 360.f, 1, 0},
     // two K-slice groups in flight (PF 2) for the 4-wave tiles: forced-only (tflops 0) until measured
-    {{128, 64, 2, 4, 1, 2}, 0.f, 3},    {{64, 64, 2, 4, 1, 2}, 0.f, 4},     {{128, 32, 4, 4, 1, 2}, 0.f, 4}};
+    {{128, 64, 2, 4, 1, 2}, 0.f, 3, 0},    {{64, 64, 2, 4, 1, 2}, 0.f, 4, 0},     {{128, 32, 4, 4, 1, 2}, 0.f, 4, 0},
+    // LDS-DMA ring kernels (force_tile 13..18): forced-only until measured
+    {{64, 64, 4, 4, 0, 6}, 0.f, 1, 1},     {{128, 64, 4, 4, 0, 5}, 0.f, 1, 2},    {{64, 128, 4, 4, 0, 5}, 0.f, 1, 3},
+    {{128, 128, 4, 4, 0, 4}, 0.f, 1, 4},   {{64, 32, 4, 4, 0, 8}, 0.f, 1, 5},     {{128, 32, 4, 4, 0, 6}, 0.f, 1, 6}};
 constexpr int kNumX3 = sizeof(kX3Tiles) / sizeof(kX3Tiles[0]);
 
 static const TileCfg &tile_cfg(const s2v_conv_params *p, int tile);
@@ -937,6 +935,13 @@ static bool uses_x3(const s2v_conv_params *p) { return tiled_x3(p) && !p->b_kn; 
 
 static int a_mode(const s2v_conv_params *p);
 
+// the LDS-DMA ring kernels take AMODE-0 convolutions (direct, zero padding, cin % 32 == 0) with no
+// prologue (in_scale / pre_act) and <= 32 filter taps, packed split weights
+static bool ring_ok(const s2v_conv_params *p) {
+    return a_mode(p) == 0 && !p->b_kn && !p->in_scale && p->pre_act == S2V_ACT_NONE && p->kh * p->kw <= 32 &&
+           !p->x_split;
+}
+
 static const TileCfg &tile_cfg(const s2v_conv_params *p, int tile) {
     return tiled_x3(p) ? kX3Tiles[tile].t : kTiles[tile];
 }
@@ -987,6 +992,7 @@ static Plan make_plan_x3(const s2v_conv_params *p, int M, Plan pl) {
     for (int i = 0; i < kNumX3; ++i) {
         const X3Cfg &c = kX3Tiles[i];
         if (c.tflops <= 0.f) continue;                          // forced-only configurations
+        if (c.ring && !ring_ok(p)) continue;
         if (p->b_kn && c.t.nw != 4) continue;
         if (c.t.bm >= 256 && c.t.bn >= 128 && am != 0 && am != 3) continue;   // generic gathers spill there
         if (c.t.bm == 256 && c.t.bn == 64 && am != 0) continue;   // measured slower than 128x64 on per-row gathers
@@ -1133,6 +1139,9 @@ static int validate(const s2v_conv_params *p, int &M, int &K) {
                 "conv2d: bad force_tile %d", p->force_tile);
     S2V_REQUIRE(!(tiled_x3(p) && p->b_kn && p->force_tile > 0 && kX3Tiles[p->force_tile - 1].t.nw != 4),
                 "conv2d: b_kn operands need a 4-wave split-bf16 tile (force_tile 4..6)");
+    S2V_REQUIRE(!(tiled_x3(p) && p->force_tile > 0 && kX3Tiles[p->force_tile - 1].ring && !ring_ok(p)),
+                "conv2d: force_tile %d is an LDS-DMA ring tile: needs a direct zero-padded conv, cin %% 32 == 0, "
+                "no in_scale / pre_act, <= 32 taps", p->force_tile);
     if (tiled_x3(p) && p->force_tile > 0) {
         // a forced tile must not read weight rows past the packed [npad] rows (the planner never
         // picks such a tile: the kernels load whole BN-row slabs of B without a row guard)
@@ -1221,7 +1230,6 @@ static ConvArgs make_args(const s2v_conv_params *p, int M, int K, const Plan &pl
     a.M = M; a.K = K; a.ktiles = pl.ktiles; a.splits = pl.splits; a.tps = pl.tps; a.ws = p->ws;
     a.y_step = p->out_step > 1 ? p->out_step : 1; a.y_h = p->out_full_h; a.y_w = p->out_full_w;
     a.d2s_c = p->d2s_cout > 0 ? p->d2s_cout : 0;
-    a.cnt = nullptr;
     a.acc_scale = ((p->x_split || tiled_x3(p)) && !p->b_kn && p->wt_scale > 0.f) ? 1.f / p->wt_scale : 1.f;
     a.pool = p->out_pool != 0;
     a.stamps = p->stamps; a.stamp_ctr = p->stamp_ctr; a.stamp_slot = p->stamp_slot;
@@ -1274,6 +1282,18 @@ static int x3_amode(const s2v_conv_params *p, const TileCfg &t) {
     return 4;
 }
 
+// Persistent blocks of a launch under s2v_conv_params.grid_cap: the 256x256 buffer-load split-precision
+// tile only (conv_x3_impl.hpp x3_has_persist), when the tile grid exceeds the cap; 0 = one block per tile
+static int persist_blocks(const s2v_conv_params *p, const Plan &pl, int M) {
+    if (p->grid_cap <= 0 || !tiled_x3(p) || p->b_kn || p->x_split || pl.tile != 0) return 0;
+    const TileCfg &t = kX3Tiles[0].t;
+    if (x3_amode(p, t) != 4) return 0;
+    const long long cap = p->grid_cap & ~7LL;
+    const int batch = p->batch > 0 ? p->batch : 1;
+    const long long tiles = (long long)cdiv(M, t.bm) * cdiv(p->cout, t.bn) * batch * pl.splits;
+    return cap > 0 && tiles > cap ? (int)cap : 0;
+}
+
 }  // namespace s2v
 
 using namespace s2v;
@@ -1296,7 +1316,7 @@ extern "C" size_t s2v_conv2d_ws_bytes(const s2v_conv_params *p) {
 }
 
 extern "C" int s2v_conv2d_plan(const s2v_conv_params *p, int *out6) {
-    for (int i = 6; i < 10; ++i) out6[i] = 0;
+    for (int i = 6; i < 11; ++i) out6[i] = 0;
     int M, K;
     int rc = validate(p, M, K);
     if (rc) return rc;
@@ -1336,11 +1356,12 @@ extern "C" int s2v_conv2d_plan(const s2v_conv_params *p, int *out6) {
     }
     const TileCfg &t = tile_cfg(p, pl.tile);
     out6[0] = t.bm; out6[1] = t.bn; out6[2] = t.wm;
-    out6[3] = tiled_x3(p) ? x3_amode(p, t) : a_mode(p);
+    out6[3] = tiled_x3(p) ? (kX3Tiles[pl.tile].ring ? 6 : x3_amode(p, t)) : a_mode(p);   // 6: conv_ring_x3
     out6[4] = p->b_kn != 0;
     out6[5] = pl.splits;
     out6[6] = tiled_x3(p) ? p->prec : 0;
     out6[7] = t.nw; out6[8] = t.ks; out6[9] = t.pf;
+    out6[10] = persist_blocks(p, pl, M);
     return 0;
 }
 
@@ -1421,25 +1442,27 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
     const bool bkn = p->b_kn != 0;
     const TileCfg &t = tile_cfg(p, pl.tile);
     dim3 grid(cdiv(M, t.bm), cdiv(p->cout, t.bn), batch * pl.splits);
-    if (pl.splits > 1 && p->tile_counters && p->n_counters >= (long long)grid.x * grid.y * batch)
-        a.cnt = p->tile_counters;                       // fold in the launch itself
-    if (tiled_x3(p)) {
+    if (tiled_x3(p) && kX3Tiles[pl.tile].ring) {
+        a.wt = (const float *)p->wt_x3;
+        if (p->prec == S2V_PREC_BF16X3) launch_conv_ring<0>(kX3Tiles[pl.tile].ring - 1, a, grid, s);
+        else launch_conv_ring<1>(kX3Tiles[pl.tile].ring - 1, a, grid, s);
+    } else if (tiled_x3(p)) {
         if (!bkn) a.wt = (const float *)p->wt_x3;
         const int am = x3_amode(p, t);
         if (am == 4) {
             a.x_bytes = (unsigned)x_extent_bytes(p);
             a.w_bytes = (unsigned)((long long)p->npad * p->kpad * 4);
         }
-        const long long cap = tune_value(S2V_TUNE_X3_GRID_CAP) & ~7LL;
-        // persistent form: the 256x256 buffer-load tile only (conv_x3_impl.hpp x3_has_persist)
-        if (cap > 0 && !a.cnt && pl.tile == 0 && am == 4 && !bkn && (long long)grid.x * grid.y * grid.z > cap) {
-            a.vgrid_x = (int)grid.x;            // persistent blocks over the tile grid (s2v.h)
+        const int cap = persist_blocks(p, pl, M);
+        if (cap > 0) {                              // persistent blocks over the tile grid (s2v.h grid_cap)
+            a.vgrid_x = (int)grid.x;
             a.vgrid_y = (int)grid.y;
             a.vgrid_z = (int)grid.z;
             grid = dim3((unsigned)cap, 1, 1);
         }
-        if (p->prec == S2V_PREC_BF16X3) launch_conv_x3<0>(pl.tile, a, am, bkn, grid, s);
-        else launch_conv_x3<1>(pl.tile, a, am, bkn, grid, s);
+        rc = p->prec == S2V_PREC_BF16X3 ? launch_conv_x3<0>(pl.tile, a, am, bkn, grid, s)
+                                        : launch_conv_x3<1>(pl.tile, a, am, bkn, grid, s);
+        if (rc) return rc;
     } else switch (pl.tile) {
         case 0: launch_tile<128, 128, 2>(a, amode, bkn, grid, s); break;
         case 1: launch_tile<128, 64, 2>(a, amode, bkn, grid, s); break;
@@ -1450,7 +1473,7 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
     }
     }
     rc = check_launch("conv_igemm");
-    if (rc || pl.splits <= 1 || a.cnt) return rc;
+    if (rc || pl.splits <= 1) return rc;
     const long long total = (long long)batch * M * (p->cout % 4 == 0 ? p->cout / 4 : p->cout);
     unsigned blocks = cdiv(total, 256);
     if (blocks > 65535u * 4u) blocks = 65535u * 4u;

@@ -35,7 +35,6 @@ struct ConvArgs {
     float *ws;
     int y_step, y_h, y_w;   // strided (polyphase) output, y_step > 1
     int d2s_c;              // depth-to-space output (s2v_conv_params.d2s_cout), 0 = off
-    int *cnt;               // split-K tile counters (in-launch fold), or null
     float acc_scale;        // accumulator factor before the epilogue (1 / the split weights' pre-scale)
     unsigned x_bytes, w_bytes;   // buffer-load extents of one batch slab of x / of the weights (AMODE 4)
     int pool;               // 2x2 average-pooled output: M runs over 2x2 output quads (quad-major),
@@ -46,7 +45,7 @@ struct ConvArgs {
     float x_scale;          // split-precision A operand pre-scale (power of two; 1 = none)
     int *nonfinite;         // set to 1 when an accumulator is non-finite (or null)
     int vgrid_x, vgrid_y, vgrid_z;   // x3 persistent launch: the tile grid gridDim.x blocks loop over
-                                     // (S2V_TUNE_X3_GRID_CAP); vgrid_x == 0: one block per tile
+                                     // (s2v_conv_params.grid_cap); vgrid_x == 0: one block per tile
 };
 
 // Launch timer: block start (atomic min) / end (atomic max) of the device real-time clock into the
@@ -466,38 +465,6 @@ __device__ __forceinline__ void epilogue_tile_fn(const ConvArgs &a, float *Cs, i
         } else {
 #pragma unroll 1
             for (int rr = tid / TPR; rr < clim; rr += RSTEP) store_epilogue(a, bidx, m0 + c0 + rr, n, Cs[rr * LDC + cn]);
-        }
-    }
-    if (a.splits > 1 && a.cnt) {
-        // In-launch split-K fold (cdna_hip_programming.md, "Projection GEMM" item 2): publish this
-        // split's slab (release at agent scope, then the ticket); the tile's last arriver acquires,
-        // sums every slab in split order — the separate reduce's sums — and runs the epilogue.
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        int *flag = (int *)Cs;
-        const int tile = (bidx * gridDim.x + m0 / BM) * gridDim.y + n0 / BN;
-        if (tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const int old = __hip_atomic_fetch_add(a.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const int last = old == a.splits - 1;
-            if (last) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __hip_atomic_store(a.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            flag[0] = last;
-        }
-        __syncthreads();
-        if (!flag[0] || !live) return;
-        const long long slab = (long long)a.M * a.cout;
-        const float *src = a.ws + (long long)bidx * a.splits * slab + n;
-#pragma unroll 1
-        for (int rr = tid / TPR; rr < mlim; rr += RSTEP) {
-            const long long m = m0 + rr;
-            float v = src[m * a.cout];
-            for (int sp = 1; sp < a.splits; ++sp) v += src[sp * slab + m * a.cout];
-            store_epilogue(a, bidx, (int)m, n, v);
         }
     }
 }

@@ -2,5 +2,5 @@
 #include "conv_x3_impl.hpp"
 
 namespace s2v {
-template void launch_conv_x3<1>(int cfg, const ConvArgs &a, int amode, bool bkn, dim3 grid, hipStream_t s);
+template int launch_conv_x3<1>(int cfg, const ConvArgs &a, int amode, bool bkn, dim3 grid, hipStream_t s);
 }  // namespace s2v

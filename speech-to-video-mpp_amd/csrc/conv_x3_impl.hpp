@@ -583,7 +583,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3(ConvArgs a) {
     launch_stamp(a, true);
 }
 
-// Persistent form (S2V_TUNE_X3_GRID_CAP, a.vgrid_*): gridDim.x blocks, block b running tiles b,
+// Persistent form (s2v_conv_params.grid_cap, a.vgrid_*): gridDim.x blocks, block b running tiles b,
 // b + gridDim.x, ...; gridDim.x is a multiple of 8, so every tile of a block has the block's XCD
 // (b & 7) in the tile order's sense.  A kernel of its own: folding the loop (or a branch to it) into
 // conv_igemm_x3 cost every one-block-per-tile launch 3-10 % (LNet 11.4 -> 11.9 ms, enhance 18.0 ->
@@ -628,10 +628,15 @@ static void launch_x3(const ConvArgs &a, int amode, bool bkn, dim3 grid, hipStre
 constexpr bool x3_has_persist(int cfg, int amode, bool bkn) { return cfg == 0 && amode == 4 && !bkn; }
 
 template <int ELT>
-void launch_conv_x3(int cfg, const ConvArgs &a, int amode, bool bkn, dim3 grid, hipStream_t s) {
+int launch_conv_x3(int cfg, const ConvArgs &a, int amode, bool bkn, dim3 grid, hipStream_t s) {
     if (a.vgrid_x > 0) {
-        if (x3_has_persist(cfg, amode, bkn)) conv_igemm_x3_persist<256, 256, 2, 8, 1, 1, 4, 0, ELT><<<grid, 512, 0, s>>>(a);
-        return;
+        // a persistent launch of a configuration without the persistent kernel would leave the output
+        // unwritten: an error, never a silent no-op (the planner only sets vgrid_* where it exists)
+        S2V_REQUIRE(x3_has_persist(cfg, amode, bkn),
+                    "conv2d: persistent launch (grid_cap) of x3 configuration %d / A mode %d, which has no "
+                    "persistent kernel", cfg, amode);
+        conv_igemm_x3_persist<256, 256, 2, 8, 1, 1, 4, 0, ELT><<<grid, 512, 0, s>>>(a);
+        return 0;
     }
     switch (cfg) {
         case 0: launch_x3<256, 256, 2, 8, 1, 1, ELT>(a, amode, bkn, grid, s); break;
@@ -647,6 +652,7 @@ void launch_conv_x3(int cfg, const ConvArgs &a, int amode, bool bkn, dim3 grid, 
         case 10: launch_x3<64, 64, 2, 4, 1, 2, ELT>(a, amode, bkn, grid, s); break;
         default: launch_x3<128, 32, 4, 4, 1, 2, ELT>(a, amode, bkn, grid, s); break;
     }
+    return 0;
 }
 
 }  // namespace s2v

@@ -321,224 +321,6 @@ __global__ __launch_bounds__(64 * NWV) void irfft2_mf(const float *__restrict__ 
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Split-fp32 MFMA variants (f16x3, the convolutions' arithmetic, conv_x3_impl.hpp): both 1-D passes
-// of a block's tile run as GEMMs on v_mfma_f32_16x16x32_f16 with every operand carried as f16
-// hi + lo halves (hi*hi + hi*lo + lo*hi, fp32 accumulate: <= 3 * 2^-22 relative per product).  The
-// 32x32x2 f32 MFMA of the kernels above runs at 1/16 of the f16 rate and left the 48x48 transforms
-// MFMA-bound at one block per CU (rfft 30 us, irfft 33 us per LNet FFC, on its critical branch).
-//   rfft2_x3   W pass  Y[(p,v)][(h,c)] = sum_w  fw[w][p][v] X[w][(h,c)]          M 2Wf, K S, N S*CG
-//              H pass  Z[(q,u)][(v,c)] = sum_(p,h) Fc[(q,u)][(p,h)] Y[(p,h)][(v,c)]   M 2S, K 2S, N Wf*CG
-//   irfft2_x3  H pass  Y[(p,h)][(v,c)] = sum_(q,u) Gc[(p,h)][(q,u)] Z[(q,u)][(v,c)]   M 2S, K 2S, N Wf*CG
-//              W pass  y[w][(h,c)]     = sum_(v,p) iw[v][p][w] Y[(2v+p)][(h,c)]      M S, K 2Wf, N S*CG
-// (Fc / Gc: the real 2x2-block forms of the complex fh / ih.)  A operands (the transform matrices,
-// fp32 in LDS) are scaled by 2^8 and split per fragment; B operands live in LDS as f16 hi / lo
-// planes [n][k] (k contiguous, one ds_read_b128 per fragment half); the accumulators are scaled
-// back by 2^-8 (exact).  Pads of K and N are zero in both operands.  One block (4 waves) per
-// (sample, CG channels); LDS: the two tables + one B plane pair (reused by the second pass).
-constexpr float FFT_ASCALE = 256.f, FFT_AINV = 1.f / 256.f;
-
-// (plain conversions, not conv_x3_impl.hpp's inline-asm v_fma_mix residual: these halves feed an
-// MFMA straight from registers, and the compiler's VALU -> MFMA hazard wait states do not cover an
-// asm-written operand — measured on MI355X: a tile scheduled right after its split lost the lo terms)
-__device__ __forceinline__ void split8h(const float (&v)[8], u32x4 &hi, u32x4 &lo) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const _Float16 h0 = (_Float16)v[2 * i], h1 = (_Float16)v[2 * i + 1];
-        const f16x2 hv = {h0, h1};
-        const f16x2 lv = {(_Float16)(v[2 * i] - (float)h0), (_Float16)(v[2 * i + 1] - (float)h1)};
-        hi[i] = __builtin_bit_cast(unsigned, hv);
-        lo[i] = __builtin_bit_cast(unsigned, lv);
-    }
-}
-
-__device__ __forceinline__ void store_split(_Float16 *hi_plane, _Float16 *lo_plane, int idx, float v) {
-    const _Float16 h = (_Float16)v;
-    hi_plane[idx] = h;
-    lo_plane[idx] = (_Float16)(v - (float)h);
-}
-
-constexpr int rup32(int v) { return (v + 31) / 32 * 32; }
-
-// C[M][N] = A[M][K] * B[K][N] over the block's 4 waves (wave w takes tiles w, w + 4, ...: slot
-// it = 0, 1, ... of the unrolled loop, so out(it, r, ...) indices are compile-time); A(m, k) -> fp32
-// (0 outside), B from the hi / lo planes [n][ldb] (k contiguous); out(it, r, m, n, value) for m < M,
-// n < N, value already unscaled
-template <int M, int N>
-constexpr int gemm_slots() { return (((M + 15) / 16) * ((N + 15) / 16) + 3) / 4; }
-
-template <int M, int K, int N, int LDB, typename AF, typename OF>
-__device__ __forceinline__ void gemm_x3(const _Float16 *bh, const _Float16 *bl, AF afun, OF out) {
-    constexpr int TM = (M + 15) / 16, TN = (N + 15) / 16, KS = rup32(K) / 32, SL = gemm_slots<M, N>();
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int l16 = lane & 15, kq = 8 * (lane >> 4);
-#pragma unroll
-    for (int it = 0; it < SL; ++it) {
-        const int t = wave + 4 * it;
-        if (t >= TM * TN) break;
-        const int tm = t / TN, tn = t - tm * TN;
-        const int m = tm * 16 + l16, nb = tn * 16 + l16;
-        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-            float av[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int k = ks * 32 + kq + j;
-                av[j] = (m < M && k < K) ? afun(m, k) * FFT_ASCALE : 0.f;
-            }
-            u32x4 ah, al;
-            split8h(av, ah, al);
-            const u32x4 bhv = *(const u32x4 *)(bh + nb * LDB + ks * 32 + kq);
-            const u32x4 blv = *(const u32x4 *)(bl + nb * LDB + ks * 32 + kq);
-            acc = mfma16x16<1>(al, bhv, acc);
-            acc = mfma16x16<1>(ah, blv, acc);
-            acc = mfma16x16<1>(ah, bhv, acc);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int mm = tm * 16 + 4 * (lane >> 4) + r;
-            if (mm < M && nb < N) out(it, r, mm, nb, acc[r] * FFT_AINV);
-        }
-    }
-}
-
-// the (it, r, m, n) positions gemm_x3<M, *, N> produced, in the same order (a replay of its output)
-template <int M, int N, typename F>
-__device__ __forceinline__ void gemm_positions(F f) {
-    constexpr int TM = (M + 15) / 16, TN = (N + 15) / 16, SL = gemm_slots<M, N>();
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-    for (int it = 0; it < SL; ++it) {
-        const int t = wave + 4 * it;
-        if (t >= TM * TN) break;
-        const int tm = t / TN, tn = t - tm * TN;
-        const int nn = tn * 16 + (lane & 15);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int m = tm * 16 + 4 * (lane >> 4) + r;
-            if (m < M && nn < N) f(it, r, m, nn);
-        }
-    }
-}
-
-template <int S, int CG>
-__global__ __launch_bounds__(256) void rfft2_x3(const float *__restrict__ x, int C, int xcs,
-                                                const float *__restrict__ tables, float *__restrict__ spec,
-                                                int scs) {
-    constexpr int WF = S / 2 + 1;
-    constexpr int N1 = S * CG, K1 = S, LD1 = rup32(K1) + 8, R1 = (N1 + 15) / 16 * 16;
-    constexpr int N2 = WF * CG, K2 = 2 * S, LD2 = rup32(K2) + 8, R2 = (N2 + 15) / 16 * 16;
-    constexpr int P1 = R1 * LD1, P2 = R2 * LD2;
-    constexpr int PB = P1 > P2 ? P1 : P2;            // halves per B plane
-    __shared__ float Tw[S * 2 * WF];                 // fw[w][p][v]
-    __shared__ float Th[S * 2 * S];                  // fh[h][p][u]
-    __shared__ __attribute__((aligned(16))) _Float16 B[2 * PB];
-    _Float16 *bh = B, *bl = B + PB;
-    const int groups = C / CG;
-    const int n = blockIdx.x / groups, c0 = (blockIdx.x - n * groups) * CG;
-    const int tid = threadIdx.x;
-    const FftTables T = fft_tables(tables, S, S);
-    for (int i = tid; i < S * 2 * WF; i += 256) Tw[i] = T.fw[i];
-    for (int i = tid; i < S * 2 * S; i += 256) Th[i] = T.fh[i];
-    for (int i = tid; i < 2 * PB; i += 256) B[i] = (_Float16)0.f;
-    __syncthreads();
-    // X as B1[k = w][n = (h, c)] -> planes [n][w]
-    for (int p = tid; p < S * S; p += 256) {
-        const int hh = p / S, ww = p - hh * S;
-        const float *src = x + ((long long)n * S * S + p) * xcs + c0;
-#pragma unroll
-        for (int c = 0; c < CG; ++c) store_split(bh, bl, (hh * CG + c) * LD1 + ww, src[c]);
-    }
-    __syncthreads();
-    // W pass: results held in registers until every wave is done with the X planes
-    float keep[gemm_slots<2 * WF, N1>()][4];
-    gemm_x3<2 * WF, K1, N1, LD1>(
-        bh, bl, [&](int m, int k) { const int pp = m >= WF ? 1 : 0; return Tw[(k * 2 + pp) * WF + m - pp * WF]; },
-        [&](int it, int r, int m, int nn, float v) { keep[it][r] = v; });
-    __syncthreads();
-    for (int i = tid; i < 2 * PB; i += 256) B[i] = (_Float16)0.f;
-    __syncthreads();
-    // Y as B2[k = (p, h)][n = (v, c)] -> planes [n][k]
-    gemm_positions<2 * WF, N1>([&](int it, int r, int m, int nn) {
-        const int pp = m >= WF ? 1 : 0, v = m - pp * WF, hh = nn / CG, c = nn - hh * CG;
-        store_split(bh, bl, (v * CG + c) * LD2 + pp * S + hh, keep[it][r]);
-    });
-    __syncthreads();
-    // H pass (complex, real 2x2 block form) -> spec[n][u*Wf + v][q*C + c0 + c]
-    gemm_x3<2 * S, K2, N2, LD2>(
-        bh, bl,
-        [&](int m, int k) {
-            const int q = m >= S ? 1 : 0, u = m - q * S, pp = k >= S ? 1 : 0, hh = k - pp * S;
-            const float fr = Th[(hh * 2) * S + u], fi = Th[(hh * 2 + 1) * S + u];
-            return q == pp ? fr : (q == 0 ? -fi : fi);
-        },
-        [&](int, int, int m, int nn, float v) {
-            const int q = m >= S ? 1 : 0, u = m - q * S, vv = nn / CG, c = nn - vv * CG;
-            spec[((long long)n * S * WF + u * WF + vv) * scs + q * C + c0 + c] = v;
-        });
-}
-
-template <int S, int CG>
-__global__ __launch_bounds__(256) void irfft2_x3(const float *__restrict__ spec, int C, int scs,
-                                                 const float *__restrict__ tables, const float *__restrict__ res,
-                                                 int rcs, float *__restrict__ y, int ycs) {
-    constexpr int WF = S / 2 + 1;
-    constexpr int N1 = WF * CG, K1 = 2 * S, LD1 = rup32(K1) + 8, R1 = (N1 + 15) / 16 * 16;
-    constexpr int N2 = S * CG, K2 = 2 * WF, LD2 = rup32(K2) + 8, R2 = (N2 + 15) / 16 * 16;
-    constexpr int P1 = R1 * LD1, P2 = R2 * LD2;
-    constexpr int PB = P1 > P2 ? P1 : P2;
-    __shared__ float Ti[S * 2 * S];                  // ih[u][p][h]
-    __shared__ float Tw[WF * 2 * S];                 // iw[v][p][w]
-    __shared__ __attribute__((aligned(16))) _Float16 B[2 * PB];
-    _Float16 *bh = B, *bl = B + PB;
-    const int groups = C / CG;
-    const int n = blockIdx.x / groups, c0 = (blockIdx.x - n * groups) * CG;
-    const int tid = threadIdx.x;
-    const FftTables T = fft_tables(tables, S, S);
-    for (int i = tid; i < S * 2 * S; i += 256) Ti[i] = T.ih[i];
-    for (int i = tid; i < WF * 2 * S; i += 256) Tw[i] = T.iw[i];
-    for (int i = tid; i < 2 * PB; i += 256) B[i] = (_Float16)0.f;
-    __syncthreads();
-    // Z as B1[k = (q, u)][n = (v, c)] -> planes [n][k]
-    for (int i = tid; i < S * WF * 2; i += 256) {
-        const int q = i & 1, f = i >> 1;
-        const int u = f / WF, v = f - u * WF;
-        const float *src = spec + ((long long)n * S * WF + f) * scs + q * C + c0;
-#pragma unroll
-        for (int c = 0; c < CG; ++c) store_split(bh, bl, (v * CG + c) * LD1 + q * S + u, src[c]);
-    }
-    __syncthreads();
-    float keep[gemm_slots<2 * S, N1>()][4];
-    gemm_x3<2 * S, K1, N1, LD1>(
-        bh, bl,
-        [&](int m, int k) {
-            const int pp = m >= S ? 1 : 0, hh = m - pp * S, q = k >= S ? 1 : 0, u = k - q * S;
-            const float gr = Ti[(u * 2) * S + hh], gi = Ti[(u * 2 + 1) * S + hh];
-            return pp == q ? gr : (pp == 0 ? -gi : gi);
-        },
-        [&](int it, int r, int m, int nn, float v) { keep[it][r] = v; });
-    __syncthreads();
-    for (int i = tid; i < 2 * PB; i += 256) B[i] = (_Float16)0.f;
-    __syncthreads();
-    // Y as B2[k = 2v + p][n = (h, c)] -> planes [n][k]
-    gemm_positions<2 * S, N1>([&](int it, int r, int m, int nn) {
-        const int pp = m >= S ? 1 : 0, hh = m - pp * S, v = nn / CG, c = nn - v * CG;
-        store_split(bh, bl, (hh * CG + c) * LD2 + 2 * v + pp, keep[it][r]);
-    });
-    __syncthreads();
-    // c2r W pass -> y[n][h][w][c0 + c] (+ res)
-    gemm_x3<S, K2, N2, LD2>(
-        bh, bl, [&](int m, int k) { return Tw[k * S + m]; },     // iw[v][p][w] at (2v + p) * S + w
-        [&](int, int, int m, int nn, float v) {
-            const int hh = nn / CG, c = nn - hh * CG;
-            const long long pix = ((long long)n * S + hh) * S + m;
-            float o = v;
-            if (res) o += res[pix * rcs + c0 + c];
-            y[pix * ycs + c0 + c] = o;
-        });
-}
-
 // 4 channels per block: the most blocks (the transforms are small, parallelism matters more
 // than table reuse), 16-byte channel vectors for the global loads / stores.
 static int pick_cg(int C, int H, int W, size_t per_cg_floats, size_t fixed_floats) {
@@ -566,13 +348,6 @@ extern "C" int s2v_rfft2(const float *x, int n, int h, int w, int c, int xcs, co
     S2V_REQUIRE(cg > 0, "rfft2: C %% 4 != 0 or the %dx%d tile does not fit in LDS", h, w);
     const bool aligned = xcs % 4 == 0 && ((uintptr_t)x % 16) == 0;
     hipStream_t st = (hipStream_t)stream;
-    if (h == w && (h == 12 || h == 24 || h == 48) && c % 4 == 0 && tune_get(S2V_TUNE_FFT_X3)) {
-        // split-fp32 MFMA transforms: 2 channels per block at 48x48 (more blocks), else 4
-        if (h == 12) rfft2_x3<12, 4><<<n * (c / 4), 256, 0, st>>>(x, c, xcs, tables, spec, scs);
-        else if (h == 24) rfft2_x3<24, 4><<<n * (c / 4), 256, 0, st>>>(x, c, xcs, tables, spec, scs);
-        else rfft2_x3<48, 2><<<n * (c / 2), 256, 0, st>>>(x, c, xcs, tables, spec, scs);
-        return check_launch("rfft2");
-    }
     if (c % FCG == 0 && aligned && h == w && (h == 12 || h == 24 || h == 48)) {
         const unsigned grid = n * (c / FCG);
         // 48x48: 8 waves per block (one block per CU by LDS).  2 channels per block (twice the blocks,
@@ -602,12 +377,6 @@ extern "C" int s2v_irfft2(const float *spec, int n, int h, int w, int c, int scs
     const int cg = pick_cg(c, h, w, per, fixed);
     S2V_REQUIRE(cg > 0, "irfft2: C %% 4 != 0 or the %dx%d tile does not fit in LDS", h, w);
     hipStream_t st = (hipStream_t)stream;
-    if (h == w && (h == 12 || h == 24 || h == 48) && c % 4 == 0 && tune_get(S2V_TUNE_FFT_X3)) {
-        if (h == 12) irfft2_x3<12, 4><<<n * (c / 4), 256, 0, st>>>(spec, c, scs, tables, res, rcs, y, ycs);
-        else if (h == 24) irfft2_x3<24, 4><<<n * (c / 4), 256, 0, st>>>(spec, c, scs, tables, res, rcs, y, ycs);
-        else irfft2_x3<48, 2><<<n * (c / 2), 256, 0, st>>>(spec, c, scs, tables, res, rcs, y, ycs);
-        return check_launch("irfft2");
-    }
     if (c % FCG == 0 && h == w && (h == 12 || h == 24 || h == 48)) {
         const unsigned grid = n * (c / FCG);
         if (h == 12) irfft2_mf<12, 4><<<grid, 256, 0, st>>>(spec, c, scs, tables, res, rcs, y, ycs);

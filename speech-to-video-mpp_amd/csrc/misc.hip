@@ -651,24 +651,40 @@ __global__ __launch_bounds__(256) void fill_kernel(float *__restrict__ y, long l
     for (long long e = blockIdx.x * 256LL + threadIdx.x; e < n; e += (long long)gridDim.x * 256) y[e] = v;
 }
 
-// max |x| of an NHWC view (the split precisions' per-layer activation range, conv x_scale): a wave
-// max per block, one atomic max on the fp32 bits (non-negative floats order as unsigned ints; a NaN
-// has the largest bits, so it propagates)
+// max |x| of an NHWC view (the split precisions' per-layer activation range, conv x_scale).  A block
+// walks pixel rows (TPR = 2^tpr_shift threads per row, 16-byte channel quads when VEC), keeps a
+// running max of the fp32 bits (non-negative floats order as unsigned ints; a NaN has the largest
+// bits, so it propagates), reduces it over the wave and the block, and folds it with one atomic max.
+// No per-element division: the row walk is a grid-stride loop over pixels.
+template <bool VEC>
 __global__ __launch_bounds__(256) void amax_kernel(const float *__restrict__ x, long long pixels, int c, int xcs,
-                                                   unsigned *__restrict__ out) {
-    const long long total = pixels * c;
+                                                   int tpr_shift, unsigned *__restrict__ out) {
+    __shared__ unsigned red[4];
+    const int tid = threadIdx.x;
+    const int tpr = 1 << tpr_shift, lane_r = tid & (tpr - 1);
+    const int rpb = 256 >> tpr_shift;
     unsigned mb = 0;
-    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
-        const long long p = e / c;
-        const unsigned b = __float_as_uint(fabsf(x[p * xcs + (e - p * c)]));
-        mb = b > mb ? b : mb;
+    for (long long p = (long long)blockIdx.x * rpb + (tid >> tpr_shift); p < pixels; p += (long long)gridDim.x * rpb) {
+        const float *row = x + p * xcs;
+        if (VEC) {
+            for (int q = lane_r; q < (c >> 2); q += tpr) {
+                const float4 v = *(const float4 *)(row + 4 * q);
+                const unsigned a = max(__float_as_uint(fabsf(v.x)), __float_as_uint(fabsf(v.y)));
+                const unsigned b = max(__float_as_uint(fabsf(v.z)), __float_as_uint(fabsf(v.w)));
+                mb = max(mb, max(a, b));
+            }
+        } else {
+            for (int j = lane_r; j < c; j += tpr) mb = max(mb, __float_as_uint(fabsf(row[j])));
+        }
     }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const unsigned t = __shfl_xor(mb, o);
-        mb = t > mb ? t : mb;
+    for (int o = 32; o > 0; o >>= 1) mb = max(mb, (unsigned)__shfl_xor((int)mb, o));
+    if ((tid & 63) == 0) red[tid >> 6] = mb;
+    __syncthreads();
+    if (tid == 0) {
+        mb = max(max(red[0], red[1]), max(red[2], red[3]));
+        if (mb) atomicMax(out, mb);
     }
-    if ((threadIdx.x & 63) == 0 && mb) atomicMax(out, mb);
 }
 
 // Per-sample StyleGAN2 weights (base_blocks.py:487-495 / stylegan2_clean_arch.py:66-80 /
@@ -925,7 +941,17 @@ extern "C" int s2v_fill(float *y, long long n, float value, s2v_stream_t stream)
 extern "C" int s2v_amax(const float *x, long long pixels, int c, int xcs, float *out, s2v_stream_t stream) {
     S2V_REQUIRE(x && out && pixels >= 0 && c > 0 && xcs >= c, "amax: bad args");
     if (pixels == 0) return 0;
-    amax_kernel<<<grid_for(pixels * c), 256, 0, (hipStream_t)stream>>>(x, pixels, c, xcs, (unsigned *)out);
+    const bool vec = c % 4 == 0 && xcs % 4 == 0 && ((uintptr_t)x % 16) == 0;
+    const int units = vec ? c / 4 : c;                  // per-row work items
+    int sh = 0;
+    while ((1 << sh) < units && sh < 6) ++sh;           // threads per row: units rounded up, at most 64
+    const long long rows_per_block = 256 >> sh;
+    long long blocks = (pixels + rows_per_block - 1) / rows_per_block;
+    if (blocks > 2048) blocks = 2048;                   // 8 blocks per CU, grid-stride beyond
+    if (vec)
+        amax_kernel<true><<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(x, pixels, c, xcs, sh, (unsigned *)out);
+    else
+        amax_kernel<false><<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(x, pixels, c, xcs, sh, (unsigned *)out);
     return check_launch("amax");
 }
 

@@ -139,10 +139,10 @@ void set_range(s2v_conv_params &p, double x_scale, const OptT &nonfinite, const 
 }
 
 std::vector<int64_t> plan_list(const s2v_conv_params &p, int64_t need) {
-    int pl[10] = {0};
+    int pl[11] = {0};
     check(s2v_conv2d_plan(&p, pl), "s2v_conv2d_plan");
     std::vector<int64_t> out{need};
-    for (int i = 0; i < 10; ++i) out.push_back(pl[i]);
+    for (int i = 0; i < 11; ++i) out.push_back(pl[i]);
     return out;
 }
 
@@ -224,7 +224,7 @@ void conv_common(s2v_conv_params &p, const Tensor &x, const Tensor &y, int64_t c
 // (and, for the split precisions, their s2v_split_weights copy).  Returns [ws_need, plan...]:
 // ws_need 0 = launched (or dry run of a launch that needs no workspace); > 0 = bytes of workspace
 // the launch needs (nothing launched when ``ws`` is smaller, or ``dry``); plan = s2v_conv2d_plan's
-// ten ints (the kernel instance the launch runs).
+// eleven ints (the kernel instance the launch runs).
 std::vector<int64_t> conv2d_(const Tensor &x, const Tensor &y, const Tensor &wt, const OptT &wt_split,
                              double wt_scale, int64_t cout, at::IntArrayRef kernel, at::IntArrayRef stride,
                              at::IntArrayRef padding, at::IntArrayRef dilation, int64_t in_mode, int64_t pad_mode,
@@ -232,7 +232,7 @@ std::vector<int64_t> conv2d_(const Tensor &x, const Tensor &y, const Tensor &wt,
                              const OptT &nc_scale, int64_t pre_act, double pre_alpha, const OptT &pix_add,
                              double pix_w, const OptT &res, at::IntArrayRef res_offset, bool res_after_act,
                              int64_t act, double alpha, int64_t out_step, bool out_pool, bool x_split, const OptT &ws,
-                             const OptT &tile_counters, int64_t force_tile, int64_t force_splits, const OptT &stamps,
+                             int64_t grid_cap, int64_t force_tile, int64_t force_splits, const OptT &stamps,
                              const OptT &stamp_ctr, at::IntArrayRef stamp_pos, double x_scale, const OptT &nonfinite,
                              bool dry) {
     const c10::DeviceGuard guard(x.device());
@@ -258,7 +258,7 @@ std::vector<int64_t> conv2d_(const Tensor &x, const Tensor &y, const Tensor &wt,
     if (prec != S2V_PREC_F32) {
         // the plan only checks that split weights are present before choosing an x3 kernel
         p.wt_x3 = p.wt;
-        int pl[10] = {0};
+        int pl[11] = {0};
         check(s2v_conv2d_plan(&p, pl), "s2v_conv2d_plan");
         p.wt_x3 = nullptr;
         if (pl[6]) {
@@ -269,12 +269,8 @@ std::vector<int64_t> conv2d_(const Tensor &x, const Tensor &y, const Tensor &wt,
             p.wt_scale = (float)wt_scale;
         }
     }
-    if (has(tile_counters)) {
-        same_dev(*tile_counters, dev, "conv tile_counters");
-        TORCH_CHECK(tile_counters->scalar_type() == at::kInt && tile_counters->is_contiguous(),
-                    "conv tile_counters: int32");
-        p.tile_counters = tile_counters->data_ptr<int>(); p.n_counters = (int)tile_counters->numel();
-    }
+    TORCH_CHECK(grid_cap >= 0 && grid_cap % 8 == 0, "conv grid_cap: 0 or a positive multiple of 8");
+    p.grid_cap = (int)grid_cap;
     set_stamps(p, stamps, stamp_ctr, stamp_pos, dev);
     set_range(p, x_scale, nonfinite, dev);
     const size_t need = s2v_conv2d_ws_bytes(&p);
@@ -344,7 +340,7 @@ std::vector<int64_t> modulated_conv2d_(const Tensor &x, const Tensor &y, const T
     bool x3 = false;
     if (prec != S2V_PREC_F32) {
         p.wt_x3 = p.wt;
-        int pl[10] = {0};
+        int pl[11] = {0};
         check(s2v_conv2d_plan(&p, pl), "s2v_conv2d_plan");
         x3 = pl[6] != 0;
         p.wt_x3 = nullptr;
@@ -823,7 +819,7 @@ TORCH_LIBRARY_FRAGMENT(s2v, m) {
           "int[2] stride, int[2] padding, int[2] dilation, int in_mode, int pad_mode, int prec, Tensor? scale, "
           "Tensor? shift, Tensor? in_scale, Tensor? nc_scale, int pre_act, float pre_alpha, Tensor? pix_add, "
           "float pix_w, Tensor? res, int[2] res_offset, bool res_after_act, int act, float alpha, int out_step, "
-          "bool out_pool, bool x_split, Tensor? ws, Tensor? tile_counters, int force_tile, int force_splits, "
+          "bool out_pool, bool x_split, Tensor? ws, int grid_cap, int force_tile, int force_splits, "
           "Tensor(s!)? stamps, Tensor? stamp_ctr, int[3] stamp_pos, float x_scale, Tensor(f!)? nonfinite, "
           "bool dry) -> int[]");
     m.def("modulated_conv2d_(Tensor x, Tensor(a!) y, Tensor wt, Tensor s, Tensor? d, Tensor(b!) wbuf, int cout, "

@@ -28,12 +28,20 @@ FUSED_TORGB = os.environ.get("S2V_ENET_FUSED_TORGB", "1") == "1"
 # (ops.modulated_conv2d d2s: the bilinear taps folded into 4 parity-class filters, written depth-to-space)
 # plus the four border lines recomputed exactly; S2V_ENET_POLY_UP=0: upsample pass + conv
 POLY_UP = os.environ.get("S2V_ENET_POLY_UP", "1") == "1"
-# the style encoder's split-precision convs (launched beside LNet) as this many persistent blocks
-# (s2v.h S2V_TUNE_X3_GRID_CAP): the CUs they leave free take LNet's latency-bound kernels as soon as
-# they are launched instead of after the encoder's 100-200 us tiles drain; 0: one block per tile.
-# 128 (half the CUs; divides every encoder layer's tile count) on MI355X, lipsync B=16: 29.1 -> 26.1-26.5
-# ms (192: 28.5, 160: 27.1, 112: 28.9, 96: 31.4, 64: 38.9; r03)
-STYLE_GRID = int(os.environ.get("S2V_ENET_STYLE_GRID", "128"))
+# the style encoder's split-precision convs (launched beside LNet) as persistent blocks on half the
+# device's CUs (s2v_conv_params.grid_cap, ops.half_chip_blocks): the CUs they leave free take LNet's
+# latency-bound kernels as soon as they are launched instead of after the encoder's 100-200 us tiles
+# drain.  On MI355X (256 CUs: 128 blocks, which divides every encoder layer's tile count), lipsync B=16
+# 29.1 -> 26.1-26.5 ms (caps 192: 28.5, 160: 27.1, 112: 28.9, 96: 31.4, 64: 38.9; r03).
+# S2V_ENET_STYLE_GRID: an explicit block count (0: one block per tile).
+STYLE_GRID = os.environ.get("S2V_ENET_STYLE_GRID", "half")
+
+
+def style_grid(device) -> int:
+    """Persistent blocks of the style encoder's convs on ``device`` (STYLE_GRID)."""
+    if STYLE_GRID == "half":
+        return ops.half_chip_blocks(device)
+    return int(STYLE_GRID)
 
 # x2 bilinear upsample (align_corners=False) followed by a 3-tap conv, per output parity r: weight of
 # input tap a (i-1, i, i+1) from conv tap p (-1, 0, 1), away from the image border
@@ -197,7 +205,7 @@ class ENetEngine:
             sst, sctx = side
             cur_st = torch.cuda.current_stream(dev)
             sst.wait_stream(cur_st)
-            with ops.x3_grid_cap(ctx, STYLE_GRID), ops.side_stream(sst, ctx.keep):
+            with ops.x3_grid_cap(sctx, style_grid(dev)), ops.side_stream(sst, ctx.keep):
                 style = self.style_code(sctx, face[:, 3:])
                 ops.conv2d(sctx, style, self.mod, svec)
         else:

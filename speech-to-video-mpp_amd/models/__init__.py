@@ -57,6 +57,32 @@ class _EngineMixin:
         self.__dict__.pop("_s2v_engines", None)
         return self
 
+    def _guarded(self, ctx, fn):
+        """Run one eager forward ``fn()`` on lane ``ctx`` under the f16x3 range guard (ops): the
+        engine's first forward calibrates every layer's activation pre-scale (one host sync, re-run when
+        a layer needed a scale); every eager forward then reads the lane's non-finite flag when it returns
+        (one host sync) and, when a launch overflowed, runs again in bf16x3 — so an out-of-range batch
+        returns correct outputs instead of silent inf / NaN.  Inside a graph capture the forward is only
+        recorded (a replayed graph's flag is read by its caller: pipeline.LipSyncPipeline.run)."""
+        if not ops.guard_active() or (ctx.device.type == "cuda" and torch.cuda.is_current_stream_capturing()):
+            return fn()
+        eng = self._s2v_engines[str(ctx.device)][0]
+        done = eng.__dict__.setdefault("_calibrated", set())
+        calibrating = ops.PRECISION not in done
+        if calibrating:
+            ops.begin_calibration(ctx)
+        out = fn()
+        state = ops.end_forward(ctx, calibrating)
+        done.add(ops.PRECISION)
+        if state == "scaled":
+            out = fn()
+            state = ops.end_forward(ctx, False)
+        if state == "overflow":
+            with ops.precision("bf16x3"):
+                out = fn()
+            ctx.reruns += 1
+        return out
+
     def __getstate__(self):
         state = dict(self.__dict__)
         state.pop("_s2v_engines", None)
@@ -89,7 +115,7 @@ class LNet(_EngineMixin, arch.LNetParams):
         x6 = NHWC.empty(n, h, w, 6, dev)
         ops.nchw_to_nhwc(ctx, face_sequences.float(), x6)
         lo = NHWC.empty(n, h, w, 3, dev)
-        eng.forward(ctx, audio_sequences.float(), x6, lo)
+        self._guarded(ctx, lambda: eng.forward(ctx, audio_sequences.float(), x6, lo))
         out = torch.empty((n, 3, h, w), device=dev)
         ops.nhwc_to_nchw(ctx, lo, out)
         if five:
@@ -122,7 +148,8 @@ class ENet(_EngineMixin, arch.ENetParams):
         dev = face_sequences.device
         out = torch.empty((n, 3, 384, 384), device=dev)
         low = torch.empty((n, 3, 96, 96), device=dev)
-        eng.forward(ctx, audio_sequences.float(), face_sequences.float(), gt_sequences.float(), out, low, noises)
+        self._guarded(ctx, lambda: eng.forward(ctx, audio_sequences.float(), face_sequences.float(),
+                                               gt_sequences.float(), out, low, noises))
         if five:
             out = torch.stack(torch.split(out, b, 0), 2)
             # F.interpolate(low_res_img, outputs.size()[3:]) (default mode 'nearest', ENet.py:134)
@@ -144,7 +171,7 @@ class DNet(_EngineMixin, arch.DNetParams):
         """``lane`` (keyword-only, not in the reference): the execution lane (see _EngineMixin)."""
         _need_cuda(input_image, driving_source)
         eng, ctx = self._engine(input_image.device, lane)
-        return eng.forward(ctx, input_image.float(), driving_source.float(), stage=stage)
+        return self._guarded(ctx, lambda: eng.forward(ctx, input_image.float(), driving_source.float(), stage=stage))
 
 
 # ----------------------------------------------------------------------------- enhancers
@@ -162,7 +189,8 @@ class GFPGANv1Clean(_EngineMixin, enhancer_arch.GFPGANv1CleanParams):
         _need_cuda(x)
         eng, ctx = self._engine(x.device)
         out = torch.empty_like(x, dtype=torch.float32)
-        return eng.forward(ctx, x.float(), out, return_rgb=return_rgb, randomize_noise=randomize_noise)
+        return self._guarded(ctx, lambda: eng.forward(ctx, x.float(), out, return_rgb=return_rgb,
+                                                      randomize_noise=randomize_noise))
 
 
 class FullGenerator(_EngineMixin, enhancer_arch.FullGeneratorParams):
@@ -183,7 +211,8 @@ class FullGenerator(_EngineMixin, enhancer_arch.FullGeneratorParams):
         eng, ctx = self._engine(inputs.device)
         out = torch.empty_like(inputs, dtype=torch.float32)
         lat = torch.empty((inputs.shape[0], self.style_dim), device=inputs.device) if return_latents else None
-        eng.forward(ctx, inputs.float(), out, input_is_latent=input_is_latent, latent_out=lat)
+        self._guarded(ctx, lambda: eng.forward(ctx, inputs.float(), out, input_is_latent=input_is_latent,
+                                               latent_out=lat))
         if return_latents:
             return out, lat.unsqueeze(1).expand(-1, self.generator.n_latent, -1)
         return out, None
@@ -205,7 +234,7 @@ class ParseNet(_EngineMixin, parse_arch.ParseNetParams):
         b, _, h, w = x.shape
         mask = torch.empty((b, self.parsing_ch, h, w), device=x.device)
         img = torch.empty((b, 3, h, w), device=x.device)
-        return eng.forward(ctx, x.float(), mask, img)
+        return self._guarded(ctx, lambda: eng.forward(ctx, x.float(), mask, img))
 
 
 class RRDBNet(_EngineMixin, sr_arch.RRDBNetParams):
@@ -227,7 +256,7 @@ class RRDBNet(_EngineMixin, sr_arch.RRDBNetParams):
             raise RuntimeError(f"RRDBNet(scale={self.scale}): input size {tuple(x.shape[2:])} must be a multiple of {r}")
         b, _, h, w = x.shape
         out = torch.empty((b, self.num_out_ch, h * self.scale, w * self.scale), device=x.device)
-        return eng.forward(ctx, x.float(), out)
+        return self._guarded(ctx, lambda: eng.forward(ctx, x.float(), out))
 
 
 # ----------------------------------------------------------------------------- loaders
@@ -249,7 +278,7 @@ class RetinaFace(_EngineMixin, retinaface_arch.RetinaFaceParams):
     def head_maps(self, x4: NHWC):
         """x4: NHWC [B,H,W,4] fp32 (BGR minus means, channel 3 zero) -> per-level fused head maps."""
         eng, ctx = self._engine(x4.t.device)
-        return eng.forward_maps(ctx, x4), ctx
+        return self._guarded(ctx, lambda: eng.forward_maps(ctx, x4)), ctx
 
     @torch.no_grad()
     def forward(self, inputs):
@@ -263,7 +292,7 @@ class RetinaFace(_EngineMixin, retinaface_arch.RetinaFaceParams):
         x4 = NHWC.empty(b, h, w, 4, inputs.device)
         ops.fill(ctx, x4.t)
         ops.nchw_to_nhwc(ctx, inputs.float(), x4.slice(0, 3))
-        maps = eng.forward_maps(ctx, x4)
+        maps = self._guarded(ctx, lambda: eng.forward_maps(ctx, x4))
         if self.phase != "test":
             return eng.split_heads(maps)
         return retina_outputs(ctx, maps, h, w)
@@ -296,7 +325,7 @@ class ReconNetWrapper(_EngineMixin, face3d_arch.ReconNetWrapperParams):
     def forward_nhwc(self, x4: NHWC) -> torch.Tensor:
         """x4: NHWC [B,H,W,4] fp32 (RGB / 255, channel 3 zero) -> coefficients [B, 257] (view)."""
         eng, ctx = self._engine(x4.t.device)
-        return eng.forward(ctx, x4)
+        return self._guarded(ctx, lambda: eng.forward(ctx, x4))
 
     @torch.no_grad()
     def forward(self, x):
@@ -310,7 +339,7 @@ class ReconNetWrapper(_EngineMixin, face3d_arch.ReconNetWrapperParams):
         x4 = NHWC.empty(b, h, w, 4, x.device)
         ops.fill(ctx, x4.t)
         ops.nchw_to_nhwc(ctx, x.float(), x4.slice(0, 3))
-        return eng.forward(ctx, x4).clone()
+        return self._guarded(ctx, lambda: eng.forward(ctx, x4)).clone()
 
 
 def define_net_recon(net_recon, use_last_fc=False, init_path=None):

@@ -47,29 +47,28 @@ if PRECISION not in _PRECISIONS:
 # f16x3 activation range guard.  The f16 halves of a split operand cover |v| < 65504, and a lo half
 # becomes an f16 subnormal (absolute spacing 2^-24) once |v| < 2^-3.  Weights are pre-scaled by a
 # power of two at packing (ConvW.split_scale); activations get a per-layer power-of-two pre-scale
-# (s2v_conv_params.x_scale) chosen from the layer input's max |v| on its first eager run (``s2v::amax_``):
-# a layer whose max lies outside [X_LO, X_HI) is scaled so that it lands in [2^13, 2^14).  Every
-# f16x3 launch also carries the lane's non-finite flag: an input that still overflows (a later
-# batch far outside the calibrated range) sets it, and check_range() raises — never silent.
-# S2V_RANGE_GUARD=0 turns both off.
+# (s2v_conv_params.x_scale) chosen from the max |v| of the operand the kernel splits (the layer input,
+# times max |in_scale| for a StyleGAN2 modulated input) on the engine's first forward: a layer whose
+# max lies outside [X_LO, X_HI) is scaled so that it lands in [2^X_TARGET, 2^(X_TARGET + 1)), 64x below
+# the f16 ceiling.  The first forward measures every layer into one device buffer and reads it with a
+# single host sync (begin_calibration / end_forward); it is re-run with the scales when any layer needed
+# one.  Every f16x3 launch also carries the lane's non-finite flag: an eager forward reads it when it
+# returns (models._EngineMixin) and re-runs itself in bf16x3 (fp32's exponent range) when it is set; a
+# graph-replayed pipeline batch copies it per batch and re-runs flagged batches the same way
+# (pipeline.LipSyncPipeline.run) — an overflow is never silent and never left in the output.
+# S2V_RANGE_GUARD=0 turns all of this off.
 RANGE_GUARD = os.environ.get("S2V_RANGE_GUARD", "1") == "1"
 X_LO, X_HI = 2.0 ** -3, 2.0 ** 14
+X_TARGET = 9
 
 
 def x_scale_for(amax: float) -> float:
-    """Power-of-two activation pre-scale for a layer whose input max |v| is ``amax``."""
+    """Power-of-two activation pre-scale for a layer whose split operand has max |v| = ``amax``."""
     if not (amax > 0.0) or math.isinf(amax):
         return 1.0
     if X_LO <= amax < X_HI:
         return 1.0
-    return float(2.0 ** (13 - math.floor(math.log2(amax))))
-
-
-# in-launch split-K fold (s2v_conv_params.tile_counters), opt-in with S2V_SPLITK_FOLD=1.  It gives
-# the separate reduce kernel's sums bit for bit, but its agent-scope release / acquire per split
-# block (L2 writeback + invalidate on this part) measured 1.5x slower end to end on MI355X (lipsync
-# 445 -> 290 frames/s, r01), so the separate reduce launch stays the default.
-USE_TILE_COUNTERS = os.environ.get("S2V_SPLITK_FOLD", "0") == "1"
+    return float(2.0 ** (X_TARGET - math.floor(math.log2(amax))))
 
 
 def set_precision(name: str) -> str:
@@ -80,6 +79,16 @@ def set_precision(name: str) -> str:
         raise ValueError(f"precision must be one of {sorted(_PRECISIONS)}, got {name!r}")
     prev, PRECISION = PRECISION, name
     return prev
+
+
+@contextlib.contextmanager
+def precision(name: str):
+    """set_precision(name) for the launches issued inside the block."""
+    prev = set_precision(name)
+    try:
+        yield
+    finally:
+        set_precision(prev)
 
 
 def prec_code() -> int:
@@ -247,18 +256,19 @@ class Ctx:
     only read-only weights, so two Ctx objects can run forwards of the same engine concurrently
     (two captured graphs replayed on two streams): nothing either graph writes is shared."""
 
-    N_COUNTERS = 1 << 18
     ALL = weakref.WeakSet()          # every context (check_all_ranges)
 
     def __init__(self, device):
         self.device = torch.device(device)
         self.ws = Workspace(self.device)
         self.lib = _lib.load()
-        self._counters = None
         self._streams = {}
         self._noise = {}
         self.keep = []          # the current forward's side-branch tensors (side_stream), dropped per forward
         self.parent = None      # side-branch contexts share their lane's range flag
+        self.grid_cap = 0       # s2v_conv_params.grid_cap of this context's convs (x3_grid_cap)
+        self.calib = None       # the lane's calibration forward in progress (begin_calibration)
+        self.reruns = 0         # forwards re-run in bf16x3 after a range overflow (end_forward)
         self._flag = None
         Ctx.ALL.add(self)
 
@@ -301,15 +311,6 @@ class Ctx:
         if key not in self._noise:
             self._noise[key] = NoiseCounter()
         return self._noise[key]
-
-    def counters(self):
-        """Zeroed split-K tile counters (s2v_conv_params.tile_counters), made once per context
-        (eagerly, before any graph capture replays the convs that use them)."""
-        if self._counters is None:
-            if self.device.type != "cuda" or torch.cuda.is_current_stream_capturing():
-                return None
-            self._counters = torch.zeros(self.N_COUNTERS, dtype=torch.int32, device=self.device)
-        return self._counters
 
     @property
     def stream(self):
@@ -484,8 +485,8 @@ def _conv(ctx, x, cw, yv, out_step, act, alpha, resv, res_after, res_offset, nc_
                             f"in {PRECISION!r} (code {prec}); split it again with split_act after set_precision")
     wsplit = cw.wt_x3(ctx, prec) if prec != PREC_F32 else None
     wscale = cw.split_scale(prec)
-    xscale, flag = _range(ctx, cw, x, prec)
-    counters = _counters(ctx)
+    xscale, flag = _range(ctx, cw, x, prec, in_scale)
+    cap = int(getattr(ctx, "grid_cap", 0))
     sc = cw.scale if scale is None else scale
     sh = cw.shift if shift is None else shift
 
@@ -493,7 +494,7 @@ def _conv(ctx, x, cw, yv, out_step, act, alpha, resv, res_after, res_offset, nc_
         return S2V.conv2d_(x.v, yv, cw.wt, wsplit, wscale, cw.cout, [cw.kh, cw.kw], [cw.sh, cw.sw], [cw.ph, cw.pw],
                            [cw.dh, cw.dw], cw.in_mode, cw.pad_mode, prec, sc, sh, in_scale, nc_scale, pre_act, pre_alpha,
                            pix_add, pix_w, resv, list(res_offset), res_after, act, alpha, out_step, pool, x_split != 0,
-                           ws, counters, force_tile, force_splits, st[0], st[1], st[2], xscale, flag, dry)
+                           ws, cap, force_tile, force_splits, st[0], st[1], st[2], xscale, flag, dry)
     _run_conv(ctx, launch, x, cw, yv, pool, in_scale, nc_scale, pix_add, resv)
 
 
@@ -503,9 +504,85 @@ def check_all_ranges(what="s2v"):
         c.check_range(what)
 
 
-def _range(ctx, cw, x, prec):
-    """(x_scale, flag) of an f16x3 launch: the layer's calibrated activation pre-scale (measured on
-    its first eager call, ``s2v::amax_``) and the lane's non-finite flag."""
+def guard_active() -> bool:
+    """The f16x3 range guard applies to launches issued now."""
+    return RANGE_GUARD and PRECISION == "f16x3"
+
+
+class _Calibration:
+    """Layers measured during one calibration forward: amax slots in one device buffer."""
+    SLOTS = 4096
+
+    def __init__(self, device):
+        self.device = device
+        self.bufs = [torch.zeros(self.SLOTS, device=device)]
+        self.n = 0
+        self.items = []          # (cw, prec, x slot, in_scale slot or -1)
+
+    def slot(self):
+        if self.n == len(self.bufs) * self.SLOTS:
+            self.bufs.append(torch.zeros(self.SLOTS, device=self.device))
+        i = self.n
+        self.n += 1
+        return i, self.bufs[i // self.SLOTS][i % self.SLOTS: i % self.SLOTS + 1]
+
+
+def _root(ctx):
+    while getattr(ctx, "parent", None) is not None:
+        ctx = ctx.parent
+    return ctx
+
+
+def _amax_into(t: torch.Tensor, out: torch.Tensor):
+    """max |t| of an NHWC view (4-D) or an [N, C] row view (2-D) into out (float32 [1])."""
+    if t.dim() == 2:
+        n, c = t.shape
+        t = t.as_strided((1, 1, n, c), (n * t.stride(0), n * t.stride(0), t.stride(0), 1))
+    S2V.amax_(t, out)
+
+
+def begin_calibration(ctx):
+    """Start a calibration forward on ``ctx``'s lane: uncalibrated f16x3 layers launch unscaled and
+    record their operand's max |v| (no host sync) until end_forward."""
+    _root(ctx).calib = _Calibration(ctx.device)
+
+
+def end_forward(ctx, calibrating: bool) -> str:
+    """After an eager forward on ``ctx``'s lane (one host sync): apply the measured scales of a
+    calibration forward and read + clear the lane's non-finite flag.  Returns "scaled" when the forward
+    must run again because a layer now carries a pre-scale, "overflow" when a launch produced a
+    non-finite value (run the forward again in bf16x3), "" otherwise."""
+    root = _root(ctx)
+    cal = getattr(root, "calib", None) if calibrating else None
+    root.calib = None
+    flag = root._flag
+    vals = [b.cpu() for b in cal.bufs] if cal is not None else []
+    bad = bool(int(flag.item())) if flag is not None else False
+    if flag is not None and bad:
+        flag.zero_()
+    scaled = False
+    if cal is not None:
+        per = {}
+        for cw, prec, xs, ss in cal.items:
+            m = float(vals[xs // _Calibration.SLOTS][xs % _Calibration.SLOTS])
+            if ss >= 0:
+                m *= float(vals[ss // _Calibration.SLOTS][ss % _Calibration.SLOTS])
+            key = (id(cw), prec)
+            per[key] = (cw, prec, max(per[key][2], m) if key in per else m)
+        for cw, prec, m in per.values():
+            sc = x_scale_for(m)
+            cw.__dict__.setdefault("_xscale", {})[prec] = sc
+            cw.x_amax = m
+            scaled = scaled or sc != 1.0
+    if scaled:
+        return "scaled"
+    return "overflow" if bad else ""
+
+
+def _range(ctx, cw, x, prec, in_scale=None):
+    """(x_scale, flag) of an f16x3 launch: the layer's calibrated activation pre-scale and the lane's
+    non-finite flag.  An uncalibrated layer is measured: into the lane's calibration buffer during a
+    calibration forward (launched unscaled), else on the spot with one host sync."""
     if prec != PREC_F16X3 or not RANGE_GUARD or int(getattr(x, "split", 0)):
         return 1.0, None
     scales = cw.__dict__.setdefault("_xscale", {})
@@ -513,9 +590,22 @@ def _range(ctx, cw, x, prec):
     if s is None:
         if x.t.is_cuda and torch.cuda.is_current_stream_capturing():
             raise _lib.S2VError("activation ranges must be calibrated by an eager run before graph capture")
-        m = torch.zeros(1, device=x.t.device)
-        S2V.amax_(x.v, m)
-        amax = float(m.item())
+        cal = getattr(_root(ctx), "calib", None)
+        if cal is not None:
+            xs, out = cal.slot()
+            _amax_into(x.v, out)
+            ss = -1
+            if in_scale is not None:
+                ss, out2 = cal.slot()
+                _amax_into(in_scale, out2)
+            cal.items.append((cw, prec, xs, ss))
+            return 1.0, ctx.range_flag()
+        m = torch.zeros(2, device=x.t.device)
+        _amax_into(x.v, m[0:1])
+        if in_scale is not None:
+            _amax_into(in_scale, m[1:2])
+        mv = m.cpu()
+        amax = float(mv[0]) * (float(mv[1]) if in_scale is not None else 1.0)
         s = x_scale_for(amax)
         scales[prec] = s
         cw.x_amax = amax
@@ -593,25 +683,20 @@ def gemm_kn(ctx: Ctx, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, ba
     return out
 
 
-def _counters(ctx: Ctx):
-    """Split-K tile counters of the opt-in in-launch fold (S2V_SPLITK_FOLD=1), else None."""
-    if not USE_TILE_COUNTERS:
-        return None
-    c = getattr(ctx, "counters", None)
-    return c() if callable(c) else None
-
-
 def _plan(ctx: Ctx, p):
-    out = (ctypes.c_int * 10)()
+    out = (ctypes.c_int * 11)()
     check(ctx.lib.s2v_conv2d_plan(ctypes.byref(p), out), "s2v_conv2d_plan")
     return list(out)
 
 
 def plan_symbol(plan) -> str:
-    """Kernel symbol (as rocprofv3 reports it, demangled) of a launch plan (s2v_conv2d_plan's ten ints)."""
-    bm, bn, wm, avec, bkn, splits, x3, nw, ks, pf = plan
+    """Kernel symbol (as rocprofv3 reports it, demangled) of a launch plan (s2v_conv2d_plan's eleven ints)."""
+    bm, bn, wm, avec, bkn, splits, x3, nw, ks, pf = plan[:10]
+    persist = plan[10] if len(plan) > 10 else 0
     if avec == 5:
         return f"void s2v::conv_glds_x3<{bm}, {bn}, {wm}, {ks}, {x3 - 1}>(s2v::ConvArgs)"
+    if avec == 6:
+        return f"void s2v::conv_ring_x3<{bm}, {bn}, {pf}, {x3 - 1}>(s2v::ConvArgs)"
     if bm == 0:
         if wm < 0:
             if bkn >= 2000:
@@ -623,8 +708,8 @@ def plan_symbol(plan) -> str:
             return f"void s2v::conv_small_cpar<{bn}, {wm}, {'true' if avec else 'false'}>(s2v::ConvArgs, int)"
         return f"void s2v::conv_direct_small<{bn}>(s2v::ConvArgs, int)"
     if x3:
-        return (f"void s2v::conv_igemm_x3<{bm}, {bn}, {wm}, {nw}, {ks}, {pf}, {avec}, {bkn}, {x3 - 1}>"
-                "(s2v::ConvArgs)")
+        name = "conv_igemm_x3_persist" if persist else "conv_igemm_x3"
+        return f"void s2v::{name}<{bm}, {bn}, {wm}, {nw}, {ks}, {pf}, {avec}, {bkn}, {x3 - 1}>(s2v::ConvArgs)"
     return f"void s2v::conv_igemm<{bm}, {bn}, {wm}, {avec}, {bkn}>(s2v::ConvArgs)"
 
 
@@ -646,8 +731,8 @@ def split_act(ctx: Ctx, x: NHWC, out: NHWC | None = None) -> NHWC:
     return out
 
 
-(TUNE_HALO_MIN_BLOCKS, TUNE_GLDS_TILE, TUNE_SMALLK_TILE, TUNE_X3_RATE_512, TUNE_IN_FUSED, TUNE_RESIZE_UP2,
- TUNE_FFT_X3, TUNE_X3_GRID_CAP, TUNE_PLAN_CUS) = (0, 1, 2, 3, 4, 5, 6, 7, 8)
+(TUNE_HALO_MIN_BLOCKS, TUNE_GLDS_TILE, TUNE_SMALLK_TILE, TUNE_X3_RATE_512, TUNE_IN_FUSED,
+ TUNE_RESIZE_UP2) = (0, 1, 2, 3, 4, 5)
 
 
 def tune(ctx: Ctx, key: int, value: int) -> int:
@@ -672,16 +757,21 @@ def tuned(ctx: Ctx, key: int, value: int):
 
 @contextlib.contextmanager
 def x3_grid_cap(ctx: Ctx, blocks: int):
-    """S2V_TUNE_X3_GRID_CAP = ``blocks`` for the launches issued (captured) inside the block: their
-    split-precision tiled convs run as that many persistent blocks (0: unchanged)."""
-    if not blocks:
-        yield
-        return
-    old = tune(ctx, TUNE_X3_GRID_CAP, blocks)
+    """s2v_conv_params.grid_cap = ``blocks`` (rounded down to a multiple of 8) for the convs issued on
+    ``ctx`` inside the block: a 256x256-tile split-precision conv with more tiles than that runs as
+    ``blocks`` persistent blocks (0: one block per tile).  Per context, not process-wide."""
+    prev = getattr(ctx, "grid_cap", 0)
+    ctx.grid_cap = max(0, int(blocks)) // 8 * 8
     try:
         yield
     finally:
-        tune(ctx, TUNE_X3_GRID_CAP, old)
+        ctx.grid_cap = prev
+
+
+def half_chip_blocks(device) -> int:
+    """Half the device's CUs, a multiple of 8 (one persistent block per CU on half the chip)."""
+    cus = torch.cuda.get_device_properties(torch.device(device)).multi_processor_count
+    return max(8, cus // 2 // 8 * 8)
 
 
 def conv_splits(ctx: Ctx, p) -> int:

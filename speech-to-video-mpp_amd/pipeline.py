@@ -88,6 +88,7 @@ class LipSyncPipeline:
         self.lanes = lanes
         self.ref_hook = ref_hook    # Step 5 (inference.py:234-238) on the uint8 references; eager batches only
         self._runner = None
+        self.reruns = 0             # replayed batches run again in bf16x3 after an f16x3 range overflow
 
     @torch.no_grad()
     def run_batch(self, mel: torch.Tensor, src: torch.Tensor, coeff: torch.Tensor, out_u8: torch.Tensor,
@@ -119,25 +120,51 @@ class LipSyncPipeline:
                              f"mel windows up to {stop} (got {src.shape[0]}, {coeffs.shape[0]}, {mel_chunks.shape[0]})")
         out = torch.empty((n, 3, 384, 384), dtype=torch.uint8, device=self.device)
         runner = None
-        for b0 in range(0, n, self.batch):
+        nb = (n + self.batch - 1) // self.batch
+        flags = torch.zeros(nb, dtype=torch.int32, device=self.device) if ops.guard_active() else None
+        replayed = []
+        for k, b0 in enumerate(range(0, n, self.batch)):
             b1 = min(n, b0 + self.batch)
             m, s, c = mel_chunks[start + b0: start + b1], src[b0:b1], coeffs[b0:b1]
             if self.graph and b1 - b0 == self.batch and self.ref_hook is None:
                 runner = self._graph_runner(m, s, c)
                 dst = out[b0:b1]
-                runner(m, s, c, out_fn=lambda o, d=dst: d.copy_(o))
+                lane = runner.next_lane()
+
+                def take(o, d=dst, k=k, lane=lane):
+                    d.copy_(o)
+                    if flags is not None:               # this batch's f16x3 non-finite flags, then clear them
+                        for f in self._lane_flags(lane):
+                            torch.maximum(flags[k:k + 1], f, out=flags[k:k + 1])
+                            f.zero_()
+                runner(m, s, c, out_fn=take)
                 out.record_stream(runner.streams[(runner.k - 1) % runner.lanes])
+                replayed.append((k, b0, b1))
             else:
                 if runner is not None:
                     runner.join()                 # the eager batch uses lane 0's workspaces
-                self.run_batch(m, s, c, out[b0:b1])
+                self.run_batch(m, s, c, out[b0:b1])   # eager: the modules guard their own forwards
         if runner is not None:
             runner.join()
-        for m in (self.dnet, self.enet):          # f16x3 range guard: never a silent overflow
-            for _, lanes in m.__dict__.get("_s2v_engines", {}).values():
-                for c in lanes.values():
-                    c.check_range(type(m).__name__)
+        if flags is not None and replayed:
+            bad = set(torch.nonzero(flags).flatten().tolist())
+            for k, b0, b1 in replayed:
+                if k in bad:                      # a replayed batch left the f16x3 range: again in bf16x3
+                    with ops.precision("bf16x3"):
+                        self.run_batch(mel_chunks[start + b0: start + b1], src[b0:b1], coeffs[b0:b1], out[b0:b1])
+                    self.reruns += 1
         return out
+
+    def _lane_flags(self, lane):
+        """The f16x3 non-finite flags of lane ``lane`` of both networks (one per module and lane)."""
+        fl = []
+        for mdl in (self.dnet, self.enet):
+            lanes = mdl.__dict__.get("_s2v_engines", {}).get(str(self.device), (None, {}))[1]
+            c = lanes.get(lane)
+            f = c.range_flag() if c is not None else None
+            if f is not None:
+                fl.append(f)
+        return fl
 
     def _graph_runner(self, m, s, c):
         """Captured run_batch per lane for full batches (~2,000 launches -> one graph replay each);

@@ -124,6 +124,16 @@ CONV_CASES = [
     # bf16x3 256x64 8-wave tile (force_tile 8: large-M, 64-channel layers)
     (2, 64, 20, 18, 64, 3, 1, 1, 1, "direct", "reflect", 8, 0),
     (1, 32, 17, 23, 40, 3, 2, 1, 1, "direct", "zero", 8, 3),
+    # LDS-DMA ring tiles (force_tile 13..18, conv_ring_x3: split-precision, AMODE-0 convs only):
+    # ragged M / N tails, split-K, stride 2, dilation, 1x1, valid (pre-padded) 3x3
+    (2, 64, 17, 19, 96, 3, 1, 1, 1, "direct", "zero", 13, 0),
+    (2, 64, 16, 16, 256, 3, 1, 1, 1, "direct", "zero", 14, 3),
+    (2, 32, 12, 12, 200, 3, 1, 1, 1, "direct", "zero", 15, 0),
+    (1, 96, 20, 12, 128, 1, 1, 0, 1, "direct", "zero", 16, 2),
+    (2, 32, 12, 12, 32, 3, 1, 1, 1, "direct", "zero", 17, 0),
+    (2, 64, 13, 11, 40, 3, 2, 1, 1, "direct", "zero", 18, 4),
+    (1, 64, 15, 15, 64, 3, 1, 2, 2, "direct", "zero", 13, 2),
+    (2, 128, 14, 14, 96, 3, 1, 0, 1, "direct", "zero", 14, 5),
 ]
 
 
@@ -191,30 +201,6 @@ def test_conv2d(ctx, prec, case, request):
         if variant == 1:
             lim = lim * 1.5
         assert (err <= lim).all(), f"variant {variant}: max err {err.max():.3e}, rel {(err / lim).max():.2f}"
-
-
-def test_splitk_fold_matches_separate_reduce(ctx, prec):
-    """The in-launch split-K fold (tile counters, last arriver sums) gives the separate reduce
-    kernel's sums bit for bit and leaves the counters zero."""
-    x = rnd(2, 64, 13, 11, seed=21)
-    wt = rnd(96, 64, 3, 3, seed=22) / 24.0
-    cw = ConvW(wt.float(), rnd(96, seed=23).float(), DEV, padding=1)
-    outs = []
-    prev = ops.USE_TILE_COUNTERS
-    try:
-        for fold in (True, False):
-            ops.USE_TILE_COUNTERS = fold
-            for tile, splits in ((4, 3), (5, 4), (0, 0)):
-                y = NHWC.empty(2, 13, 11, 96, DEV)
-                ops.conv2d(ctx, nhwc(x.float()), cw, y, act=ops.ACT_LRELU, alpha=0.2, force_tile=tile,
-                           force_splits=splits)
-                outs.append(y.t.cpu())
-    finally:
-        ops.USE_TILE_COUNTERS = prev
-    for a, b in zip(outs[:3], outs[3:]):
-        assert torch.equal(a, b)
-    torch.cuda.synchronize()
-    assert int(ctx.counters().abs().sum()) == 0
 
 
 @pytest.mark.parametrize("cfg", [
@@ -639,12 +625,13 @@ def test_f16x3_operand_range(ctx, mag):
 
 
 @pytest.mark.parametrize("n,cin,h,w,cout,tile", [(2, 64, 12, 16, 96, 0), (2, 32, 8, 8, 64, 5), (1, 256, 16, 16, 256, 1),
-                                                 (3, 4, 10, 6, 40, 0), (2, 64, 6, 10, 48, 8)])
+                                                 (3, 4, 10, 6, 40, 0), (2, 64, 6, 10, 48, 8),
+                                                 (2, 64, 12, 16, 96, 14), (1, 32, 10, 14, 32, 17)])
 def test_conv2d_pooled_epilogue(ctx, prec, n, cin, h, w, cout, tile):
     """out_pool: the 2x2 mean of lrelu(conv + b) (ResBlock conv1 + bilinear x0.5, base_blocks.py:40-49)
     written at half size; M runs over 2x2 quads, so every tile holds whole quads."""
     if tile > 6 and prec == "f32":
-        pytest.skip("tiles 7-8 exist in the split-precision table only")
+        pytest.skip("tiles 7-18 exist in the split-precision table only")
     wt = rnd(cout, cin, 3, 3, seed=61) / math.sqrt(cin * 9)
     bias = rnd(cout, seed=62)
     x = rnd(n, cin, h, w, seed=63)
@@ -701,11 +688,12 @@ def test_instnorm_fused_small_planes(ctx, n, c, h, w):
 
 @pytest.mark.parametrize("tile,splits,cap", [(1, 0, 8), (1, 0, 24), (1, 2, 16), (4, 3, 40)])
 def test_conv_x3_grid_cap_bit_exact(ctx, tile, splits, cap):
-    """S2V_TUNE_X3_GRID_CAP: ``cap`` persistent blocks looping over the tile grid (more tiles than
-    blocks, a ragged last round) compute every tile exactly as the one-block-per-tile launch does —
-    same K order, same epilogue — so the outputs are bit-identical (with and without split-K);
-    both are checked against the fp64 reference at the f16x3 bound.  The persistent kernel exists
-    for the 256x256 tile (force_tile 1); other tiles ignore the cap (force_tile 4)."""
+    """s2v_conv_params.grid_cap (ops.x3_grid_cap, per context): ``cap`` persistent blocks looping over
+    the tile grid (more tiles than blocks, a ragged last round) compute every tile exactly as the
+    one-block-per-tile launch does — same K order, same epilogue — so the outputs are bit-identical (with
+    and without split-K); both are checked against the fp64 reference at the f16x3 bound.  The persistent
+    kernel exists for the 256x256 tile (force_tile 1) and the plan says it is taken; other tiles ignore
+    the cap (force_tile 4)."""
     n, cin, h, w, cout = 2, 64, 64, 64, 160
     wt = rnd(cout, cin, 3, 3, seed=11) / math.sqrt(cin * 9)
     bias = rnd(cout, seed=12)
@@ -713,18 +701,33 @@ def test_conv_x3_grid_cap_bit_exact(ctx, tile, splits, cap):
     x = rnd(n, cin, h, w, seed=13)
     prev_p = ops.set_precision("f16x3")
     try:
-        outs = []
+        outs, syms = [], []
         for c in (0, cap):
-            prev = ops.tune(ctx, ops.TUNE_X3_GRID_CAP, c)
-            try:
+            with ops.x3_grid_cap(ctx, c):
                 y = NHWC.empty(n, h, w, cout, DEV)
                 ops.conv2d(ctx, nhwc(x.float()), cw, y, act=ops.ACT_LRELU, alpha=0.2, force_tile=tile,
                            force_splits=splits)
                 outs.append(y)
-            finally:
-                ops.tune(ctx, ops.TUNE_X3_GRID_CAP, prev)
+                seen = {}
+
+                def hook(c_, p, flops, launch):
+                    seen["plan"] = p.plan
+                    launch()
+                ops.CONV_HOOK = hook
+                try:
+                    ops.conv2d(ctx, nhwc(x.float()), cw, NHWC.empty(n, h, w, cout, DEV), force_tile=tile,
+                               force_splits=splits)
+                finally:
+                    ops.CONV_HOOK = None
+                syms.append((seen["plan"][10], ops.plan_symbol(seen["plan"])))
+        assert ctx.grid_cap == 0
     finally:
         ops.set_precision(prev_p)
+    assert syms[0][0] == 0 and "persist" not in syms[0][1]
+    if tile == 1:
+        assert syms[1][0] == cap and syms[1][1].startswith("void s2v::conv_igemm_x3_persist<256, 256,"), syms[1]
+    else:
+        assert syms[1][0] == 0 and "persist" not in syms[1][1]
     assert torch.equal(outs[0].t, outs[1].t)
     ref = F.leaky_relu(F.conv2d(x, wt, bias, padding=1), 0.2)
     lim = REL["f16x3"] * (conv_bound(x, wt, 1, 1, 1) + 1) + 1e-6

@@ -133,3 +133,28 @@ def test_graph_replay_after_an_eager_ragged_batch(nets_pair):
     again = pipe.run(chunks, src[:n].to(DEV), coeffs, 0, n)
     d = (one.cpu().int() - again.cpu().int()).abs().flatten(1).max(1).values.tolist()
     assert torch.equal(one.cpu(), again.cpu()), d
+
+
+def test_replayed_batch_out_of_range_reruns_in_bf16x3(nets_pair):
+    """A graph-replayed batch whose activations leave the f16x3 range calibrated on the first run
+    (DNet source frames 1e5 x larger) is flagged per batch and run again in bf16x3: its frames equal an
+    eager bf16x3 run of the same batch, the in-range batch keeps its f16x3 frames, nothing raises."""
+    from s2v_amd import audio, ops, pipeline as P
+    if ops.PRECISION != "f16x3":
+        pytest.skip("the range guard is f16x3's")
+    dnet, enet = nets_pair
+    wav, semantic, expression, src = _clip(4, 4)
+    chunks = audio.mel_chunks(audio.melspectrogram(torch.from_numpy(wav).to(DEV)))
+    coeffs = torch.from_numpy(P.dnet_coefficients(semantic[:4], expression)).to(DEV)
+    pipe = P.LipSyncPipeline(dnet, enet, DEV, batch=2)                    # two replayed batches
+    first = pipe.run(chunks, src[:4].to(DEV), coeffs, 0, 4)
+    assert pipe.reruns == 0
+    bad = src[:4].clone()
+    bad[2:] *= 1.0e5                                                      # the second batch only
+    got = pipe.run(chunks, bad.to(DEV), coeffs, 0, 4)
+    assert pipe.reruns == 1
+    assert torch.equal(got[:2].cpu(), first[:2].cpu())
+    ref = torch.empty((2, 3, 384, 384), dtype=torch.uint8, device=DEV)
+    with ops.precision("bf16x3"):
+        pipe.run_batch(chunks[2:4], bad[2:4].to(DEV), coeffs[2:4], ref)
+    assert torch.equal(got[2:].cpu(), ref.cpu())

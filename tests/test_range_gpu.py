@@ -81,3 +81,74 @@ def test_modulated_conv_range(f16x3):
     ref = F.conv2d(x.float().double(), wt.float().double(), None, 1, 1)      # 0.5 * 2.0 = 1
     bound = F.conv2d(x.float().double().abs(), wt.float().double().abs(), None, 1, 1)
     assert torch.isfinite(got).all() and ((got - ref).abs() <= 2 * REL * bound).all()
+
+
+def test_in_scale_operand_is_what_calibrates(f16x3):
+    """A StyleGAN2 modulated input (in_scale, GPEN / GFPGAN) is split as x * in_scale: the calibration
+    measures that operand (max |x| * max |in_scale|), so an in_scale that lifts an in-range x past the
+    f16 ceiling still gets a pre-scale and the result stays finite and within the f16x3 bound."""
+    x, wt = _case(4)
+    ctx = ops.Ctx(DEV)
+    cw = ConvW(wt.float(), None, DEV, padding=1)
+    xv = NHWC(x.permute(0, 2, 3, 1).float().contiguous().to(DEV))
+    y = NHWC.empty(2, 13, 11, 96, DEV)
+    s = torch.full((2, 64), 2.0e5, device=DEV)
+    ops.conv2d(ctx, xv, cw, y, in_scale=s)
+    ctx.check_range()
+    assert cw._xscale[ops.PREC_F16X3] < 1.0
+    xs = x.float().double() * 2.0e5
+    got = y.t.permute(0, 3, 1, 2).double().cpu()
+    ref = F.conv2d(xs, wt.float().double(), None, 1, 1)
+    bound = F.conv2d(xs.abs(), wt.float().double().abs(), None, 1, 1)
+    assert torch.isfinite(got).all() and ((got - ref).abs() <= REL * bound + 1e-30).all()
+
+
+def test_in_scale_overflow_after_calibration_is_flagged(f16x3):
+    """Calibrated with in_scale 1, then an in_scale of 1e6 pushes the split operand over 65504: the
+    launch flags it and check_range raises (never silent)."""
+    x, wt = _case(5)
+    ctx = ops.Ctx(DEV)
+    cw = ConvW(wt.float(), None, DEV, padding=1)
+    xv = NHWC((x * 100).permute(0, 2, 3, 1).float().contiguous().to(DEV))
+    y = NHWC.empty(2, 13, 11, 96, DEV)
+    ops.conv2d(ctx, xv, cw, y, in_scale=torch.ones((2, 64), device=DEV))
+    ctx.check_range()
+    ops.conv2d(ctx, xv, cw, y, in_scale=torch.full((2, 64), 1.0e6, device=DEV))
+    with pytest.raises(_lib.S2VError, match="non-finite"):
+        ctx.check_range()
+
+
+def test_scale_up_keeps_headroom():
+    """A small-range layer is scaled into [2^9, 2^10): 64x headroom below the f16 ceiling for later
+    batches, and in-range layers keep x_scale 1."""
+    for amax in (1e-6, 0.01, 0.1):
+        m = amax * ops.x_scale_for(amax)
+        assert 2 ** 9 <= m < 2 ** 10
+    assert ops.x_scale_for(0.5) == 1.0 and ops.x_scale_for(1e4) == 1.0
+    assert 2 ** 9 <= 1e5 * ops.x_scale_for(1e5) < 2 ** 10
+
+
+def test_model_forward_out_of_range_batch_reruns_in_bf16x3(f16x3):
+    """An eager model forward whose batch leaves the range calibrated on the first forward (face
+    input 1e5 x larger: the first conv's split operand passes 65504) reads the lane's flag when it
+    returns and runs again in bf16x3: the returned output is the bf16x3 forward's, bit for bit, not
+    inf / NaN; in-range forwards return f16x3 outputs without a re-run."""
+    from helpers import synth_sd
+    from s2v_amd import models
+    net = models.LNet()
+    net.load_state_dict(synth_sd("lnet"), strict=True)
+    net.eval()
+    g = torch.Generator(device=DEV).manual_seed(7)
+    mel = torch.rand((2, 1, 80, 16), generator=g, device=DEV) * 8 - 4
+    face = torch.rand((2, 6, 96, 96), generator=g, device=DEV)
+    net(mel, face)                                       # first forward: calibration
+    ctx = net._s2v_engines[str(face.device)][1][0]
+    assert ctx.reruns == 0
+    ok = net(mel, face)
+    assert ctx.reruns == 0 and torch.isfinite(ok).all()
+    big = face * 1.0e5
+    out = net(mel, big)
+    assert ctx.reruns == 1 and torch.isfinite(out).all()
+    with ops.precision("bf16x3"):
+        ref = net(mel, big)
+    assert torch.equal(out, ref)
