@@ -193,7 +193,7 @@ def live_roofline(forward, workload="lipsync"):
     # HBM bytes per launch of the same symbol from the PMC passes of this workload (tools/gpu_profile.sh:
     # separate FETCH_SIZE / WRITE_SIZE runs of this bench command; the newest round's file wins)
     traffic, traffic_src = None, None
-    for rnd in ("r03", "r02", "r01"):
+    for rnd in ("r04", "r03", "r02", "r01"):
         pmc = os.path.join(ROOT, "profiles", f"pmc_{rnd}_{workload}.json")
         if os.path.exists(pmc):
             with open(pmc) as f:
@@ -208,19 +208,22 @@ def live_roofline(forward, workload="lipsync"):
         "flops_per_launch": d["flops"] / d["launches"],
         "conv_family": {"achieved": round(total_flops / (total_ms * 1e-3) / 1e12, 2),
                         "ms_per_step": round(total_ms, 3), "symbols": len(per)},
+        "per_kernel": per,
     }
 
 
 class Stamper:
-    """In-kernel launch timer of one kernel symbol in captured, replayed steps (ops.STAMP /
+    """In-kernel launch timer of a set of kernel symbols in captured, replayed steps (ops.STAMP /
     s2v_conv_params.stamps): per lane a replay counter (bumped by the first kernel of every replay)
-    and a [reps, launches, 2] buffer of (first block start, last block end) device real-time clock
-    values (s_memrealtime, 100 MHz) per launch of the symbol in that replay."""
+    and, per symbol, a [reps, launches, 2] buffer of (first block start, last block end) device
+    real-time clock values (s_memrealtime, 100 MHz) per launch of that symbol in that replay, plus the
+    algorithmic FLOPs of each launch slot.  ``kernels``: {symbol: max launches per step}."""
 
     CLOCK_HZ = 100e6
 
-    def __init__(self, kernel, launches, reps, device):
-        self.kernel, self.stride, self.reps, self.device = kernel, max(1, launches), reps, device
+    def __init__(self, kernels, reps, device):
+        self.kernels = dict(kernels)
+        self.reps, self.device = reps, device
         self.lanes = {}
         self.cur = None
 
@@ -229,61 +232,84 @@ class Stamper:
         (captured as the graph's first kernel) and restart the launch numbering."""
         from s2v_amd import ops
         if lane not in self.lanes:
-            buf = torch.zeros((self.reps, self.stride, 2), dtype=torch.int64, device=self.device)
-            self.lanes[lane] = {"buf": buf, "ctr": torch.zeros(1, dtype=torch.int64, device=self.device), "n": 0}
+            self.lanes[lane] = {"ctr": torch.zeros(1, dtype=torch.int64, device=self.device), "n": {},
+                                "buf": {k: torch.zeros((self.reps, m, 2), dtype=torch.int64, device=self.device)
+                                        for k, m in self.kernels.items()},
+                                "flops": {k: [0.0] * m for k, m in self.kernels.items()}}
         L = self.lanes[lane]
-        L["n"] = 0
+        L["n"] = {}
         self.cur = L
         ops.S2V.counter_add_(L["ctr"], 1)
 
     def __call__(self, info, flops):
         from s2v_amd import ops
-        if self.cur is None or ops.plan_symbol(info.plan) != self.kernel:
+        sym = ops.plan_symbol(info.plan)
+        if self.cur is None or sym not in self.kernels:
             return None
         L = self.cur
-        slot = L["n"]
-        L["n"] += 1
-        if slot >= self.stride:
+        slot = L["n"].get(sym, 0)
+        L["n"][sym] = slot + 1
+        stride = self.kernels[sym]
+        if slot >= stride:
             return None
-        return L["buf"], L["ctr"], [slot, self.stride, self.reps]
+        L["flops"][sym][slot] = flops
+        return L["buf"][sym], L["ctr"], [slot, stride, self.reps]
 
     def arm(self):
         torch.cuda.synchronize()
         for L in self.lanes.values():
-            L["buf"][..., 0] = -1              # uint64 max: atomic min start
-            L["buf"][..., 1] = 0
+            for buf in L["buf"].values():
+                buf[..., 0] = -1              # uint64 max: atomic min start
+                buf[..., 1] = 0
             L["c0"] = int(L["ctr"].item())
 
-    def durations_us(self):
-        """Per-launch durations (us) of every stamped launch of the timed replays."""
+    def launches(self):
+        """{symbol: [(duration us, flops), ...]} of every stamped launch of the timed replays."""
         torch.cuda.synchronize()
-        out = []
+        out = {}
         for L in self.lanes.values():
             c1 = int(L["ctr"].item())
-            buf = L["buf"].cpu()
-            for r in range(L["c0"] + 1, c1 + 1):
-                for s0, s1 in buf[r % self.reps].tolist():
-                    if s0 != -1 and s1 > 0:
-                        out.append((s1 - s0) / self.CLOCK_HZ * 1e6)
+            for sym, buf in L["buf"].items():
+                b = buf.cpu()
+                for r in range(L["c0"] + 1, c1 + 1):
+                    for slot, (s0, s1) in enumerate(b[r % self.reps].tolist()):
+                        if s0 != -1 and s1 > 0:
+                            out.setdefault(sym, []).append(((s1 - s0) / self.CLOCK_HZ * 1e6, L["flops"][sym][slot]))
         return out
 
 
+def _peak(sym):
+    return X3_PEAK_TFLOPS if ("conv_igemm_x3" in sym or "conv_ring_x3" in sym or "conv_glds_x3" in sym) \
+        else FP32_MFMA_PEAK_TFLOPS
+
+
 def replay_roofline(pre, stamper):
-    """roofline of the dominant kernel from the timed (graph-replayed, overlapped) launches."""
-    d = stamper.durations_us() if stamper is not None else []
+    """roofline of the dominant kernel from the timed (graph-replayed, overlapped) launches, plus
+    the same figure for every other stamped kernel symbol (``by_kernel``): the style encoder's
+    persistent launches (conv_igemm_x3_persist, half the chip by design) are their own entry."""
+    st = stamper.launches() if stamper is not None else {}
     r = dict(pre)
     iso = {"avg_launch_us": pre["avg_launch_us"], "frac": pre["frac"], "achieved": pre["achieved"],
            "how": "un-graphed pass, side branches serialised, each launch repeated back to back between HIP events"}
+    by = {}
+    for sym, recs in sorted(st.items(), key=lambda kv: -sum(d for d, _ in kv[1])):
+        us = sum(d for d, _ in recs)
+        fl = sum(f for _, f in recs)
+        ach = fl / (us * 1e-6) / 1e12
+        by[sym] = {"launches": len(recs), "avg_launch_us": round(us / len(recs), 2),
+                   "flops_per_launch": fl / len(recs), "achieved": round(ach, 2), "peak": round(_peak(sym), 1),
+                   "frac": round(ach / _peak(sym), 4)}
+    d = st.get(pre["kernel"], [])
     if not d:
         r["timing"] = "isolated (no stamped launches in the timed run)"
-        return r
-    avg = sum(d) / len(d)
-    ach = pre["flops_per_launch"] / (avg * 1e-6) / 1e12
-    r.update(achieved=round(ach, 2), frac=round(ach / pre["peak"], 4), avg_launch_us=round(avg, 2),
-             timed_launches=len(d),
-             timing="in-kernel clock stamps (s_memrealtime, first block start to last block end) of every launch "
-                    "of this kernel in the timed, graph-replayed steps",
-             isolated=iso)
+    else:
+        e = by[pre["kernel"]]
+        r.update(achieved=e["achieved"], frac=e["frac"], avg_launch_us=e["avg_launch_us"], timed_launches=e["launches"],
+                 timing="in-kernel clock stamps (s_memrealtime, first block start to last block end) of every launch "
+                        "of this kernel in the timed, graph-replayed steps",
+                 isolated=iso)
+    if by:
+        r["by_kernel"] = by
     return r
 
 
@@ -881,7 +907,14 @@ def worker(args):
         ops.set_precision(args.precision)
         pre = live_roofline(wl.forward, args.workload)
         if not args.no_graph:
-            stamper = Stamper(pre["kernel"], pre["launches"], args.warmup + args.steps + 2 * args.lanes + 4, dev)
+            # the dominant symbol, the next three by time and the persistent form of the dominant one
+            # (the style encoder's grid-capped launches, which the serialised pre-pass does not make)
+            ks = {k: v["launches"] for k, v in pre["per_kernel"].items()}
+            top = sorted(pre["per_kernel"], key=lambda k: -pre["per_kernel"][k]["ms"])[:4]
+            kern = {k: ks[k] + 4 for k in top}
+            if "conv_igemm_x3<" in pre["kernel"]:
+                kern[pre["kernel"].replace("conv_igemm_x3<", "conv_igemm_x3_persist<")] = ks[pre["kernel"]] + 4
+            stamper = Stamper(kern, args.warmup + args.steps + 2 * args.lanes + 4, dev)
     elapsed = timed(args.precision, stamper)
     if cuda:
         ops.check_all_ranges(args.workload)     # f16x3 range guard: raises if a timed launch overflowed
@@ -905,14 +938,16 @@ def worker(args):
     config["conv_arith"] = ARITH[args.precision]
     if pre is not None:
         result["roofline"] = replay_roofline(pre, stamper)
+        result["roofline"].pop("per_kernel", None)
         from s2v_amd.engine import enet as _enet
-        if args.workload in ("lipsync", "pipeline", "clip") and _enet.OVERLAP and _enet.STYLE_GRID:
+        if args.workload in ("lipsync", "pipeline", "clip") and _enet.OVERLAP and _enet.style_grid(dev):
             result["roofline"]["grid_cap"] = (
-                f"the style encoder's launches of this kernel (beside LNet) run as {_enet.STYLE_GRID} persistent "
-                "blocks, half the CUs (S2V_ENET_STYLE_GRID): the replayed average is over launches that hold "
-                "half the chip by design; 'isolated' is the full-grid rate")
+                f"the style encoder's launches of the 256x256 tile (beside LNet) run as {_enet.style_grid(dev)} "
+                "persistent blocks on half the CUs (conv_igemm_x3_persist, s2v_conv_params.grid_cap): reported "
+                "separately under by_kernel; the headline entry is the full-grid launches only")
     elif rank == 0 and not args.no_roofline and cuda:
         result["roofline"] = live_roofline(wl.forward, args.workload)
+        result["roofline"].pop("per_kernel", None)
     if world == 1 and not args.no_alt and cuda and wl.graphable:
         result["alt_precision"] = {}
         for other in ARITH:

@@ -163,6 +163,19 @@ size_t s2v_conv2d_ws_bytes(const s2v_conv_params *p);
  * conv_smallk<QPT,PX>.  force_tile: 0 = planner, 1..6 (f32) / 1..18 (split precisions: 13..18 the LDS-DMA
  * ring tiles) a fixed tile of the selected precision's table (tests / tuning). */
 int s2v_conv2d_plan(const s2v_conv_params *p, int *out11);
+/* Up to S2V_CONV_GROUP_MAX independent convolutions as ONE kernel launch (a tile table over the members'
+ * tile grids on one tile configuration, each member with its own split-K factor), plus one launch
+ * folding every member's split-K partials with that member's epilogue.  Replaces a fork of independent
+ * convs that read the same block input (LNet's FFC: convl2l + convg2l, convl2g and the spectral
+ * branch's first 1x1, ffc.py:176-233) — one launch filling the chip instead of three under-filled ones.
+ * Members: split precision (one prec for all), packed split weights, a direct zero-padded conv with
+ * cin % 32 == 0 and <= 32 taps, batch 1, no in_scale / pre_act / out_pool / grid_cap / x_split /
+ * force_tile.  The workspace is member 0's (ws, ws_bytes >= s2v_conv2d_group_ws_bytes); plan: out[0] =
+ * the x3 tile configuration (force_tile - 1 numbering), out[1 + i] = member i's split-K factor. */
+#define S2V_CONV_GROUP_MAX 4
+int s2v_conv2d_group(const s2v_conv_params *ps, int n, s2v_stream_t stream);
+size_t s2v_conv2d_group_ws_bytes(const s2v_conv_params *ps, int n);
+int s2v_conv2d_group_plan(const s2v_conv_params *ps, int n, int *out);
 /* Planner knobs (tests / tuning; process-wide, not thread-safe against concurrent planning):
  *   S2V_TUNE_HALO_MIN_BLOCKS  the halo-tiled small-Cout kernel needs at least this many 8x128 tiles
  *                             (default 0, env S2V_HALO_MIN_BLOCKS; fewer go channel-parallel).  Below

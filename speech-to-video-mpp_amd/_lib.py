@@ -57,6 +57,9 @@ _SIGS = {
     "s2v_conv2d": (_c_int, [ctypes.POINTER(ConvParams), _vp]),
     "s2v_conv2d_ws_bytes": (_c_size, [ctypes.POINTER(ConvParams)]),
     "s2v_conv2d_plan": (_c_int, [ctypes.POINTER(ConvParams), ctypes.POINTER(_c_int)]),
+    "s2v_conv2d_group": (_c_int, [ctypes.POINTER(ConvParams), _c_int, _vp]),
+    "s2v_conv2d_group_ws_bytes": (_c_size, [ctypes.POINTER(ConvParams), _c_int]),
+    "s2v_conv2d_group_plan": (_c_int, [ctypes.POINTER(ConvParams), _c_int, ctypes.POINTER(_c_int)]),
     "s2v_tune": (_c_int, [_c_int, _c_ll, ctypes.POINTER(_c_ll)]),
     "s2v_layernorm2d": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_float, _c_int, _c_float,
                                  _c_int, _vp, _c_int, _vp, _c_int, _vp, _c_size, _vp]),

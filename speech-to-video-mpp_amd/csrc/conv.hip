@@ -27,6 +27,8 @@ template <int ELT>   // LDS-DMA kernels on split-layout inputs (conv_glds.hip): 
 void launch_conv_glds(int cfg, const ConvArgs &a, dim3 grid, hipStream_t s);
 template <int ELT>   // LDS-DMA ring kernels on fp32 inputs (conv_ring.hip), cfg = X3Cfg::ring - 1
 void launch_conv_ring(int cfg, const ConvArgs &a, dim3 grid, hipStream_t s);
+template <int ELT>   // grouped x3 launches (conv_x3_impl.hpp conv_igemm_x3_group): 0 or an error
+int launch_conv_x3_group(int cfg, const ConvGroup &g, dim3 grid, hipStream_t s);
 
 template <int BM, int BN, int AR, int BR, int BKN>
 __device__ __forceinline__ void store_ab(float *As, float *Bs, int tid, const f4 (&ra)[AR],
@@ -196,6 +198,36 @@ __global__ void splitk_reduce(ConvArgs a, int batch, int vec) {
             float s = src[0];
             for (int sp = 1; sp < a.splits; ++sp) s += src[sp * slab];
             store_epilogue(a, bidx, m, q, s);
+        }
+    }
+}
+
+// Split-K fold of a conv group (s2v_conv2d_group): member p folds with the blocks
+// [rstart[p], rstart[p + 1]) (none when it has one split), otherwise as splitk_reduce.
+__global__ void splitk_reduce_group(ConvGroup g) {
+    int p = 0;
+#pragma unroll
+    for (int i = 1; i < kConvGroupMax; ++i)
+        if (i < g.n && (int)blockIdx.x >= g.rstart[i]) p = i;
+    const ConvArgs &a = g.a[p];
+    const int nb = g.rstart[p + 1] - g.rstart[p];
+    const int cv = (a.cout & 3) == 0 ? 4 : 1;
+    const int nq = a.cout / cv;
+    const long long total = (long long)a.M * nq;               // one batch entry (group members: batch 1)
+    const long long slab = (long long)a.M * a.cout;
+    for (long long idx = (blockIdx.x - g.rstart[p]) * (long long)blockDim.x + threadIdx.x; idx < total;
+         idx += (long long)nb * blockDim.x) {
+        const unsigned u = (unsigned)idx;
+        const int m = (int)(u / (unsigned)nq), q = (int)(u - (unsigned)m * (unsigned)nq);
+        const float *src = a.ws + (long long)m * a.cout + q * cv;
+        if (cv == 4) {
+            f4 sum = *(const f4 *)src;
+            for (int sp = 1; sp < a.splits; ++sp) sum += *(const f4 *)(src + sp * slab);
+            store_epilogue4(a, 0, m, 4 * q, sum, g.vec[p] != 0, false);
+        } else {
+            float sum = src[0];
+            for (int sp = 1; sp < a.splits; ++sp) sum += src[sp * slab];
+            store_epilogue(a, 0, m, q, sum);
         }
     }
 }
@@ -1294,9 +1326,174 @@ static int persist_blocks(const s2v_conv_params *p, const Plan &pl, int M) {
     return cap > 0 && tiles > cap ? (int)cap : 0;
 }
 
+// ------------------------------------------------------------------ grouped launches
+// A group of independent split-precision convs (s2v_conv2d_group: LNet's FFC conv_to_l, l2g and the
+// spectral branch's first 1x1, which all read the block input) as one launch on one tile
+// configuration, each member with its own split-K factor, plus one launch folding every member's
+// partials.  Plan: minimise  rounds * (T0 + max_p tps_p * t_slice) + [reduce]  over the grouped tiles
+// and per-member splits in {1, 2, 4, 8, 16}, where t_slice = max(the tile's per-slice latency floor,
+// its share of the full-chip rate) — the latency floor is what one block alone on a CU takes per
+// 32-deep K slice (measured on MI355X r04, graph-timed: 0.5 us for the 4-wave tiles).
+struct GroupPlan {
+    int cfg;
+    int splits[kConvGroupMax];
+    Plan plan[kConvGroupMax];
+    int M[kConvGroupMax];
+};
+
+static bool group_member_ok(const s2v_conv_params *p, int cfg) {
+    return tiled_x3(p) && !p->b_kn && !p->x_split && p->grid_cap == 0 && p->force_tile == 0 && !p->out_pool &&
+           (p->batch <= 1) && x3_amode(p, kX3Tiles[cfg].t) == 4 && !p->in_scale && p->pre_act == S2V_ACT_NONE;
+}
+
+static int group_plan(const s2v_conv_params *ps, int n, GroupPlan &gp) {
+    S2V_REQUIRE(ps && n >= 1 && n <= kConvGroupMax, "conv2d_group: 1..%d members", kConvGroupMax);
+    int K[kConvGroupMax];
+    for (int i = 0; i < n; ++i) {
+        const int rc = validate(&ps[i], gp.M[i], K[i]);
+        if (rc) return rc;
+        S2V_REQUIRE(ps[i].prec == ps[0].prec, "conv2d_group: members of one precision");
+    }
+    static const int cands[] = {4, 3, 1};
+    const int cus = plan_cus();
+    double best = 1e30;
+    gp.cfg = -1;
+    for (int cfg : cands) {
+        bool ok = true;
+        for (int i = 0; i < n && ok; ++i) ok = group_member_ok(&ps[i], cfg) &&
+                                              (long long)cdiv(ps[i].cout, kX3Tiles[cfg].t.bn) * kX3Tiles[cfg].t.bn <= ps[i].npad;
+        if (!ok) continue;
+        const X3Cfg &c = kX3Tiles[cfg];
+        const double lat = c.t.nw == 4 ? 0.5e-6 : 0.6e-6;
+        const double slots = (double)cus * c.bpc;
+        int s[kConvGroupMax] = {1, 1, 1, 1};
+        long long tiles[kConvGroupMax];
+        for (int i = 0; i < n; ++i) tiles[i] = (long long)cdiv(gp.M[i], c.t.bm) * cdiv(ps[i].cout, c.t.bn);
+        int combos = 1;
+        for (int i = 0; i < n; ++i) combos *= 5;
+        for (int cb = 0; cb < combos; ++cb) {
+            int v = cb;
+            long long blocks = 0;
+            int maxtps = 0;
+            double red = 0.0;
+            bool any_split = false, bad = false;
+            for (int i = 0; i < n; ++i) {
+                s[i] = 1 << (v % 5);
+                v /= 5;
+                const int kt = (K[i] + 31) / 32;
+                if (s[i] > 1 && s[i] > kt / 4) { bad = true; break; }
+                const int tps = (kt + s[i] - 1) / s[i];
+                blocks += tiles[i] * s[i];
+                maxtps = tps > maxtps ? tps : maxtps;
+                if (s[i] > 1) {
+                    any_split = true;
+                    red += (double)gp.M[i] * ps[i].cout * 4.0 * (s[i] + 1) / 4e12;
+                }
+            }
+            if (bad) continue;
+            const double conc = blocks < slots ? (double)blocks : slots;
+            const double thr = 2.0 * c.t.bm * c.t.bn * 32.0 / (c.tflops * 1e12 / (conc > cus ? conc : cus));
+            const double rounds = std::ceil((double)blocks / slots);
+            double t = rounds * (2e-6 + maxtps * (thr > lat ? thr : lat));
+            if (any_split) t += 7e-6 + red;
+            if (t < best * 0.97) {
+                best = t;
+                gp.cfg = cfg;
+                for (int i = 0; i < n; ++i) gp.splits[i] = s[i];
+            }
+        }
+    }
+    S2V_REQUIRE(gp.cfg >= 0, "conv2d_group: members need the split-precision buffer-load path (direct zero-padded "
+                "conv, cin %% 32 == 0, <= 32 taps, no in_scale / pre_act / pool / grid_cap / force_tile, batch 1)");
+    for (int i = 0; i < n; ++i) {
+        Plan &pl = gp.plan[i];
+        pl.tile = gp.cfg;
+        pl.ktiles = (K[i] + 31) / 32;
+        finish_plan(pl, gp.splits[i]);
+        gp.splits[i] = pl.splits;
+    }
+    return 0;
+}
+
+static size_t group_ws_bytes(const s2v_conv_params *ps, int n, const GroupPlan &gp) {
+    size_t b = 0;
+    for (int i = 0; i < n; ++i)
+        if (gp.plan[i].splits > 1) b += ((size_t)gp.plan[i].splits * gp.M[i] * ps[i].cout * sizeof(float) + 255) / 256 * 256;
+    return b;
+}
+
 }  // namespace s2v
 
 using namespace s2v;
+
+extern "C" size_t s2v_conv2d_group_ws_bytes(const s2v_conv_params *ps, int n) {
+    GroupPlan gp;
+    if (group_plan(ps, n, gp)) return 0;
+    return group_ws_bytes(ps, n, gp);
+}
+
+extern "C" int s2v_conv2d_group_plan(const s2v_conv_params *ps, int n, int *out) {
+    GroupPlan gp;
+    const int rc = group_plan(ps, n, gp);
+    if (rc) return rc;
+    out[0] = gp.cfg;
+    for (int i = 0; i < n; ++i) out[1 + i] = gp.plan[i].splits;
+    return 0;
+}
+
+extern "C" int s2v_conv2d_group(const s2v_conv_params *ps, int n, s2v_stream_t stream) {
+    GroupPlan gp;
+    int rc = group_plan(ps, n, gp);
+    if (rc) return rc;
+    const size_t need = group_ws_bytes(ps, n, gp);
+    if (need && (!ps[0].ws || ps[0].ws_bytes < need)) {
+        set_error("conv2d_group: split-K workspace of %zu bytes required in member 0 (have %zu)", need, ps[0].ws_bytes);
+        return S2V_E_WORKSPACE;
+    }
+    ConvGroup g{};
+    g.n = n;
+    const TileCfg &t = kX3Tiles[gp.cfg].t;
+    long long blocks = 0, rblocks = 0;
+    size_t off = 0;
+    for (int i = 0; i < n; ++i) {
+        const s2v_conv_params *p = &ps[i];
+        ConvArgs &a = g.a[i];
+        a = make_args(p, gp.M[i], p->kh * p->kw * p->cin, gp.plan[i]);
+        a.wt = (const float *)p->wt_x3;
+        a.x_bytes = (unsigned)x_extent_bytes(p);
+        a.w_bytes = (unsigned)((long long)p->npad * p->kpad * 4);
+        a.stamps = nullptr;
+        if (gp.plan[i].splits > 1) {
+            a.ws = (float *)((char *)ps[0].ws + off);
+            off += ((size_t)gp.plan[i].splits * gp.M[i] * p->cout * sizeof(float) + 255) / 256 * 256;
+        }
+        g.gx[i] = (int)cdiv(gp.M[i], t.bm);
+        g.gy[i] = (int)cdiv(p->cout, t.bn);
+        g.start[i] = (int)blocks;
+        blocks += (long long)g.gx[i] * g.gy[i] * gp.plan[i].splits;
+        g.rstart[i] = (int)rblocks;
+        if (gp.plan[i].splits > 1) {
+            long long items = (long long)gp.M[i] * (p->cout % 4 == 0 ? p->cout / 4 : p->cout);
+            long long rb = (items + 255) / 256;
+            if (rb > 1024) rb = 1024;
+            rblocks += rb;
+        }
+        g.vec[i] = epi_vec4(p);
+    }
+    for (int i = n; i <= kConvGroupMax; ++i) {
+        g.start[i] = (int)blocks;
+        g.rstart[i] = (int)rblocks;
+    }
+    S2V_REQUIRE(blocks < (1LL << 31), "conv2d_group: too many tiles");
+    hipStream_t s = (hipStream_t)stream;
+    rc = ps[0].prec == S2V_PREC_BF16X3 ? launch_conv_x3_group<0>(gp.cfg, g, dim3((unsigned)blocks), s)
+                                       : launch_conv_x3_group<1>(gp.cfg, g, dim3((unsigned)blocks), s);
+    if (rc) return rc;
+    rc = check_launch("conv2d_group");
+    if (rc || rblocks == 0) return rc;
+    splitk_reduce_group<<<(unsigned)rblocks, 256, 0, s>>>(g);
+    return check_launch("splitk_reduce_group");
+}
 
 extern "C" int s2v_tune(int key, long long value, long long *old_value) {
     S2V_REQUIRE(key >= 0 && key < S2V_TUNE_COUNT, "tune: bad key %d", key);

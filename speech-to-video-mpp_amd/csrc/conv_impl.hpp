@@ -48,6 +48,19 @@ struct ConvArgs {
                                      // (s2v_conv_params.grid_cap); vgrid_x == 0: one block per tile
 };
 
+// A group of independent convolutions launched as one kernel (s2v_conv2d_group): member p owns the
+// blocks [start[p], start[p + 1]) of the launch, laid out as its own (gx, gy, gz) tile grid; the
+// split-K fold of the members with splits > 1 owns the reduce blocks [rstart[p], rstart[p + 1]).
+constexpr int kConvGroupMax = 4;
+struct ConvGroup {
+    ConvArgs a[kConvGroupMax];
+    int start[kConvGroupMax + 1];
+    int gx[kConvGroupMax], gy[kConvGroupMax];
+    int rstart[kConvGroupMax + 1];
+    int vec[kConvGroupMax];
+    int n;
+};
+
 // Launch timer: block start (atomic min) / end (atomic max) of the device real-time clock into the
 // slot of the current replay.  One lane per block; vector-memory 64-bit atomics.
 __device__ __forceinline__ void launch_stamp(const ConvArgs &a, bool end) {

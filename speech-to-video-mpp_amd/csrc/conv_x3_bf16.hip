@@ -3,4 +3,5 @@
 
 namespace s2v {
 template int launch_conv_x3<0>(int cfg, const ConvArgs &a, int amode, bool bkn, dim3 grid, hipStream_t s);
+template int launch_conv_x3_group<0>(int cfg, const ConvGroup &g, dim3 grid, hipStream_t s);
 }  // namespace s2v

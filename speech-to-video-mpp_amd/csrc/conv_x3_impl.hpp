@@ -600,6 +600,20 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3_persist(ConvArgs a) 
     launch_stamp(a, true);
 }
 
+// Grouped form (s2v_conv2d_group): member p of the group runs the blocks [start[p], start[p + 1]) as
+// its own tile grid.  The member index is block-uniform; the ConvArgs are read from the kernarg
+// segment at that index (scalar loads).
+template <int BM, int BN, int WAVES_M, int NW, int KS, int PF, int ELT>
+__global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3_group(ConvGroup g) {
+    const int L = blockIdx.x;
+    int p = 0;
+#pragma unroll
+    for (int i = 1; i < kConvGroupMax; ++i)
+        if (i < g.n && L >= g.start[i]) p = i;
+    conv_x3_tile<BM, BN, WAVES_M, NW, KS, PF, 4, 0, ELT>(g.a[p], L - g.start[p], g.gx[p], g.gy[p],
+                                                         g.start[p + 1] - g.start[p]);
+}
+
 template <int BM, int BN, int WM, int NW, int KS, int PF, int ELT>
 static void launch_x3(const ConvArgs &a, int amode, bool bkn, dim3 grid, hipStream_t s) {
     constexpr int NT = 64 * NW;
@@ -651,6 +665,20 @@ int launch_conv_x3(int cfg, const ConvArgs &a, int amode, bool bkn, dim3 grid, h
         case 9: launch_x3<128, 64, 2, 4, 1, 2, ELT>(a, amode, bkn, grid, s); break;
         case 10: launch_x3<64, 64, 2, 4, 1, 2, ELT>(a, amode, bkn, grid, s); break;
         default: launch_x3<128, 32, 4, 4, 1, 2, ELT>(a, amode, bkn, grid, s); break;
+    }
+    return 0;
+}
+
+// grouped launches exist for the 4-wave 64x64 / 128x64 and the 8-wave 128x128 buffer-load tiles
+constexpr bool x3_has_group(int cfg) { return cfg == 1 || cfg == 3 || cfg == 4; }
+
+template <int ELT>
+int launch_conv_x3_group(int cfg, const ConvGroup &g, dim3 grid, hipStream_t s) {
+    switch (cfg) {
+        case 1: conv_igemm_x3_group<128, 128, 2, 8, 1, 1, ELT><<<grid, 512, 0, s>>>(g); break;
+        case 3: conv_igemm_x3_group<128, 64, 2, 4, 1, 1, ELT><<<grid, 256, 0, s>>>(g); break;
+        case 4: conv_igemm_x3_group<64, 64, 2, 4, 1, 1, ELT><<<grid, 256, 0, s>>>(g); break;
+        default: S2V_REQUIRE(false, "conv2d_group: x3 configuration %d has no grouped kernel", cfg);
     }
     return 0;
 }

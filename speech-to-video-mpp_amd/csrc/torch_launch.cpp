@@ -220,6 +220,59 @@ void conv_common(s2v_conv_params &p, const Tensor &x, const Tensor &y, int64_t c
     p.prec = (int)prec;
 }
 
+// Conv groups (s2v_conv2d_group): between group_begin_() and group_end_() every conv2d_ call is
+// validated and recorded instead of launched; group_end_ launches the recorded convs as one group
+// (or, when they cannot form one, one after the other).  Per thread: the recording belongs to the
+// Python thread issuing the forward.
+thread_local std::vector<s2v_conv_params> g_group;
+thread_local bool g_recording = false;
+thread_local int g_group_dev = 0;             // device index of the members (the launch goes to its stream)
+
+void group_begin_() {
+    TORCH_CHECK(!g_recording, "conv group: group_begin_ inside an open group");
+    g_group.clear();
+    g_recording = true;
+}
+
+void group_abort_() {
+    g_group.clear();
+    g_recording = false;
+}
+
+// Returns [ws_need] while the workspace is short (nothing launched, the group stays open), else
+// [0, grouped] after the launch (grouped 1: one group launch; 0: the members launched one by one).
+std::vector<int64_t> group_end_(const OptT &ws, bool dry) {
+    TORCH_CHECK(g_recording, "conv group: group_end_ without group_begin_");
+    const int n = (int)g_group.size();
+    if (n == 0) {
+        group_abort_();
+        return {0, 0};
+    }
+    const at::Device dev(at::kCUDA, (c10::DeviceIndex)g_group_dev);
+    const c10::DeviceGuard guard(dev);
+    const Ws w = workspace(ws, dev);
+    int gp[1 + S2V_CONV_GROUP_MAX] = {0};
+    const bool grouped = n <= S2V_CONV_GROUP_MAX && s2v_conv2d_group_plan(g_group.data(), n, gp) == 0;
+    size_t need = 0;
+    if (grouped) {
+        need = s2v_conv2d_group_ws_bytes(g_group.data(), n);
+    } else {
+        for (const auto &p : g_group) need = std::max(need, s2v_conv2d_ws_bytes(&p));
+    }
+    if (dry || w.bytes < need) return {(int64_t)need};
+    if (grouped) {
+        g_group[0].ws = (float *)w.p; g_group[0].ws_bytes = w.bytes;
+        check(s2v_conv2d_group(g_group.data(), n, stream()), "s2v_conv2d_group");
+    } else {
+        for (auto &p : g_group) {
+            p.ws = (float *)w.p; p.ws_bytes = w.bytes;
+            check(s2v_conv2d(&p, stream()), "s2v_conv2d");
+        }
+    }
+    group_abort_();
+    return {0, grouped ? 1 : 0};
+}
+
 // Implicit-GEMM convolution (s2v_conv_params, include/s2v.h) with packed weights [npad][kpad]
 // (and, for the split precisions, their s2v_split_weights copy).  Returns [ws_need, plan...]:
 // ws_need 0 = launched (or dry run of a launch that needs no workspace); > 0 = bytes of workspace
@@ -273,6 +326,14 @@ std::vector<int64_t> conv2d_(const Tensor &x, const Tensor &y, const Tensor &wt,
     p.grid_cap = (int)grid_cap;
     set_stamps(p, stamps, stamp_ctr, stamp_pos, dev);
     set_range(p, x_scale, nonfinite, dev);
+    if (g_recording && !dry) {            // conv group: record (validated by the plan) instead of launching
+        TORCH_CHECK(!p.stamps, "conv group: no launch stamps on group members");
+        TORCH_CHECK(g_group.empty() || g_group_dev == dev.index(), "conv group: members on one device");
+        auto out = plan_list(p, 0);
+        g_group_dev = dev.index();
+        g_group.push_back(p);
+        return out;
+    }
     const size_t need = s2v_conv2d_ws_bytes(&p);
     const Ws w = workspace(ws, dev);
     if (dry || w.bytes < need) return plan_list(p, (int64_t)need);
@@ -297,6 +358,7 @@ std::vector<int64_t> modulated_conv2d_(const Tensor &x, const Tensor &y, const T
                                        int64_t d2s) {
     const c10::DeviceGuard guard(x.device());
     const at::Device dev = x.device();
+    TORCH_CHECK(!g_recording, "conv group: modulated convs cannot be group members");
     s2v_conv_params p{};
     const int64_t one[2] = {1, 1}, zero[2] = {0, 0};
     TORCH_CHECK(in_mode == S2V_IN_DIRECT || in_mode == S2V_IN_NEAREST_UP2, "modconv: direct or nearest-x2 input");
@@ -829,6 +891,10 @@ TORCH_LIBRARY_FRAGMENT(s2v, m) {
           "bool res_after_act, int act, float alpha, Tensor? ws, int force_splits, Tensor(s!)? stamps, Tensor? stamp_ctr, "
           "int[3] stamp_pos, float x_scale, Tensor(f!)? nonfinite, bool dry, int d2s=0) -> int[]");
     m.def("amax_(Tensor x, Tensor(a!) out) -> ()");
+    // conv groups: host-side recording, no tensor to dispatch on (catch-all kernels)
+    m.def("group_begin_() -> ()", &group_begin_);
+    m.def("group_abort_() -> ()", &group_abort_);
+    m.def("group_end_(Tensor? ws, bool dry) -> int[]", &group_end_);
     m.def("gemm_kn_(Tensor a, Tensor b, Tensor(a!) out, int batch, int a_bs, int b_bs, int out_bs, Tensor? res, "
           "int res_bs, int act, float alpha, int prec, Tensor? ws, int force_tile, int force_splits, bool dry) -> int[]");
     m.def("split_weights_(Tensor w, Tensor(a!) out, int prec, float scale) -> ()");

@@ -18,6 +18,10 @@ LRELU = 0.1        # LNet.py:91
 LRELU_FFC = 0.01   # FineADAINLama built with nn.LeakyReLU() default (base_blocks.py:369 via :393/:419)
 # FFC products on concurrent side streams (S2V_LNET_BRANCHES=0 serialises them on one stream)
 BRANCHES = os.environ.get("S2V_LNET_BRANCHES", "1") == "1"
+# the FFC's three products that read the block input (conv_to_l, l2g, the spectral branch's st1) as
+# ONE grouped launch (ops.conv_group / s2v_conv2d_group) followed by the spectral chain on the same
+# stream, instead of three side-stream branches whose launches each under-fill the chip
+GROUP = os.environ.get("S2V_LNET_GROUP", "1") == "1"
 # FFC 3x3 reflect convs over a pre-padded input (S2V_LNET_PREPAD=0: reflect addressing in the gather)
 PREPAD = os.environ.get("S2V_LNET_PREPAD", "1") == "1"
 # with PREPAD: the InstanceNorm that ends an FFC writes the next FFC's reflect-padded input itself
@@ -186,7 +190,16 @@ class FFCLama:
                        force_splits=SPEC_SPLITS)
             ops.irfft2(c, spec2.t.view(b, self.F, 2 * cc), self.fft, u, res=t1)   # irfftn + x (ffc.py:120-126, :158)
 
-        if branches is None:
+        if GROUP and not fs_c2l and not fs_l2g:
+            with ops.conv_group(ctx):
+                ops.conv2d(ctx, xr, self.conv_to_l, y.slice(0, cl))
+                l2g(ctx)
+                ops.conv2d(ctx, x.slice(cl, cg), self.st1, t1, act=ops.ACT_RELU)
+            ops.rfft2(ctx, t1, self.fft, spec)
+            ops.conv2d(ctx, NHWC(spec.view(b, self.F, 1, 2 * cc)), self.fu, spec2, act=ops.ACT_RELU,
+                       force_splits=SPEC_SPLITS)
+            ops.irfft2(ctx, spec2.t.view(b, self.F, 2 * cc), self.fft, u, res=t1)
+        elif branches is None:
             ops.conv2d(ctx, xr, self.conv_to_l, y.slice(0, cl), force_splits=fs_c2l)
             l2g(ctx)
             spectral(ctx)
@@ -336,10 +349,11 @@ class LNetEngine:
                 pa = NHWC.empty(cur.n, cur.h + 2, cur.w + 2, c, dev)
                 pc = NHWC.empty(cur.n, cur.h + 2, cur.w + 2, c, dev)
             nblk = len(lv["blocks"])
+            fbr = None if GROUP else br                         # grouped FFC: one stream
             for bi, (l1, l2) in enumerate(lv["blocks"]):
-                l1.pre_norm(ctx, cur, ya, br, xpad=pc if bi > 0 else None)
+                l1.pre_norm(ctx, cur, ya, fbr, xpad=pc if bi > 0 else None)
                 l1.norm(ctx, self.bank, ap, ya, ya, pad_out=pa)
-                l2.pre_norm(ctx, ya, yb, br, xpad=pa)
+                l2.pre_norm(ctx, ya, yb, fbr, xpad=pa)
                 l2.norm(ctx, self.bank, ap, yb, cur, res=cur,    # FFCResnetBlock: id + conv2(conv1(x))
                         pad_out=pc if bi + 1 < nblk else None)
             up = lv["up"](ctx, cur)

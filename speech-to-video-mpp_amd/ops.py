@@ -103,6 +103,8 @@ CONV_HOOK = None
 # [slot, stride, reps]) for the kernel's in-launch clock stamps (s2v_conv_params.stamps).
 STAMP = None
 _NOSTAMP = (None, None, [0, 1, 1])
+_GROUPING = False       # inside conv_group: launches are recorded (no per-launch stamps)
+LAST_GROUP = 0          # 1: the last conv_group launched as one grouped kernel, 0: one by one
 
 
 class _Dispatch:
@@ -498,6 +500,41 @@ def _conv(ctx, x, cw, yv, out_step, act, alpha, resv, res_after, res_offset, nc_
     _run_conv(ctx, launch, x, cw, yv, pool, in_scale, nc_scale, pix_add, resv)
 
 
+@contextlib.contextmanager
+def conv_group(ctx: Ctx, enabled: bool = True):
+    """Launch the convs issued on ``ctx`` inside the block as ONE grouped kernel (s2v_conv2d_group:
+    independent convs that read the same input, each with its own split-K factor, plus one grouped
+    split-K fold) at the end of the block.  The members must not depend on each other.  Off when
+    ``enabled`` is false or a CONV_HOOK observes launches (the roofline pre-pass times convs one by
+    one): then the convs launch as they are issued."""
+    if not enabled or CONV_HOOK is not None:
+        yield
+        return
+    global _GROUPING
+    S2V.group_begin_()
+    _GROUPING = True
+    try:
+        yield
+    except BaseException:
+        S2V.group_abort_()
+        raise
+    finally:
+        _GROUPING = False
+    global LAST_GROUP
+    res = []
+
+    def end(ws):
+        r = S2V.group_end_(ws, False)
+        res[:] = r
+        return r[0]
+    try:
+        _with_ws(ctx, end)
+    except BaseException:
+        S2V.group_abort_()
+        raise
+    LAST_GROUP = res[1] if len(res) > 1 else 0
+
+
 def check_all_ranges(what="s2v"):
     """Ctx.check_range over every live context (raises on the first flagged lane)."""
     for c in list(Ctx.ALL):
@@ -626,7 +663,7 @@ def _run_conv(ctx, launch, x, cw, yv, pool, in_scale=None, nc_scale=None, pix_ad
                       in_scale=in_scale is not None, nc_scale=nc_scale is not None, pix_add=pix_add is not None,
                       res=resv is not None, res_is_y=resv is not None and resv.data_ptr() == yv.data_ptr())
     flops = _conv_flops(x, cw, yv, pool)
-    if STAMP is not None:
+    if STAMP is not None and not _GROUPING:
         st = STAMP(info, flops) or _NOSTAMP
     if CONV_HOOK is None:
         go()

@@ -10,6 +10,7 @@ run in both arithmetic modes (``prec`` fixture):
   * f16x3  (the same split on v_mfma_f32_32x32x16_f16): 3e-6 * sum|a*b| — 3 * 2^-22 = 7.2e-7 per
            product in the f16 normal range (weights pre-scaled into it), plus the fp32 sums.
 """
+import ctypes
 import math
 
 import numpy as np
@@ -732,3 +733,65 @@ def test_conv_x3_grid_cap_bit_exact(ctx, tile, splits, cap):
     ref = F.leaky_relu(F.conv2d(x, wt, bias, padding=1), 0.2)
     lim = REL["f16x3"] * (conv_bound(x, wt, 1, 1, 1) + 1) + 1e-6
     assert ((to_nchw(outs[1]) - ref).abs() <= lim).all()
+
+
+@pytest.mark.parametrize("sprec", ["f16x3", "bf16x3"])
+def test_conv_group_matches_reference(ctx, sprec):
+    """s2v_conv2d_group (ops.conv_group): LNet's FFC fork as one launch — a K-heavy 3x3 valid conv, a
+    wide 3x3 on a channel slice and a 1x1 with a BN-style epilogue + ReLU on another slice of the same
+    input, each with its own split-K factor — against fp64 references at the split-precision bound,
+    and the grouped plan really forms one group."""
+    n, h, w = 2, 12, 12
+    cin, cl = 256, 64
+    x = rnd(n, cin, h + 2, w + 2, seed=71)                 # pre-padded block input
+    xin = rnd(n, cin, h, w, seed=72)
+    w1 = rnd(64, cin, 3, 3, seed=73) / math.sqrt(cin * 9)
+    w2 = rnd(192, cl, 3, 3, seed=74) / math.sqrt(cl * 9)
+    w3 = rnd(96, cin - cl, 1, 1, seed=75) / math.sqrt(cin - cl)
+    sc, sh = rnd(96, seed=76, lo=0.5, hi=1.5), rnd(96, seed=77)
+    cw1 = ConvW(w1.float(), None, DEV)
+    cw2 = ConvW(w2.float(), None, DEV)
+    cw3 = ConvW(w3.float(), None, DEV, post_scale=sc.float())
+    cw3.shift = (sh.float()).to(DEV)
+    prev = ops.set_precision(sprec)
+    try:
+        xp, xi = nhwc(x.float()), nhwc(xin.float())
+        y = NHWC.empty(n, h, w, 256, DEV)
+        t = NHWC.empty(n, h, w, 96, DEV)
+        with ops.conv_group(ctx):
+            ops.conv2d(ctx, xp, cw1, y.slice(0, 64))
+            ops.conv2d(ctx, xp.slice(0, cl), cw2, y.slice(64, 192))
+            ops.conv2d(ctx, xi.slice(cl, cin - cl), cw3, t, act=ops.ACT_RELU)
+        torch.cuda.synchronize()
+        params = []
+        for xv, cw, yv in ((xp, cw1, y.slice(0, 64)), (xp.slice(0, cl), cw2, y.slice(64, 192)),
+                           (xi.slice(cl, cin - cl), cw3, t)):
+            p = _params_of(ctx, xv, cw, yv)
+            params.append(p)
+        arr = (ops._lib.ConvParams * 3)(*params)
+        out = (ctypes.c_int * 5)()
+        assert ctx.lib.s2v_conv2d_group_plan(arr, 3, out) == 0, ctx.lib.s2v_last_error()
+        assert ops.LAST_GROUP == 1                        # the launch above was one grouped kernel
+    finally:
+        ops.set_precision(prev)
+    r1 = F.conv2d(x, w1)
+    r2 = F.conv2d(x[:, :cl], w2)
+    r3 = F.relu(F.conv2d(xin[:, cl:], w3) * sc[None, :, None, None] + sh[None, :, None, None])
+    for got, ref, bound in ((to_nchw(y.slice(0, 64)), r1, conv_bound(x, w1, 1, 0, 1)),
+                            (to_nchw(y.slice(64, 192)), r2, conv_bound(x[:, :cl], w2, 1, 0, 1)),
+                            (to_nchw(t), r3, conv_bound(xin[:, cl:], w3, 1, 0, 1) * sc.abs()[None, :, None, None])):
+        err = (got - ref).abs()
+        assert (err <= REL[sprec] * (bound + 1) + 1e-6).all(), f"max err {err.max():.3e}"
+
+
+def _params_of(ctx, x, cw, y):
+    """s2v_conv_params of a plain conv2d launch (ctypes), for the C ABI plan calls."""
+    p = ops._lib.ConvParams()
+    p.x, p.n, p.h, p.w, p.cin, p.xcs = x.ptr, x.n, x.h, x.w, x.c, x.cs
+    p.kh, p.kw, p.sh, p.sw, p.ph, p.pw, p.dh, p.dw = cw.kh, cw.kw, cw.sh, cw.sw, cw.ph, cw.pw, cw.dh, cw.dw
+    p.wt, p.kpad, p.npad, p.cout = cw.wt.data_ptr(), cw.kpad, cw.npad, cw.cout
+    p.y, p.oh, p.ow, p.ycs = y.ptr, y.h, y.w, y.cs
+    p.prec = ops.prec_code()
+    p.wt_x3 = cw.wt_x3(ctx, p.prec).data_ptr()
+    p.batch = 1
+    return p
