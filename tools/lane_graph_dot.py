@@ -22,14 +22,13 @@ import s2v_import  # noqa: E402,F401
 
 
 def parse_dot(path):
-    nodes, edges = {}, []
-    for line in open(path):
-        m = re.match(r'\s*"?([\w]+)"?\s*\[(.*)\]\s*;?\s*$', line)
-        e = re.match(r'\s*"?([\w]+)"?\s*->\s*"?([\w]+)"?', line)
-        if e:
-            edges.append((e.group(1), e.group(2)))
-        elif m and "label" in m.group(2):
-            nodes[m.group(1)] = m.group(2)
+    """hipGraphDebugDotPrint output: multi-line record nodes ``"graph_0_node_N"[... label="{ KERNEL | {ID | N |
+    symbol\\<\\<\\<grid...`` and edges ``"a" -> "b"``; returns ({node: "KIND symbol"}, [(src, dst)])."""
+    text = open(path).read()
+    nodes = {}
+    for m in re.finditer(r'"(\w+)"\[[^\n]*label="\{\s*\n?(\w+)\s*\n?\|\s*\{ID \| \d+ \| ([^\\|<]*)', text):
+        nodes[m.group(1)] = f"{m.group(2)} {m.group(3).strip()}"
+    edges = re.findall(r'"(\w+)"\s*->\s*"(\w+)"', text)
     return nodes, edges
 
 
@@ -59,45 +58,60 @@ def main():
             model(mel, face, gt, lane=lane)
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
-        cg = torch.cuda.CUDAGraph()
+        cg = torch.cuda.CUDAGraph(keep_graph=True)     # the captured graph object survives capture_end
         cg.enable_debug_mode()
         with torch.cuda.graph(cg):
             model(mel, face, gt, lane=lane)
         torch.cuda.synchronize()
         path = os.path.join(a.out, f"lane{lane}.dot")
         cg.debug_dump(path)
-        nodes, edges = parse_dot(path)
-        parents = {}
-        for s, d in edges:
-            parents.setdefault(d, set()).add(s)
-        order = sorted(nodes, key=lambda k: int(re.sub(r"\D", "", k) or 0))
-        kern = [k for k in order if "Kernel" in nodes[k] or "kernel" in nodes[k]]
-        up = [k for k in kern if "up2_bilinear" in nodes[k] or "resize" in nodes[k]]
-
-        def ancestors(k):
-            seen, st = set(), [k]
-            while st:
-                for p in parents.get(st.pop(), ()):
-                    if p not in seen:
-                        seen.add(p)
-                        st.append(p)
-            return seen
-        print(f"lane {lane}: {len(nodes)} nodes ({len(kern)} kernels), {len(edges)} edges, {len(up)} resize / up2 "
-              f"nodes", flush=True)
-        for k in up:
-            i = kern.index(k)
-            anc = ancestors(k)
-            # the capture-order predecessors that are on a path into this node
-            prev = [p for p in kern[max(0, i - 6):i]]
-            linked = [p for p in prev if p in anc]
-            label = re.search(r"label=\"?([^\"]*)", nodes[k])
-            name = (label.group(1) if label else nodes[k])[:80]
-            ok = bool(linked) or i == 0
-            bad += not ok
-            print(f"  {k}: {name!r} parents={sorted(parents.get(k, ()))} ancestors={len(anc)} "
-                  f"linked-prev={linked[-2:]} {'OK' if ok else 'NO PATH FROM ITS PREDECESSORS'}", flush=True)
+        if not os.path.exists(path):
+            sys.exit(f"debug_dump wrote nothing to {path}")
+        bad += check(lane, path)
     sys.exit(1 if bad else 0)
 
 
+def check(lane, path):
+    """Edge check of one dumped lane graph; returns the number of up2 / resize nodes that have no path
+    from any of their six capture-order predecessors."""
+    nodes, edges = parse_dot(path)
+    parents = {}
+    for s, d in edges:
+        parents.setdefault(d, set()).add(s)
+    order = sorted(nodes, key=lambda k: int(re.sub(r"\D", "", k.rsplit("_", 1)[-1]) or 0))
+    kern = [k for k in order if nodes[k].startswith("KERNEL")]
+    up = [k for k in kern if "up2_bilinear" in nodes[k] or "resize" in nodes[k]]
+
+    def ancestors(k):
+        seen, st = set(), [k]
+        while st:
+            for p in parents.get(st.pop(), ()):
+                if p not in seen:
+                    seen.add(p)
+                    st.append(p)
+        return seen
+    roots = [k for k in nodes if k not in parents]
+    print(f"lane {lane}: {len(nodes)} nodes ({len(kern)} kernels), {len(edges)} edges, {len(roots)} roots, "
+          f"{len(up)} resize / up2 nodes", flush=True)
+    bad = 0
+    for k in up:
+        i = kern.index(k)
+        anc = ancestors(k)
+        prev = kern[max(0, i - 6):i]
+        linked = [p for p in prev if p in anc]
+        ok = bool(linked) or i == 0
+        bad += not ok
+        print(f"  {k}: {nodes[k][7:80]!r} parents={sorted(parents.get(k, ()))} ancestors={len(anc)} "
+              f"linked-prev={linked[-2:]} {'OK' if ok else 'NO PATH FROM ITS PREDECESSORS'}", flush=True)
+    return bad
+
+
+def parse_only(paths):
+    """Check already dumped .dot files (no GPU)."""
+    sys.exit(1 if sum(check(i, p) for i, p in enumerate(paths)) else 0)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 2 and sys.argv[1] == "--check":
+        parse_only(sys.argv[2:])
     main()
