@@ -68,7 +68,7 @@ def main():
                           f"ends {(max(big) - lo) / 1e3:8.1f} us")
 
 
-if __name__ == "__main__" and "--lnet" not in sys.argv:
+if __name__ == "__main__" and "--lnet" not in sys.argv and "--ffc" not in sys.argv:
     main()
 
 
@@ -92,3 +92,26 @@ def lnet_levels(path):
 
 if __name__ == "__main__" and "--lnet" in sys.argv:
     lnet_levels(sys.argv[1])
+
+
+def lnet_ffc(path, k=4):
+    """Every kernel of the k-th FFC of each decoder level in the last LNet forward of the trace (from the
+    k-th rfft2 of that size back to the previous FFC's InstanceNorm, up to the k-th FFC's InstanceNorm):
+    start offset, duration, end offset and name, so the per-FFC critical path can be read off."""
+    ks = load(path)
+    for h in (12, 24, 48):
+        rf = [i for i, (n, a, b) in enumerate(ks) if n.startswith(f"void s2v::rfft2_mf<{h},")]
+        if len(rf) < 18:
+            continue
+        r = rf[-18 + k]
+        ins = [i for i, (n, a, b) in enumerate(ks) if n.startswith("void s2v::in_")]
+        prev = max(i for i in ins if i < r)
+        nxt = min(i for i in ins if i > r)
+        t0 = ks[prev][2]
+        print(f"level {h}x{h}, FFC {k}: {(ks[nxt][2] - t0) / 1e3:.1f} us from the previous InstanceNorm's end")
+        for n, a, b in ks[prev + 1: nxt + 1]:
+            print(f"  +{(a - t0) / 1e3:7.1f} {(b - a) / 1e3:7.1f} us -> +{(b - t0) / 1e3:7.1f}  {n.split('(')[0][:90]}")
+
+
+if __name__ == "__main__" and "--ffc" in sys.argv:
+    lnet_ffc(sys.argv[1])
