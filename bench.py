@@ -27,6 +27,8 @@ Other workloads (not the headline metric):
   --workload enhance    one step = B 512x512 faces through GFPGANv1Clean and GPEN-512;
   --workload lnet       one step = LNet forward alone on B=16 (BASELINE configs[1]): 256x256 crops
                         bilinear-resized to 96x96 as ENet.py:104 does, then models/LNet.py:122-139;
+  --workload dnet       one step = DNet forward alone on B=16 256x256 source crops + coefficient windows
+                        (the pipeline's DNet phase, models/DNet.py:20-28);
   --workload mouth      one step = B 720x720 frames through the mouth-region post-process
                         (FaceParse-512 mask of the face box + 10-level Laplacian blend,
                         inference.py:302-313, s2v_amd.post.MouthBlend);
@@ -447,6 +449,47 @@ class LNetOnly(Workload):
                 "sample": f"{n} frames (2-frame batches) of LNet at 96x96 in {el:.1f}s, torch CPU fp32, {threads} threads"}
 
 
+class DNetOnly(Workload):
+    """The pipeline's DNet phase alone (DNet.py:20-28 on B 256x256 source crops + coefficient windows),
+    graph-replayed: its FLOP rate is the DNet-phase roofline (101.45 GFLOP/frame)."""
+    metric = "DNet frames/sec/GPU (B=16 256x256 source crops + [73, 26] coefficient windows)"
+    gflop_per_unit = 101.45
+
+    def __init__(self, args, dev, rank, world=1):
+        import numpy as np
+        from s2v_amd import models, pipeline, synth
+        from s2v_amd.models import arch
+        self.batch = args.batch or 16
+        self.sd = synth.synth_torch_state_dict(arch.DNetParams())
+        self.model = models.DNet()
+        self.model.load_state_dict(self.sd)
+        self.model.eval()
+        rng = np.random.default_rng(1)
+        semantic = rng.standard_normal((self.batch + 40, 262)).astype(np.float32)
+        semantic[:, -3] = 1.0 + 0.1 * rng.random(semantic.shape[0])
+        coeffs = pipeline.dnet_coefficients(semantic, rng.standard_normal(64).astype(np.float32))
+        g = torch.Generator(device=dev)
+        g.manual_seed(3000 + rank)
+        self.inputs = [torch.rand((self.batch, 3, 256, 256), generator=g, device=dev) * 2 - 1,
+                       torch.from_numpy(coeffs[: self.batch]).to(dev)]
+        self.fn = lambda s, c: self.model(s, c)  # noqa: E731
+        self.fn_lane = lambda lane, s, c: self.model(s, c, lane=lane)  # noqa: E731
+        self.config = {"workload": f"DNet forward, B={self.batch} synthetic 256x256 source crops + coefficient windows "
+                                   f"{tuple(self.inputs[1].shape[1:])} (models/DNet.py:20-28)"}
+
+    def forward(self):
+        return self.fn(*self.inputs)
+
+    def cpu(self, threads, seconds):
+        from oracle import nets
+        torch.set_num_threads(threads)
+        s, c = (t[:2].cpu() for t in self.inputs)
+        n, el = _timed_cpu(lambda: nets.dnet_forward(self.sd, s, c), 2, seconds, 8)
+        return {"value": round(n / el, 4), "unit": "frames/s", "cores": threads, "kind": "port",
+                "sample": f"{n} frames (2-frame batches) of DNet at 256x256 in {el:.1f}s, torch CPU fp32, "
+                          f"{threads} threads"}
+
+
 class Pipeline(Workload):
     metric = "full DNet->LNet->ENet frames/sec/GPU (uint8 384x384 output)"
     gflop_per_unit = 508.91            # SURVEY.md §8d config 3: ENet+LNet 407.46 + DNet 101.45 (live)
@@ -781,7 +824,7 @@ class Clip(Pipeline):
         return self.result
 
 
-WORKLOADS = {"lipsync": LipSync, "lnet": LNetOnly, "pipeline": Pipeline, "enhance": Enhance, "mouth": Mouth,
+WORKLOADS = {"lipsync": LipSync, "lnet": LNetOnly, "dnet": DNetOnly, "pipeline": Pipeline, "enhance": Enhance, "mouth": Mouth,
              "sr": SuperRes, "gpen2048": GPEN2048, "face3d": Face3D, "clip": Clip, "selftest": SelfTest}
 
 

@@ -496,6 +496,78 @@ __global__ __launch_bounds__(256) void adain_heads(const float *__restrict__ hid
         if (b0 + i < batch) out[(long long)(b0 + i) * out_ns + o] = acc[i] + bb;
 }
 
+// ADAIN heads v2: a block owns 64 consecutive outputs and a chunk of <= 16 samples; its 4 waves split
+// the hidden units (wave q: units [q nh / 4, (q + 1) nh / 4)), lane = output, so every weight row
+// piece is one coalesced 256-byte load and the weights are read once per 16 samples.  The hidden
+// vectors of the (few) segments the block's outputs use are staged in LDS as [segment][unit][sample],
+// read as float4 broadcasts; the four partial sums meet in LDS.  (v1 read 8 samples' hidden values
+// from global memory per weight load: 264 us for 26 MB of weights, r03.)
+constexpr int ADAIN_BO = 64, ADAIN_NB = 16, ADAIN_SEGW = 4, ADAIN_NHMAX = 128;
+__global__ __launch_bounds__(256) void adain_heads2(const float *__restrict__ hid, int batch, int hid_ns, int nh,
+                                                    const float *__restrict__ w2t, const float *__restrict__ bias,
+                                                    const int *__restrict__ seg, int total, float *__restrict__ out,
+                                                    int out_ns) {
+    __shared__ __attribute__((aligned(16))) float hs[ADAIN_SEGW][ADAIN_NHMAX][ADAIN_NB];
+    __shared__ float part[4][ADAIN_NB][ADAIN_BO + 1];
+    __shared__ int srange[2];
+    const int tid = threadIdx.x, lane = tid & 63, q = tid >> 6;
+    const int o0 = blockIdx.x * ADAIN_BO, b0 = blockIdx.y * ADAIN_NB;
+    const int nb = min(ADAIN_NB, batch - b0);
+    const int o = o0 + lane;
+    const bool ok = o < total;
+    const int sg = ok ? seg[o] : 0x7fffffff;
+    if (q == 0) {
+        int lo = sg, hi = ok ? sg : -1;
+        for (int d = 32; d > 0; d >>= 1) {
+            lo = min(lo, __shfl_xor(lo, d));
+            hi = max(hi, __shfl_xor(hi, d));
+        }
+        if (lane == 0) { srange[0] = lo; srange[1] = hi; }
+    }
+    __syncthreads();
+    const int smin = srange[0], smax = srange[1];
+    const int j0 = q * nh / 4, j1 = (q + 1) * nh / 4;
+    float acc[ADAIN_NB];
+#pragma unroll
+    for (int i = 0; i < ADAIN_NB; ++i) acc[i] = 0.f;
+    for (int w0 = smin; w0 <= smax; w0 += ADAIN_SEGW) {
+        if (w0 > smin) __syncthreads();                 // previous window's reads done
+        const int ns = min(ADAIN_SEGW, smax - w0 + 1);
+        for (int e = tid; e < ns * nh * ADAIN_NB; e += 256) {
+            const int b = e % ADAIN_NB, j = (e / ADAIN_NB) % nh, s = e / (ADAIN_NB * nh);
+            hs[s][j][b] = b < nb ? hid[(long long)(b0 + b) * hid_ns + (long long)(w0 + s) * nh + j] : 0.f;
+        }
+        __syncthreads();
+        if (ok && sg >= w0 && sg < w0 + ns) {
+            const float *hr = &hs[sg - w0][0][0];
+            const float *wp = w2t + o;
+#pragma unroll 8
+            for (int j = j0; j < j1; ++j) {
+                const float wv = wp[(long long)j * total];
+                const float4 h0 = *(const float4 *)(hr + j * ADAIN_NB), h1 = *(const float4 *)(hr + j * ADAIN_NB + 4);
+                const float4 h2 = *(const float4 *)(hr + j * ADAIN_NB + 8), h3 = *(const float4 *)(hr + j * ADAIN_NB + 12);
+                acc[0] = fmaf(wv, h0.x, acc[0]); acc[1] = fmaf(wv, h0.y, acc[1]);
+                acc[2] = fmaf(wv, h0.z, acc[2]); acc[3] = fmaf(wv, h0.w, acc[3]);
+                acc[4] = fmaf(wv, h1.x, acc[4]); acc[5] = fmaf(wv, h1.y, acc[5]);
+                acc[6] = fmaf(wv, h1.z, acc[6]); acc[7] = fmaf(wv, h1.w, acc[7]);
+                acc[8] = fmaf(wv, h2.x, acc[8]); acc[9] = fmaf(wv, h2.y, acc[9]);
+                acc[10] = fmaf(wv, h2.z, acc[10]); acc[11] = fmaf(wv, h2.w, acc[11]);
+                acc[12] = fmaf(wv, h3.x, acc[12]); acc[13] = fmaf(wv, h3.y, acc[13]);
+                acc[14] = fmaf(wv, h3.z, acc[14]); acc[15] = fmaf(wv, h3.w, acc[15]);
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < ADAIN_NB; ++i) part[q][i][lane] = acc[i];
+    __syncthreads();
+    // 64 outputs x nb samples: thread t sums the four partials of (sample t / 64 + 4 k, output t % 64)
+    const float bb = ok && bias ? bias[o] : 0.f;
+    for (int i = q; i < nb; i += 4) {
+        const float v = part[0][i][lane] + part[1][i][lane] + part[2][i][lane] + part[3][i][lane];
+        if (ok) out[(long long)(b0 + i) * out_ns + o] = v + bb;
+    }
+}
+
 // One wave per output channel o; lanes stride over cin (coalesced rows of wsq), each lane keeps
 // the partial sums of up to 16 samples so a wsq row is read once for the whole batch chunk.
 constexpr int DEMOD_NB = 16;
@@ -671,6 +743,11 @@ extern "C" int s2v_adain_params(const float *hid, int batch, int hid_ns, int nhi
                                 s2v_stream_t stream) {
     S2V_REQUIRE(hid && w2t && seg && out && batch > 0 && nhidden > 0 && total > 0 && out_ns >= total,
                 "adain_params: bad args");
+    if (nhidden <= ADAIN_NHMAX) {
+        adain_heads2<<<dim3(cdiv(total, ADAIN_BO), cdiv(batch, ADAIN_NB)), 256, 0, (hipStream_t)stream>>>(
+            hid, batch, hid_ns, nhidden, w2t, bias, seg, total, out, out_ns);
+        return check_launch("adain_heads2");
+    }
     adain_heads<<<dim3(cdiv(total, 256), cdiv(batch, 8)), 256, 0, (hipStream_t)stream>>>(
         hid, batch, hid_ns, nhidden, w2t, bias, seg, total, out, out_ns);
     return check_launch("adain_heads");

@@ -376,11 +376,16 @@ def test_row_layernorm_attention(ctx):
     assert (o.double().cpu() - ref).abs().max() < 1e-5
 
 
-def test_adain_params_and_demod(ctx):
-    b, nh, L = 3, 128, 5
+@pytest.mark.parametrize("b,nh,L,total,contig", [(3, 128, 5, 300, False), (20, 100, 9, 1000, True),
+                                                  (16, 128, 12, 4000, True), (2, 160, 3, 130, False)])
+def test_adain_params_and_demod(ctx, b, nh, L, total, contig):
+    """adain_heads2 (nh <= 128: 64-output blocks, 16-sample chunks, segment windows of 4) and the v1
+    kernel (nh > 128); segments random per output or in contiguous runs as AdainBank lays them out."""
     hid = rnd(b, L * nh, seed=26).float().to(DEV)
-    total = 300
-    seg = torch.randint(0, L, (total,), generator=torch.Generator().manual_seed(0)).int()
+    if contig:
+        seg = (torch.arange(total) * L // total).int()
+    else:
+        seg = torch.randint(0, L, (total,), generator=torch.Generator().manual_seed(0)).int()
     w2 = rnd(total, nh, seed=27).float()
     bias = rnd(total, seed=28).float()
     out = torch.empty(b, total, device=DEV)

@@ -104,7 +104,7 @@ def lnet_ffc(path, k=4):
         if len(rf) < 18:
             continue
         r = rf[-18 + k]
-        ins = [i for i, (n, a, b) in enumerate(ks) if n.startswith("void s2v::in_")]
+        ins = [i for i, (n, a, b) in enumerate(ks) if "s2v::in_" in n.split("(")[0]]
         prev = max(i for i in ins if i < r)
         nxt = min(i for i in ins if i > r)
         t0 = ks[prev][2]
