@@ -266,6 +266,14 @@ int s2v_resize(const float *x, int n, int c, int ih, int iw, long long xsn, long
 int s2v_torgb_up2(const float *x, int n, int h, int w, int c, int xcs, const float *wt, int kpad, const float *s,
                   int s_ns, const float *bias, const float *skip, int skcs, float *y, int ycs, s2v_stream_t stream);
 
+/* Row-tap packing of a small-channel input for a kh x kw conv (r04): y[n][h][w][dx * c + ci] =
+ * x[n][h][w + dx - pw][ci] (zero outside the row), channels [kw * c, ycs) zero; the conv then runs as
+ * a kh x 1 conv over ycs channels with the taps' weights at the same channel positions.  No
+ * reference counterpart (a layout step of this framework's 7x7 first-layer convs: LNet.py:33-34
+ * first_inp / first_ref, DNet.py:93 input_layer, base_blocks.py:267 EditingNet first). */
+int s2v_row_pack(const float *x, int n, int h, int w, int c, int xcs, int kw, int pw, float *y, int ycs,
+                 s2v_stream_t stream);
+
 /* F.pad(mode='reflect') on NHWC (ENet.py:119). */
 int s2v_pad_reflect(const float *x, int n, int h, int w, int c, int xcs, int pt, int pb, int pl, int pr,
                     float *y, int ycs, s2v_stream_t stream);

@@ -75,6 +75,7 @@ _SIGS = {
                                _c_int, _vp, _c_int, _vp]),
     "s2v_resize": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_ll, _c_ll, _c_ll, _c_ll, _vp, _c_int, _c_int,
                             _c_ll, _c_ll, _c_ll, _c_ll, _c_float, _c_float, _c_int, _vp]),
+    "s2v_row_pack": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp]),
     "s2v_pad_reflect": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp,
                                  _c_int, _vp]),
     "s2v_row_layernorm": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _vp, _c_float, _vp, _c_int, _vp]),

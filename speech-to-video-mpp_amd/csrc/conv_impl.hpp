@@ -232,6 +232,15 @@ __device__ __forceinline__ void a_rows_init(const ConvArgs &a, int m0, int ar, A
     a_rows_init_at<AR, AMODE>(a, m0, rows, R);
 }
 
+// pre-activation of 4 gathered values (NONE / RELU / LRELU: max(v, slope v) for slopes in [0, 1])
+__device__ __forceinline__ void pre_act4(const ConvArgs &a, f4 &v) {
+    const float sl = a.pre_act == S2V_ACT_RELU ? 0.f : a.pre_alpha;
+    v.x = v.x >= 0.f ? v.x : v.x * sl;
+    v.y = v.y >= 0.f ? v.y : v.y * sl;
+    v.z = v.z >= 0.f ? v.z : v.z * sl;
+    v.w = v.w >= 0.f ? v.w : v.w * sl;
+}
+
 // prologue of 4 gathered channels [c, c + 4) of tile row j: StyleGAN2 input modulation s[n, c]
 // (zero padding stays zero), then the pre-activation (NONE / RELU / LRELU only on these paths)
 template <int AR, int AMODE>

@@ -99,6 +99,9 @@ __device__ __forceinline__ void split4(const f4 &v, u32x2 &hi, u32x2 &lo) {
 #ifndef X3_MFMA16
 #define X3_MFMA16 1
 #endif
+#ifndef X3_APIPE
+#define X3_APIPE 1
+#endif
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 // one 16x16x32 MFMA on 16-byte fragments holding 8 halves of type ELT each
@@ -341,6 +344,11 @@ __device__ __forceinline__ void conv_x3_tile(const ConvArgs &a, int L, int gx, i
 
     f4 ra[PF][KS][AR];
     int rc[PF][KS];                  // A8: channel base of the staged slice (for the deferred prologue)
+    // input scale s[n, c] (StyleGAN2 modulation with shared weights) loaded with the A operand in issue()
+    // instead of in the store phase, where its load was waited for right away (one memory round trip per
+    // K-slice); only in tiles with register room (the 256-row / 512-row tiles keep the old path)
+    constexpr bool PSC = A8 && BM * BN <= 128 * 128;
+    f4 rsc[PF][KS][PSC ? 2 * AR8 : 1];
     u32x4 rbp[PF][KS][BKN ? 1 : BR];
     f4 rbk[PF][KS][BKN ? BKR : 1];
     constexpr bool M16 = X3_MFMA16;
@@ -371,6 +379,16 @@ __device__ __forceinline__ void conv_x3_tile(const ConvArgs &a, int L, int gx, i
             if constexpr (BUF) {
                 const int c8 = ld.cs * 32 + 8 * (tid & 3);
                 rc[p][u] = c8;
+                if constexpr (PSC) {
+                    if (a.in_scale) {
+#pragma unroll
+                        for (int j = 0; j < AR8; ++j) {
+                            const float *sp = a.in_scale + (long long)R.img[j] * a.in_scale_ns + c8;
+                            rsc[p][u][2 * j] = *(const f4 *)sp;
+                            rsc[p][u][2 * j + 1] = *(const f4 *)(sp + 4);
+                        }
+                    }
+                }
                 const int toff = ((ld.ky * a.dh * a.w + ld.kx * a.dw) * a.xcs + ld.cs * 32) * 4;
 #pragma unroll
                 for (int j = 0; j < AR8; ++j) {
@@ -386,6 +404,16 @@ __device__ __forceinline__ void conv_x3_tile(const ConvArgs &a, int L, int gx, i
                 f4 t0[AR8], t1[AR8];
                 const int c8 = ld.cs * 32 + 8 * (tid & 3);
                 rc[p][u] = c8;
+                if constexpr (PSC) {
+                    if (a.in_scale) {
+#pragma unroll
+                        for (int j = 0; j < AR8; ++j) {
+                            const float *sp = a.in_scale + (long long)R.img[j] * a.in_scale_ns + c8;
+                            rsc[p][u][2 * j] = *(const f4 *)sp;
+                            rsc[p][u][2 * j + 1] = *(const f4 *)(sp + 4);
+                        }
+                    }
+                }
                 load_a_tap<AR8, AMODE, false>(a, x, ld.ky, ld.kx, c8, R, t0);
                 load_a_tap<AR8, AMODE, false>(a, x, ld.ky, ld.kx, c8 + 4, R, t1);
 #pragma unroll
@@ -408,7 +436,16 @@ __device__ __forceinline__ void conv_x3_tile(const ConvArgs &a, int L, int gx, i
         for (int u = 0; u < KS; ++u) {
             char *sb = st + u * SUB;
             if constexpr (A8) {
-                if (a.in_scale || a.pre_act) {
+                if constexpr (PSC) {
+                    if (a.in_scale) {
+#pragma unroll
+                        for (int j = 0; j < 2 * AR8; ++j) ra[p][u][j] *= rsc[p][u][j];
+                    }
+                    if (a.pre_act) {
+#pragma unroll
+                        for (int j = 0; j < 2 * AR8; ++j) pre_act4(a, ra[p][u][j]);
+                    }
+                } else if (a.in_scale || a.pre_act) {
 #pragma unroll
                     for (int j = 0; j < AR8; ++j) {
                         prologue4<AR8, AMODE>(a, R, j, rc[p][u], ra[p][u][2 * j]);
@@ -441,7 +478,16 @@ __device__ __forceinline__ void conv_x3_tile(const ConvArgs &a, int L, int gx, i
             const char *As = st + u * SUB;
             const char *Bs = As + BM * 128;
             if constexpr (M16) {
+                // A fragments double-buffered: row block i + 1 is read from LDS before the MFMAs of row
+                // block i are issued, so its LDS latency hides under them (X3_APIPE; with one buffer
+                // each row block waited lgkmcnt(0) on reads issued after the previous block's MFMAs)
                 u32x4 bh[TN16], bl[TN16];
+                u32x4 ah[X3_APIPE ? 2 : 1], al[X3_APIPE ? 2 : 1];
+                const char *pa = As + (wm * WTM + l16) * 128;
+                if constexpr (X3_APIPE) {
+                    ah[0] = *(const u32x4 *)(pa + hs16);
+                    al[0] = *(const u32x4 *)(pa + ls16);
+                }
 #pragma unroll
                 for (int j = 0; j < TN16; ++j) {
                     const char *p = Bs + (wn * WTN + j * 16 + l16) * 128;
@@ -450,14 +496,21 @@ __device__ __forceinline__ void conv_x3_tile(const ConvArgs &a, int L, int gx, i
                 }
 #pragma unroll
                 for (int i = 0; i < TM16; ++i) {
-                    const char *p = As + (wm * WTM + i * 16 + l16) * 128;
-                    const u32x4 ah = *(const u32x4 *)(p + hs16);
-                    const u32x4 al = *(const u32x4 *)(p + ls16);
+                    const int c = X3_APIPE ? (i & 1) : 0;
+                    if constexpr (X3_APIPE) {
+                        if (i + 1 < TM16) {
+                            ah[c ^ 1] = *(const u32x4 *)(pa + (i + 1) * 16 * 128 + hs16);
+                            al[c ^ 1] = *(const u32x4 *)(pa + (i + 1) * 16 * 128 + ls16);
+                        }
+                    } else {
+                        ah[0] = *(const u32x4 *)(pa + i * 16 * 128 + hs16);
+                        al[0] = *(const u32x4 *)(pa + i * 16 * 128 + ls16);
+                    }
 #pragma unroll
                     for (int j = 0; j < TN16; ++j) {
-                        acc4[i][j] = mfma16x16<ELT>(al, bh[j], acc4[i][j]);
-                        acc4[i][j] = mfma16x16<ELT>(ah, bl[j], acc4[i][j]);
-                        acc4[i][j] = mfma16x16<ELT>(ah, bh[j], acc4[i][j]);
+                        acc4[i][j] = mfma16x16<ELT>(al[c], bh[j], acc4[i][j]);
+                        acc4[i][j] = mfma16x16<ELT>(ah[c], bl[j], acc4[i][j]);
+                        acc4[i][j] = mfma16x16<ELT>(ah[c], bh[j], acc4[i][j]);
                     }
                 }
                 continue;

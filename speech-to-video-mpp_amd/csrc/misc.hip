@@ -165,6 +165,31 @@ __global__ __launch_bounds__(256) void pad_reflect_kernel(const float *__restric
     }
 }
 
+// Row-tap packing for small-channel wide-kernel convs (s2v_row_pack): y[n, h, w, dx * c + ci] =
+// x[n, h, w + dx - pw, ci] (zero outside the row), channels [kw * c, ycs) zero.  A kh x kw conv over
+// c <= 8 channels then runs as a kh x 1 conv over ycs (a multiple of 32) channels on the buffer-load
+// tiles instead of the per-element gather (LNet first_inp / first_ref, DNet input_layer / e_first: 7x7
+// over 3 or 6 channels).  One output channel quad per thread, one float4 store.
+__global__ __launch_bounds__(256) void row_pack_kernel(const float *__restrict__ x, int n, int h, int w, int c,
+                                                       int xcs, int kw, int pw, float *__restrict__ y, int ycs) {
+    const int q4 = ycs >> 2;
+    const long long total = (long long)n * h * w * q4;
+    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+        const int q = (int)(e % q4);
+        const long long pix = e / q4;
+        const int ox = (int)(pix % w);
+        const float *xr = x + (pix - ox) * xcs;            // pixel (n, h, 0) of this row
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int ch = 4 * q + i, dx = ch / c, ci = ch - dx * c;
+            const int ix = ox + dx - pw;
+            v[i] = (dx < kw && (unsigned)ix < (unsigned)w) ? xr[(long long)ix * xcs + ci] : 0.f;
+        }
+        *(float4 *)(y + pix * ycs + 4 * q) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+}
+
 // float4 form (c, pitches % 4 == 0, 16-byte aligned): one channel quad per thread
 __global__ __launch_bounds__(256) void pad_reflect4_kernel(const float *__restrict__ x, int n, int h, int w, int c4,
                                                            int xcs, int pt, int pl, int oh, int ow,
@@ -754,6 +779,17 @@ extern "C" int s2v_resize(const float *x, int n, int c, int ih, int iw, long lon
     resize_kernel<<<grid_for((long long)n * oh * ow * c), 256, 0, (hipStream_t)stream>>>(
         x, n, c, ih, iw, xsn, xsc, xsy, xsx, y, oh, ow, ysn, ysc, ysy, ysx, scale_h, scale_w, mode);
     return check_launch("resize");
+}
+
+extern "C" int s2v_row_pack(const float *x, int n, int h, int w, int c, int xcs, int kw, int pw, float *y, int ycs,
+                            s2v_stream_t stream) {
+    S2V_REQUIRE(x && y && n > 0 && h > 0 && w > 0 && c > 0 && xcs >= c && kw > 0 && pw >= 0,
+                "row_pack: bad args");
+    S2V_REQUIRE(ycs % 4 == 0 && ycs >= kw * c && ((uintptr_t)y & 15) == 0,
+                "row_pack: output pitch must be a multiple of 4 floats holding kw * c channels, 16-byte aligned");
+    row_pack_kernel<<<grid_for((long long)n * h * w * (ycs / 4)), 256, 0, (hipStream_t)stream>>>(
+        x, n, h, w, c, xcs, kw, pw, y, ycs);
+    return check_launch("row_pack");
 }
 
 extern "C" int s2v_pad_reflect(const float *x, int n, int h, int w, int c, int xcs, int pt, int pb, int pl, int pr,

@@ -654,6 +654,15 @@ void resize_(const Tensor &x, int64_t x_off, at::IntArrayRef x_size, at::IntArra
           "s2v_resize");
 }
 
+void row_pack_(const Tensor &x, const Tensor &y, int64_t kw, int64_t pw) {
+    const c10::DeviceGuard guard(x.device());
+    const at::Device dev = x.device();
+    const NV xv = nhwc(x, dev, "row_pack x"), yv = nhwc(y, dev, "row_pack y");
+    TORCH_CHECK(yv.n == xv.n && yv.h == xv.h && yv.w == xv.w && yv.c == yv.cs && yv.c >= kw * xv.c,
+                "row_pack: y must be a dense [n, h, w, >= kw * c] tensor");
+    check(s2v_row_pack(xv.p, xv.n, xv.h, xv.w, xv.c, xv.cs, (int)kw, (int)pw, yv.p, yv.cs, stream()), "s2v_row_pack");
+}
+
 void pad_reflect_(const Tensor &x, const Tensor &y, at::IntArrayRef pads) {
     const c10::DeviceGuard guard(x.device());
     const at::Device dev = x.device();
@@ -911,6 +920,7 @@ TORCH_LIBRARY_FRAGMENT(s2v, m) {
     m.def("resize_(Tensor x, int x_off, int[4] x_size, int[4] x_stride, Tensor(a!) y, int y_off, int[4] y_size, "
           "int[4] y_stride, float scale_h, float scale_w, int mode) -> ()");
     m.def("pad_reflect_(Tensor x, Tensor(a!) y, int[4] pads) -> ()");
+    m.def("row_pack_(Tensor x, Tensor(a!) y, int kw, int pw) -> ()");
     m.def("torgb_up2_(Tensor x, Tensor wt, Tensor s, Tensor? bias, Tensor skip, Tensor(a!) y) -> ()");
     m.def("flow_warp_(Tensor flow, Tensor src, Tensor(a!) y) -> ()");
     m.def("fill_value_(Tensor(a!) y, float value) -> ()");
@@ -943,6 +953,7 @@ TORCH_LIBRARY_IMPL(s2v, CUDA, m) {
     m.impl("attention_", &attention_);
     m.impl("resize_", &resize_);
     m.impl("pad_reflect_", &pad_reflect_);
+    m.impl("row_pack_", &row_pack_);
     m.impl("torgb_up2_", &torgb_up2_);
     m.impl("flow_warp_", &flow_warp_);
     m.impl("fill_value_", &fill_value_);

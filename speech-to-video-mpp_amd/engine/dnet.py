@@ -12,7 +12,7 @@ import torch
 from .. import ops
 from ..ops import NHWC, ConvW
 from .common import AdainBank, make_conv
-from .lnet import ConvNormAct
+from .lnet import ROWPACK, ConvNormAct
 
 LRELU = 0.1  # DNet.py:35, :69, :105
 
@@ -29,6 +29,8 @@ class DNetEngine:
         self.bank = AdainBank(self.desc_nc)
         h = "warpping_net.hourglass."
         self.input_layer = make_conv(sd, h + "encoder.input_layer.", dev, padding=3)
+        if ROWPACK and self.input_layer.cin * self.input_layer.kw <= 64:
+            self.input_layer.make_rowpack(dev)         # 7x7 over the RGB source: row-tap packed 7x1 conv
         self.enc = []
         for i in range(5):
             e = f"{h}encoder.encoder{i}."

@@ -18,14 +18,23 @@ LRELU = 0.1        # LNet.py:91
 LRELU_FFC = 0.01   # FineADAINLama built with nn.LeakyReLU() default (base_blocks.py:369 via :393/:419)
 # FFC products on concurrent side streams (S2V_LNET_BRANCHES=0 serialises them on one stream)
 BRANCHES = os.environ.get("S2V_LNET_BRANCHES", "1") == "1"
-# the FFC's three products that read the block input (conv_to_l, l2g, the spectral branch's st1) as
-# ONE grouped launch (ops.conv_group / s2v_conv2d_group) followed by the spectral chain on the same
-# stream, instead of three side-stream branches whose launches each under-fill the chip
-GROUP = os.environ.get("S2V_LNET_GROUP", "1") == "1"
+# S2V_LNET_GROUP=1: the FFC's three products that read the block input (conv_to_l, l2g, the spectral
+# branch's st1) as ONE grouped launch (ops.conv_group / s2v_conv2d_group) followed by the spectral chain
+# on the same stream, instead of the three side-stream branches.  Measured on MI355X (r04, 3 interleaved
+# pairs): LNet B=16 10.78 ms grouped vs 10.48 ms branched, lipsync 24.31 vs 24.30 ms — the grouped
+# launch serialises the spectral chain behind the two big convs, which the branches overlap — so the
+# branches stay the default (the up2 polyphase classes use the grouped launch, ops.conv2d).
+GROUP = os.environ.get("S2V_LNET_GROUP", "0") == "1"
 # FFC 3x3 reflect convs over a pre-padded input (S2V_LNET_PREPAD=0: reflect addressing in the gather)
 PREPAD = os.environ.get("S2V_LNET_PREPAD", "1") == "1"
 # with PREPAD: the InstanceNorm that ends an FFC writes the next FFC's reflect-padded input itself
 FUSED_PAD = os.environ.get("S2V_LNET_FUSED_PAD", "1") == "1"
+# nearest-x2 UpBlock convs as four parity-class 2x2 convs of the un-upsampled input
+# (ConvW.make_up2_polyphase; S2V_UP2_POLY=0: the upsampling gather of the direct 3x3 conv)
+UP2_POLY = os.environ.get("S2V_UP2_POLY", "1") == "1"
+# 7x7 convs over <= 8 channels as row-tap packed 7x1 convs (ConvW.make_rowpack + ops.row_pack;
+# S2V_ROWPACK=0: the per-element gather of the direct conv)
+ROWPACK = os.environ.get("S2V_ROWPACK", "1") == "1"
 # split-K factor forced on the FourierUnit chain's 1x1 convs (st1, fu, st2); 0 = the planner's choice.  1 (no
 # split-K, no reduce launch on the branch): LNet B=16 11.97 -> 11.69 ms on MI355X (r03), lipsync unchanged
 SPEC_SPLITS = int(os.environ.get("S2V_LNET_SPEC_SPLITS", "1"))
@@ -47,6 +56,10 @@ class ConvNormAct:
     def __init__(self, sd, p, device, k, pool=False, up=False):
         self.conv = make_conv(sd, p + "model.0.", device, padding=k // 2,
                               in_mode=ops.IN_NEAREST_UP2 if up else ops.IN_DIRECT)
+        if up and UP2_POLY and k == 3 and self.conv.cin % 32 == 0:
+            self.conv.make_up2_polyphase(device)      # 4 parity-class 2x2 convs of the un-upsampled input
+        elif not up and ROWPACK and k >= 5 and self.conv.cin * k <= 64:
+            self.conv.make_rowpack(device)            # 7x7 over 3 / 6 channels: row-tap packed kh x 1 conv
         self.ln_w = sd[p + "model.1.weight"].float().reshape(-1).contiguous().to(device)
         self.ln_b = sd[p + "model.1.bias"].float().reshape(-1).contiguous().to(device)
         self.pool = pool

@@ -98,6 +98,9 @@ def prec_code() -> int:
 # where info is the launch's ConvLaunch (kernel plan + shape) and launch() performs the conv; the
 # hook may bracket it with events.
 CONV_HOOK = None
+# nearest-x2 polyphase convs (ConvW.make_up2_polyphase) whose input has at most this many pixels launch
+# their four parity classes as one grouped kernel (conv_group)
+UP2_GROUP_PIXELS = 16 * 48 * 48
 # Optional launch timer (bench.py's roofline of the benchmarked, graph-replayed launches): called as
 # STAMP(info, flops) for every conv launch (info: ConvLaunch); returns None or (stamps, stamp_ctr,
 # [slot, stride, reps]) for the kernel's in-launch clock stamps (s2v_conv_params.stamps).
@@ -342,7 +345,7 @@ class ConvW:
             w = w.transpose(0, 1)
             in_mode = IN_TRANSPOSED
         self.cout, self.cin, self.kh, self.kw = (int(s) for s in w.shape)
-        self._w_oihw = w if in_mode == IN_TRANSPOSED else None
+        self._w_oihw = w if in_mode in (IN_TRANSPOSED, IN_NEAREST_UP2) else None
         self.poly = None
         pair = lambda v: (v, v) if isinstance(v, int) else tuple(v)  # noqa: E731
         self.sh, self.sw = pair(stride)
@@ -423,6 +426,51 @@ class ConvW:
         self.poly = plans
         return self
 
+    # nearest-x2 3x3 fold: source offset a of output parity r collects the conv taps k with F[r][a][k] = 1
+    _UP2_FOLD = (((1, 0, 0), (0, 1, 1)), ((1, 1, 0), (0, 0, 1)))
+
+    def make_up2_polyphase(self, device):
+        """Polyphase plan of a 3x3 stride-1 zero-padded conv over a nearest-x2 upsampled input
+        (IN_NEAREST_UP2: UpBlock2d, models/base_blocks.py:104-118, LNet / DNet decoders).  Output parity
+        class (ry, rx) only reads the 2x2 source pixels its taps land on, so it is a 2x2 conv of the
+        un-upsampled input with the taps that hit one source pixel summed (parity 0: source offsets
+        {-1, 0} with weights {w0, w1 + w2}, padding 1; parity 1: {0, +1} with {w0 + w1, w2}, padding 0),
+        written with output step 2 at offset (ry, rx) like a transposed conv's classes (``poly``).
+        4/9 of the direct conv's multiply-adds, and each class takes the buffer-load A path instead of
+        the per-row upsample gather; the 2x2 tap sums are formed in fp64 and rounded once."""
+        assert self.in_mode == IN_NEAREST_UP2 and (self.kh, self.kw) == (3, 3) and (self.ph, self.pw) == (1, 1)
+        assert (self.sh, self.sw, self.dh, self.dw) == (1, 1, 1, 1) and self.pad_mode == PAD_ZERO
+        f = torch.tensor(self._UP2_FOLD, dtype=torch.float64)
+        w = self._w_oihw.double()
+        plans = []
+        for ry in range(2):
+            for rx in range(2):
+                sub = torch.einsum("ap,bq,oipq->oiab", f[ry], f[rx], w).float()
+                cw = ConvW(sub, None, device, padding=(1 - ry, 1 - rx))
+                cw.scale, cw.shift = self.scale, self.shift
+                plans.append(((ry, rx), cw, (ry, rx)))
+        self.poly = plans
+        return self
+
+    def make_rowpack(self, device):
+        """Row-tap packed form of a kh x kw stride-1 zero-padded conv over c <= 8 channels: the input is
+        packed by ``row_pack`` into kw * c channels (padded to a multiple of 32) and the conv runs as a
+        kh x 1 conv whose weight channel dx * c + ci holds tap (ky, dx) of input channel ci — the same
+        products and sums (in a different order), on the buffer-load tiles instead of the per-element
+        gather that small channel counts otherwise take."""
+        assert self.in_mode == IN_DIRECT and (self.sh, self.sw, self.dh, self.dw) == (1, 1, 1, 1)
+        assert self.pad_mode == PAD_ZERO and self.cin * self.kw <= 64 and 2 * self.pw + 1 == self.kw
+        w = self.wt[: self.cout, : self.K].cpu().reshape(self.cout, self.kh, self.kw, self.cin)   # [o, ky, kx, ci]
+        cp = (self.kw * self.cin + 31) // 32 * 32
+        wp = torch.zeros(self.cout, cp, self.kh, 1)
+        wp[:, : self.kw * self.cin, :, 0] = w.permute(0, 2, 3, 1).reshape(self.cout, self.kw * self.cin, self.kh)
+        cw = ConvW(wp, None, device, padding=(self.ph, 0))
+        cw.scale, cw.shift = self.scale, self.shift
+        self.rowpack = cw
+        return self
+
+    rowpack = None
+
     def out_hw(self, h, w):
         if self.in_mode == IN_TRANSPOSED:
             return ((h - 1) * self.sh - 2 * self.ph + self.dh * (self.kh - 1) + self.oph + 1,
@@ -444,18 +492,30 @@ def conv2d(ctx: Ctx, x: NHWC, cw: ConvW, y: NHWC, *, act=ACT_NONE, alpha=0.0, re
     device tensors.  A transposed ConvW with a polyphase plan (``cw.poly``) runs as one stride-1 conv
     per output parity class, each writing every second pixel of y.  ``pool``: y is the 2x2 average
     pool of the activated conv output (half the conv's size)."""
+    if cw.rowpack is not None:
+        # small-channel wide-kernel conv: row-tap packed input, kh x 1 conv over the packed channels
+        assert x.c == cw.cin, f"conv: input has {x.c} channels, weights expect {cw.cin}"
+        assert in_scale is None, "row-packed conv: no input scale"
+        xp = NHWC.empty(x.n, x.h, x.w, cw.rowpack.cin, x.t.device)
+        row_pack(ctx, x, xp, cw.kw, cw.pw)
+        return conv2d(ctx, xp, cw.rowpack, y, act=act, alpha=alpha, res=res, res_after=res_after, res_offset=res_offset,
+                      nc_scale=nc_scale, in_scale=None, pre_act=pre_act, pre_alpha=pre_alpha, pix_add=pix_add,
+                      pix_w=pix_w, scale=scale, shift=shift, force_tile=force_tile, force_splits=force_splits, pool=pool)
     if getattr(cw, "poly", None) is not None:
         assert pix_add is None, "polyphase transposed conv: no pix_add epilogue"
         assert res is None or (res.t.data_ptr() == y.t.data_ptr() and res.coff == y.coff and not res_after), \
             "polyphase transposed conv: only an in-place residual (res is the output view)"
         oh, ow = cw.out_hw(x.h, x.w)
         assert (y.n, y.h, y.w, y.c) == (x.n, oh, ow, cw.cout), "conv_transpose: output view mismatch"
-        for (ry, rx), sub, _ in cw.poly:
-            if (oh - ry + 1) // 2 <= 0 or (ow - rx + 1) // 2 <= 0:
-                continue
-            yc = y.t[:, ry::2, rx::2, y.coff: y.coff + y.c]          # one output parity class
-            _conv(ctx, x, sub, yc, 2, act, alpha, yc if res is not None else None, False, (0, 0), nc_scale,
-                  in_scale, pre_act, pre_alpha, None, 0.0, scale, shift, force_tile, force_splits)
+        # the four classes of a small nearest-x2 conv (LNet's decoder up convs) as one grouped launch
+        grouped = cw.in_mode == IN_NEAREST_UP2 and x.n * x.h * x.w <= UP2_GROUP_PIXELS and not force_tile
+        with conv_group(ctx, enabled=grouped):
+            for (ry, rx), sub, _ in cw.poly:
+                if (oh - ry + 1) // 2 <= 0 or (ow - rx + 1) // 2 <= 0:
+                    continue
+                yc = y.t[:, ry::2, rx::2, y.coff: y.coff + y.c]          # one output parity class
+                _conv(ctx, x, sub, yc, 2, act, alpha, yc if res is not None else None, False, (0, 0), nc_scale,
+                      in_scale, pre_act, pre_alpha, None, 0.0, scale, shift, force_tile, force_splits)
         return y
     oh, ow = cw.out_hw(x.h, x.w)
     assert x.c == cw.cin, f"conv: input has {x.c} channels, weights expect {cw.cin}"
@@ -898,6 +958,12 @@ def torgb_up2(ctx: Ctx, x: NHWC, cw: "ConvW", s: torch.Tensor, skip: NHWC, y: NH
     assert cw.kh == cw.kw == 1 and cw.cout == 3 and x.c == cw.cin, "torgb_up2: a 1x1 conv to 3 channels"
     assert (y.n, y.h, y.w, y.c) == (x.n, x.h, x.w, 4) and (skip.n, 2 * skip.h, 2 * skip.w, skip.c) == (x.n, x.h, x.w, 4)
     S2V.torgb_up2_(x.v, cw.wt, s, cw.shift, skip.v, y.v)
+    return y
+
+
+def row_pack(ctx: Ctx, x: NHWC, y: NHWC, kw: int, pw: int):
+    """y[n, h, w, dx * c + ci] = x[n, h, w + dx - pw, ci] (zero outside the row and past kw * c)."""
+    S2V.row_pack_(x.v, y.v, kw, pw)
     return y
 
 

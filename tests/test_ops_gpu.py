@@ -800,3 +800,65 @@ def _params_of(ctx, x, cw, y):
     p.wt_x3 = cw.wt_x3(ctx, p.prec).data_ptr()
     p.batch = 1
     return p
+
+
+@pytest.mark.parametrize("sprec", ["f16x3", "bf16x3", "f32"])
+@pytest.mark.parametrize("n,h,w,cin,cout", [(2, 12, 12, 256, 64), (1, 20, 17, 64, 96), (4, 48, 48, 64, 32)])
+def test_conv_up2_polyphase_matches_reference(ctx, sprec, n, h, w, cin, cout):
+    """ConvW.make_up2_polyphase (UpBlock2d: nearest x2 then 3x3 zero-padded conv) as four parity-class 2x2
+    convs of the un-upsampled input, grouped into one launch for small inputs, against fp64
+    F.interpolate(nearest) + F.conv2d with bias: the whole output including the zero-padded borders
+    and odd / even image sizes."""
+    x = rnd(n, cin, h, w, seed=81)
+    wt = rnd(cout, cin, 3, 3, seed=82) / math.sqrt(cin * 9)
+    b = rnd(cout, seed=83)
+    cw = ConvW(wt.float(), b.float(), DEV, padding=1, in_mode=ops.IN_NEAREST_UP2).make_up2_polyphase(DEV)
+    prev = ops.set_precision(sprec)
+    try:
+        y = NHWC.empty(n, 2 * h, 2 * w, cout, DEV)
+        ops.conv2d(ctx, nhwc(x.float()), cw, y)
+        torch.cuda.synchronize()
+        grouped = ops.LAST_GROUP
+    finally:
+        ops.set_precision(prev)
+    xu = F.interpolate(x, scale_factor=2, mode="nearest")
+    ref = F.conv2d(xu, wt, b, padding=1)
+    err = (to_nchw(y) - ref).abs()
+    bound = conv_bound(xu, wt, 1, 1, 1)
+    assert (err <= REL[sprec] * (bound + 1) + 1e-6).all(), f"max err {err.max():.3e}"
+    if sprec != "f32" and n * h * w <= ops.UP2_GROUP_PIXELS:
+        assert grouped == 1                                # the four classes went out as one grouped launch
+
+
+@pytest.mark.parametrize("sprec", ["f16x3", "bf16x3", "f32"])
+@pytest.mark.parametrize("n,h,w,cin,cout,k,sl", [(2, 20, 23, 3, 64, 7, True), (3, 17, 16, 6, 64, 7, False),
+                                                 (1, 9, 9, 8, 32, 5, False)])
+def test_conv_rowpack_matches_reference(ctx, sprec, n, h, w, cin, cout, k, sl):
+    """ConvW.make_rowpack (7x7 / 5x5 over <= 8 channels as a kh x 1 conv over row-tap packed channels,
+    ops.row_pack) with bias + LeakyReLU, on a channel slice of a wider tensor (LNet's face6[..., :3]) or a
+    dense input, against fp64 F.conv2d; and row_pack's layout itself (zero past the row and past kw*c)."""
+    xt = rnd(n, 2 * cin if sl else cin, h, w, seed=91)
+    wt = rnd(cout, cin, k, k, seed=92) / math.sqrt(cin * k * k)
+    b = rnd(cout, seed=93)
+    cw = ConvW(wt.float(), b.float(), DEV, padding=k // 2).make_rowpack(DEV)
+    xv = nhwc(xt.float())
+    xin = xv.slice(cin, cin) if sl else xv
+    xr = xt[:, cin:] if sl else xt
+    prev = ops.set_precision(sprec)
+    try:
+        y = NHWC.empty(n, h, w, cout, DEV)
+        ops.conv2d(ctx, xin, cw, y, act=ops.ACT_LRELU, alpha=0.1)
+        packed = NHWC.empty(n, h, w, cw.rowpack.cin, DEV)
+        ops.row_pack(ctx, xin, packed, k, k // 2)
+        torch.cuda.synchronize()
+    finally:
+        ops.set_precision(prev)
+    ref = F.leaky_relu(F.conv2d(xr, wt, b, padding=k // 2), 0.1)
+    err = (to_nchw(y) - ref).abs()
+    bound = conv_bound(xr, wt, 1, k // 2, 1)
+    assert (err <= REL[sprec] * (bound + 1) + 1e-6).all(), f"max err {err.max():.3e}"
+    xp = F.pad(xr, (k // 2, k // 2))                                    # [n, c, h, w + k - 1]
+    want = torch.zeros(n, h, w, cw.rowpack.cin, dtype=torch.float64)
+    for dx in range(k):
+        want[..., dx * cin:(dx + 1) * cin] = xp[:, :, :, dx:dx + w].permute(0, 2, 3, 1)
+    assert torch.equal(packed.t.double().cpu(), want.float().double())
