@@ -705,22 +705,22 @@ static void launch_small(const ConvArgs &a, int batch, bool cpar, hipStream_t s)
 
 
 // Halo-tiled direct conv for Cout <= 4 heads with a wide square filter (DNet's 7x7 64 -> 3 tanh
-// head at 256^2, LNet's 7x7 64 -> 3 sigmoid head): a block owns an 8 x 128 output tile; per chunk
-// of 4 input channels it stages the (8 + KS - 1) x (128 + KS - 1) input halo once in LDS (planar
-// per channel), and each thread computes 4 horizontally adjacent pixels x CO outputs from 16-byte
-// LDS row reads, so every staged value feeds up to 4 * KS taps.  The per-pixel gather of
-// conv_small_cpar re-read each input pixel KS^2 times from L1/L2 (DNet head: 1.5 ms per 16 frames
-// at 185 GB/s).  Filter values are block-uniform (scalar loads).  fp32 VALU, exact products.
-#ifndef HALO_SMALL
-#define HALO_SMALL 1
-#endif
-template <int CO, int KS>
+// head at 256^2, LNet's 7x7 64 -> 4 sigmoid head): a block owns an 8 x (32 PX) output tile; per chunk
+// of CC input channels it stages the (8 + KS - 1) x (32 PX + KS - 1) input halo once in LDS (planar per
+// channel), and each thread computes PX horizontally adjacent pixels x CO outputs from 16-byte LDS
+// row reads, so every staged value feeds up to PX * KS taps.  CC = 16 (r04): each staged pixel is one
+// 64-byte piece of its channel row, so consecutive chunks do not re-fetch a line they share (with
+// 4-channel chunks the 256^2 DNet head read 3.8 GB from HBM for 0.27 GB of input, 573 us).  Filter
+// values are block-uniform (scalar loads).  fp32 VALU, exact products.
+template <int CO, int KS, int CC = 16, int PX = 2>
 __global__ __launch_bounds__(256) void conv_halo_small(ConvArgs a, int tiles_x, int tiles_y) {
-    constexpr int TH = 8, PX = 4, TW = 32 * PX;
+    constexpr int TH = 8, TW = 32 * PX;
     constexpr int IH = TH + KS - 1, IW = TW + KS - 1, IWP = (IW + 3) / 4 * 4;
-    constexpr int NV = (PX + KS - 1 + 3) / 4;                 // float4 row reads per (channel, ky)
-    static_assert(4 * 31 + 4 * NV <= IWP, "halo row reads stay inside the padded LDS row");
-    __shared__ __attribute__((aligned(16))) float tile[4][IH][IWP];
+    constexpr int NR2 = (PX + KS - 1 + 1) / 2;               // float2 row reads per (channel, ky)
+    constexpr int CQ = CC / 4;
+    static_assert(PX * 31 + 2 * NR2 <= IWP, "halo row reads stay inside the padded LDS row");
+    static_assert(PX % 2 == 0 || PX == 1, "row reads start 8-byte aligned");
+    __shared__ __attribute__((aligned(16))) float tile[CC][IH][IWP];
     const int tid = threadIdx.x, r = tid >> 5, cg = tid & 31;
     int t = blockIdx.x;
     const int txi = t % tiles_x;
@@ -738,10 +738,12 @@ __global__ __launch_bounds__(256) void conv_halo_small(ConvArgs a, int tiles_x, 
 #pragma unroll
         for (int o = 0; o < CO; ++o) acc[p][o] = 0.f;
     const bool refl = a.pad_mode == S2V_PAD_REFLECT;
-    for (int c0 = cb; c0 < ce; c0 += 4) {
+    for (int c0 = cb; c0 < ce; c0 += CC) {
+        const int nq = min(CQ, (ce - c0) / 4);
         __syncthreads();                                      // the previous chunk has been consumed
-        for (int e = tid; e < IH * IW; e += 256) {
-            const int iy = e / IW, ix = e - iy * IW;
+        for (int e = tid; e < IH * IW * CQ; e += 256) {
+            const int q = e % CQ, px = e / CQ;
+            const int iy = px / IW, ix = px - iy * IW;
             int gy = oy0 + iy - a.ph, gx = ox0 + ix - a.pw;
             if (refl) {
                 gy = reflect_idx(gy, a.h);
@@ -749,23 +751,22 @@ __global__ __launch_bounds__(256) void conv_halo_small(ConvArgs a, int tiles_x, 
             }
             // halo rows / columns past the image (tiles overhanging the bottom / right edge, or
             // beyond a single reflection) feed only outputs that are never stored
-            const bool ok = (unsigned)gy < (unsigned)a.h && (unsigned)gx < (unsigned)a.w;
+            const bool ok = q < nq && (unsigned)gy < (unsigned)a.h && (unsigned)gx < (unsigned)a.w;
             f4 v = f4{0.f, 0.f, 0.f, 0.f};
-            if (ok) v = *(const f4 *)(xb + ((long long)gy * a.w + gx) * a.xcs + c0);
-            tile[0][iy][ix] = v.x;
-            tile[1][iy][ix] = v.y;
-            tile[2][iy][ix] = v.z;
-            tile[3][iy][ix] = v.w;
+            if (ok) v = *(const f4 *)(xb + ((long long)gy * a.w + gx) * a.xcs + c0 + 4 * q);
+            tile[4 * q + 0][iy][ix] = v.x;
+            tile[4 * q + 1][iy][ix] = v.y;
+            tile[4 * q + 2][iy][ix] = v.z;
+            tile[4 * q + 3][iy][ix] = v.w;
         }
         __syncthreads();
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
+        for (int c = 0; c < 4 * nq; ++c) {
 #pragma unroll
             for (int ky = 0; ky < KS; ++ky) {
-                float row[4 * NV];
-                const float *src = &tile[c][r + ky][4 * cg];
+                float row[2 * NR2];
+                const float *src = &tile[c][r + ky][PX * cg];
 #pragma unroll
-                for (int j = 0; j < NV; ++j) *(f4 *)&row[4 * j] = *(const f4 *)(src + 4 * j);
+                for (int j = 0; j < NR2; ++j) *(float2 *)&row[2 * j] = *(const float2 *)(src + 2 * j);
 #pragma unroll
                 for (int kx = 0; kx < KS; ++kx) {
                     const long long k = (long long)(ky * KS + kx) * a.cin + c0 + c;
@@ -784,7 +785,7 @@ __global__ __launch_bounds__(256) void conv_halo_small(ConvArgs a, int tiles_x, 
     if (oy >= a.oh) return;
 #pragma unroll
     for (int p = 0; p < PX; ++p) {
-        const int ox = ox0 + 4 * cg + p;
+        const int ox = ox0 + PX * cg + p;
         if (ox >= a.ow) continue;
         const int m = (img * a.oh + oy) * a.ow + ox;
         if (a.splits > 1) {
@@ -827,6 +828,8 @@ static int plan_cus() { return device_cus() > 0 ? device_cus() : 256; }
 
 long long tune_get(int key) { return tune_value(key); }
 
+constexpr int kHaloTW = 64;              // conv_halo_small output tile width (32 PX, PX = 2)
+
 static int halo_ks(const s2v_conv_params *p) {
     const int batch = p->batch > 0 ? p->batch : 1;
     if (p->cout > 4 || p->kh != p->kw || (p->kh != 3 && p->kh != 5 && p->kh != 7)) return 0;
@@ -837,14 +840,14 @@ static int halo_ks(const s2v_conv_params *p) {
     // 8 x 128 output tiles: on small images (LNet's 96^2 RGB head, DNet's 64^2 flow head) too few
     // blocks cover the chip and a 128-wide tile runs part empty; the channel-parallel kernel (lanes
     // split K per pixel) has the parallelism there.  S2V_HALO_MIN_BLOCKS overrides (tuning).
-    const long long blocks = (long long)p->n * cdiv(p->ow, 128) * cdiv(p->oh, 8);
+    const long long blocks = (long long)p->n * cdiv(p->ow, kHaloTW) * cdiv(p->oh, 8);
     if (blocks < tune_value(S2V_TUNE_HALO_MIN_BLOCKS)) return 0;
     return p->kh;
 }
 
 // channel splits of the halo kernel: about three blocks per CU, at least 8 channels per split
 static int halo_splits(const s2v_conv_params *p, int &per) {
-    const long long blocks = (long long)p->n * cdiv(p->ow, 128) * cdiv(p->oh, 8);
+    const long long blocks = (long long)p->n * cdiv(p->ow, kHaloTW) * cdiv(p->oh, 8);
     const int cus = plan_cus();
     const int quads = p->cin / 4;
     int s = blocks >= 3LL * cus ? 1 : (int)((3LL * cus + blocks - 1) / blocks);
@@ -856,7 +859,7 @@ static int halo_splits(const s2v_conv_params *p, int &per) {
 
 template <int CO>
 static void launch_halo(const ConvArgs &a, int ks, hipStream_t s) {
-    const int tiles_x = (int)cdiv(a.ow, 128), tiles_y = (int)cdiv(a.oh, 8);
+    const int tiles_x = (int)cdiv(a.ow, kHaloTW), tiles_y = (int)cdiv(a.oh, 8);
     const dim3 grid((unsigned)((long long)a.n * tiles_x * tiles_y), (unsigned)a.splits);
     if (ks == 3) conv_halo_small<CO, 3><<<grid, 256, 0, s>>>(a, tiles_x, tiles_y);
     else if (ks == 5) conv_halo_small<CO, 5><<<grid, 256, 0, s>>>(a, tiles_x, tiles_y);
@@ -1099,7 +1102,7 @@ static Plan make_plan(const s2v_conv_params *p_in, int M, int K) {
         pl.tile = -1;
         pl.splits = 1;
         pl.tps = pl.ktiles;
-        if (HALO_SMALL && halo_ks(p)) pl.splits = halo_splits(p, pl.tps);   // tps: channels per split
+        if (halo_ks(p)) pl.splits = halo_splits(p, pl.tps);   // tps: channels per split
         return pl;
     }
     int tppx, qpt;
@@ -1533,7 +1536,7 @@ extern "C" int s2v_conv2d_plan(const s2v_conv_params *p, int *out6) {
         out6[4] = p->cin == 4 && p->kh == p->kw && (p->kh == 1 || p->kh == 3) ? 2000 + p->kh * p->kw : 0;
         return 0;
     }
-    if (pl.tile < 0 && HALO_SMALL && halo_ks(p)) {
+    if (pl.tile < 0 && halo_ks(p)) {
         out6[0] = 0; out6[1] = p->cout < 4 ? p->cout : 4;
         out6[2] = 0; out6[3] = 0;
         out6[4] = 1000 + halo_ks(p); out6[5] = pl.splits;  // conv_halo_small<CO, KS>
@@ -1588,7 +1591,7 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
         else conv_smallk<2, 1><<<grid, 256, lds, s>>>(a, batch, tppx, iters, vec);
         return check_launch("conv_smallk");
     }
-    if (pl.tile < 0 && HALO_SMALL && halo_ks(p)) {
+    if (pl.tile < 0 && halo_ks(p)) {
         if (pl.splits > 1) {
             const size_t need = (size_t)pl.splits * (size_t)M * p->cout * sizeof(float);
             if (!p->ws || p->ws_bytes < need) {

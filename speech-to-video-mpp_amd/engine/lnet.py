@@ -29,6 +29,9 @@ GROUP = os.environ.get("S2V_LNET_GROUP", "0") == "1"
 PREPAD = os.environ.get("S2V_LNET_PREPAD", "1") == "1"
 # with PREPAD: the InstanceNorm that ends an FFC writes the next FFC's reflect-padded input itself
 FUSED_PAD = os.environ.get("S2V_LNET_FUSED_PAD", "1") == "1"
+# S2V_LNET_HALVES=k (k >= 1): batches of >= 2k frames run as two concurrent half-batch forwards (two
+# chains of latency-bound kernels side by side instead of one chain of twice-as-wide kernels)
+HALVES = int(os.environ.get("S2V_LNET_HALVES", "0"))
 # nearest-x2 UpBlock convs as four parity-class 2x2 convs of the un-upsampled input
 # (ConvW.make_up2_polyphase; S2V_UP2_POLY=0: the upsampling gather of the direct 3x3 conv)
 UP2_POLY = os.environ.get("S2V_UP2_POLY", "1") == "1"
@@ -304,7 +307,25 @@ class LNetEngine:
                 pad_rgb: bool = False):
         """audio: [B,1,80,16] device tensor; face6: NHWC [B,96,96,6] = [masked | ref];
         out: NHWC [B,96,96,3] receives sigmoid(final conv) ([B,96,96,4] with a 4th constant channel
-        when ``pad_rgb``)."""
+        when ``pad_rgb``).  With HALVES the two halves of the batch run as two concurrent forwards (the
+        second on a side stream with its own Ctx: workspaces, FFC branch streams)."""
+        b = face6.n
+        side = ctx.streams(("lnet-half", id(self)), 1) if HALVES and b >= 2 * HALVES else None
+        if side is None:
+            return self._forward(ctx, audio, face6, out, logits, pad_rgb)
+        h = b // 2
+        rows = lambda v, a, z: None if v is None else NHWC(v.t[a:z], v.coff, v.c)  # noqa: E731
+        st, c2 = side[0]
+        cur = torch.cuda.current_stream(self.device)
+        st.wait_stream(cur)
+        with ops.side_stream(st, ctx.keep):
+            self._forward(c2, audio[h:], rows(face6, h, b), rows(out, h, b), rows(logits, h, b), pad_rgb)
+        self._forward(ctx, audio[:h], rows(face6, 0, h), rows(out, 0, h), rows(logits, 0, h), pad_rgb)
+        cur.wait_stream(st)
+        return out
+
+    def _forward(self, ctx, audio: torch.Tensor, face6: NHWC, out: NHWC, logits: NHWC | None = None,
+                 pad_rgb: bool = False):
         dev = self.device
         b = face6.n
         # ---- visual encoder (LNet.py:30-43) and audio encoder (LNet.py:102-120): the masked-face

@@ -150,7 +150,9 @@ def side_stream(stream, keep: list):
     corruption (tests/test_lanes_gpu.py).  Allocated on the capture stream they are graph-owned;
     kept alive to the join they are never reused while the branch still reads them."""
     prev = getattr(_SIDE, "v", None)
-    _SIDE.v = (torch.cuda.current_stream(), keep)
+    # nested branches (a branch forking its own side streams) still allocate from the outermost calling
+    # stream, the one the capture runs on
+    _SIDE.v = (prev[0] if prev is not None else torch.cuda.current_stream(), keep)
     try:
         with torch.cuda.stream(stream):
             yield
@@ -308,6 +310,7 @@ class Ctx:
             self._streams[key] = [(torch.cuda.Stream(self.device), Ctx(self.device)) for _ in range(n)]
             for _, c in self._streams[key]:
                 c.parent = self
+                c.keep = self.keep      # branch tensors live until the lane's next forward, like the lane's own
         assert len(self._streams[key]) >= n
         return self._streams[key][:n]
 

@@ -82,6 +82,10 @@ class LipSyncPipeline:
                  ref_hook=None):
         self.dnet, self.enet = dnet, enet
         self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:
+            # the modules key their per-device engines (and lane flags, _lane_flags) by the inputs'
+            # device, which always carries an index
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.batch = batch
         self.ctx = Ctx(self.device)
         self.graph = graph          # full batches of ``run`` replay captured HIP graphs

@@ -92,7 +92,7 @@ CONV_CASES = [
     (2, 32, 8, 8, 48, 3, 1, 1, 1, "up2", "zero", 0, 0),
     (2, 64, 6, 7, 32, 3, 2, 1, 1, "transposed", "zero", 0, 0),
     (2, 64, 9, 9, 3, 7, 1, 3, 1, "direct", "zero", 0, 0),     # direct small-N kernel
-    # halo-tiled small-Cout kernel (8 x 128 output tiles): ragged tiles in both directions, reflect
+    # halo-tiled small-Cout kernel (8 x 64 output tiles, 16-channel chunks): ragged tiles in both directions, reflect
     # halos, 3 / 5 / 7 filters, 1..4 outputs (DNet's 7x7 64 -> 3 head at 256^2 is the model case);
     # rows with w >= 96 run it with the planner's block-count floor off (halo_everywhere)
     (2, 64, 37, 150, 3, 7, 1, 3, 1, "direct", "zero", 0, 0),
