@@ -890,8 +890,8 @@ static const X3Cfg kX3Tiles[] = {
     {{256, 256, 2, 8, 1, 1}, 400.f, 1, 0}, {{128, 128, 2, 8, 1, 1}, 330.f, 2, 0}, {{64, 128, 2, 8, 1, 1}, 260.f, 3, 0},
     {{128, 64, 2, 4, 1, 1}, 290.f, 3, 0},  {{64, 64, 2, 4, 1, 1}, 265.f, 4, 0},   {{128, 32, 4, 4, 1, 1}, 235.f, 4, 0},
     {{256, 128, 4, 8, 1, 1}, 335.f, 1, 0}, {{256, 64, 8, 8, 1, 1}, 300.f, 2, 0},  {{512, 128, 4, 8, 1, 1}, 360.f, 1, 0},
-    // two K-slice groups in flight (PF 2) for the 4-wave tiles: forced-only (tflops 0) until measured
-    {{128, 64, 2, 4, 1, 2}, 0.f, 3, 0},    {{64, 64, 2, 4, 1, 2}, 0.f, 4, 0},     {{128, 32, 4, 4, 1, 2}, 0.f, 4, 0},
+    // narrow-N tiles with 64-row waves (r04): forced-only (tflops 0) until measured
+    {{512, 64, 8, 8, 1, 1}, 0.f, 1, 0},    {{256, 64, 4, 4, 1, 1}, 0.f, 2, 0},    {{256, 32, 4, 4, 1, 1}, 0.f, 2, 0},
     // LDS-DMA ring kernels (force_tile 13..18): forced-only until measured
     {{64, 64, 4, 4, 0, 6}, 0.f, 1, 1},     {{128, 64, 4, 4, 0, 5}, 0.f, 1, 2},    {{64, 128, 4, 4, 0, 5}, 0.f, 1, 3},
     {{128, 128, 4, 4, 0, 4}, 0.f, 1, 4},   {{64, 32, 4, 4, 0, 8}, 0.f, 1, 5},     {{128, 32, 4, 4, 0, 6}, 0.f, 1, 6}};

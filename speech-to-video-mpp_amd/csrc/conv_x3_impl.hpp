@@ -347,7 +347,7 @@ __device__ __forceinline__ void conv_x3_tile(const ConvArgs &a, int L, int gx, i
     // input scale s[n, c] (StyleGAN2 modulation with shared weights) loaded with the A operand in issue()
     // instead of in the store phase, where its load was waited for right away (one memory round trip per
     // K-slice); only in tiles with register room (the 256-row / 512-row tiles keep the old path)
-    constexpr bool PSC = A8 && BM * BN <= 128 * 128;
+    constexpr bool PSC = A8 && (BM * BN <= 128 * 128 || (BN == 64 && AR8 <= 4));
     f4 rsc[PF][KS][PSC ? 2 * AR8 : 1];
     u32x4 rbp[PF][KS][BKN ? 1 : BR];
     f4 rbk[PF][KS][BKN ? BKR : 1];
@@ -715,9 +715,11 @@ int launch_conv_x3(int cfg, const ConvArgs &a, int amode, bool bkn, dim3 grid, h
         case 6: launch_x3<256, 128, 4, 8, 1, 1, ELT>(a, amode, bkn, grid, s); break;
         case 7: launch_x3<256, 64, 8, 8, 1, 1, ELT>(a, amode, bkn, grid, s); break;
         case 8: launch_x3<512, 128, 4, 8, 1, 1, ELT>(a, amode, bkn, grid, s); break;   // N = 128 layers
-        case 9: launch_x3<128, 64, 2, 4, 1, 2, ELT>(a, amode, bkn, grid, s); break;
-        case 10: launch_x3<64, 64, 2, 4, 1, 2, ELT>(a, amode, bkn, grid, s); break;
-        default: launch_x3<128, 32, 4, 4, 1, 2, ELT>(a, amode, bkn, grid, s); break;
+        // narrow-N tiles whose waves each cover 64 rows (r04): fewer LDS operand reads per MFMA than the
+        // 256x64 / 128x32 tiles (A fragments reused over all of N): 64-channel layers at 256^2 / 512^2
+        case 9: launch_x3<512, 64, 8, 8, 1, 1, ELT>(a, amode, bkn, grid, s); break;
+        case 10: launch_x3<256, 64, 4, 4, 1, 1, ELT>(a, amode, bkn, grid, s); break;
+        default: launch_x3<256, 32, 4, 4, 1, 1, ELT>(a, amode, bkn, grid, s); break;
     }
     return 0;
 }

@@ -125,6 +125,14 @@ CONV_CASES = [
     # bf16x3 256x64 8-wave tile (force_tile 8: large-M, 64-channel layers)
     (2, 64, 20, 18, 64, 3, 1, 1, 1, "direct", "reflect", 8, 0),
     (1, 32, 17, 23, 40, 3, 2, 1, 1, "direct", "zero", 8, 3),
+    # narrow-N tiles with 64-row waves (force_tile 10 / 11 / 12: 512x64 8-wave, 256x64 and 256x32 4-wave):
+    # ragged M / N tails, split-K, reflect padding (per-row gather), up2
+    (2, 64, 23, 29, 64, 3, 1, 1, 1, "direct", "zero", 10, 0),
+    (1, 96, 19, 21, 40, 3, 1, 1, 1, "direct", "reflect", 10, 3),
+    (2, 64, 17, 15, 64, 3, 1, 1, 1, "direct", "zero", 11, 2),
+    (2, 32, 9, 10, 48, 3, 1, 1, 1, "up2", "zero", 11, 0),
+    (2, 64, 20, 18, 32, 3, 1, 1, 1, "direct", "zero", 12, 0),
+    (1, 128, 13, 17, 24, 3, 2, 1, 1, "direct", "zero", 12, 4),
     # LDS-DMA ring tiles (force_tile 13..18, conv_ring_x3: split-precision, AMODE-0 convs only):
     # ragged M / N tails, split-K, stride 2, dilation, 1x1, valid (pre-padded) 3x3
     (2, 64, 17, 19, 96, 3, 1, 1, 1, "direct", "zero", 13, 0),
@@ -289,14 +297,21 @@ def test_modulated_conv_per_sample_weights(ctx, prec, n, cin, h, w, cout, k, mod
     assert (err <= 2 * REL[prec] * bound + 1e-6).all(), f"max err {err.max():.3e}"
 
 
-def test_conv2d_prologue(ctx, prec):
-    n, cin, h, w, cout = 2, 32, 10, 10, 64
+@pytest.mark.parametrize("tile", [0, 4, 5, 6, 8, 9, 10, 11, 12])
+def test_conv2d_prologue(ctx, prec, tile):
+    """Input scale s[n, c] + pre-activation prologue on every tile family: the small tiles load s with
+    the A operand (issue), the wide ones in the store phase; 3 images of 10x10 so one tile spans
+    several images (per-row image index)."""
+    if prec == "f32" and tile > 6:
+        pytest.skip("the f32 table has 6 tiles")
+    n, cin, h, w, cout = 3, 64, 10, 10, 64
     wt = rnd(cout, cin, 3, 3, seed=7) / math.sqrt(cin * 9)
     x = rnd(n, cin, h, w, seed=8)
     s = rnd(n, cin, seed=9, lo=0.5, hi=2.0)
     cw = ConvW(wt.float(), None, DEV, padding=1)
     y = NHWC.empty(n, h, w, cout, DEV)
-    ops.conv2d(ctx, nhwc(x.float()), cw, y, in_scale=s.float().to(DEV), pre_act=ops.ACT_LRELU, pre_alpha=0.1)
+    ops.conv2d(ctx, nhwc(x.float()), cw, y, in_scale=s.float().to(DEV), pre_act=ops.ACT_LRELU, pre_alpha=0.1,
+               force_tile=tile)
     ref = F.conv2d(F.leaky_relu(x * s[:, :, None, None], 0.1), wt, padding=1)
     bound = conv_bound(F.leaky_relu(x * s[:, :, None, None], 0.1), wt, 1, 1, 1)
     assert ((to_nchw(y) - ref).abs() <= 2 * REL[prec] * (bound + 1) + 1e-6).all()
