@@ -18,6 +18,12 @@ LRELU = 0.1        # LNet.py:91
 LRELU_FFC = 0.01   # FineADAINLama built with nn.LeakyReLU() default (base_blocks.py:369 via :393/:419)
 # FFC products on concurrent side streams (S2V_LNET_BRANCHES=0 serialises them on one stream)
 BRANCHES = os.environ.get("S2V_LNET_BRANCHES", "1") == "1"
+# FFC branches: the spectral chain st1 -> rfft -> fu -> irfft (the longest) on the calling stream and
+# conv_to_l / l2g on the side streams (S2V_LNET_SPEC_MAIN=0: conv_to_l on the calling stream).  A
+# kernel that waits on another stream's kernel starts ~12 us after it ends in the replayed graph
+# (profiles/r04 LNet FFC dumps: st2 after the side-stream irfft), so the chain that ends last
+# should not cross streams before st2.
+SPEC_MAIN = os.environ.get("S2V_LNET_SPEC_MAIN", "1") == "1"
 # S2V_LNET_GROUP=1: the FFC's three products that read the block input (conv_to_l, l2g, the spectral
 # branch's st1) as ONE grouped launch (ops.conv_group / s2v_conv2d_group) followed by the spectral chain
 # on the same stream, instead of the three side-stream branches.  Measured on MI355X (r04, 3 interleaved
@@ -219,6 +225,11 @@ class FFCLama:
             ops.conv2d(ctx, xr, self.conv_to_l, y.slice(0, cl), force_splits=fs_c2l)
             l2g(ctx)
             spectral(ctx)
+        elif SPEC_MAIN:
+            # the spectral chain (the FFC's critical path) on the calling stream: no cross-stream
+            # dependency between its kernels and st2 / the InstanceNorm after it
+            branches.run(ctx, spectral, lambda c: ops.conv2d(c, xr, self.conv_to_l, y.slice(0, cl), force_splits=fs_c2l),
+                         l2g)
         else:
             branches.run(ctx, lambda c: ops.conv2d(c, xr, self.conv_to_l, y.slice(0, cl), force_splits=fs_c2l), l2g,
                          spectral)
