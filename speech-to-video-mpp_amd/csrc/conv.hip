@@ -1030,7 +1030,8 @@ static Plan make_plan_x3(const s2v_conv_params *p, int M, Plan pl) {
         if (c.ring && !ring_ok(p)) continue;
         if (p->b_kn && c.t.nw != 4) continue;
         if (c.t.bm >= 256 && c.t.bn >= 128 && am != 0 && am != 3) continue;   // generic gathers spill there
-        if (c.t.bm == 256 && c.t.bn == 64 && am != 0) continue;   // measured slower than 128x64 on per-row gathers
+        // the 256 / 512-row narrow-N tiles on per-row gathers: measured slower than 128x64 (256x64, r02)
+        if (c.t.bm >= 256 && c.t.bn <= 64 && am != 0) continue;
         if (!p->b_kn && (long long)cdiv(p->cout, c.t.bn) * c.t.bn > p->npad) continue;   // weight rows
         const long long tiles = (long long)cdiv(M, c.t.bm) * cdiv(p->cout, c.t.bn) * batch;
         const double slots = (double)cus * c.bpc;

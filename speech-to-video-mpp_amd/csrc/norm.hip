@@ -132,6 +132,57 @@ __global__ __launch_bounds__(256) void ln_apply(const float *__restrict__ x, int
     }
 }
 
+// float4 form of the pooled apply (ConvNormAct pool=True: LNet / DNet DownBlock2d): one output pixel
+// channel quad per thread, its 2x2 source quads loaded as four float4s (the scalar ln_apply ran the
+// DNet 256^2 x 64 pooled LayerNorm at 2 TB/s)
+__global__ __launch_bounds__(256) void ln_apply4_pool(const float *__restrict__ x, int h, int w, int c4, int xcs,
+                                                      const float *__restrict__ weight, const float *__restrict__ bias,
+                                                      float eps, int act, float alpha, const float *res, int res_cs,
+                                                      float *y, int ycs, const double *__restrict__ part, int nblk) {
+    const int n = blockIdx.y;
+    __shared__ float st[2];
+    {
+        double s = 0.0, q = 0.0;
+        for (int i = threadIdx.x; i < nblk; i += 256) {
+            s += part[((long long)n * nblk + i) * 2 + 0];
+            q += part[((long long)n * nblk + i) * 2 + 1];
+        }
+        block_sum2(s, q);
+        if (threadIdx.x == 0) {
+            const double cnt = (double)h * w * c4 * 4;
+            const double mean = s / cnt;
+            double var = q / cnt - mean * mean;
+            if (var < 0.0) var = 0.0;
+            st[0] = (float)mean;
+            st[1] = (float)(1.0 / sqrt(var + (double)eps));
+        }
+        __syncthreads();
+    }
+    const int oh = h / 2, ow = w / 2;
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= oh * ow * c4) return;
+    const float mean = st[0], rstd = st[1];
+    const int p = e / c4, cq = e - p * c4, cc = 4 * cq;
+    const int oy = p / ow, ox = p - oy * ow;
+    const float4 wv = *(const float4 *)(weight + cc), bv = *(const float4 *)(bias + cc);
+    const float *px = x + (((long long)n * h + 2 * oy) * w + 2 * ox) * xcs + cc;
+    const float4 a0 = *(const float4 *)px, a1 = *(const float4 *)(px + xcs);
+    const float4 a2 = *(const float4 *)(px + (long long)w * xcs), a3 = *(const float4 *)(px + (long long)w * xcs + xcs);
+    const float slope = act == S2V_ACT_LRELU ? alpha : 0.f;
+    auto f = [&](float v, float g, float b) { return apply_act((v - mean) * (g * rstd) + b, act, slope); };
+    float4 o;
+    o.x = 0.25f * (f(a0.x, wv.x, bv.x) + f(a1.x, wv.x, bv.x) + f(a2.x, wv.x, bv.x) + f(a3.x, wv.x, bv.x));
+    o.y = 0.25f * (f(a0.y, wv.y, bv.y) + f(a1.y, wv.y, bv.y) + f(a2.y, wv.y, bv.y) + f(a3.y, wv.y, bv.y));
+    o.z = 0.25f * (f(a0.z, wv.z, bv.z) + f(a1.z, wv.z, bv.z) + f(a2.z, wv.z, bv.z) + f(a3.z, wv.z, bv.z));
+    o.w = 0.25f * (f(a0.w, wv.w, bv.w) + f(a1.w, wv.w, bv.w) + f(a2.w, wv.w, bv.w) + f(a3.w, wv.w, bv.w));
+    const long long op = (long long)n * oh * ow + p;
+    if (res) {
+        const float4 r = *(const float4 *)(res + op * res_cs + cc);
+        o.x += r.x; o.y += r.y; o.z += r.z; o.w += r.w;
+    }
+    *(float4 *)(y + op * ycs + cc) = o;
+}
+
 // float4 form without pooling (c, pitches % 4 == 0, 16-byte aligned): one channel quad per thread
 // and no grid-stride loop, so no load waits behind an earlier store of the same wave
 __global__ __launch_bounds__(256) void ln_apply4(const float *__restrict__ x, int hw, int c4, int xcs,
@@ -627,10 +678,15 @@ extern "C" int s2v_layernorm2d(const float *x, int n, int h, int w, int c, int x
     ln_stats<<<dim3(nblk, n), 256, 0, s>>>(x, h * w, c, xcs, nblk, (double *)ws);
     int rc = check_launch("ln_stats");
     if (rc) return rc;
-    const bool vec = !pool && c % 4 == 0 && xcs % 4 == 0 && ycs % 4 == 0 && (!res || res_cs % 4 == 0) &&
+    const bool vec = c % 4 == 0 && xcs % 4 == 0 && ycs % 4 == 0 && (!res || res_cs % 4 == 0) &&
                      ((uintptr_t)x % 16) == 0 && ((uintptr_t)y % 16) == 0 && ((uintptr_t)weight % 16) == 0 &&
                      ((uintptr_t)bias % 16) == 0 && (!res || ((uintptr_t)res % 16) == 0) &&
                      (long long)h * w * (c / 4) < (1LL << 31);
+    if (vec && pool) {
+        ln_apply4_pool<<<dim3(cdiv((long long)(h / 2) * (w / 2) * (c / 4), 256), n), 256, 0, s>>>(
+            x, h, w, c / 4, xcs, weight, bias, eps, act, alpha, res, res_cs, y, ycs, (const double *)ws, nblk);
+        return check_launch("ln_apply");
+    }
     if (vec) {
         ln_apply4<<<dim3(cdiv((long long)h * w * (c / 4), 256), n), 256, 0, s>>>(
             x, h * w, c / 4, xcs, weight, bias, eps, act, alpha, res, res_cs, y, ycs, (const double *)ws, nblk);

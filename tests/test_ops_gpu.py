@@ -330,13 +330,15 @@ def test_gemm_kn_batched(ctx, prec):
     assert ((out.double().cpu() - ref).abs() <= REL[prec] * (bound + 1) + 1e-6).all()
 
 
-@pytest.mark.parametrize("c", [40, 42])                # float4 apply (no pool), scalar apply
-def test_layernorm2d(ctx, c):
-    x = rnd(2, c, 12, 10, seed=13) * 3 + 1
+@pytest.mark.parametrize("c", [40, 42])                # float4 apply (pooled and not), scalar apply
+@pytest.mark.parametrize("hw", [(12, 10), (13, 11)])   # odd sizes: the pool drops the last row / column
+def test_layernorm2d(ctx, c, hw):
+    h, w = hw
+    x = rnd(2, c, h, w, seed=13) * 3 + 1
     wgt, b = rnd(c, seed=14), rnd(c, seed=15)
     xv = nhwc(x.float())
     for pool in (False, True):
-        oh, ow = (6, 5) if pool else (12, 10)
+        oh, ow = (h // 2, w // 2) if pool else (h, w)
         res = rnd(2, c, oh, ow, seed=16 + pool)
         y = NHWC.empty(2, oh, ow, c, DEV)
         ops.layernorm2d(ctx, xv, wgt.float().to(DEV), b.float().to(DEV), y, act=ops.ACT_LRELU, alpha=0.1, pool=pool,
