@@ -329,14 +329,16 @@ class LNetEngine:
         st, c2 = side[0]
         cur = torch.cuda.current_stream(self.device)
         st.wait_stream(cur)
+        # each half is one serial chain: no branch streams forked from the half's side stream (a capture
+        # with forks nested two streams deep crashed in hipStreamEndCapture on this ROCm)
         with ops.side_stream(st, ctx.keep):
-            self._forward(c2, audio[h:], rows(face6, h, b), rows(out, h, b), rows(logits, h, b), pad_rgb)
-        self._forward(ctx, audio[:h], rows(face6, 0, h), rows(out, 0, h), rows(logits, 0, h), pad_rgb)
+            self._forward(c2, audio[h:], rows(face6, h, b), rows(out, h, b), rows(logits, h, b), pad_rgb, False)
+        self._forward(ctx, audio[:h], rows(face6, 0, h), rows(out, 0, h), rows(logits, 0, h), pad_rgb, False)
         cur.wait_stream(st)
         return out
 
     def _forward(self, ctx, audio: torch.Tensor, face6: NHWC, out: NHWC, logits: NHWC | None = None,
-                 pad_rgb: bool = False):
+                 pad_rgb: bool = False, branches: bool = True):
         dev = self.device
         b = face6.n
         # ---- visual encoder (LNet.py:30-43) and audio encoder (LNet.py:102-120): the masked-face
@@ -371,7 +373,7 @@ class LNetEngine:
                 x = y
             st["adain"] = self.bank.run(cx, x)
 
-        br = self._branches(ctx) if BRANCHES else None
+        br = self._branches(ctx) if BRANCHES and branches else None
         if br is None:
             masked(ctx)
             reference(ctx)
