@@ -118,7 +118,7 @@ def test_lnet_halves_match_one_chain(prec, lnet, monkeypatch):
     runner = GraphRunner(lambda a, b: lnet(a, b), [m, f], warmup=1)
     rep = runner.replay().clone()
     torch.cuda.synchronize()
-    assert (two - one).abs().max() < 2e-4, float((two - one).abs().max())
+    assert (two - one).abs().max() < 2 * TOL[prec]["lnet"][0], float((two - one).abs().max())
     assert torch.equal(rep, two)
     with torch.no_grad():
         ro = nets.lnet_forward(synth_sd("lnet"), torch.from_numpy(mel[:1]), torch.from_numpy(face[:1]))
