@@ -890,8 +890,11 @@ static const X3Cfg kX3Tiles[] = {
     {{256, 256, 2, 8, 1, 1}, 400.f, 1, 0}, {{128, 128, 2, 8, 1, 1}, 330.f, 2, 0}, {{64, 128, 2, 8, 1, 1}, 260.f, 3, 0},
     {{128, 64, 2, 4, 1, 1}, 290.f, 3, 0},  {{64, 64, 2, 4, 1, 1}, 265.f, 4, 0},   {{128, 32, 4, 4, 1, 1}, 235.f, 4, 0},
     {{256, 128, 4, 8, 1, 1}, 335.f, 1, 0}, {{256, 64, 8, 8, 1, 1}, 300.f, 2, 0},  {{512, 128, 4, 8, 1, 1}, 360.f, 1, 0},
-    // narrow-N tiles with 64-row waves (r04): forced-only (tflops 0) until measured
-    {{512, 64, 8, 8, 1, 1}, 0.f, 1, 0},    {{256, 64, 4, 4, 1, 1}, 0.f, 2, 0},    {{256, 32, 4, 4, 1, 1}, 0.f, 2, 0},
+    // narrow-N tiles with 64-row waves (r04, tools/r04_nsweep.sh on MI355X, graph-timed 3x3 64-channel
+    // convs): 4x512^2 128 -> 64 199 (256x64 8-wave) -> 225 (512x64) / 233 (256x64 4-wave) TFLOP/s,
+    // 16x256^2 64 -> 64 156 -> 171 / 183; at 96^2 and below 128x64 stays ahead (more blocks).  The
+    // rates keep that order in the planner's model.  256x32 (4-wave): no faster than 128x32, forced-only.
+    {{512, 64, 8, 8, 1, 1}, 335.f, 1, 0},  {{256, 64, 4, 4, 1, 1}, 350.f, 2, 0},  {{256, 32, 4, 4, 1, 1}, 0.f, 2, 0},
     // LDS-DMA ring kernels (force_tile 13..18): forced-only until measured
     {{64, 64, 4, 4, 0, 6}, 0.f, 1, 1},     {{128, 64, 4, 4, 0, 5}, 0.f, 1, 2},    {{64, 128, 4, 4, 0, 5}, 0.f, 1, 3},
     {{128, 128, 4, 4, 0, 4}, 0.f, 1, 4},   {{64, 32, 4, 4, 0, 8}, 0.f, 1, 5},     {{128, 32, 4, 4, 0, 6}, 0.f, 1, 6}};

@@ -18,12 +18,6 @@ LRELU = 0.1        # LNet.py:91
 LRELU_FFC = 0.01   # FineADAINLama built with nn.LeakyReLU() default (base_blocks.py:369 via :393/:419)
 # FFC products on concurrent side streams (S2V_LNET_BRANCHES=0 serialises them on one stream)
 BRANCHES = os.environ.get("S2V_LNET_BRANCHES", "1") == "1"
-# FFC branches: the spectral chain st1 -> rfft -> fu -> irfft (the longest) on the calling stream and
-# conv_to_l / l2g on the side streams (S2V_LNET_SPEC_MAIN=0: conv_to_l on the calling stream).  A
-# kernel that waits on another stream's kernel starts ~12 us after it ends in the replayed graph
-# (profiles/r04 LNet FFC dumps: st2 after the side-stream irfft), so the chain that ends last
-# should not cross streams before st2.
-SPEC_MAIN = os.environ.get("S2V_LNET_SPEC_MAIN", "1") == "1"
 # S2V_LNET_GROUP=1: the FFC's three products that read the block input (conv_to_l, l2g, the spectral
 # branch's st1) as ONE grouped launch (ops.conv_group / s2v_conv2d_group) followed by the spectral chain
 # on the same stream, instead of the three side-stream branches.  Measured on MI355X (r04, 3 interleaved
@@ -35,9 +29,6 @@ GROUP = os.environ.get("S2V_LNET_GROUP", "0") == "1"
 PREPAD = os.environ.get("S2V_LNET_PREPAD", "1") == "1"
 # with PREPAD: the InstanceNorm that ends an FFC writes the next FFC's reflect-padded input itself
 FUSED_PAD = os.environ.get("S2V_LNET_FUSED_PAD", "1") == "1"
-# S2V_LNET_HALVES=k (k >= 1): batches of >= 2k frames run as two concurrent half-batch forwards (two
-# chains of latency-bound kernels side by side instead of one chain of twice-as-wide kernels)
-HALVES = int(os.environ.get("S2V_LNET_HALVES", "0"))
 # nearest-x2 UpBlock convs as four parity-class 2x2 convs of the un-upsampled input
 # (ConvW.make_up2_polyphase; S2V_UP2_POLY=0: the upsampling gather of the direct 3x3 conv)
 UP2_POLY = os.environ.get("S2V_UP2_POLY", "1") == "1"
@@ -225,11 +216,6 @@ class FFCLama:
             ops.conv2d(ctx, xr, self.conv_to_l, y.slice(0, cl), force_splits=fs_c2l)
             l2g(ctx)
             spectral(ctx)
-        elif SPEC_MAIN:
-            # the spectral chain (the FFC's critical path) on the calling stream: no cross-stream
-            # dependency between its kernels and st2 / the InstanceNorm after it
-            branches.run(ctx, spectral, lambda c: ops.conv2d(c, xr, self.conv_to_l, y.slice(0, cl), force_splits=fs_c2l),
-                         l2g)
         else:
             branches.run(ctx, lambda c: ops.conv2d(c, xr, self.conv_to_l, y.slice(0, cl), force_splits=fs_c2l), l2g,
                          spectral)
@@ -318,27 +304,7 @@ class LNetEngine:
                 pad_rgb: bool = False):
         """audio: [B,1,80,16] device tensor; face6: NHWC [B,96,96,6] = [masked | ref];
         out: NHWC [B,96,96,3] receives sigmoid(final conv) ([B,96,96,4] with a 4th constant channel
-        when ``pad_rgb``).  With HALVES the two halves of the batch run as two concurrent forwards (the
-        second on a side stream with its own Ctx: workspaces, FFC branch streams)."""
-        b = face6.n
-        side = ctx.streams(("lnet-half", id(self)), 1) if HALVES and b >= 2 * HALVES else None
-        if side is None:
-            return self._forward(ctx, audio, face6, out, logits, pad_rgb)
-        h = b // 2
-        rows = lambda v, a, z: None if v is None else NHWC(v.t[a:z], v.coff, v.c)  # noqa: E731
-        st, c2 = side[0]
-        cur = torch.cuda.current_stream(self.device)
-        st.wait_stream(cur)
-        # each half is one serial chain: no branch streams forked from the half's side stream (a capture
-        # with forks nested two streams deep crashed in hipStreamEndCapture on this ROCm)
-        with ops.side_stream(st, ctx.keep):
-            self._forward(c2, audio[h:], rows(face6, h, b), rows(out, h, b), rows(logits, h, b), pad_rgb, False)
-        self._forward(ctx, audio[:h], rows(face6, 0, h), rows(out, 0, h), rows(logits, 0, h), pad_rgb, False)
-        cur.wait_stream(st)
-        return out
-
-    def _forward(self, ctx, audio: torch.Tensor, face6: NHWC, out: NHWC, logits: NHWC | None = None,
-                 pad_rgb: bool = False, branches: bool = True):
+        when ``pad_rgb``)."""
         dev = self.device
         b = face6.n
         # ---- visual encoder (LNet.py:30-43) and audio encoder (LNet.py:102-120): the masked-face
@@ -373,7 +339,7 @@ class LNetEngine:
                 x = y
             st["adain"] = self.bank.run(cx, x)
 
-        br = self._branches(ctx) if BRANCHES and branches else None
+        br = self._branches(ctx) if BRANCHES else None
         if br is None:
             masked(ctx)
             reference(ctx)

@@ -103,28 +103,6 @@ def test_lnet_5d_input_fold(lnet):
     assert (out5[:, :, 0] - flat[:2]).abs().max() < 1e-6 and (out5[:, :, 1] - flat[2:]).abs().max() < 1e-6
 
 
-def test_lnet_halves_match_one_chain(prec, lnet, monkeypatch):
-    """S2V_LNET_HALVES: the batch as two concurrent half-batch forwards (second half on a side stream
-    with its own Ctx) equals the single-chain forward up to the split-K plan of the smaller batch, eager
-    and graph-captured (the timed form), and frame 0 stays within the oracle bound."""
-    from oracle import nets
-    from s2v_amd.engine import lnet as L
-    from s2v_amd.runtime import GraphRunner
-    mel, face, _ = synth.lipsync_inputs("lnet.halves", 8, 96)
-    m, f = torch.from_numpy(mel).to(DEV), torch.from_numpy(face).to(DEV)
-    one = lnet(m, f).clone()
-    monkeypatch.setattr(L, "HALVES", 2)
-    two = lnet(m, f).clone()
-    runner = GraphRunner(lambda a, b: lnet(a, b), [m, f], warmup=1)
-    rep = runner.replay().clone()
-    torch.cuda.synchronize()
-    assert (two - one).abs().max() < 2 * TOL[prec]["lnet"][0], float((two - one).abs().max())
-    assert torch.equal(rep, two)
-    with torch.no_grad():
-        ro = nets.lnet_forward(synth_sd("lnet"), torch.from_numpy(mel[:1]), torch.from_numpy(face[:1]))
-    within(two[:1], ro, TOL[prec]["lnet"], "halves frame 0")
-
-
 def test_enet_matches_reference(prec, enet, golden):
     for size in (256, 384):
         g = golden(f"enet_b1_{size}")
