@@ -708,11 +708,12 @@ static void launch_small(const ConvArgs &a, int batch, bool cpar, hipStream_t s)
 // head at 256^2, LNet's 7x7 64 -> 4 sigmoid head): a block owns an 8 x (32 PX) output tile; per chunk
 // of CC input channels it stages the (8 + KS - 1) x (32 PX + KS - 1) input halo once in LDS (planar per
 // channel), and each thread computes PX horizontally adjacent pixels x CO outputs from 16-byte LDS
-// row reads, so every staged value feeds up to PX * KS taps.  CC = 16 (r04): each staged pixel is one
-// 64-byte piece of its channel row, so consecutive chunks do not re-fetch a line they share (with
-// 4-channel chunks the 256^2 DNet head read 3.8 GB from HBM for 0.27 GB of input, 573 us).  Filter
-// values are block-uniform (scalar loads).  fp32 VALU, exact products.
-template <int CO, int KS, int CC = 16, int PX = 2>
+// row reads, so every staged value feeds up to PX * KS taps.  r04: 16-channel chunks, one per block
+// (halo_splits; the channel splits meet in splitk_reduce), so each staged pixel is one 64-byte piece of
+// its channel row read once (4-channel chunks looped in the block re-fetched the lines they share: the
+// DNet 256^2 head read 3.8 GB from HBM for 0.27 GB of input, 573 us).  Filter values are block-uniform
+// (scalar loads).  fp32 VALU, exact products.
+template <int CO, int KS, int CC = 16, int PX = 4>
 __global__ __launch_bounds__(256) void conv_halo_small(ConvArgs a, int tiles_x, int tiles_y) {
     constexpr int TH = 8, TW = 32 * PX;
     constexpr int IH = TH + KS - 1, IW = TW + KS - 1, IWP = (IW + 3) / 4 * 4;
@@ -828,7 +829,8 @@ static int plan_cus() { return device_cus() > 0 ? device_cus() : 256; }
 
 long long tune_get(int key) { return tune_value(key); }
 
-constexpr int kHaloTW = 64;              // conv_halo_small output tile width (32 PX, PX = 2)
+constexpr int kHaloTW = 128;             // conv_halo_small output tile width (32 PX, PX = 4)
+constexpr int kHaloCC = 16;              // conv_halo_small channels per staged chunk
 
 static int halo_ks(const s2v_conv_params *p) {
     const int batch = p->batch > 0 ? p->batch : 1;
@@ -845,15 +847,12 @@ static int halo_ks(const s2v_conv_params *p) {
     return p->kh;
 }
 
-// channel splits of the halo kernel: about three blocks per CU, at least 8 channels per split
+// channel splits of the halo kernel: one 16-channel chunk per block.  A block then reads each staged
+// pixel's 64-byte channel piece once and never comes back to its lines (with the chunks looped inside
+// the block, 4-channel chunks, the halo tiles of one XCD's blocks overflowed its L2 between chunks: the
+// DNet 256^2 head re-read its input 8x, 3.8 GB for 0.27 GB); the partial sums meet in splitk_reduce
 static int halo_splits(const s2v_conv_params *p, int &per) {
-    const long long blocks = (long long)p->n * cdiv(p->ow, kHaloTW) * cdiv(p->oh, 8);
-    const int cus = plan_cus();
-    const int quads = p->cin / 4;
-    int s = blocks >= 3LL * cus ? 1 : (int)((3LL * cus + blocks - 1) / blocks);
-    if (s > quads / 2) s = quads / 2;
-    if (s < 1) s = 1;
-    per = 4 * ((quads + s - 1) / s);
+    per = kHaloCC;
     return (p->cin + per - 1) / per;
 }
 

@@ -347,8 +347,19 @@ __device__ __forceinline__ void conv_x3_tile(const ConvArgs &a, int L, int gx, i
     // input scale s[n, c] (StyleGAN2 modulation with shared weights) loaded with the A operand in issue()
     // instead of in the store phase, where its load was waited for right away (one memory round trip per
     // K-slice); only in tiles with register room (the 256-row / 512-row tiles keep the old path)
-    constexpr bool PSC = A8 && (BM * BN <= 128 * 128 || (BN == 64 && AR8 <= 4));
+    constexpr bool PSC = A8 && (BM * BN <= 128 * 128 || (BN == 64 && AR8 <= 4 && NW == 4));
+    static_assert(!PSC || (PF == 1 && KS == 1), "the input-scale registers follow one in-flight slice");
     f4 rsc[PF][KS][PSC ? 2 * AR8 : 1];
+    // a tile whose rows all lie in one image (every tile of the 256^2 / 512^2 enhancer and DNet layers)
+    // needs one s[n, c8 .. c8 + 7] pair per thread, reloaded only when the channel slice changes (every
+    // kh * kw K-slices in the channel-slice-major order), instead of two loads per row per slice
+    // (the 256 / 512-row tiles: the smaller ones keep their register budget and the per-row loads)
+    constexpr bool PSC1 = PSC && BM >= 256;
+    const int hw_img = a.oh * a.ow;
+    const bool one_img = PSC1 && a.in_scale && m0 / hw_img == (min(m0 + BM, a.M) - 1) / hw_img;
+    const float *sc_base = PSC1 && a.in_scale ? a.in_scale + (long long)(m0 / hw_img) * a.in_scale_ns : nullptr;
+    f4 sc0 = {1.f, 1.f, 1.f, 1.f}, sc1 = {1.f, 1.f, 1.f, 1.f};
+    int sc_cs = -1;
     u32x4 rbp[PF][KS][BKN ? 1 : BR];
     f4 rbk[PF][KS][BKN ? BKR : 1];
     constexpr bool M16 = X3_MFMA16;
@@ -380,7 +391,13 @@ __device__ __forceinline__ void conv_x3_tile(const ConvArgs &a, int L, int gx, i
                 const int c8 = ld.cs * 32 + 8 * (tid & 3);
                 rc[p][u] = c8;
                 if constexpr (PSC) {
-                    if (a.in_scale) {
+                    if (PSC1 && one_img) {
+                        if (ld.cs != sc_cs) {
+                            sc0 = *(const f4 *)(sc_base + c8);
+                            sc1 = *(const f4 *)(sc_base + c8 + 4);
+                            sc_cs = ld.cs;
+                        }
+                    } else if (a.in_scale) {
 #pragma unroll
                         for (int j = 0; j < AR8; ++j) {
                             const float *sp = a.in_scale + (long long)R.img[j] * a.in_scale_ns + c8;
@@ -405,7 +422,13 @@ __device__ __forceinline__ void conv_x3_tile(const ConvArgs &a, int L, int gx, i
                 const int c8 = ld.cs * 32 + 8 * (tid & 3);
                 rc[p][u] = c8;
                 if constexpr (PSC) {
-                    if (a.in_scale) {
+                    if (PSC1 && one_img) {
+                        if (ld.cs != sc_cs) {
+                            sc0 = *(const f4 *)(sc_base + c8);
+                            sc1 = *(const f4 *)(sc_base + c8 + 4);
+                            sc_cs = ld.cs;
+                        }
+                    } else if (a.in_scale) {
 #pragma unroll
                         for (int j = 0; j < AR8; ++j) {
                             const float *sp = a.in_scale + (long long)R.img[j] * a.in_scale_ns + c8;
@@ -437,7 +460,13 @@ __device__ __forceinline__ void conv_x3_tile(const ConvArgs &a, int L, int gx, i
             char *sb = st + u * SUB;
             if constexpr (A8) {
                 if constexpr (PSC) {
-                    if (a.in_scale) {
+                    if (PSC1 && one_img) {
+#pragma unroll
+                        for (int j = 0; j < AR8; ++j) {
+                            ra[p][u][2 * j] *= sc0;
+                            ra[p][u][2 * j + 1] *= sc1;
+                        }
+                    } else if (a.in_scale) {
 #pragma unroll
                         for (int j = 0; j < 2 * AR8; ++j) ra[p][u][j] *= rsc[p][u][j];
                     }

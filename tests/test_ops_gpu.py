@@ -298,13 +298,16 @@ def test_modulated_conv_per_sample_weights(ctx, prec, n, cin, h, w, cout, k, mod
 
 
 @pytest.mark.parametrize("tile", [0, 4, 5, 6, 8, 9, 10, 11, 12])
-def test_conv2d_prologue(ctx, prec, tile):
+@pytest.mark.parametrize("nhw", [(3, 10, 10), (2, 32, 32)])
+def test_conv2d_prologue(ctx, prec, tile, nhw):
     """Input scale s[n, c] + pre-activation prologue on every tile family: the small tiles load s with
-    the A operand (issue), the wide ones in the store phase; 3 images of 10x10 so one tile spans
-    several images (per-row image index)."""
+    the A operand (issue), the 256-row tiles one s pair per channel slice when the tile lies in one
+    image, the wide ones in the store phase; 3 images of 10x10 (one tile spans several images: per-row
+    image index) and 2 of 32x32 (every 256-row tile inside one image)."""
     if prec == "f32" and tile > 6:
         pytest.skip("the f32 table has 6 tiles")
-    n, cin, h, w, cout = 3, 64, 10, 10, 64
+    n, h, w = nhw
+    cin, cout = 64, 64
     wt = rnd(cout, cin, 3, 3, seed=7) / math.sqrt(cin * 9)
     x = rnd(n, cin, h, w, seed=8)
     s = rnd(n, cin, seed=9, lo=0.5, hi=2.0)
