@@ -281,7 +281,7 @@ class Stamper:
 
 
 def _peak(sym):
-    return X3_PEAK_TFLOPS if ("conv_igemm_x3" in sym or "conv_ring_x3" in sym or "conv_glds_x3" in sym) \
+    return X3_PEAK_TFLOPS if ("conv_igemm_x3" in sym or "conv_glds_x3" in sym) \
         else FP32_MFMA_PEAK_TFLOPS
 
 

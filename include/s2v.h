@@ -157,11 +157,10 @@ size_t s2v_conv2d_ws_bytes(const s2v_conv_params *p);
 /* The launch plan s2v_conv2d would use: out11 = {BM, BN, WAVES_M, AVEC, B_KN, splits, prec, NW, KS, PF,
  * PERSIST} of the conv_igemm<BM,BN,WAVES_M,AVEC,B_KN> (prec 0) or
  * conv_igemm_x3<BM,BN,WAVES_M,NW,KS,PF,AVEC,B_KN,prec-1> (prec 1 / 2) instance — conv_igemm_x3_persist<...>
- * with PERSIST (> 0) blocks under ``grid_cap``, conv_ring_x3<BM,BN,PF,prec-1> when AVEC == 6,
- * conv_glds_x3<BM,BN,WAVES_M,KS,prec-1> when AVEC == 5 — or {0, CO, TPP, LW, 0, 1, 0, ...} for
- * conv_small_cpar<CO,TPP,LW> (conv_direct_small<CO> when TPP == 0), or {0, cout, -QPT, PX, 0, 1, ...} for
- * conv_smallk<QPT,PX>.  force_tile: 0 = planner, 1..6 (f32) / 1..18 (split precisions: 13..18 the LDS-DMA
- * ring tiles) a fixed tile of the selected precision's table (tests / tuning). */
+ * with PERSIST (> 0) blocks under ``grid_cap``, conv_glds_x3<BM,BN,WAVES_M,KS,prec-1> when AVEC == 5 —
+ * or {0, CO, TPP, LW, 0, 1, 0, ...} for conv_small_cpar<CO,TPP,LW> (conv_direct_small<CO> when TPP == 0),
+ * or {0, cout, -QPT, PX, 0, 1, ...} for conv_smallk<QPT,PX>.  force_tile: 0 = planner, 1..6 (f32) / 1..12
+ * (split precisions) a fixed tile of the selected precision's table (tests / tuning). */
 int s2v_conv2d_plan(const s2v_conv_params *p, int *out11);
 /* Up to S2V_CONV_GROUP_MAX independent convolutions as ONE kernel launch (a tile table over the members'
  * tile grids on one tile configuration, each member with its own split-K factor), plus one launch

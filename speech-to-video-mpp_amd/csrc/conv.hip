@@ -25,8 +25,6 @@ template <int ELT>   // 0 = bf16, 1 = f16 halves (conv_x3_impl.hpp; instances in
 int launch_conv_x3(int tile, const ConvArgs &a, int amode, bool bkn, dim3 grid, hipStream_t s);
 template <int ELT>   // LDS-DMA kernels on split-layout inputs (conv_glds.hip): cfg 0 = 256x256, 1 = 256x128
 void launch_conv_glds(int cfg, const ConvArgs &a, dim3 grid, hipStream_t s);
-template <int ELT>   // LDS-DMA ring kernels on fp32 inputs (conv_ring.hip), cfg = X3Cfg::ring - 1
-void launch_conv_ring(int cfg, const ConvArgs &a, dim3 grid, hipStream_t s);
 template <int ELT>   // grouped x3 launches (conv_x3_impl.hpp conv_igemm_x3_group): 0 or an error
 int launch_conv_x3_group(int cfg, const ConvGroup &g, dim3 grid, hipStream_t s);
 
@@ -705,23 +703,19 @@ static void launch_small(const ConvArgs &a, int batch, bool cpar, hipStream_t s)
 
 
 // Halo-tiled direct conv for Cout <= 4 heads with a wide square filter (DNet's 7x7 64 -> 3 tanh
-// head at 256^2, LNet's 7x7 64 -> 4 sigmoid head): a block owns an 8 x (32 PX) output tile; per chunk
-// of CC input channels it stages the (8 + KS - 1) x (32 PX + KS - 1) input halo once in LDS (planar per
-// channel), and each thread computes PX horizontally adjacent pixels x CO outputs from 16-byte LDS
-// row reads, so every staged value feeds up to PX * KS taps.  r04: 16-channel chunks, one per block
-// (halo_splits; the channel splits meet in splitk_reduce), so each staged pixel is one 64-byte piece of
-// its channel row read once (4-channel chunks looped in the block re-fetched the lines they share: the
-// DNet 256^2 head read 3.8 GB from HBM for 0.27 GB of input, 573 us).  Filter values are block-uniform
-// (scalar loads).  fp32 VALU, exact products.
-template <int CO, int KS, int CC = 16, int PX = 4>
+// head at 256^2, LNet's 7x7 64 -> 3 sigmoid head): a block owns an 8 x 128 output tile; per chunk
+// of 4 input channels it stages the (8 + KS - 1) x (128 + KS - 1) input halo once in LDS (planar
+// per channel), and each thread computes 4 horizontally adjacent pixels x CO outputs from 16-byte
+// LDS row reads, so every staged value feeds up to 4 * KS taps.  The per-pixel gather of
+// conv_small_cpar re-read each input pixel KS^2 times from L1/L2 (DNet head: 1.5 ms per 16 frames
+// at 185 GB/s).  Filter values are block-uniform (scalar loads).  fp32 VALU, exact products.
+template <int CO, int KS>
 __global__ __launch_bounds__(256) void conv_halo_small(ConvArgs a, int tiles_x, int tiles_y) {
-    constexpr int TH = 8, TW = 32 * PX;
+    constexpr int TH = 8, PX = 4, TW = 32 * PX;
     constexpr int IH = TH + KS - 1, IW = TW + KS - 1, IWP = (IW + 3) / 4 * 4;
-    constexpr int NR2 = (PX + KS - 1 + 1) / 2;               // float2 row reads per (channel, ky)
-    constexpr int CQ = CC / 4;
-    static_assert(PX * 31 + 2 * NR2 <= IWP, "halo row reads stay inside the padded LDS row");
-    static_assert(PX % 2 == 0 || PX == 1, "row reads start 8-byte aligned");
-    __shared__ __attribute__((aligned(16))) float tile[CC][IH][IWP];
+    constexpr int NV = (PX + KS - 1 + 3) / 4;                 // float4 row reads per (channel, ky)
+    static_assert(4 * 31 + 4 * NV <= IWP, "halo row reads stay inside the padded LDS row");
+    __shared__ __attribute__((aligned(16))) float tile[4][IH][IWP];
     const int tid = threadIdx.x, r = tid >> 5, cg = tid & 31;
     int t = blockIdx.x;
     const int txi = t % tiles_x;
@@ -739,12 +733,10 @@ __global__ __launch_bounds__(256) void conv_halo_small(ConvArgs a, int tiles_x, 
 #pragma unroll
         for (int o = 0; o < CO; ++o) acc[p][o] = 0.f;
     const bool refl = a.pad_mode == S2V_PAD_REFLECT;
-    for (int c0 = cb; c0 < ce; c0 += CC) {
-        const int nq = min(CQ, (ce - c0) / 4);
+    for (int c0 = cb; c0 < ce; c0 += 4) {
         __syncthreads();                                      // the previous chunk has been consumed
-        for (int e = tid; e < IH * IW * CQ; e += 256) {
-            const int q = e % CQ, px = e / CQ;
-            const int iy = px / IW, ix = px - iy * IW;
+        for (int e = tid; e < IH * IW; e += 256) {
+            const int iy = e / IW, ix = e - iy * IW;
             int gy = oy0 + iy - a.ph, gx = ox0 + ix - a.pw;
             if (refl) {
                 gy = reflect_idx(gy, a.h);
@@ -752,22 +744,23 @@ __global__ __launch_bounds__(256) void conv_halo_small(ConvArgs a, int tiles_x, 
             }
             // halo rows / columns past the image (tiles overhanging the bottom / right edge, or
             // beyond a single reflection) feed only outputs that are never stored
-            const bool ok = q < nq && (unsigned)gy < (unsigned)a.h && (unsigned)gx < (unsigned)a.w;
+            const bool ok = (unsigned)gy < (unsigned)a.h && (unsigned)gx < (unsigned)a.w;
             f4 v = f4{0.f, 0.f, 0.f, 0.f};
-            if (ok) v = *(const f4 *)(xb + ((long long)gy * a.w + gx) * a.xcs + c0 + 4 * q);
-            tile[4 * q + 0][iy][ix] = v.x;
-            tile[4 * q + 1][iy][ix] = v.y;
-            tile[4 * q + 2][iy][ix] = v.z;
-            tile[4 * q + 3][iy][ix] = v.w;
+            if (ok) v = *(const f4 *)(xb + ((long long)gy * a.w + gx) * a.xcs + c0);
+            tile[0][iy][ix] = v.x;
+            tile[1][iy][ix] = v.y;
+            tile[2][iy][ix] = v.z;
+            tile[3][iy][ix] = v.w;
         }
         __syncthreads();
-        for (int c = 0; c < 4 * nq; ++c) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
 #pragma unroll
             for (int ky = 0; ky < KS; ++ky) {
-                float row[2 * NR2];
-                const float *src = &tile[c][r + ky][PX * cg];
+                float row[4 * NV];
+                const float *src = &tile[c][r + ky][4 * cg];
 #pragma unroll
-                for (int j = 0; j < NR2; ++j) *(float2 *)&row[2 * j] = *(const float2 *)(src + 2 * j);
+                for (int j = 0; j < NV; ++j) *(f4 *)&row[4 * j] = *(const f4 *)(src + 4 * j);
 #pragma unroll
                 for (int kx = 0; kx < KS; ++kx) {
                     const long long k = (long long)(ky * KS + kx) * a.cin + c0 + c;
@@ -786,7 +779,7 @@ __global__ __launch_bounds__(256) void conv_halo_small(ConvArgs a, int tiles_x, 
     if (oy >= a.oh) return;
 #pragma unroll
     for (int p = 0; p < PX; ++p) {
-        const int ox = ox0 + PX * cg + p;
+        const int ox = ox0 + 4 * cg + p;
         if (ox >= a.ow) continue;
         const int m = (img * a.oh + oy) * a.ow + ox;
         if (a.splits > 1) {
@@ -829,9 +822,6 @@ static int plan_cus() { return device_cus() > 0 ? device_cus() : 256; }
 
 long long tune_get(int key) { return tune_value(key); }
 
-constexpr int kHaloTW = 128;             // conv_halo_small output tile width (32 PX, PX = 4)
-constexpr int kHaloCC = 16;              // conv_halo_small channels per staged chunk
-
 static int halo_ks(const s2v_conv_params *p) {
     const int batch = p->batch > 0 ? p->batch : 1;
     if (p->cout > 4 || p->kh != p->kw || (p->kh != 3 && p->kh != 5 && p->kh != 7)) return 0;
@@ -842,23 +832,26 @@ static int halo_ks(const s2v_conv_params *p) {
     // 8 x 128 output tiles: on small images (LNet's 96^2 RGB head, DNet's 64^2 flow head) too few
     // blocks cover the chip and a 128-wide tile runs part empty; the channel-parallel kernel (lanes
     // split K per pixel) has the parallelism there.  S2V_HALO_MIN_BLOCKS overrides (tuning).
-    const long long blocks = (long long)p->n * cdiv(p->ow, kHaloTW) * cdiv(p->oh, 8);
+    const long long blocks = (long long)p->n * cdiv(p->ow, 128) * cdiv(p->oh, 8);
     if (blocks < tune_value(S2V_TUNE_HALO_MIN_BLOCKS)) return 0;
     return p->kh;
 }
 
-// channel splits of the halo kernel: one 16-channel chunk per block.  A block then reads each staged
-// pixel's 64-byte channel piece once and never comes back to its lines (with the chunks looped inside
-// the block, 4-channel chunks, the halo tiles of one XCD's blocks overflowed its L2 between chunks: the
-// DNet 256^2 head re-read its input 8x, 3.8 GB for 0.27 GB); the partial sums meet in splitk_reduce
+// channel splits of the halo kernel: about three blocks per CU, at least 8 channels per split
 static int halo_splits(const s2v_conv_params *p, int &per) {
-    per = kHaloCC;
+    const long long blocks = (long long)p->n * cdiv(p->ow, 128) * cdiv(p->oh, 8);
+    const int cus = plan_cus();
+    const int quads = p->cin / 4;
+    int s = blocks >= 3LL * cus ? 1 : (int)((3LL * cus + blocks - 1) / blocks);
+    if (s > quads / 2) s = quads / 2;
+    if (s < 1) s = 1;
+    per = 4 * ((quads + s - 1) / s);
     return (p->cin + per - 1) / per;
 }
 
 template <int CO>
 static void launch_halo(const ConvArgs &a, int ks, hipStream_t s) {
-    const int tiles_x = (int)cdiv(a.ow, kHaloTW), tiles_y = (int)cdiv(a.oh, 8);
+    const int tiles_x = (int)cdiv(a.ow, 128), tiles_y = (int)cdiv(a.oh, 8);
     const dim3 grid((unsigned)((long long)a.n * tiles_x * tiles_y), (unsigned)a.splits);
     if (ks == 3) conv_halo_small<CO, 3><<<grid, 256, 0, s>>>(a, tiles_x, tiles_y);
     else if (ks == 5) conv_halo_small<CO, 5><<<grid, 256, 0, s>>>(a, tiles_x, tiles_y);
@@ -877,26 +870,20 @@ static const TileCfg kTiles[] = {
 // and resident blocks per CU (LDS / waves) for the planner's cost model
 // (512x128: 360, set end to end on MI355X r03 — lipsync 29.11 -> 28.35 ms, its 400^2 N = 128 StyleConvs;
 // 420 also displaces the 256x256 tile on N = 256 layers: 28.80 ms)
-// ring > 0: the LDS-DMA ring kernel conv_ring_x3<BM, BN, NST = pf> (conv_ring.hip launch_conv_ring cfg
-// ring - 1; 4 waves stacked along M), for AMODE-0 convolutions without a prologue
 struct X3Cfg {
     TileCfg t;
     float tflops;
     int bpc;
-    int ring;
 };
 static const X3Cfg kX3Tiles[] = {
-    {{256, 256, 2, 8, 1, 1}, 400.f, 1, 0}, {{128, 128, 2, 8, 1, 1}, 330.f, 2, 0}, {{64, 128, 2, 8, 1, 1}, 260.f, 3, 0},
-    {{128, 64, 2, 4, 1, 1}, 290.f, 3, 0},  {{64, 64, 2, 4, 1, 1}, 265.f, 4, 0},   {{128, 32, 4, 4, 1, 1}, 235.f, 4, 0},
-    {{256, 128, 4, 8, 1, 1}, 335.f, 1, 0}, {{256, 64, 8, 8, 1, 1}, 300.f, 2, 0},  {{512, 128, 4, 8, 1, 1}, 360.f, 1, 0},
+    {{256, 256, 2, 8, 1, 1}, 400.f, 1}, {{128, 128, 2, 8, 1, 1}, 330.f, 2}, {{64, 128, 2, 8, 1, 1}, 260.f, 3},
+    {{128, 64, 2, 4, 1, 1}, 290.f, 3},  {{64, 64, 2, 4, 1, 1}, 265.f, 4},   {{128, 32, 4, 4, 1, 1}, 235.f, 4},
+    {{256, 128, 4, 8, 1, 1}, 335.f, 1}, {{256, 64, 8, 8, 1, 1}, 300.f, 2},  {{512, 128, 4, 8, 1, 1}, 360.f, 1},
     // narrow-N tiles with 64-row waves (r04, tools/r04_nsweep.sh on MI355X, graph-timed 3x3 64-channel
     // convs): 4x512^2 128 -> 64 199 (256x64 8-wave) -> 225 (512x64) / 233 (256x64 4-wave) TFLOP/s,
     // 16x256^2 64 -> 64 156 -> 171 / 183; at 96^2 and below 128x64 stays ahead (more blocks).  The
     // rates keep that order in the planner's model.  256x32 (4-wave): no faster than 128x32, forced-only.
-    {{512, 64, 8, 8, 1, 1}, 335.f, 1, 0},  {{256, 64, 4, 4, 1, 1}, 350.f, 2, 0},  {{256, 32, 4, 4, 1, 1}, 0.f, 2, 0},
-    // LDS-DMA ring kernels (force_tile 13..18): forced-only until measured
-    {{64, 64, 4, 4, 0, 6}, 0.f, 1, 1},     {{128, 64, 4, 4, 0, 5}, 0.f, 1, 2},    {{64, 128, 4, 4, 0, 5}, 0.f, 1, 3},
-    {{128, 128, 4, 4, 0, 4}, 0.f, 1, 4},   {{64, 32, 4, 4, 0, 8}, 0.f, 1, 5},     {{128, 32, 4, 4, 0, 6}, 0.f, 1, 6}};
+    {{512, 64, 8, 8, 1, 1}, 335.f, 1},  {{256, 64, 4, 4, 1, 1}, 350.f, 2},  {{256, 32, 4, 4, 1, 1}, 0.f, 2}};
 constexpr int kNumX3 = sizeof(kX3Tiles) / sizeof(kX3Tiles[0]);
 
 static const TileCfg &tile_cfg(const s2v_conv_params *p, int tile);
@@ -972,12 +959,6 @@ static bool uses_x3(const s2v_conv_params *p) { return tiled_x3(p) && !p->b_kn; 
 
 static int a_mode(const s2v_conv_params *p);
 
-// the LDS-DMA ring kernels take AMODE-0 convolutions (direct, zero padding, cin % 32 == 0) with no
-// prologue (in_scale / pre_act) and <= 32 filter taps, packed split weights
-static bool ring_ok(const s2v_conv_params *p) {
-    return a_mode(p) == 0 && !p->b_kn && !p->in_scale && p->pre_act == S2V_ACT_NONE && p->kh * p->kw <= 32 &&
-           !p->x_split;
-}
 
 static const TileCfg &tile_cfg(const s2v_conv_params *p, int tile) {
     return tiled_x3(p) ? kX3Tiles[tile].t : kTiles[tile];
@@ -1029,7 +1010,6 @@ static Plan make_plan_x3(const s2v_conv_params *p, int M, Plan pl) {
     for (int i = 0; i < kNumX3; ++i) {
         const X3Cfg &c = kX3Tiles[i];
         if (c.tflops <= 0.f) continue;                          // forced-only configurations
-        if (c.ring && !ring_ok(p)) continue;
         if (p->b_kn && c.t.nw != 4) continue;
         if (c.t.bm >= 256 && c.t.bn >= 128 && am != 0 && am != 3) continue;   // generic gathers spill there
         // the 256 / 512-row narrow-N tiles on per-row gathers: measured slower than 128x64 (256x64, r02)
@@ -1177,9 +1157,6 @@ static int validate(const s2v_conv_params *p, int &M, int &K) {
                 "conv2d: bad force_tile %d", p->force_tile);
     S2V_REQUIRE(!(tiled_x3(p) && p->b_kn && p->force_tile > 0 && kX3Tiles[p->force_tile - 1].t.nw != 4),
                 "conv2d: b_kn operands need a 4-wave split-bf16 tile (force_tile 4..6)");
-    S2V_REQUIRE(!(tiled_x3(p) && p->force_tile > 0 && kX3Tiles[p->force_tile - 1].ring && !ring_ok(p)),
-                "conv2d: force_tile %d is an LDS-DMA ring tile: needs a direct zero-padded conv, cin %% 32 == 0, "
-                "no in_scale / pre_act, <= 32 taps", p->force_tile);
     if (tiled_x3(p) && p->force_tile > 0) {
         // a forced tile must not read weight rows past the packed [npad] rows (the planner never
         // picks such a tile: the kernels load whole BN-row slabs of B without a row guard)
@@ -1559,7 +1536,7 @@ extern "C" int s2v_conv2d_plan(const s2v_conv_params *p, int *out6) {
     }
     const TileCfg &t = tile_cfg(p, pl.tile);
     out6[0] = t.bm; out6[1] = t.bn; out6[2] = t.wm;
-    out6[3] = tiled_x3(p) ? (kX3Tiles[pl.tile].ring ? 6 : x3_amode(p, t)) : a_mode(p);   // 6: conv_ring_x3
+    out6[3] = tiled_x3(p) ? x3_amode(p, t) : a_mode(p);
     out6[4] = p->b_kn != 0;
     out6[5] = pl.splits;
     out6[6] = tiled_x3(p) ? p->prec : 0;
@@ -1645,11 +1622,7 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
     const bool bkn = p->b_kn != 0;
     const TileCfg &t = tile_cfg(p, pl.tile);
     dim3 grid(cdiv(M, t.bm), cdiv(p->cout, t.bn), batch * pl.splits);
-    if (tiled_x3(p) && kX3Tiles[pl.tile].ring) {
-        a.wt = (const float *)p->wt_x3;
-        if (p->prec == S2V_PREC_BF16X3) launch_conv_ring<0>(kX3Tiles[pl.tile].ring - 1, a, grid, s);
-        else launch_conv_ring<1>(kX3Tiles[pl.tile].ring - 1, a, grid, s);
-    } else if (tiled_x3(p)) {
+    if (tiled_x3(p)) {
         if (!bkn) a.wt = (const float *)p->wt_x3;
         const int am = x3_amode(p, t);
         if (am == 4) {
