@@ -484,6 +484,33 @@ __device__ __forceinline__ void epilogue_tile_fn(const ConvArgs &a, float *Cs, i
                 if (rsrc && e.res_after) v += rv;
                 yb[out_row(a, m)] = v;
             }
+        } else if (a.y_step <= 1 && a.d2s_c <= 0 && (!e.res || e.res_simple)) {
+            // per-(image, channel) scale and / or per-pixel add on a dense output (GPEN / GFPGAN StyledConv:
+            // demod scale + noise): the row's image index advances incrementally instead of a division per
+            // element (store_epilogue), which made the epilogue as long as the main loop of a 64-channel tile
+            const int hw = a.oh * a.ow;
+            const int rr0 = tid / TPR;
+            int m = m0 + c0 + rr0;
+            int img = m / hw, rem = m - img * hw;
+            float *__restrict__ yb = a.y + (long long)bidx * a.y_bs + out_col(a, n);
+            const float *pix = e.pix_add ? e.pix_add + (long long)bidx * a.oh * a.ow * a.n : nullptr;
+            const float *rsrc = e.res ? e.res + (long long)bidx * a.res_bs + n : nullptr;
+#pragma unroll 1
+            for (int rr = rr0; rr < clim; rr += RSTEP, m += RSTEP, rem += RSTEP) {
+                while (rem >= hw) { rem -= hw; ++img; }
+                float v = Cs[rr * LDC + cn] * sc;
+                if (e.nc_scale) v *= e.nc_scale[(long long)img * e.nc_ns + n];
+                v += sh;
+                if (pix) v += e.pix_w * pix[m];
+                float rv = 0.f;
+                if (rsrc) {
+                    rv = rsrc[(long long)m * e.res_cs];
+                    if (!e.res_after) v += rv;
+                }
+                v = fast_act(v, e.act, slope);
+                if (rsrc && e.res_after) v += rv;
+                yb[(long long)m * a.ycs] = v;
+            }
         } else {
 #pragma unroll 1
             for (int rr = tid / TPR; rr < clim; rr += RSTEP) store_epilogue(a, bidx, m0 + c0 + rr, n, Cs[rr * LDC + cn]);
