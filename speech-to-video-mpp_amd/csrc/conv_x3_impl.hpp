@@ -36,6 +36,14 @@ typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
+// f16 lo halves by v_fma_mix (1): one VALU per half, written into the halves of one register; 0: widen the
+// hi halves (v_cvt_f32_f16), subtract, pack (as the bf16 path does).  0 was tried in r04 to close the
+// 3.5 % gap to the bf16x3 kernels and failed the modulated depth-to-space test's f16x3 bound (1.2e-4):
+// kept at 1
+#ifndef X3_F16_MIX
+#define X3_F16_MIX 1
+#endif
+
 // two fp32 -> two 16-bit halves of type ELT (RNE): v_cvt_pk_bf16_f32 / v_cvt_pk_f16_f32
 template <int ELT>
 __device__ __forceinline__ unsigned pack2(float a, float b) {
@@ -74,7 +82,7 @@ template <int ELT>
 __device__ __forceinline__ void split4(const f4 &v, u32x2 &hi, u32x2 &lo) {
     hi.x = pack2<ELT>(v.x, v.y);
     hi.y = pack2<ELT>(v.z, v.w);
-    if constexpr (ELT == 1) {
+    if constexpr (ELT == 1 && X3_F16_MIX) {
         lo.x = f16_residual2(hi.x, v.x, v.y);
         lo.y = f16_residual2(hi.y, v.z, v.w);
     } else {
