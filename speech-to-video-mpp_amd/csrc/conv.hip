@@ -1290,9 +1290,18 @@ static long long x_extent_bytes(const s2v_conv_params *p) {
     return ((long long)p->n * p->h * p->w - 1) * p->xcs * 4 + (long long)p->cin * 4;
 }
 
+// 1x1 convs over cin % 8 == 0 (not % 32) channels take the buffer-load path too: the last 32-channel
+// K-slice is partial and the lanes whose 8 channels lie past cin load zeros (r04: LNet's 48^2 st2 over
+// 48 channels ran the per-row float4 gather)
+static bool x3_partial_1x1(const s2v_conv_params *p) {
+    return p->kh == 1 && p->kw == 1 && p->cin % 8 == 0 && p->cin % 32 != 0 && p->in_mode == S2V_IN_DIRECT &&
+           p->pad_mode == S2V_PAD_ZERO && !p->b_kn && !p->x_split && a_mode(p) == 1 && p->pre_act == S2V_ACT_NONE &&
+           !p->in_scale;   // (an input scale would be read past cin by the masked lanes' prologue)
+}
+
 static int x3_amode(const s2v_conv_params *p, const TileCfg &t) {
-    const int am = a_mode(p);
-    if (am != 0 || p->b_kn || p->kh * p->kw > 32 || t.bm % (16 * t.nw) != 0) return am;
+    const int am = x3_partial_1x1(p) ? 0 : a_mode(p);
+    if (am != 0 || p->b_kn || p->kh * p->kw > 32 || t.bm % (16 * t.nw) != 0) return a_mode(p);
     if (x_extent_bytes(p) >= (1LL << 31) || (long long)p->npad * p->kpad * 4 >= (1LL << 31)) return am;
     return 4;
 }

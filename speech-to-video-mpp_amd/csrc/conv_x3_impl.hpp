@@ -308,7 +308,8 @@ __device__ __forceinline__ void conv_x3_tile(const ConvArgs &a, int L, int gx, i
     const char *__restrict__ wtb = (const char *)wtf;                      // split view (packed)
     const int kt0 = split * a.tps;
     const int kt1 = min(a.ktiles, kt0 + a.tps);
-    const int taps = a.kh * a.kw, nsl = a.cin >> 5;
+    // buffer loads: a partial last channel slice (1x1, cin % 8 == 0, conv.hip x3_partial_1x1)
+    const int taps = a.kh * a.kw, nsl = BUF ? (a.cin + 31) >> 5 : a.cin >> 5;
     const bool kperm = (AMODE == 0 || AMODE == 3) && !BKN && taps > 1;
     const int ak = (tid & 7) * 4;
 
@@ -397,15 +398,18 @@ __device__ __forceinline__ void conv_x3_tile(const ConvArgs &a, int L, int gx, i
             const int kt = (AMODE == 0 || AMODE == 3) ? ld.kt(nsl) : ld.i;
             if constexpr (BUF) {
                 const int c8 = ld.cs * 32 + 8 * (tid & 3);
+                const bool cok = c8 < a.cin;             // false only in a partial last slice
                 rc[p][u] = c8;
                 if constexpr (PSC) {
                     if (PSC1 && one_img) {
                         if (ld.cs != sc_cs) {
-                            sc0 = *(const f4 *)(sc_base + c8);
-                            sc1 = *(const f4 *)(sc_base + c8 + 4);
+                            if (cok) {
+                                sc0 = *(const f4 *)(sc_base + c8);
+                                sc1 = *(const f4 *)(sc_base + c8 + 4);
+                            }
                             sc_cs = ld.cs;
                         }
-                    } else if (a.in_scale) {
+                    } else if (a.in_scale && cok) {
 #pragma unroll
                         for (int j = 0; j < AR8; ++j) {
                             const float *sp = a.in_scale + (long long)R.img[j] * a.in_scale_ns + c8;
@@ -417,7 +421,7 @@ __device__ __forceinline__ void conv_x3_tile(const ConvArgs &a, int L, int gx, i
                 const int toff = ((ld.ky * a.dh * a.w + ld.kx * a.dw) * a.xcs + ld.cs * 32) * 4;
 #pragma unroll
                 for (int j = 0; j < AR8; ++j) {
-                    const int vo = ((tmask[j] >> ld.tap) & 1u) ? rowoff[j] + toff : (int)0x80000000;
+                    const int vo = (cok && ((tmask[j] >> ld.tap) & 1u)) ? rowoff[j] + toff : (int)0x80000000;
                     ra[p][u][2 * j] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(xrs, vo, 0, 0));
                     ra[p][u][2 * j + 1] =
                         __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(xrs, vo + 16, 0, 0));

@@ -872,3 +872,28 @@ def test_conv_rowpack_matches_reference(ctx, sprec, n, h, w, cin, cout, k, sl):
     for dx in range(k):
         want[..., dx * cin:(dx + 1) * cin] = xp[:, :, :, dx:dx + w].permute(0, 2, 3, 1)
     assert torch.equal(packed.t.double().cpu(), want.float().double())
+
+
+@pytest.mark.parametrize("cin,cout,tile", [(48, 96, 0), (40, 64, 4), (24, 48, 5), (8, 32, 0), (48, 256, 1), (72, 128, 11)])
+def test_conv1x1_partial_slice_buffer_path(ctx, prec, cin, cout, tile):
+    """1x1 convs over cin % 8 == 0 but not % 32 channels (LNet's 48^2 st2: 48 channels) on the buffer-load
+    x3 path with a partial last K-slice (lanes past cin load zeros), on a channel slice of a wider tensor,
+    with residual + bias + act, split-K, against fp64 F.conv2d."""
+    if prec == "f32" and tile > 6:
+        pytest.skip("the f32 table has 6 tiles")
+    n, h, w = 2, 19, 23
+    x = rnd(n, cin + 8, h, w, seed=101)
+    wt = rnd(cout, cin, 1, 1, seed=102) / math.sqrt(cin)
+    b = rnd(cout, seed=103)
+    r = rnd(n, cout, h, w, seed=104)
+    cw = ConvW(wt.float(), b.float(), DEV)
+    xv = nhwc(x.float()).slice(8, cin)
+    y = NHWC.empty(n, h, w, cout, DEV)
+    rv = nhwc(r.float())
+    ops.conv2d(ctx, xv, cw, y, act=ops.ACT_LRELU, alpha=0.2, res=rv, force_tile=tile,
+               force_splits=2 if cin > 32 else 0)
+    xr = x[:, 8:]
+    ref = F.leaky_relu(F.conv2d(xr, wt, b) + r, 0.2)
+    err = (to_nchw(y) - ref).abs()
+    bound = conv_bound(xr, wt, 1, 0, 1)
+    assert (err <= REL[prec] * (bound + 1) + 1e-5).all(), f"max err {err.max():.3e}"
