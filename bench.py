@@ -127,6 +127,11 @@ def live_roofline(forward, workload="lipsync"):
     from s2v_amd.engine import enet as _enet, lnet as _lnet
     saved = (_lnet.BRANCHES, _enet.OVERLAP)
     _lnet.BRANCHES = _enet.OVERLAP = False
+    # one unhooked forward first: a kernel's first launch in the process also loads its code object
+    # (HIP loads kernels lazily), which made a 28 us conv the "dominant" symbol of a cold pre-pass
+    with torch.no_grad():
+        forward()
+    torch.cuda.synchronize()
     ops.CONV_HOOK = hook
     try:
         with torch.no_grad():

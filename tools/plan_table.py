@@ -88,7 +88,8 @@ class PlanOps:
         p.nc_scale = nc_scale.data_ptr() if nc_scale is not None else None
         p.pix_add = pix_add.data_ptr() if pix_add is not None else None
         if res is not None:
-            p.res, p.res_cs, p.res_h, p.res_w = res.data_ptr(), res.stride(2), res.shape[1], res.shape[2]
+            _, rh, rw, _, rcs, _ = _nv(res, out_step)
+            p.res, p.res_cs, p.res_h, p.res_w = res.data_ptr(), rcs, rh, rw
         p.act, p.batch, p.out_pool, p.x_split, p.prec = act, 1, int(out_pool), int(x_split), prec
         p.force_tile, p.force_splits, p.grid_cap = force_tile, force_splits, grid_cap
         p.wt_x3 = wt.data_ptr() if prec else None
@@ -96,7 +97,7 @@ class PlanOps:
 
     def modulated_conv2d_(self, x, y, wt, s, d, wbuf, cout, kernel, padding, in_mode, prec, x_split, scale, shift,
                           pix_add, pix_w, res, res_after, act, alpha, ws, force_splits, st0, st1, st2, x_scale, flag,
-                          dry, d2s=0):
+                          dry, d2s=0, *rest):
         p = _lib.ConvParams()
         n, h, w, c, xcs, xns = _nv(x)
         p.x, p.n, p.h, p.w, p.cin, p.xcs = x.data_ptr(), 1, h, w, c, xcs
@@ -123,7 +124,7 @@ class PlanOps:
         return self._plan(p, "modconv", (n, h, w, c, oh, ow, cout, p.kh, p.kw, 0))
 
     def gemm_kn_(self, a, b, out, batch, a_bs, b_bs, out_bs, res, res_bs, act, alpha, prec, ws, force_tile,
-                 force_splits, dry):
+                 force_splits, dry, *rest):
         p = _lib.ConvParams()
         M, K, N = a.shape[-2], a.shape[-1], b.shape[-1]
         p.x, p.n, p.h, p.w, p.cin, p.xcs = a.data_ptr(), 1, 1, M, K, K
