@@ -107,6 +107,22 @@ UP2_GROUP_PIXELS = 16 * 48 * 48
 STAMP = None
 _NOSTAMP = (None, None, [0, 1, 1])
 _GROUPING = False       # inside conv_group: launches are recorded (no per-launch stamps)
+# Tuned (x3 tile, split-K) of split-precision conv launches whose planner choice (csrc/conv.hip
+# make_plan_x3's time model) measured slower than another configuration: a table measured on MI355X by
+# tools/tune_perfdb.py (every conv launch of the LNet / ENet / DNet forwards, each candidate tile and
+# split factor graph-timed against the planner's own choice), keyed by conv_key().  Only entries that
+# beat the planner by more than 3 % are kept; every other launch stays with the planner.
+# S2V_PERFDB=0 ignores the table.
+PERFDB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "perfdb_mi355x.json")
+PERFDB = {}
+if os.environ.get("S2V_PERFDB", "1") != "0" and os.path.exists(PERFDB_PATH):
+    import json as _json
+    with open(PERFDB_PATH) as _f:
+        PERFDB = {k: (int(v["tile"]), int(v["splits"])) for k, v in _json.load(_f)["entries"].items()}
+# tools/tune_perfdb.py: called as TUNE(ctx, key, relaunch, plan_of, yv, resv) for every launch conv_key()
+# covers; relaunch(tile, splits) runs the conv with that forced configuration, plan_of(tile, splits) is its
+# s2v_conv2d_plan (0, 0: the planner's own choice)
+TUNE = None
 LAST_GROUP = 0          # 1: the last conv_group launched as one grouped kernel, 0: one by one
 
 
@@ -539,6 +555,14 @@ def _conv_flops(x, cw, yv, pool):
     return 2.0 * pix * cw.kh * cw.kw * cw.cin * cw.cout
 
 
+def conv_key(x, cw, yv, out_step, pool, prec) -> str:
+    """Signature of a conv launch for PERFDB: input view geometry, filter geometry and modes, output
+    view geometry, output step / pool, precision code (what the planner's choice depends on)."""
+    return (f"x{x.n}x{x.h}x{x.w}x{x.c}c{x.cs}|k{cw.kh}x{cw.kw}s{cw.sh}x{cw.sw}p{cw.ph}x{cw.pw}d{cw.dh}x{cw.dw}"
+            f"m{cw.in_mode}{cw.pad_mode}|y{yv.shape[1]}x{yv.shape[2]}x{cw.cout}c{yv.stride(2)}|o{out_step}{int(pool)}"
+            f"|p{prec}")
+
+
 def _conv(ctx, x, cw, yv, out_step, act, alpha, resv, res_after, res_offset, nc_scale, in_scale, pre_act, pre_alpha,
           pix_add, pix_w, scale, shift, force_tile, force_splits, pool=False):
     """One ``s2v::conv2d_`` launch: x an NHWC view, yv / resv torch views (out_step 2: a strided
@@ -554,12 +578,21 @@ def _conv(ctx, x, cw, yv, out_step, act, alpha, resv, res_after, res_offset, nc_
     cap = int(getattr(ctx, "grid_cap", 0))
     sc = cw.scale if scale is None else scale
     sh = cw.shift if shift is None else shift
+    key = None
+    if (PERFDB or TUNE is not None) and prec != PREC_F32 and not (force_tile or force_splits or x_split or cap or
+                                                                   _GROUPING):
+        key = conv_key(x, cw, yv, out_step, pool, prec)
+        force_tile, force_splits = PERFDB.get(key, (0, 0))
 
-    def launch(ws, dry=False, st=_NOSTAMP):
+    def launch(ws, dry=False, st=_NOSTAMP, ft=None, fs=None):
         return S2V.conv2d_(x.v, yv, cw.wt, wsplit, wscale, cw.cout, [cw.kh, cw.kw], [cw.sh, cw.sw], [cw.ph, cw.pw],
                            [cw.dh, cw.dw], cw.in_mode, cw.pad_mode, prec, sc, sh, in_scale, nc_scale, pre_act, pre_alpha,
                            pix_add, pix_w, resv, list(res_offset), res_after, act, alpha, out_step, pool, x_split != 0,
-                           ws, cap, force_tile, force_splits, st[0], st[1], st[2], xscale, flag, dry)
+                           ws, cap, force_tile if ft is None else ft, force_splits if fs is None else fs, st[0], st[1],
+                           st[2], xscale, flag, dry)
+    if TUNE is not None and key is not None:
+        TUNE(ctx, key, lambda ft, fs: _with_ws(ctx, lambda ws: launch(ws, False, _NOSTAMP, ft, fs)[0]),
+             lambda ft, fs: launch(ctx.ws.tensor(), True, _NOSTAMP, ft, fs)[1:], yv, resv)
     _run_conv(ctx, launch, x, cw, yv, pool, in_scale, nc_scale, pix_add, resv)
 
 

@@ -111,3 +111,49 @@ def test_parsenet_plan(dry):
     eng.forward(ops.Ctx("cpu"), x, torch.empty(2, 19, 512, 512), torch.empty(2, 3, 512, 512))
     # encoder conv + 4 down blocks (3 convs) + 10 body blocks (2) + 4 up blocks (3) + 2 heads
     assert dry.calls["conv2d_"] == 1 + 12 + 20 + 12 + 2 and dry.calls["eltwise_"] == 1
+
+
+def test_perfdb_table_and_lookup(dry, monkeypatch):
+    """The shipped perf-db (ops.PERFDB_PATH, tools/tune_perfdb.py) is well formed, and a conv whose
+    conv_key() is in the table is launched with the table's forced (tile, split-K); an explicit
+    force_tile, or a key not in the table, leaves the planner's choice (0, 0)."""
+    import json
+    import os
+    with open(ops.PERFDB_PATH) as f:
+        db = json.load(f)
+    assert db["entries"] and set(db["workloads"]) >= {"lnet", "dnet", "lipsync", "enhance"}
+    for k, v in db["entries"].items():
+        assert k.startswith("x") and k.count("|") == 4, k
+        assert 1 <= v["tile"] <= 11 and v["splits"] in (1, 2, 3, 4, 6, 8, 12, 16), (k, v)
+        assert v["us"] < 0.97 * v["planner_us"], (k, v)
+    if os.environ.get("S2V_PERFDB", "1") != "0":
+        assert len(ops.PERFDB) == len(db["entries"])
+    seen = []
+    real = ops.S2V
+
+    class Rec:
+        def __getattr__(self, name):
+            fn = getattr(real, name)
+            if name != "conv2d_":
+                return fn
+
+            def rec(*a):
+                seen.append(tuple(a[31:33]))
+                return fn(*a)
+            return rec
+    monkeypatch.setattr(ops, "S2V", Rec())
+    prev = ops.set_precision("f16x3")
+    try:
+        ctx = ops.Ctx("cpu")
+        x = ops.NHWC(torch.zeros(16, 14, 14, 64))
+        cw = ops.ConvW(torch.zeros(96, 64, 3, 3), None, "cpu")
+        y = ops.NHWC(torch.zeros(16, 12, 12, 96))
+        key = ops.conv_key(x, cw, y.v, 1, False, ops.PREC_F16X3)
+        monkeypatch.setattr(ops, "PERFDB", {key: (7, 12)})
+        ops.conv2d(ctx, x, cw, y)
+        ops.conv2d(ctx, x, cw, y, force_tile=2)
+        monkeypatch.setattr(ops, "PERFDB", {key + "?": (7, 12)})
+        ops.conv2d(ctx, x, cw, y)
+    finally:
+        ops.set_precision(prev)
+    assert seen == [(7, 12), (2, 0), (0, 0)], seen
