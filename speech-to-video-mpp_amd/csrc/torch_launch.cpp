@@ -355,7 +355,7 @@ std::vector<int64_t> modulated_conv2d_(const Tensor &x, const Tensor &y, const T
                                        double pix_w, const OptT &res, bool res_after_act, int64_t act, double alpha,
                                        const OptT &ws, int64_t force_splits, const OptT &stamps, const OptT &stamp_ctr,
                                        at::IntArrayRef stamp_pos, double x_scale, const OptT &nonfinite, bool dry,
-                                       int64_t d2s) {
+                                       int64_t d2s, int64_t force_tile) {
     const c10::DeviceGuard guard(x.device());
     const at::Device dev = x.device();
     TORCH_CHECK(!g_recording, "conv group: modulated convs cannot be group members");
@@ -371,7 +371,7 @@ std::vector<int64_t> modulated_conv2d_(const Tensor &x, const Tensor &y, const T
         const Tensor yc = y.slice(1, 0, y.size(1), 2).slice(2, 0, y.size(2), 2);   // parity class (0, 0)
         conv_common(p, x, yc, cout / 4, kernel, at::IntArrayRef(one, 2), padding, at::IntArrayRef(one, 2), in_mode,
                     S2V_PAD_ZERO, scale, shift, c10::nullopt, 0.0, res, at::IntArrayRef(zero, 2), false, act, alpha, 2,
-                    false, x_split, true, prec, 0, force_splits);
+                    false, x_split, true, prec, force_tile, force_splits);
         p.cout = (int)cout;
         p.d2s_cout = (int)(cout / 4);
         TORCH_CHECK(!p.scale || (scale->numel() >= cout), "modconv d2s: scale needs cout entries");
@@ -386,7 +386,7 @@ std::vector<int64_t> modulated_conv2d_(const Tensor &x, const Tensor &y, const T
     } else {
         conv_common(p, x, y, cout, kernel, at::IntArrayRef(one, 2), padding, at::IntArrayRef(one, 2), in_mode,
                     S2V_PAD_ZERO, scale, shift, pix_add, pix_w, res, at::IntArrayRef(zero, 2), res_after_act, act, alpha,
-                    1, false, x_split, true, prec, 0, force_splits);
+                    1, false, x_split, true, prec, force_tile, force_splits);
     }
     f32(wt, dev, "modconv wt");
     TORCH_CHECK(wt.dim() == 2 && wt.is_contiguous() && wt.size(0) >= cout, "modconv wt: packed [npad, kpad]");
@@ -898,7 +898,7 @@ TORCH_LIBRARY_FRAGMENT(s2v, m) {
           "Tensor? pix_add, "
           "float pix_w, Tensor? res, "
           "bool res_after_act, int act, float alpha, Tensor? ws, int force_splits, Tensor(s!)? stamps, Tensor? stamp_ctr, "
-          "int[3] stamp_pos, float x_scale, Tensor(f!)? nonfinite, bool dry, int d2s=0) -> int[]");
+          "int[3] stamp_pos, float x_scale, Tensor(f!)? nonfinite, bool dry, int d2s=0, int force_tile=0) -> int[]");
     m.def("amax_(Tensor x, Tensor(a!) out) -> ()");
     // conv groups: host-side recording, no tensor to dispatch on (catch-all kernels)
     m.def("group_begin_() -> ()", &group_begin_);

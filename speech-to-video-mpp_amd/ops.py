@@ -793,12 +793,20 @@ def modulated_conv2d(ctx: Ctx, x: NHWC, cw: ConvW, y: NHWC, s: torch.Tensor, d: 
                             f"conv runs in {PRECISION!r} (code {prec})")
     sh = cw.shift if shift is None else shift            # the layer bias (epilogue shift) unless overridden
     xscale, flag = _range(ctx, cw, x, prec)
+    key, force_tile = None, 0
+    if (PERFDB or TUNE is not None) and prec != PREC_F32 and not (force_splits or x_split):
+        key = conv_key(x, cw, yv, 1, False, prec) + f"|mod{int(d is not None)}{int(d2s)}"
+        force_tile, force_splits = PERFDB.get(key, (0, 0))
 
-    def launch(ws, dry=False, st=_NOSTAMP):
+    def launch(ws, dry=False, st=_NOSTAMP, ft=None, fs=None):
         return S2V.modulated_conv2d_(x.v, yv, cw.wt, s, d, wbuf, cw.cout, [cw.kh, cw.kw], [cw.ph, cw.pw], cw.in_mode,
                                      prec,
                                      x_split != 0, cw.scale, sh, pix_add, pix_w, resv, res_after, act, alpha, ws,
-                                     force_splits, st[0], st[1], st[2], xscale, flag, dry, int(d2s))
+                                     force_splits if fs is None else fs, st[0], st[1], st[2], xscale, flag, dry, int(d2s),
+                                     force_tile if ft is None else ft)
+    if TUNE is not None and key is not None:
+        TUNE(ctx, key, lambda ft, fs: _with_ws(ctx, lambda ws: launch(ws, False, _NOSTAMP, ft, fs)[0]),
+             lambda ft, fs: launch(ctx.ws.tensor(), True, _NOSTAMP, ft, fs)[1:], yv, resv)
     # roofline accounting on the conv's own grid (one parity class of y x all 4 x c columns = the
     # upsampled conv's FLOPs)
     _run_conv(ctx, launch, x, cw, yv[:, ::2, ::2, :] if d2s else yv, False, pix_add=pix_add, resv=resv)

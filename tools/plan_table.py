@@ -97,7 +97,7 @@ class PlanOps:
 
     def modulated_conv2d_(self, x, y, wt, s, d, wbuf, cout, kernel, padding, in_mode, prec, x_split, scale, shift,
                           pix_add, pix_w, res, res_after, act, alpha, ws, force_splits, st0, st1, st2, x_scale, flag,
-                          dry, d2s=0, *rest):
+                          dry, d2s=0, force_tile=0, *rest):
         p = _lib.ConvParams()
         n, h, w, c, xcs, xns = _nv(x)
         p.x, p.n, p.h, p.w, p.cin, p.xcs = x.data_ptr(), 1, h, w, c, xcs
@@ -119,7 +119,7 @@ class PlanOps:
         p.pix_add = pix_add.data_ptr() if pix_add is not None else None
         if res is not None:
             p.res, p.res_cs, p.res_h, p.res_w = res.data_ptr(), res.stride(2), res.shape[1], res.shape[2]
-        p.act, p.prec, p.x_split, p.force_splits = act, prec, int(x_split), force_splits
+        p.act, p.prec, p.x_split, p.force_splits, p.force_tile = act, prec, int(x_split), force_splits, force_tile
         p.wt_x3 = wbuf.data_ptr() if prec else None
         return self._plan(p, "modconv", (n, h, w, c, oh, ow, cout, p.kh, p.kw, 0))
 
