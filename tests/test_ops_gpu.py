@@ -343,6 +343,30 @@ def test_layernorm2d(ctx, c, hw):
         assert (to_nchw(y) - (ref + res)).abs().max() < 2e-5
 
 
+@pytest.mark.parametrize("strided", [False, True])
+def test_layernorm2d_multiblock(ctx, strided):
+    """Several statistics blocks per image (dense rows: the contiguous four-loads-in-flight reduction;
+    a channel slice of a wider tensor: the strided one) and LN_EPT-step applies with ragged tails."""
+    n, c, h, w = 2, 64, 66, 50
+    x = rnd(n, c, h, w, seed=23) * 2 + 0.5
+    wgt, b = rnd(c, seed=24), rnd(c, seed=25)
+    if strided:
+        wide = NHWC(torch.zeros(n, h, w, c + 8, device=DEV))
+        wide.t[..., 4: 4 + c] = x.float().permute(0, 2, 3, 1).to(DEV)
+        xv = wide.slice(4, c)
+    else:
+        xv = nhwc(x.float())
+    for pool in (False, True):
+        oh, ow = (h // 2, w // 2) if pool else (h, w)
+        y = NHWC.empty(n, oh, ow, c, DEV)
+        ops.layernorm2d(ctx, xv, wgt.float().to(DEV), b.float().to(DEV), y, act=ops.ACT_LRELU, alpha=0.2, pool=pool)
+        ref = F.leaky_relu(F.layer_norm(x, x.shape[1:], wgt[:, None, None].expand(x.shape[1:]),
+                                        b[:, None, None].expand(x.shape[1:]), 1e-5), 0.2)
+        if pool:
+            ref = F.avg_pool2d(ref, 2)
+        assert (to_nchw(y) - ref).abs().max() < 2e-5
+
+
 @pytest.mark.parametrize("c", [70, 72, 300])          # scalar path, float4 path, two 256-channel blocks
 def test_instnorm_adain(ctx, c):
     for (h, w) in ((12, 12), (70, 40)):
