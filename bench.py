@@ -111,6 +111,7 @@ def live_roofline(forward, workload="lipsync"):
     durations are then re-measured with each launch repeated back to back (second pass)."""
     from s2v_amd import ops
     recs = []
+    grids = {}      # round(flops) -> {symbol: grid work-items} (to find a launch shape's PMC row)
 
     def hook(ctx, p, flops, launch):
         sym = ops.conv_symbol(ctx, p)
@@ -121,6 +122,10 @@ def live_roofline(forward, workload="lipsync"):
         e.record()
         recs.append((sym, flops, splits, s, e, (p.n, p.h, p.w, p.cin, p.oh, p.ow, p.cout, p.kh, p.kw,
                                                 p.in_scale, p.nc_scale, p.pix_add, p.res)))
+        pl = p.plan     # [bm, bn, wm, amode, b_kn, splits, prec, nw, ...]: the launch's work-items
+        if pl[0] > 0 and pl[1] > 0:
+            grids.setdefault(round(flops), {})[sym] = (-(-p.n * p.oh * p.ow // pl[0]) * -(-p.cout // pl[1]) *
+                                                       max(1, pl[5]) * 64 * max(1, pl[7]))
 
     # per-kernel durations are measured with the side-stream branches serialised (engine.lnet
     # BRANCHES, engine.enet OVERLAP), so concurrent kernels do not inflate each other's time
@@ -199,15 +204,7 @@ def live_roofline(forward, workload="lipsync"):
     total_flops = sum(v["flops"] for v in per.values())
     # HBM bytes per launch of the same symbol from the PMC passes of this workload (tools/gpu_profile.sh:
     # separate FETCH_SIZE / WRITE_SIZE runs of this bench command; the newest round's file wins)
-    traffic, traffic_src = None, None
-    for rnd in ("r04", "r03", "r02", "r01"):
-        pmc = os.path.join(ROOT, "profiles", f"pmc_{rnd}_{workload}.json")
-        if os.path.exists(pmc):
-            with open(pmc) as f:
-                traffic = json.load(f).get("per_launch_bytes", {}).get(dom)
-            if traffic is not None:
-                traffic_src = os.path.relpath(pmc, ROOT)
-                break
+    traffic, traffic_src = pmc_traffic(workload, dom)
     return {
         "bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
         "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
@@ -216,6 +213,8 @@ def live_roofline(forward, workload="lipsync"):
         "conv_family": {"achieved": round(total_flops / (total_ms * 1e-3) / 1e12, 2),
                         "ms_per_step": round(total_ms, 3), "symbols": len(per)},
         "per_kernel": per,
+        "_grids": grids,
+        "_workload": workload,
     }
 
 
@@ -290,6 +289,29 @@ def _peak(sym):
         else FP32_MFMA_PEAK_TFLOPS
 
 
+PMC_ROUND = "r04"     # only this round's PMC passes describe the current build
+
+
+def pmc_traffic(workload, sym, grid=None):
+    """HBM bytes per launch of ``sym`` from this round's PMC passes of the workload
+    (profiles/pmc_<round>_<workload>.json, tools/pmc_traffic.py): the (symbol, grid) row nearest to
+    ``grid`` work-items when given, else the symbol's average; (None, None) without a file."""
+    pmc = os.path.join(ROOT, "profiles", f"pmc_{PMC_ROUND}_{workload}.json")
+    if not os.path.exists(pmc):
+        return None, None
+    with open(pmc) as f:
+        doc = json.load(f)
+    src = os.path.relpath(pmc, ROOT)
+    rows = {int(k.rsplit("grid=", 1)[1]): v for k, v in doc.get("per_grid", {}).items()
+            if k.startswith(sym + " grid=") and k.rsplit("grid=", 1)[1].isdigit()}
+    if grid and rows:
+        g = min(rows, key=lambda r: abs(r - grid) / max(r, grid))
+        if abs(g - grid) <= 0.05 * max(g, grid):
+            return rows[g]["bytes_per_launch"], f"{src} [grid={g}]"
+    t = doc.get("per_launch_bytes", {}).get(sym)
+    return (t, src + " (symbol average)") if t is not None else (None, None)
+
+
 def replay_roofline(pre, stamper):
     """roofline of the dominant kernel from the timed (graph-replayed, overlapped) launches, plus
     the same figure for every other stamped kernel symbol (``by_kernel``): the style encoder's
@@ -310,11 +332,30 @@ def replay_roofline(pre, stamper):
     if not d:
         r["timing"] = "isolated (no stamped launches in the timed run)"
     else:
-        e = by[pre["kernel"]]
+        # the dominant symbol's launches grouped by problem (FLOPs per launch): the headline entry is the
+        # group with the most stamped time — one launch shape, so one grid, as rocprof's by-grid rows
+        # (a symbol-wide average also counts the symbol's small launches of other layers, e.g. LNet
+        # convs the perf-db puts on the same tile); the symbol-wide figure stays in by_kernel
+        groups = {}
+        for du, fl in d:
+            groups.setdefault(round(fl), []).append(du)
+        shapes = []
+        for fl, ds in groups.items():
+            us = sum(ds)
+            ach = fl * len(ds) / (us * 1e-6) / 1e12
+            shapes.append({"flops_per_launch": fl, "launches": len(ds), "avg_launch_us": round(us / len(ds), 2),
+                           "achieved": round(ach, 2), "frac": round(ach / _peak(pre["kernel"]), 4), "_us": us})
+        shapes.sort(key=lambda g: -g["_us"])
+        for g in shapes:
+            g.pop("_us")
+        e = shapes[0]
+        grid = pre.get("_grids", {}).get(e["flops_per_launch"], {}).get(pre["kernel"])
+        tr, src = pmc_traffic(pre.get("_workload", ""), pre["kernel"], grid)
         r.update(achieved=e["achieved"], frac=e["frac"], avg_launch_us=e["avg_launch_us"], timed_launches=e["launches"],
+                 flops_per_launch=e["flops_per_launch"], traffic=tr, traffic_source=src,
                  timing="in-kernel clock stamps (s_memrealtime, first block start to last block end) of every launch "
-                        "of this kernel in the timed, graph-replayed steps",
-                 isolated=iso)
+                        "of this kernel and launch shape in the timed, graph-replayed steps",
+                 shape_groups=shapes[:6], isolated=iso)
     if by:
         r["by_kernel"] = by
     return r
@@ -986,7 +1027,8 @@ def worker(args):
     config["conv_arith"] = ARITH[args.precision]
     if pre is not None:
         result["roofline"] = replay_roofline(pre, stamper)
-        result["roofline"].pop("per_kernel", None)
+        for k in ("per_kernel", "_grids", "_workload"):
+            result["roofline"].pop(k, None)
         from s2v_amd.engine import enet as _enet
         if args.workload in ("lipsync", "pipeline", "clip") and _enet.OVERLAP and _enet.style_grid(dev):
             result["roofline"]["grid_cap"] = (
@@ -995,7 +1037,8 @@ def worker(args):
                 "separately under by_kernel; the headline entry is the full-grid launches only")
     elif rank == 0 and not args.no_roofline and cuda:
         result["roofline"] = live_roofline(wl.forward, args.workload)
-        result["roofline"].pop("per_kernel", None)
+        for k in ("per_kernel", "_grids", "_workload"):
+            result["roofline"].pop(k, None)
     if world == 1 and not args.no_alt and cuda and wl.graphable:
         result["alt_precision"] = {}
         for other in ARITH:

@@ -32,18 +32,23 @@ def per_dispatch(root, counter):
                 if row.get("Counter_Name") != counter:
                     continue
                 key = (path, row.get("Dispatch_Id") or row.get("Correlation_Id"))
-                vals[key] = (row["Kernel_Name"], float(row["Counter_Value"]) + vals.get(key, ("", 0.0))[1])
+                dur = (float(row.get("End_Timestamp") or 0) - float(row.get("Start_Timestamp") or 0)) / 1e3
+                vals[key] = (row["Kernel_Name"], float(row["Counter_Value"]) + vals.get(key, ("", 0.0))[1],
+                             row.get("Grid_Size", ""), dur)
     return vals
 
 
 def summarise(fetch_dir, write_dir):
-    agg = defaultdict(lambda: {"fetch_kib": 0.0, "write_kib": 0.0, "fetch_n": 0, "write_n": 0})
-    for (_, _), (name, v) in per_dispatch(fetch_dir, "FETCH_SIZE").items():
-        agg[name]["fetch_kib"] += v
-        agg[name]["fetch_n"] += 1
-    for (_, _), (name, v) in per_dispatch(write_dir, "WRITE_SIZE").items():
-        agg[name]["write_kib"] += v
-        agg[name]["write_n"] += 1
+    agg = defaultdict(lambda: {"fetch_kib": 0.0, "write_kib": 0.0, "fetch_n": 0, "write_n": 0, "us": 0.0})
+    for (_, _), (name, v, grid, dur) in per_dispatch(fetch_dir, "FETCH_SIZE").items():
+        for k in (name, f"{name} grid={grid}"):
+            agg[k]["fetch_kib"] += v
+            agg[k]["fetch_n"] += 1
+            agg[k]["us"] += dur
+    for (_, _), (name, v, grid, _) in per_dispatch(write_dir, "WRITE_SIZE").items():
+        for k in (name, f"{name} grid={grid}"):
+            agg[k]["write_kib"] += v
+            agg[k]["write_n"] += 1
     out = {}
     for name, a in agg.items():
         if not a["fetch_n"] or not a["write_n"]:
@@ -51,7 +56,7 @@ def summarise(fetch_dir, write_dir):
         f = a["fetch_kib"] / a["fetch_n"]
         w = a["write_kib"] / a["write_n"]
         out[name] = {"launches": a["fetch_n"], "fetch_kib_raw": round(f, 3), "write_kib": round(w, 3),
-                     "bytes_per_launch": round(1024 * (2 * f + w))}
+                     "bytes_per_launch": round(1024 * (2 * f + w)), "pass_us": round(a["us"], 1)}
     return out
 
 
@@ -61,8 +66,11 @@ def main():
     kern = summarise(fetch_dir, write_dir)
     doc = {"label": label,
            "formula": "bytes = 1024 * (2 * FETCH_SIZE + WRITE_SIZE) per launch, averaged per kernel symbol "
-                      "(gfx950 FETCH_SIZE half-count correction, MI355X_MICROARCH.md §HBM)",
-           "per_launch_bytes": {k: v["bytes_per_launch"] for k, v in kern.items()},
+                      "and per (symbol, grid) ('<symbol> grid=<work-items>'; pass_us = the launches' summed "
+                      "duration in this PMC pass) (gfx950 FETCH_SIZE half-count correction, MI355X_MICROARCH.md §HBM)",
+           "per_launch_bytes": {k: v["bytes_per_launch"] for k, v in kern.items() if " grid=" not in k},
+           "per_grid": {k: {"bytes_per_launch": v["bytes_per_launch"], "launches": v["launches"], "pass_us": v["pass_us"]}
+                        for k, v in kern.items() if " grid=" in k},
            "kernels": dict(sorted(kern.items(), key=lambda kv: -kv[1]["bytes_per_launch"] * kv[1]["launches"]))}
     with open(out_path, "w") as f:
         json.dump(doc, f, indent=1)

@@ -3,7 +3,7 @@
 # graph replay or one of the few eager calibration / capture forwards), by symbol and by grid, phase timeline;
 # then the same bench command's stamped roofline for comparison
 set -o pipefail
-OUT=gpurun_out/profcheck; mkdir -p $OUT
+OUT=${OUT:-gpurun_out/profcheck}; mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/lipsync" -o run -- \
   python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-alt --no-roofline > "$OUT/lipsync.log" 2>&1 || exit $?
