@@ -599,12 +599,15 @@ __global__ __launch_bounds__(256) void adain_heads(const float *__restrict__ hid
 // vectors of the (few) segments the block's outputs use are staged in LDS as [segment][unit][sample],
 // read as float4 broadcasts; the four partial sums meet in LDS.  (v1 read 8 samples' hidden values
 // from global memory per weight load: 264 us for 26 MB of weights, r03.)
-constexpr int ADAIN_BO = 64, ADAIN_NB = 16, ADAIN_SEGW = 4, ADAIN_NHMAX = 128;
+// SEGW x NHMAX: the staged window (4 segments of <= 128 units: LNet's ADAIN heads; 1 segment of <= 512
+// units: GFPGAN's per-layer style modulations, one 512-d latent per decoder layer)
+constexpr int ADAIN_BO = 64, ADAIN_NB = 16, ADAIN_NHMAX = 128, ADAIN_NHMAX_WIDE = 512;
+template <int ADAIN_SEGW, int NHMAX>
 __global__ __launch_bounds__(256) void adain_heads2(const float *__restrict__ hid, int batch, int hid_ns, int nh,
                                                     const float *__restrict__ w2t, const float *__restrict__ bias,
                                                     const int *__restrict__ seg, int total, float *__restrict__ out,
                                                     int out_ns) {
-    __shared__ __attribute__((aligned(16))) float hs[ADAIN_SEGW][ADAIN_NHMAX][ADAIN_NB];
+    __shared__ __attribute__((aligned(16))) float hs[ADAIN_SEGW][NHMAX][ADAIN_NB];
     __shared__ float part[4][ADAIN_NB][ADAIN_BO + 1];
     __shared__ int srange[2];
     const int tid = threadIdx.x, lane = tid & 63, q = tid >> 6;
@@ -846,8 +849,14 @@ extern "C" int s2v_adain_params(const float *hid, int batch, int hid_ns, int nhi
     S2V_REQUIRE(hid && w2t && seg && out && batch > 0 && nhidden > 0 && total > 0 && out_ns >= total,
                 "adain_params: bad args");
     if (nhidden <= ADAIN_NHMAX) {
-        adain_heads2<<<dim3(cdiv(total, ADAIN_BO), cdiv(batch, ADAIN_NB)), 256, 0, (hipStream_t)stream>>>(
+        adain_heads2<4, ADAIN_NHMAX><<<dim3(cdiv(total, ADAIN_BO), cdiv(batch, ADAIN_NB)), 256, 0, (hipStream_t)stream>>>(
             hid, batch, hid_ns, nhidden, w2t, bias, seg, total, out, out_ns);
+        return check_launch("adain_heads2");
+    }
+    if (nhidden <= ADAIN_NHMAX_WIDE) {
+        adain_heads2<1, ADAIN_NHMAX_WIDE><<<dim3(cdiv(total, ADAIN_BO), cdiv(batch, ADAIN_NB)), 256, 0,
+                                            (hipStream_t)stream>>>(hid, batch, hid_ns, nhidden, w2t, bias, seg, total,
+                                                                   out, out_ns);
         return check_launch("adain_heads2");
     }
     adain_heads<<<dim3(cdiv(total, 256), cdiv(batch, 8)), 256, 0, (hipStream_t)stream>>>(

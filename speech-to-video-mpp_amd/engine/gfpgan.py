@@ -64,8 +64,25 @@ class GFPGANEngine:
         self.rgb1 = StyleLayer(sd, d + "to_rgb1.", dev, False, False, True)
         self.convs = [StyleLayer(sd, f"{d}style_convs.{j}.", dev, True, j % 2 == 0, False) for j in range(2 * nd)]
         self.rgbs = [StyleLayer(sd, f"{d}to_rgbs.{i}.", dev, False, False, True) for i in range(nd)]
-        for L in [self.conv1, self.rgb1] + self.convs + self.rgbs:
-            L.mod = ConvW(L.mod_w, L.mod_b, dev)
+        # every decoder layer's style modulation (a Linear on its own 512-d latent, different_w,
+        # stylegan2_clean_arch.py:66-99) as ONE segmented GEMV launch (ops.adain_params, the kernel of
+        # LNet's ADAIN bank) instead of one small conv per layer: layer L's s is columns
+        # [style_off[L], + L.cin) of its output, segment = the layer's latent index
+        order = [(self.conv1, 0), (self.rgb1, 1)]
+        for lvl in range(nd):
+            i = 1 + 2 * lvl
+            order += [(self.convs[2 * lvl], i), (self.convs[2 * lvl + 1], i + 1), (self.rgbs[lvl], i + 2)]
+        ws, bs, segs, self.style_off, off = [], [], [], {}, 0
+        for L, j in order:
+            ws.append(L.mod_w)
+            bs.append(L.mod_b)
+            segs.append(torch.full((L.cin,), j if different_w else 0, dtype=torch.int32))
+            self.style_off[id(L)] = off
+            off += L.cin
+        self.style_w2t = torch.cat(ws, 0).t().contiguous().to(dev)         # [num_style_feat, total]
+        self.style_b = torch.cat(bs).contiguous().to(dev)
+        self.style_seg = torch.cat(segs).contiguous().to(dev)
+        self.style_total = off
         self.noise_bufs = [sd[f"{d}noises.noise{i}"].float().reshape(-1).to(dev) for i in range(2 * nd + 1)]
         self._noise_cache = {}
         self.noise_seed = 0x6F9A
@@ -91,14 +108,14 @@ class GFPGANEngine:
         ops.conv2d(ctx, tr, c2, out, act=ops.ACT_LRELU, alpha=LRELU, res=out, res_after=True)
         return out
 
-    def _style(self, ctx, L, lat: NHWC):
-        s = NHWC.empty(lat.n, 1, 1, L.cin, self.device)
-        ops.conv2d(ctx, lat, L.mod, s)
-        return s.t.view(lat.n, -1)
+    def _style(self, L, sall):
+        """Layer L's modulation s [B, cin] (a column range of the bank output ``sall``)."""
+        o = self.style_off[id(L)]
+        return sall[:, o: o + L.cin]
 
-    def _style_conv(self, ctx, L, x: NHWC, lat: NHWC, noise):
+    def _style_conv(self, ctx, L, x: NHWC, sall, noise):
         b, dev = x.n, self.device
-        s = self._style(ctx, L, lat)
+        s = self._style(L, sall)
         if L.upsample:
             xu = NHWC.empty(b, 2 * x.h, 2 * x.w, x.c, dev)
             ops.resize_nhwc(ctx, x, xu, scale_factor=2)
@@ -151,8 +168,8 @@ class GFPGANEngine:
         # ---- StyleGAN2 decoder with SFT (gfpganv1_clean_arch.py:89-117)
         nsf = self.nsf
 
-        def lat(j):
-            return NHWC(style.t, j * nsf if self.different_w else 0, nsf)
+        sall = ops.empty((b, self.style_total), dev)
+        ops.adain_params(ctx, style.t.view(b, -1), nsf, self.style_w2t, self.style_b, self.style_seg, sall)
         nl = 2 * self.levels + 1
         if noises is not None:
             noise = [None if t is None else t.reshape(b, -1).contiguous() for t in noises]
@@ -167,23 +184,23 @@ class GFPGANEngine:
         else:
             noise = self._stored_noise(b)
         cur = NHWC(self.const.expand(b, -1, -1, -1).contiguous())
-        cur = self._style_conv(ctx, self.conv1, cur, lat(0), noise[0])
+        cur = self._style_conv(ctx, self.conv1, cur, sall, noise[0])
         skip = NHWC.empty(b, cur.h, cur.w, 3, dev)
-        s = self._style(ctx, self.rgb1, lat(1))
+        s = self._style(self.rgb1, sall)
         ops.conv2d(ctx, cur, self.rgb1.conv, skip, in_scale=s)
         i = 1
         for lvl in range(self.levels):
-            cur = self._style_conv(ctx, self.convs[2 * lvl], cur, lat(i), noise[2 * lvl + 1])
+            cur = self._style_conv(ctx, self.convs[2 * lvl], cur, sall, noise[2 * lvl + 1])
             if i < 2 * len(conds):
                 scale, shift = conds[(i - 1) // 2]
                 half = cur.c // 2 if self.sft_half else 0
                 part = cur.slice(half, cur.c - half)
                 ops.eltwise(ctx, part, part, mul=scale, add=shift)
-            cur = self._style_conv(ctx, self.convs[2 * lvl + 1], cur, lat(i + 1), noise[2 * lvl + 2])
+            cur = self._style_conv(ctx, self.convs[2 * lvl + 1], cur, sall, noise[2 * lvl + 2])
             R = self.rgbs[lvl]
             rgb = NHWC.empty(b, cur.h, cur.w, 3, dev)
             ops.resize_nhwc(ctx, skip, rgb, scale_factor=2)
-            s = self._style(ctx, R, lat(i + 2))
+            s = self._style(R, sall)
             ops.conv2d(ctx, cur, R.conv, rgb, in_scale=s, res=rgb)
             skip = rgb
             i += 2

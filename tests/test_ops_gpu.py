@@ -411,10 +411,12 @@ def test_row_layernorm_attention(ctx):
 
 
 @pytest.mark.parametrize("b,nh,L,total,contig", [(3, 128, 5, 300, False), (20, 100, 9, 1000, True),
-                                                  (16, 128, 12, 4000, True), (2, 160, 3, 130, False)])
+                                                  (16, 128, 12, 4000, True), (2, 160, 3, 130, False),
+                                                  (4, 512, 23, 1700, True), (3, 600, 2, 100, False)])
 def test_adain_params_and_demod(ctx, b, nh, L, total, contig):
-    """adain_heads2 (nh <= 128: 64-output blocks, 16-sample chunks, segment windows of 4) and the v1
-    kernel (nh > 128); segments random per output or in contiguous runs as AdainBank lays them out."""
+    """adain_heads2 (nh <= 128: 64-output blocks, 16-sample chunks, segment windows of 4; nh <= 512:
+    one-segment windows — GFPGAN's per-layer style bank) and the v1 kernel (nh > 512); segments random
+    per output or in contiguous runs as AdainBank / the GFPGAN bank lay them out."""
     hid = rnd(b, L * nh, seed=26).float().to(DEV)
     if contig:
         seg = (torch.arange(total) * L // total).int()
