@@ -74,10 +74,17 @@ class _EngineMixin:
         out = fn()
         state = ops.end_forward(ctx, calibrating)
         done.add(ops.PRECISION)
-        if state == "scaled":
+        for _ in range(ops.CALIB_PASSES):
+            if state not in ("scaled", "recalibrate"):
+                break
+            # "recalibrate": an upstream overflow hid some layer's range; measure it again behind the
+            # layers scaled so far.  "scaled": run again with the new pre-scales.
+            recal = state == "recalibrate"
+            if recal:
+                ops.begin_calibration(ctx)
             out = fn()
-            state = ops.end_forward(ctx, False)
-        if state == "overflow":
+            state = ops.end_forward(ctx, recal)
+        if state:                               # overflow, or calibration still unsettled after the passes
             with ops.precision("bf16x3"):
                 out = fn()
             ctx.reruns += 1

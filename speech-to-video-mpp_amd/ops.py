@@ -674,6 +674,12 @@ def _amax_into(t: torch.Tensor, out: torch.Tensor):
     S2V.amax_(t, out)
 
 
+# calibration passes of an engine's first eager forward beyond the first (models._EngineMixin._guarded):
+# each pass measures the layers an upstream overflow left unmeasured; past the limit the forward runs in
+# bf16x3
+CALIB_PASSES = 4
+
+
 def begin_calibration(ctx):
     """Start a calibration forward on ``ctx``'s lane: uncalibrated f16x3 layers launch unscaled and
     record their operand's max |v| (no host sync) until end_forward."""
@@ -682,9 +688,12 @@ def begin_calibration(ctx):
 
 def end_forward(ctx, calibrating: bool) -> str:
     """After an eager forward on ``ctx``'s lane (one host sync): apply the measured scales of a
-    calibration forward and read + clear the lane's non-finite flag.  Returns "scaled" when the forward
-    must run again because a layer now carries a pre-scale, "overflow" when a launch produced a
-    non-finite value (run the forward again in bf16x3), "" otherwise."""
+    calibration forward and read + clear the lane's non-finite flag.  Returns "recalibrate" when a layer
+    measured a non-finite operand (an upstream layer overflowed before its own pre-scale existed: the
+    layer stays uncalibrated and the next forward must be a calibration forward again, which measures it
+    behind the now-scaled upstream layers), "scaled" when the forward must run again because a layer now
+    carries a pre-scale, "overflow" when a launch produced a non-finite value (run the forward again in
+    bf16x3), "" otherwise."""
     root = _root(ctx)
     cal = getattr(root, "calib", None) if calibrating else None
     root.calib = None
@@ -702,11 +711,17 @@ def end_forward(ctx, calibrating: bool) -> str:
                 m *= float(vals[ss // _Calibration.SLOTS][ss % _Calibration.SLOTS])
             key = (id(cw), prec)
             per[key] = (cw, prec, max(per[key][2], m) if key in per else m)
+        recal = False
         for cw, prec, m in per.values():
+            if not math.isfinite(m):
+                recal = True                  # left uncalibrated: measured again by the next calibration pass
+                continue
             sc = x_scale_for(m)
             cw.__dict__.setdefault("_xscale", {})[prec] = sc
             cw.x_amax = m
             scaled = scaled or sc != 1.0
+        if recal:
+            return "recalibrate"
     if scaled:
         return "scaled"
     return "overflow" if bad else ""

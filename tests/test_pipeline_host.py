@@ -107,3 +107,98 @@ def test_broadcast_and_gather_world2_gloo(n):
         p.join(120)
         assert p.exitcode == 0
     assert q.get(timeout=10) == [i % 251 for i in range(n)]
+
+
+# ---------------------------------------------------------------- run_sharded end to end
+class _CodedPipeline:
+    """Stand-in for LipSyncPipeline.run: frame i of the range [start, stop) is coded from everything the
+    real device path consumes for it — its mel window (chunks[start + i], indexed absolutely), its DNet
+    coefficient window (coeffs[i], this rank's slice of dnet_coefficients) and its source frame
+    (src[i] from src_provider) — so a wrong window, coefficient range or source shard changes the clip."""
+    device = torch.device("cpu")
+
+    def run(self, chunks, src, coeffs, start, stop):
+        n = stop - start
+        assert src.shape[0] == n and coeffs.shape[0] == n and stop <= chunks.shape[0]
+        out = torch.zeros((n, 3, 4, 4), dtype=torch.uint8)
+        for i in range(n):
+            out[i, 0] = int(chunks[start + i].double().sum().item()) % 251
+            out[i, 1] = int(abs(coeffs[i].double() * torch.arange(1, 27, dtype=torch.float64)).sum().item() * 7) % 251
+            out[i, 2] = int(src[i].double().sum().item()) % 251
+        return out
+
+
+def _stub_audio(monkeypatch):
+    """CPU stand-ins for the two HIP mel ops: an index-coded [80, 1 + len // 200] 'spectrogram' and the
+    real window starts (audio.chunk_starts, inference.py:209-216)."""
+    from s2v_amd import audio
+
+    def mel(wav, pad_mode="constant"):
+        t = 1 + wav.numel() // 200
+        return (torch.arange(t, dtype=torch.float32)[None, :] + torch.arange(80, dtype=torch.float32)[:, None] * 0.5
+                + float(wav.double().sum()) * 1e-3)
+
+    def chunks(m, fps=25.0, step=16):
+        st = audio.chunk_starts(m.shape[1], fps, step)
+        return torch.stack([m[None, :, s: s + step] for s in st])
+    monkeypatch.setattr(P.audio, "melspectrogram", mel)
+    monkeypatch.setattr(P.audio, "mel_chunks", chunks)
+
+
+def _clip_inputs(frames, samples):
+    rng = np.random.default_rng(5)
+    wav = rng.standard_normal(samples).astype(np.float32)
+    sem = rng.standard_normal((frames, 262)).astype(np.float32)
+    exp = rng.standard_normal(64).astype(np.float32)
+    return wav, sem, exp
+
+
+def _src_provider(start, stop):
+    return torch.stack([torch.full((3, 8, 8), float(i % 97), dtype=torch.float32) for i in range(start, stop)]) \
+        if stop > start else torch.zeros((0, 3, 8, 8))
+
+
+def _sharded_worker(rank, world, port, frames, samples, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mp_ = pytest.MonkeyPatch()
+        _stub_audio(mp_)
+        wav, sem, exp = _clip_inputs(frames, samples)
+        if rank != 0:                     # only rank 0 holds the per-clip host data (inference.py:209-222)
+            wav = sem = exp = None
+        out = P.run_sharded(_CodedPipeline(), wav, sem, exp, _src_provider)
+        if rank == 0:
+            q.put(out.numpy())
+        else:
+            q.put(None if out is None else "rank 1 returned frames")
+        mp_.undo()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("frames,samples", [(30, 16000), (9, 16000 * 3), (1, 3200)])
+def test_run_sharded_world2_gloo_matches_world1(monkeypatch, frames, samples):
+    """pipeline.run_sharded at world 2 (gloo): meta broadcast, the per-clip tensor broadcasts, per-rank
+    mel windows and coefficient windows, the per-rank pipeline.run on its shard and the gather to rank 0.
+    Rank 0's clip equals the world-1 clip and rank 1 gets None (pipeline.py:239-262; reference contract
+    inference.py:209-222: n = min(mel chunks, frames)).  The cases cover more frames than mel windows,
+    more windows than frames, and a one-frame clip that leaves rank 1 an empty shard."""
+    _stub_audio(monkeypatch)
+    wav, sem, exp = _clip_inputs(frames, samples)
+    ref = P.run_sharded(_CodedPipeline(), wav, sem, exp, _src_provider).numpy()     # world 1
+    n_chunks = len(P.audio.chunk_starts(1 + samples // 200))
+    assert ref.shape == (min(n_chunks, frames), 3, 4, 4)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, 2, port, frames, samples, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(2)]
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    assert sum(g is None for g in got) == 1, got
+    clip = next(g for g in got if g is not None)
+    assert isinstance(clip, np.ndarray) and np.array_equal(clip, ref)

@@ -152,3 +152,47 @@ def test_model_forward_out_of_range_batch_reruns_in_bf16x3(f16x3):
     with ops.precision("bf16x3"):
         ref = net(mel, big)
     assert torch.equal(out, ref)
+
+
+def test_first_forward_out_of_range_recalibrates(f16x3):
+    """the engine's first (calibration) forward at a face input 1e5 x larger.  The first conv's
+    split operand passes 65504, so in the unscaled calibration pass every layer behind it measures a
+    non-finite amax.  Those layers stay uncalibrated and the next pass calibrates them again behind the
+    now pre-scaled first conv (ops.end_forward -> "recalibrate"): no layer keeps a scale measured from
+    inf / NaN, nothing falls back to bf16x3, and the output matches the exact-f32 forward."""
+    from helpers import synth_sd
+    from s2v_amd import models
+    net = models.LNet()
+    net.load_state_dict(synth_sd("lnet"), strict=True)
+    net.eval()
+    g = torch.Generator(device=DEV).manual_seed(11)
+    mel = torch.rand((2, 1, 80, 16), generator=g, device=DEV) * 8 - 4
+    big = torch.rand((2, 6, 96, 96), generator=g, device=DEV) * 1.0e5
+    out = net(mel, big)                                  # first forward: calibration passes
+    eng, lanes = net._s2v_engines[str(big.device)]
+    ctx = lanes[0]
+    assert ctx.reruns == 0 and torch.isfinite(out).all()
+    amaxes = []
+
+    def walk(o, seen):
+        if id(o) in seen:
+            return
+        seen.add(id(o))
+        if isinstance(o, ConvW) and ops.PREC_F16X3 in o.__dict__.get("_xscale", {}):
+            amaxes.append(o.x_amax)            # (a ConvW's launched forms: .rowpack / .poly, walked below)
+        if isinstance(o, (list, tuple)):
+            for v in o:
+                walk(v, seen)
+        elif isinstance(o, dict):
+            for v in o.values():
+                walk(v, seen)
+        elif hasattr(o, "__dict__") and type(o).__module__.startswith("s2v_amd"):
+            for v in vars(o).values():
+                walk(v, seen)
+    walk(eng, set())
+    assert len(amaxes) > 100 and all(math.isfinite(m) for m in amaxes)
+    assert max(amaxes) > 65504                           # the first conv's operand, scaled down
+    with ops.precision("f32"):
+        ref = net(mel, big)
+    d = (out - ref).abs()
+    assert float(d.max()) <= 1e-4 and float(d.mean()) <= 1e-5, (float(d.max()), float(d.mean()))

@@ -50,21 +50,67 @@ def test_lipsync_b16_graph_replay_vs_oracle():
     finally:
         ops.CONV_HOOK = None
     assert any(s.startswith("void s2v::conv_igemm_x3_persist<256, 256,") for s in syms), "style encoder grid cap"
-    outs = []
+    outs, lows = [], []
     for _ in range(3):
-        out, _low = runner.replay()
+        out, low = runner.replay()
         outs.append(out.clone())
+        lows.append(low.clone())
     torch.cuda.synchronize()
-    for o in outs[1:]:
-        assert torch.equal(o, outs[0])
+    for o, lo in zip(outs[1:], lows[1:]):
+        assert torch.equal(o, outs[0]) and torch.equal(lo, lows[0])
     idx = [0, 1, 14, 15]
     sd = synth_sd("enet")
     with torch.no_grad():
-        ro, _ = nets.enet_forward(sd, torch.from_numpy(mel[idx]), torch.from_numpy(face[idx]),
-                                  torch.from_numpy(gt[idx]))
+        ro, rl = nets.enet_forward(sd, torch.from_numpy(mel[idx]), torch.from_numpy(face[idx]),
+                                   torch.from_numpy(gt[idx]))
     got = outs[-1][idx]
     within(clamp01(got), clamp01(ro), BAR, "replayed b16 clamped bar")
     within(got, ro, TOL["f16x3"]["enet"], "replayed b16 out")
+    # LNet's B=16 output inside the replayed step (ENet.forward's ``low``: the 96x96 LNet frames)
+    within(lows[-1][idx], rl, TOL["f16x3"]["low"], "replayed b16 low")
+
+
+def test_lnet_bench_capture_vs_oracle():
+    """configs[1] as bench.py times it (bench.LNetOnly: the device bilinear resize of B=16 256x256
+    crops to 96x96, then LNet.forward, captured by runtime.GraphRunner with warmup 1 and replayed):
+    frames 0, 1, 14, 15 of the third replay against oracle.nets.lnet_forward on F.interpolate'd crops,
+    at the LNet bounds of tests/test_models_gpu.py.  The pre-sigmoid logits are captured in the same
+    graph (the engine's ``logits=`` output: one more 7x7 conv at the end) and compared too."""
+    import argparse
+
+    import torch.nn.functional as F
+
+    import bench
+    from oracle import nets
+    from s2v_amd.ops import NHWC
+    from s2v_amd.runtime import GraphRunner
+    if ops.PRECISION != "f16x3":
+        pytest.skip("the benchmarked arithmetic is f16x3")
+    args = argparse.Namespace(batch=16, size=256, lanes=1)
+    wl = bench.LNetOnly(args, torch.device(DEV, torch.cuda.current_device()), 0)
+    eng = wl.model._engine(wl.inputs[1].device)[0]
+    logits = NHWC.empty(16, 96, 96, 3, DEV)
+    orig = eng.forward
+    eng.forward = lambda ctx, a, f, o, logits_=None, pad_rgb=False: orig(ctx, a, f, o, logits=logits, pad_rgb=pad_rgb)
+    try:
+        runner = GraphRunner(lambda *x: wl.fn_lane(0, *x), list(wl.inputs), warmup=1)
+    finally:
+        del eng.forward
+    outs, lgs = [], []
+    for _ in range(3):
+        outs.append(runner.replay().clone())
+        lgs.append(logits.t.clone())
+    torch.cuda.synchronize()
+    for o, lg in zip(outs[1:], lgs[1:]):
+        assert torch.equal(o, outs[0]) and torch.equal(lg, lgs[0])
+    idx = [0, 1, 14, 15]
+    mel = wl.inputs[0][idx].cpu()
+    f96 = F.interpolate(wl.inputs[1][idx].cpu(), (96, 96), mode="bilinear", align_corners=False)
+    with torch.no_grad():
+        ro, aux = nets.lnet_forward(wl.sd, mel, f96, return_aux=True)
+    within(outs[-1][idx], ro, BAR, "lnet bench clamped bar")
+    within(outs[-1][idx], ro, TOL["f16x3"]["lnet"], "lnet bench out")
+    within(lgs[-1][idx].permute(0, 3, 1, 2), aux["logits"], TOL["f16x3"]["logits"], "lnet bench logits")
 
 
 def test_pipeline_full_batch_graph_replay_vs_oracle():

@@ -95,22 +95,21 @@ if __name__ == "__main__" and "--lnet" in sys.argv:
 
 
 def lnet_ffc(path, k=4):
-    """Every kernel of the k-th FFC of each decoder level in the last LNet forward of the trace (from the
-    k-th rfft2 of that size back to the previous FFC's InstanceNorm, up to the k-th FFC's InstanceNorm):
-    start offset, duration, end offset and name, so the per-FFC critical path can be read off."""
+    """Every kernel of the k-th FFC of each decoder level in the last LNet forward of the trace: the
+    kernels that start between the (k-1)-th and the (k+1)-th rfft2 launch of that size, sorted by start,
+    as start offset / duration / end offset / name, so the per-FFC critical path can be read off."""
     ks = load(path)
     for h in (12, 24, 48):
         rf = [i for i, (n, a, b) in enumerate(ks) if n.startswith(f"void s2v::rfft2_mf<{h},")]
         if len(rf) < 18:
+            print(f"level {h}: {len(rf)} rfft2 launches in the trace")
             continue
-        r = rf[-18 + k]
-        ins = [i for i, (n, a, b) in enumerate(ks) if "s2v::in_" in n.split("(")[0]]
-        prev = max(i for i in ins if i < r)
-        nxt = min(i for i in ins if i > r)
-        t0 = ks[prev][2]
-        print(f"level {h}x{h}, FFC {k}: {(ks[nxt][2] - t0) / 1e3:.1f} us from the previous InstanceNorm's end")
-        for n, a, b in ks[prev + 1: nxt + 1]:
-            print(f"  +{(a - t0) / 1e3:7.1f} {(b - a) / 1e3:7.1f} us -> +{(b - t0) / 1e3:7.1f}  {n.split('(')[0][:90]}")
+        lo, hi = ks[rf[-18 + k - 1]][1], ks[rf[-18 + k + 1]][1]
+        seg = sorted((a, b, n) for n, a, b in ks if lo <= a < hi)
+        t0 = ks[rf[-18 + k]][1]
+        print(f"level {h}x{h}, FFC {k}: window {(hi - lo) / 2e3:.1f} us per FFC, {len(seg)} kernels, offsets vs its rfft2")
+        for a, b, n in seg:
+            print(f"  {(a - t0) / 1e3:+8.1f} {(b - a) / 1e3:7.1f} us -> {(b - t0) / 1e3:+8.1f}  {n.split('(')[0][:90]}")
 
 
 if __name__ == "__main__" and "--ffc" in sys.argv:
