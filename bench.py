@@ -273,8 +273,10 @@ class Stamper:
         """{symbol: [(duration us, flops), ...]} of every stamped launch of the timed replays."""
         torch.cuda.synchronize()
         out = {}
+        self.replays = 0
         for L in self.lanes.values():
             c1 = int(L["ctr"].item())
+            self.replays += c1 - L["c0"]
             for sym, buf in L["buf"].items():
                 b = buf.cpu()
                 for r in range(L["c0"] + 1, c1 + 1):
@@ -328,6 +330,12 @@ def replay_roofline(pre, stamper):
         by[sym] = {"launches": len(recs), "avg_launch_us": round(us / len(recs), 2),
                    "flops_per_launch": fl / len(recs), "achieved": round(ach, 2), "peak": round(_peak(sym), 1),
                    "frac": round(ach / _peak(sym), 4)}
+        if "_persist<" in sym and pre.get("grid_cap_blocks"):
+            # persistent launches hold grid_cap_blocks CUs by design (one 512-thread block per CU): their rate
+            # against the chip's peak and against the share of the peak those CUs carry
+            held = pre["grid_cap_blocks"]
+            by[sym].update(held_cus=held, cus=pre.get("cus", 256),
+                           frac_of_held=round(ach / (_peak(sym) * held / pre.get("cus", 256)), 4))
     d = st.get(pre["kernel"], [])
     if not d:
         r["timing"] = "isolated (no stamped launches in the timed run)"
@@ -351,13 +359,21 @@ def replay_roofline(pre, stamper):
         e = shapes[0]
         grid = pre.get("_grids", {}).get(e["flops_per_launch"], {}).get(pre["kernel"])
         tr, src = pmc_traffic(pre.get("_workload", ""), pre["kernel"], grid)
-        r.update(achieved=e["achieved"], frac=e["frac"], avg_launch_us=e["avg_launch_us"], timed_launches=e["launches"],
+        reps = max(1, getattr(stamper, "replays", 0))
+        r.update(symbol_launches_per_forward=r.pop("launches", None),
+                 launches=round(e["launches"] / reps, 2),      # launches of THIS shape per step (avg_launch_us's set)
+                 achieved=e["achieved"], frac=e["frac"], avg_launch_us=e["avg_launch_us"], timed_launches=e["launches"],
                  flops_per_launch=e["flops_per_launch"], traffic=tr, traffic_source=src,
                  timing="in-kernel clock stamps (s_memrealtime, first block start to last block end) of every launch "
                         "of this kernel and launch shape in the timed, graph-replayed steps",
                  shape_groups=shapes[:6], isolated=iso)
     if by:
         r["by_kernel"] = by
+        # the stamped symbol with the most kernel time in the timed steps (the lipsync step's persistent
+        # style-encoder launches), as a first-class entry beside the headline launch shape
+        top = max(st.items(), key=lambda kv: sum(d for d, _ in kv[1]))[0]
+        r["time_dominant"] = dict(by[top], kernel=top,
+                                  ms_per_step=round(sum(d for d, _ in st[top]) / 1e3 / max(1, getattr(stamper, "replays", 1)), 3))
     return r
 
 
@@ -1026,10 +1042,13 @@ def worker(args):
     }
     config["conv_arith"] = ARITH[args.precision]
     if pre is not None:
-        result["roofline"] = replay_roofline(pre, stamper)
-        for k in ("per_kernel", "_grids", "_workload"):
-            result["roofline"].pop(k, None)
         from s2v_amd.engine import enet as _enet
+        if args.workload in ("lipsync", "pipeline", "clip") and _enet.OVERLAP and _enet.style_grid(dev):
+            pre["grid_cap_blocks"] = _enet.style_grid(dev)
+            pre["cus"] = torch.cuda.get_device_properties(dev).multi_processor_count
+        result["roofline"] = replay_roofline(pre, stamper)
+        for k in ("per_kernel", "_grids", "_workload", "grid_cap_blocks", "cus"):
+            result["roofline"].pop(k, None)
         if args.workload in ("lipsync", "pipeline", "clip") and _enet.OVERLAP and _enet.style_grid(dev):
             result["roofline"]["grid_cap"] = (
                 f"the style encoder's launches of the 256x256 tile (beside LNet) run as {_enet.style_grid(dev)} "

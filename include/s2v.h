@@ -336,6 +336,35 @@ int s2v_rfft2(const float *x, int n, int h, int w, int c, int xcs, const float *
 int s2v_irfft2(const float *spec, int n, int h, int w, int c, int scs, const float *tables, const float *res,
                int rcs, float *y, int ycs, s2v_stream_t stream);
 
+/* LNet's FFC (FineADAINLama, models/base_blocks.py:368-386; FFC models/ffc.py:176-233 with ratio 0.75) as
+ * three fused kernels per FFC at the decoder levels h in {12, 24, 48} (C = s2v_ffc_channels(h) = 1024 /
+ * 256 / 128; cl = C/4, cg = 3C/4, cc = cg/2; F = h (h/2 + 1)), n images.  Replaces the launch chain
+ * st1 -> rfft2 -> fu -> irfft2 -> st2 -> instnorm (the reference's SpectralTransform / FourierUnit
+ * forward, ffc.py:60-173, and ADAIN, base_blocks.py:127-157):
+ *   s2v_ffc_spec_fwd: t1 = relu(bn1(x_g conv1)) -> t1 [n][h*h][cc] dense, spec = rfftn(t1, ortho) ->
+ *                     spec [n][F][2cc] dense ((part, c) channel order, as s2v_rfft2); x_g: the block input's
+ *                     global channels (pitch xcs)
+ *   s2v_ffc_spec_inv: u = irfftn(relu(bn_fu(spec conv_fu))) + t1 -> u [n][h*h][cc] dense
+ *   s2v_ffc_norm:     z = [y_l | y_g + u conv2] (y [n][h*h][C] with conv_to_l's and conv_l2g's outputs, pitch
+ *                     ycs), out = act((z - mean) rstd (1 + gamma) + beta) (+ res); pad (optional, [n][h+2][h+2]
+ *                     pitch pad_cs) also receives F.pad(out, 1, 'reflect').  out may be y itself.
+ * w1 / wfu / w2: packed weights in the split layout of prec (s2v_split_weights with weight pre-scale
+ * wt_scale; kpad >= the K of the conv, npad >= 128); scale / shift: folded BatchNorm per output channel (may
+ * be NULL); x_scale: the f16x3 activation pre-scale of the conv's input (power of two, 1 = none); tables:
+ * s2v_fft_tables for (h, h); flag (may be NULL): set to 1 when an accumulator is not finite (the f16x3 range
+ * guard).  prec: S2V_PREC_F16X3 or S2V_PREC_BF16X3 (the exact-f32 arithmetic uses the separate kernels). */
+int s2v_ffc_channels(int h);
+int s2v_ffc_spec_fwd(const float *x_g, int xcs, int n, int h, const void *w1, int w1_kpad, float wt_scale, float x_scale,
+                     const float *scale, const float *shift, const float *tables, float *t1, float *spec, int *flag,
+                     int prec, s2v_stream_t stream);
+int s2v_ffc_spec_inv(const float *spec, int n, int h, const void *wfu, int wfu_kpad, float wt_scale, float x_scale,
+                     const float *scale, const float *shift, const float *tables, const float *t1, float *u, int *flag,
+                     int prec, s2v_stream_t stream);
+int s2v_ffc_norm(const float *y, int ycs, int n, int h, const float *u, const void *w2, int w2_kpad, float wt_scale,
+                 float x_scale, const float *gamma, const float *beta, int gb_ns, float eps, int act, float alpha,
+                 const float *res, int res_cs, float *out, int out_cs, float *pad, int pad_cs, int *flag, int prec,
+                 s2v_stream_t stream);
+
 /* Per-sample modulated conv weights (StyleGAN2 ModulatedConv2d, base_blocks.py:487-495,
  * stylegan2_clean_arch.py:66-80, gpen_model.py:245-256) from packed [npad][kpad] weights:
  *   out[b][o][k] = wt[o][k] * s[b][k % cin] * (d ? d[b][o] : 1)   (k < K; padding stays 0)

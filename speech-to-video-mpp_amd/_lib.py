@@ -94,6 +94,13 @@ _SIGS = {
     "s2v_fft_tables_floats": (_c_size, [_c_int, _c_int]),
     "s2v_rfft2": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_int, _vp]),
     "s2v_irfft2": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_int, _vp, _c_int, _vp]),
+    "s2v_ffc_channels": (_c_int, [_c_int]),
+    "s2v_ffc_spec_fwd": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_float, _c_float, _vp, _vp, _vp, _vp, _vp,
+                                  _vp, _c_int, _vp]),
+    "s2v_ffc_spec_inv": (_c_int, [_vp, _c_int, _c_int, _vp, _c_int, _c_float, _c_float, _vp, _vp, _vp, _vp, _vp, _vp,
+                                  _c_int, _vp]),
+    "s2v_ffc_norm": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _vp, _c_int, _c_float, _c_float, _vp, _vp, _c_int,
+                              _c_float, _c_int, _c_float, _vp, _c_int, _vp, _c_int, _vp, _c_int, _vp, _c_int, _vp]),
     "s2v_split_weights": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_float, _vp, _vp]),
     "s2v_split_act": (_c_int, [_vp, _c_ll, _c_int, _c_int, _c_int, _vp, _c_int, _vp]),
     "s2v_amax": (_c_int, [_vp, _c_ll, _c_int, _c_int, _vp, _vp]),

@@ -883,7 +883,11 @@ static const X3Cfg kX3Tiles[] = {
     // convs): 4x512^2 128 -> 64 199 (256x64 8-wave) -> 225 (512x64) / 233 (256x64 4-wave) TFLOP/s,
     // 16x256^2 64 -> 64 156 -> 171 / 183; at 96^2 and below 128x64 stays ahead (more blocks).  The
     // rates keep that order in the planner's model.  256x32 (4-wave): no faster than 128x32, forced-only.
-    {{512, 64, 8, 8, 1, 1}, 335.f, 1},  {{256, 64, 4, 4, 1, 1}, 350.f, 2},  {{256, 32, 4, 4, 1, 1}, 0.f, 2}};
+    {{512, 64, 8, 8, 1, 1}, 335.f, 1},  {{256, 64, 4, 4, 1, 1}, 350.f, 2},  {{256, 32, 4, 4, 1, 1}, 0.f, 2},
+    // deep-stage 4-wave tiles (r05): 2 or 4 K-slices per LDS stage, so a latency-bound small-grid conv (LNet's
+    // 12^2 - 48^2 layers: one block per CU, K loops of 6 - 72 slices) waits on half / a quarter as many
+    // load round trips; one block per CU by LDS.  Forced-only until measured (tools/lnet_convs.py --tiles)
+    {{64, 64, 2, 4, 4, 1}, 0.f, 1},     {{128, 64, 2, 4, 2, 1}, 0.f, 1},   {{128, 32, 4, 4, 2, 1}, 0.f, 1}};
 constexpr int kNumX3 = sizeof(kX3Tiles) / sizeof(kX3Tiles[0]);
 
 static const TileCfg &tile_cfg(const s2v_conv_params *p, int tile);
@@ -1302,7 +1306,9 @@ static bool x3_partial_1x1(const s2v_conv_params *p) {
 static int x3_amode(const s2v_conv_params *p, const TileCfg &t) {
     const int am = x3_partial_1x1(p) ? 0 : a_mode(p);
     if (am != 0 || p->b_kn || p->kh * p->kw > 32 || t.bm % (16 * t.nw) != 0) return a_mode(p);
-    if (x_extent_bytes(p) >= (1LL << 31) || (long long)p->npad * p->kpad * 4 >= (1LL << 31)) return am;
+    // past the 2^31-byte buffer offsets: the gather path the conv would take without buffer loads (a_mode,
+    // never AMODE 0 for a partial 1x1, which assumes whole 32-channel K-slices)
+    if (x_extent_bytes(p) >= (1LL << 31) || (long long)p->npad * p->kpad * 4 >= (1LL << 31)) return a_mode(p);
     return 4;
 }
 

@@ -356,7 +356,7 @@ __device__ __forceinline__ void conv_x3_tile(const ConvArgs &a, int L, int gx, i
     // input scale s[n, c] (StyleGAN2 modulation with shared weights) loaded with the A operand in issue()
     // instead of in the store phase, where its load was waited for right away (one memory round trip per
     // K-slice); only in tiles with register room (the 256-row / 512-row tiles keep the old path)
-    constexpr bool PSC = A8 && (BM * BN <= 128 * 128 || (BN == 64 && AR8 <= 4 && NW == 4));
+    constexpr bool PSC = A8 && KS == 1 && PF == 1 && (BM * BN <= 128 * 128 || (BN == 64 && AR8 <= 4 && NW == 4));
     static_assert(!PSC || (PF == 1 && KS == 1), "the input-scale registers follow one in-flight slice");
     f4 rsc[PF][KS][PSC ? 2 * AR8 : 1];
     // a tile whose rows all lie in one image (every tile of the 256^2 / 512^2 enhancer and DNet layers)
@@ -709,31 +709,74 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3_group(ConvGroup g) {
 }
 
 template <int BM, int BN, int WM, int NW, int KS, int PF, int ELT>
-static void launch_x3(const ConvArgs &a, int amode, bool bkn, dim3 grid, hipStream_t s) {
+static bool launch_x3(const ConvArgs &a, int amode, bool bkn, dim3 grid, hipStream_t s) {
     constexpr int NT = 64 * NW;
+    if constexpr (KS > 1) {
+        // the deep-stage tiles exist for the buffer-load A path only (compile time: 2 instances, not 10)
+        if (bkn || amode != 4) return false;
+        conv_igemm_x3<BM, BN, WM, NW, KS, PF, 4, 0, ELT><<<grid, NT, 0, s>>>(a);
+        return true;
+    }
     if (bkn) {
         if constexpr (NW == 4) {
             if (amode == 0) conv_igemm_x3<BM, BN, WM, NW, KS, PF, 0, 1, ELT><<<grid, NT, 0, s>>>(a);
             else if (amode == 1) conv_igemm_x3<BM, BN, WM, NW, KS, PF, 1, 1, ELT><<<grid, NT, 0, s>>>(a);
             else conv_igemm_x3<BM, BN, WM, NW, KS, PF, 2, 1, ELT><<<grid, NT, 0, s>>>(a);
+            return true;
         }
-        return;
+        return false;
     }
     switch (amode) {
         case 4:
             if constexpr (BM % (16 * NW) == 0) conv_igemm_x3<BM, BN, WM, NW, KS, PF, 4, 0, ELT><<<grid, NT, 0, s>>>(a);
+            else return false;
             break;
         case 0: conv_igemm_x3<BM, BN, WM, NW, KS, PF, 0, 0, ELT><<<grid, NT, 0, s>>>(a); break;
         case 1: conv_igemm_x3<BM, BN, WM, NW, KS, PF, 1, 0, ELT><<<grid, NT, 0, s>>>(a); break;
         case 2: conv_igemm_x3<BM, BN, WM, NW, KS, PF, 2, 0, ELT><<<grid, NT, 0, s>>>(a); break;
         default: conv_igemm_x3<BM, BN, WM, NW, KS, PF, 3, 0, ELT><<<grid, NT, 0, s>>>(a); break;
     }
+    return true;
 }
 
 // x3 kernel configurations (index = the host planner's tile id, conv.hip kX3Tiles)
 // the persistent form exists for the 256x256 tile with buffer-load A (the ENet style encoder's
 // layers; conv.hip only sets a.vgrid_* for that configuration)
 constexpr bool x3_has_persist(int cfg, int amode, bool bkn) { return cfg == 0 && amode == 4 && !bkn; }
+
+// The tile configurations are instantiated in three parts (conv_x3_{f16,bf16}{,_1,_2}.hip) so the six
+// translation units compile in parallel: part 0 = configurations 0 - 5, 1 = 6 - 11, 2 = 12 - 14.
+template <int ELT, int PART>
+bool launch_conv_x3_part(int cfg, const ConvArgs &a, int amode, bool bkn, dim3 grid, hipStream_t s) {
+    if constexpr (PART == 0) {
+        switch (cfg) {
+            case 0: return launch_x3<256, 256, 2, 8, 1, 1, ELT>(a, amode, bkn, grid, s);
+            case 1: return launch_x3<128, 128, 2, 8, 1, 1, ELT>(a, amode, bkn, grid, s);
+            case 2: return launch_x3<64, 128, 2, 8, 1, 1, ELT>(a, amode, bkn, grid, s);
+            case 3: return launch_x3<128, 64, 2, 4, 1, 1, ELT>(a, amode, bkn, grid, s);
+            case 4: return launch_x3<64, 64, 2, 4, 1, 1, ELT>(a, amode, bkn, grid, s);
+            default: return launch_x3<128, 32, 4, 4, 1, 1, ELT>(a, amode, bkn, grid, s);
+        }
+    } else if constexpr (PART == 1) {
+        switch (cfg) {
+            case 6: return launch_x3<256, 128, 4, 8, 1, 1, ELT>(a, amode, bkn, grid, s);
+            case 7: return launch_x3<256, 64, 8, 8, 1, 1, ELT>(a, amode, bkn, grid, s);
+            case 8: return launch_x3<512, 128, 4, 8, 1, 1, ELT>(a, amode, bkn, grid, s);   // N = 128 layers
+            // narrow-N tiles whose waves each cover 64 rows (r04): fewer LDS operand reads per MFMA than the
+            // 256x64 / 128x32 tiles (A fragments reused over all of N): 64-channel layers at 256^2 / 512^2
+            case 9: return launch_x3<512, 64, 8, 8, 1, 1, ELT>(a, amode, bkn, grid, s);
+            case 10: return launch_x3<256, 64, 4, 4, 1, 1, ELT>(a, amode, bkn, grid, s);
+            default: return launch_x3<256, 32, 4, 4, 1, 1, ELT>(a, amode, bkn, grid, s);
+        }
+    } else {
+        // deep-stage 4-wave tiles (KS 4 / 2 / 2): fewer load round trips in latency-bound small grids
+        switch (cfg) {
+            case 12: return launch_x3<64, 64, 2, 4, 4, 1, ELT>(a, amode, bkn, grid, s);
+            case 13: return launch_x3<128, 64, 2, 4, 2, 1, ELT>(a, amode, bkn, grid, s);
+            default: return launch_x3<128, 32, 4, 4, 2, 1, ELT>(a, amode, bkn, grid, s);
+        }
+    }
+}
 
 template <int ELT>
 int launch_conv_x3(int cfg, const ConvArgs &a, int amode, bool bkn, dim3 grid, hipStream_t s) {
@@ -746,22 +789,11 @@ int launch_conv_x3(int cfg, const ConvArgs &a, int amode, bool bkn, dim3 grid, h
         conv_igemm_x3_persist<256, 256, 2, 8, 1, 1, 4, 0, ELT><<<grid, 512, 0, s>>>(a);
         return 0;
     }
-    switch (cfg) {
-        case 0: launch_x3<256, 256, 2, 8, 1, 1, ELT>(a, amode, bkn, grid, s); break;
-        case 1: launch_x3<128, 128, 2, 8, 1, 1, ELT>(a, amode, bkn, grid, s); break;
-        case 2: launch_x3<64, 128, 2, 8, 1, 1, ELT>(a, amode, bkn, grid, s); break;
-        case 3: launch_x3<128, 64, 2, 4, 1, 1, ELT>(a, amode, bkn, grid, s); break;
-        case 4: launch_x3<64, 64, 2, 4, 1, 1, ELT>(a, amode, bkn, grid, s); break;
-        case 5: launch_x3<128, 32, 4, 4, 1, 1, ELT>(a, amode, bkn, grid, s); break;
-        case 6: launch_x3<256, 128, 4, 8, 1, 1, ELT>(a, amode, bkn, grid, s); break;
-        case 7: launch_x3<256, 64, 8, 8, 1, 1, ELT>(a, amode, bkn, grid, s); break;
-        case 8: launch_x3<512, 128, 4, 8, 1, 1, ELT>(a, amode, bkn, grid, s); break;   // N = 128 layers
-        // narrow-N tiles whose waves each cover 64 rows (r04): fewer LDS operand reads per MFMA than the
-        // 256x64 / 128x32 tiles (A fragments reused over all of N): 64-channel layers at 256^2 / 512^2
-        case 9: launch_x3<512, 64, 8, 8, 1, 1, ELT>(a, amode, bkn, grid, s); break;
-        case 10: launch_x3<256, 64, 4, 4, 1, 1, ELT>(a, amode, bkn, grid, s); break;
-        default: launch_x3<256, 32, 4, 4, 1, 1, ELT>(a, amode, bkn, grid, s); break;
-    }
+    const bool ok = cfg < 6 ? launch_conv_x3_part<ELT, 0>(cfg, a, amode, bkn, grid, s)
+                  : cfg < 12 ? launch_conv_x3_part<ELT, 1>(cfg, a, amode, bkn, grid, s)
+                             : launch_conv_x3_part<ELT, 2>(cfg, a, amode, bkn, grid, s);
+    // a configuration / A-mode pair without a kernel would leave the output unwritten: an error
+    S2V_REQUIRE(ok, "conv2d: x3 configuration %d has no kernel for A mode %d%s", cfg, amode, bkn ? " (b_kn)" : "");
     return 0;
 }
 

@@ -757,6 +757,105 @@ void rfft2_(const Tensor &x, const Tensor &tables, const Tensor &spec) {
           "s2v_rfft2");
 }
 
+// ------------------------------------------------------------------------------------------ LNet FFC
+// split packed weights [npad, kpad] (s2v_split_weights output, float32 storage of the 16-bit halves)
+const void *split_rows(const Tensor &w, const at::Device &dev, int64_t rows, int64_t k, const char *what) {
+    f32(w, dev, what);
+    TORCH_CHECK(w.dim() == 2 && w.is_contiguous() && w.size(0) >= rows && w.size(1) >= k && w.size(1) % 32 == 0, what,
+                ": split packed weights [npad >= ", rows, ", kpad >= ", k, "] expected, got ", w.sizes());
+    return w.data_ptr();
+}
+
+int *range_flag(const OptT &flag, const at::Device &dev) {
+    if (!has(flag)) return nullptr;
+    same_dev(*flag, dev, "ffc flag");
+    TORCH_CHECK(flag->scalar_type() == at::kInt && flag->numel() >= 1, "ffc flag: int32 [1]");
+    return flag->data_ptr<int>();
+}
+
+// x_g: NHWC [N, h, h, cg] channel view of the FFC input; t1 [N, h, h, cc], spec [N, F, 2cc] dense
+void ffc_spec_fwd_(const Tensor &xg, const Tensor &w1, double wt_scale, double x_scale, const OptT &scale,
+                   const OptT &shift, const Tensor &tables, const Tensor &t1, const Tensor &spec, const OptT &flag,
+                   int64_t prec) {
+    const c10::DeviceGuard guard(xg.device());
+    const at::Device dev = xg.device();
+    const NV xv = nhwc(xg, dev, "ffc x_g");
+    const int c = s2v_ffc_channels(xv.h), cg = c - c / 4, cc = cg / 2;
+    TORCH_CHECK(c > 0 && xv.w == xv.h && xv.c == cg, "ffc_spec_fwd: x_g [N, h, h, 3C/4] with h in {12, 24, 48}");
+    const NV tv = nhwc(t1, dev, "ffc t1");
+    TORCH_CHECK(tv.n == xv.n && tv.h == xv.h && tv.w == xv.w && tv.c == cc && tv.cs == cc, "ffc t1: dense [N, h, h, cc]");
+    f32(spec, dev, "ffc spec");
+    TORCH_CHECK(spec.dim() == 3 && spec.is_contiguous() && spec.size(0) == xv.n &&
+                    spec.size(1) == (int64_t)xv.h * (xv.h / 2 + 1) && spec.size(2) == 2 * cc,
+                "ffc spec: dense [N, F, 2cc]");
+    vec(tables, dev, (int64_t)s2v_fft_tables_floats(xv.h, xv.h), "ffc tables");
+    check(s2v_ffc_spec_fwd(xv.p, xv.cs, xv.n, xv.h, split_rows(w1, dev, cc, cg, "ffc w1"), (int)w1.size(1),
+                           (float)wt_scale, (float)x_scale, vec(scale, dev, cc, "ffc scale1"), vec(shift, dev, cc, "ffc shift1"),
+                           tables.data_ptr<float>(), tv.p, spec.data_ptr<float>(), range_flag(flag, dev), (int)prec,
+                           stream()),
+          "s2v_ffc_spec_fwd");
+}
+
+void ffc_spec_inv_(const Tensor &spec, const Tensor &wfu, double wt_scale, double x_scale, const OptT &scale,
+                   const OptT &shift, const Tensor &tables, const Tensor &t1, const Tensor &u, const OptT &flag,
+                   int64_t prec) {
+    const c10::DeviceGuard guard(spec.device());
+    const at::Device dev = spec.device();
+    const NV tv = nhwc(t1, dev, "ffc t1"), uv = nhwc(u, dev, "ffc u");
+    const int c = s2v_ffc_channels(tv.h), cg = c - c / 4, cc = cg / 2;
+    TORCH_CHECK(c > 0 && tv.w == tv.h && tv.c == cc && tv.cs == cc, "ffc t1: dense [N, h, h, cc]");
+    TORCH_CHECK(uv.n == tv.n && uv.h == tv.h && uv.w == tv.w && uv.c == cc && uv.cs == cc, "ffc u: dense [N, h, h, cc]");
+    f32(spec, dev, "ffc spec");
+    TORCH_CHECK(spec.dim() == 3 && spec.is_contiguous() && spec.size(0) == tv.n &&
+                    spec.size(1) == (int64_t)tv.h * (tv.h / 2 + 1) && spec.size(2) == 2 * cc,
+                "ffc spec: dense [N, F, 2cc]");
+    vec(tables, dev, (int64_t)s2v_fft_tables_floats(tv.h, tv.h), "ffc tables");
+    check(s2v_ffc_spec_inv(spec.data_ptr<float>(), tv.n, tv.h, split_rows(wfu, dev, 2 * cc, cg, "ffc wfu"),
+                           (int)wfu.size(1), (float)wt_scale, (float)x_scale, vec(scale, dev, 2 * cc, "ffc scale_fu"),
+                           vec(shift, dev, 2 * cc, "ffc shift_fu"), tables.data_ptr<float>(), tv.p, uv.p,
+                           range_flag(flag, dev), (int)prec, stream()),
+          "s2v_ffc_spec_inv");
+}
+
+// y: [N, h, h, C] (conv_to_l | conv_l2g outputs), u dense [N, h, h, cc]; gamma / beta [N, C] row views
+void ffc_norm_(const Tensor &y, const Tensor &u, const Tensor &w2, double wt_scale, double x_scale, const OptT &gamma,
+               const OptT &beta, double eps, int64_t act, double alpha, const OptT &res, const Tensor &out,
+               const OptT &pad_out, const OptT &flag, int64_t prec) {
+    const c10::DeviceGuard guard(y.device());
+    const at::Device dev = y.device();
+    const NV yv = nhwc(y, dev, "ffc_norm y"), uv = nhwc(u, dev, "ffc_norm u"), ov = nhwc(out, dev, "ffc_norm out");
+    const int c = s2v_ffc_channels(yv.h), cg = c - c / 4, cc = cg / 2;
+    TORCH_CHECK(c > 0 && yv.w == yv.h && yv.c == c, "ffc_norm: y [N, h, h, C] with h in {12, 24, 48}");
+    TORCH_CHECK(uv.n == yv.n && uv.h == yv.h && uv.w == yv.w && uv.c == cc && uv.cs == cc, "ffc_norm u: dense [N, h, h, cc]");
+    TORCH_CHECK(ov.n == yv.n && ov.h == yv.h && ov.w == yv.w && ov.c == c, "ffc_norm: out shape");
+    TORCH_CHECK(has(gamma) == has(beta), "ffc_norm: gamma and beta together");
+    const float *gp = nullptr, *bp = nullptr;
+    int ns = 0;
+    if (has(gamma)) {
+        ns = (int)rows_view(*gamma, dev, yv.n, c, "ffc_norm gamma");
+        TORCH_CHECK(rows_view(*beta, dev, yv.n, c, "ffc_norm beta") == ns, "ffc_norm: gamma / beta row strides");
+        gp = gamma->data_ptr<float>(); bp = beta->data_ptr<float>();
+    }
+    const float *rp = nullptr;
+    int rcs = 0;
+    if (has(res)) {
+        const NV rv = nhwc(*res, dev, "ffc_norm res");
+        TORCH_CHECK(rv.n == yv.n && rv.h == yv.h && rv.w == yv.w && rv.c == c, "ffc_norm: res shape");
+        rp = rv.p; rcs = rv.cs;
+    }
+    float *pp = nullptr;
+    int pcs = 0;
+    if (has(pad_out)) {
+        const NV pv = nhwc(*pad_out, dev, "ffc_norm pad_out");
+        TORCH_CHECK(pv.n == yv.n && pv.h == yv.h + 2 && pv.w == yv.w + 2 && pv.c == c, "ffc_norm pad_out: [N, h+2, h+2, C]");
+        pp = pv.p; pcs = pv.cs;
+    }
+    check(s2v_ffc_norm(yv.p, yv.cs, yv.n, yv.h, uv.p, split_rows(w2, dev, cg, cc, "ffc w2"), (int)w2.size(1),
+                       (float)wt_scale, (float)x_scale, gp, bp, ns, (float)eps, (int)act, (float)alpha, rp, rcs, ov.p,
+                       ov.cs, pp, pcs, range_flag(flag, dev), (int)prec, stream()),
+          "s2v_ffc_norm");
+}
+
 void irfft2_(const Tensor &spec, const Tensor &tables, const OptT &res, const Tensor &y) {
     const c10::DeviceGuard guard(spec.device());
     const at::Device dev = spec.device();
@@ -928,6 +1027,12 @@ TORCH_LIBRARY_FRAGMENT(s2v, m) {
     m.def("counter_add_(Tensor(a!) ctr, int inc) -> ()");
     m.def("rfft2_(Tensor x, Tensor tables, Tensor(a!) spec) -> ()");
     m.def("irfft2_(Tensor spec, Tensor tables, Tensor? res, Tensor(a!) y) -> ()");
+    m.def("ffc_spec_fwd_(Tensor x_g, Tensor w1, float wt_scale, float x_scale, Tensor? scale, Tensor? shift, "
+          "Tensor tables, Tensor(a!) t1, Tensor(b!) spec, Tensor? flag, int prec) -> ()");
+    m.def("ffc_spec_inv_(Tensor spec, Tensor wfu, float wt_scale, float x_scale, Tensor? scale, Tensor? shift, "
+          "Tensor tables, Tensor t1, Tensor(a!) u, Tensor? flag, int prec) -> ()");
+    m.def("ffc_norm_(Tensor y, Tensor u, Tensor w2, float wt_scale, float x_scale, Tensor? gamma, Tensor? beta, "
+          "float eps, int act, float alpha, Tensor? res, Tensor(a!) out, Tensor(b!)? pad_out, Tensor? flag, int prec) -> ()");
     m.def("eltwise_(Tensor x, Tensor? mul, Tensor? add, Tensor? bias, float a, int act, float alpha, float post, "
           "Tensor(a!) y) -> ()");
     m.def("fir2d_(Tensor x, Tensor kernel, Tensor(a!) y, int up, int down, int pad_y0, int pad_x0, float gain, "
@@ -961,6 +1066,9 @@ TORCH_LIBRARY_IMPL(s2v, CUDA, m) {
     m.impl("counter_add_", &counter_add_);
     m.impl("rfft2_", &rfft2_);
     m.impl("irfft2_", &irfft2_);
+    m.impl("ffc_spec_fwd_", &ffc_spec_fwd_);
+    m.impl("ffc_spec_inv_", &ffc_spec_inv_);
+    m.impl("ffc_norm_", &ffc_norm_);
     m.impl("eltwise_", &eltwise_);
     m.impl("fir2d_", &fir2d_);
     m.impl("lipsync_inputs_", &lipsync_inputs_);

@@ -41,6 +41,10 @@ SPEC_SPLITS = int(os.environ.get("S2V_LNET_SPEC_SPLITS", "1"))
 # encoder branches: calling stream first, then the two side streams (m = masked face, r = reference
 # face, a = audio encoder + ADAIN heads)
 ENC_ORDER = os.environ.get("S2V_LNET_ENC_ORDER", "mra")
+# the FFC's spectral branch and norm as three fused kernels (ops.ffc_spec_fwd / ffc_spec_inv / ffc_norm,
+# csrc/ffc.hip) instead of st1 -> rfft2 -> fu -> irfft2 -> st2 -> instnorm (split-precision arithmetic only;
+# S2V_LNET_FUSED=1; default off: measured slower on MI355X, r05 — LNet B=16 13.2 vs 10.05 ms)
+FUSED = os.environ.get("S2V_LNET_FUSED", "0") == "1"
 # split-K forced on the FFC's conv_to_l / l2g at the 12^2 level (0 = the planner's choice)
 C2L_SPLITS = int(os.environ.get("S2V_LNET_C2L_SPLITS", "0"))
 L2G_SPLITS = int(os.environ.get("S2V_LNET_L2G_SPLITS", "0"))
@@ -166,6 +170,9 @@ class FFCLama:
         self.gid = bank.add_group(sd, [(p + "bn_l.", self.cl), (p + "bn_g.", self.cg)])
         self.device = device
 
+    def fused(self) -> bool:
+        return FUSED and not GROUP and ops.ffc_fused_ok()
+
     def pre_norm(self, ctx, x: NHWC, y: NHWC, branches=None, xpad: NHWC | None = None):
         """y <- [l2l(x_l)+g2l(x_g) | l2g(x_l) + spectral(x_g)] (before ADAIN).
 
@@ -173,10 +180,16 @@ class FFCLama:
         (stream, Ctx) pairs, see Branches) is given: conv_to_l on the calling stream, l2g on the
         first side stream, the spectral chain st1 -> rfft2 -> fu -> irfft2 on the second; st2 joins
         them (it accumulates onto l2g's output).  At 12x12 each product fills only a fraction of
-        the 256 CUs, so running them side by side is what fills the chip."""
+        the 256 CUs, so running them side by side is what fills the chip.
+
+        Fused (``self.fused()``): the spectral branch is ops.ffc_spec_fwd + ops.ffc_spec_inv (two launches,
+        u = irfft(fu(rfft(t1))) + t1) and st2 moves into ``norm`` (ops.ffc_norm adds u conv2 to l2g's output
+        per channel slice before the statistics); returns u, which ``norm`` takes."""
         b = x.n
         cl, cg, cc, dev = self.cl, self.cg, self.cc, self.device
         yg = y.slice(cl, cg)
+        if self.fused():
+            return self._pre_norm_fused(ctx, x, y, branches, xpad)
         t1 = NHWC.empty(b, self.h, self.w, cc, dev)
         spec = torch.empty((b, self.F, 2 * cc), device=dev)
         spec2 = NHWC.empty(b, self.F, 1, 2 * cc, dev)
@@ -220,11 +233,52 @@ class FFCLama:
             branches.run(ctx, lambda c: ops.conv2d(c, xr, self.conv_to_l, y.slice(0, cl), force_splits=fs_c2l), l2g,
                          spectral)
         ops.conv2d(ctx, u, self.st2, yg, res=yg, force_splits=SPEC_SPLITS)
+        return None
+
+    def _pre_norm_fused(self, ctx, x: NHWC, y: NHWC, branches, xpad):
+        b = x.n
+        cl, cg, cc, dev = self.cl, self.cg, self.cc, self.device
+        yg = y.slice(cl, cg)
+        t1 = NHWC.empty(b, self.h, self.w, cc, dev)
+        spec = torch.empty((b, self.F, 2 * cc), device=dev)
+        u = NHWC.empty(b, self.h, self.w, cc, dev)
+        xr = x
+        if PREPAD and xpad is not None:
+            xr = xpad
+        elif PREPAD:
+            xr = NHWC.empty(b, self.h + 2, self.w + 2, x.c, dev)
+            ops.pad_reflect(ctx, x, xr, (1, 1, 1, 1))
+        small = self.h <= 12
+        fs_l2g = L2G_SPLITS if small else 0
+        fs_c2l = C2L_SPLITS if small else 0
+
+        def c2l(c):
+            ops.conv2d(c, xr, self.conv_to_l, y.slice(0, cl), force_splits=fs_c2l)
+
+        def l2g(c):
+            ops.conv2d(c, xr.slice(0, cl), self.conv_l2g, yg, force_splits=fs_l2g)
+
+        def spectral(c):
+            ops.ffc_spec_fwd(c, x.slice(cl, cg), self.st1, self.fft, t1, spec)   # st1 + rfftn (ffc.py:98-104, :158)
+            ops.ffc_spec_inv(c, spec, self.fu, self.fft, t1, u)                  # fu + irfftn + x (ffc.py:106-126)
+
+        if branches is None:
+            c2l(ctx)
+            l2g(ctx)
+            spectral(ctx)
+        else:
+            branches.run(ctx, c2l, l2g, spectral)
+        return u
 
     def norm(self, ctx, bank: AdainBank, params, y: NHWC, out: NHWC, res: NHWC | None = None,
-             pad_out: NHWC | None = None):
+             pad_out: NHWC | None = None, u: NHWC | None = None):
+        """ADAIN(bn_l | bn_g) + LeakyReLU (+ residual); with ``u`` (the fused pre_norm's FourierUnit output)
+        the spectral branch's st2 conv is added to y's global channels first (ops.ffc_norm)."""
         g, bt = bank.gamma_beta(self.gid, params)
-        ops.instnorm(ctx, y, out, g, bt, act=ops.ACT_LRELU, alpha=LRELU_FFC, res=res, pad_out=pad_out)
+        if u is not None:
+            ops.ffc_norm(ctx, y, u, self.st2, out, g, bt, act=ops.ACT_LRELU, alpha=LRELU_FFC, res=res, pad_out=pad_out)
+        else:
+            ops.instnorm(ctx, y, out, g, bt, act=ops.ACT_LRELU, alpha=LRELU_FFC, res=res, pad_out=pad_out)
 
 
 class Branches:
@@ -364,11 +418,11 @@ class LNetEngine:
             nblk = len(lv["blocks"])
             fbr = None if GROUP else br                         # grouped FFC: one stream
             for bi, (l1, l2) in enumerate(lv["blocks"]):
-                l1.pre_norm(ctx, cur, ya, fbr, xpad=pc if bi > 0 else None)
-                l1.norm(ctx, self.bank, ap, ya, ya, pad_out=pa)
-                l2.pre_norm(ctx, ya, yb, fbr, xpad=pa)
+                u1 = l1.pre_norm(ctx, cur, ya, fbr, xpad=pc if bi > 0 else None)
+                l1.norm(ctx, self.bank, ap, ya, ya, pad_out=pa, u=u1)
+                u2 = l2.pre_norm(ctx, ya, yb, fbr, xpad=pa)
                 l2.norm(ctx, self.bank, ap, yb, cur, res=cur,    # FFCResnetBlock: id + conv2(conv1(x))
-                        pad_out=pc if bi + 1 < nblk else None)
+                        pad_out=pc if bi + 1 < nblk else None, u=u2)
             up = lv["up"](ctx, cur)
             skip = skips.pop()
             lv["jump"](ctx, skip, out=up, res=up)               # jump(skip) + out

@@ -106,7 +106,13 @@ UP2_GROUP_PIXELS = 16 * 48 * 48
 # [slot, stride, reps]) for the kernel's in-launch clock stamps (s2v_conv_params.stamps).
 STAMP = None
 _NOSTAMP = (None, None, [0, 1, 1])
-_GROUPING = False       # inside conv_group: launches are recorded (no per-launch stamps)
+# inside conv_group on this thread: launches are recorded (no per-launch stamps); thread-local like the
+# C++ group recording it mirrors (torch_launch.cpp g_recording)
+_TLS = threading.local()
+
+
+def _grouping() -> bool:
+    return getattr(_TLS, "grouping", False)
 # Tuned (x3 tile, split-K) of split-precision conv launches whose planner choice (csrc/conv.hip
 # make_plan_x3's time model) measured slower than another configuration: a table measured on MI355X by
 # tools/tune_perfdb.py (every conv launch of the LNet / ENet / DNet forwards, each candidate tile and
@@ -115,10 +121,27 @@ _GROUPING = False       # inside conv_group: launches are recorded (no per-launc
 # S2V_PERFDB=0 ignores the table.
 PERFDB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "perfdb_mi355x.json")
 PERFDB = {}
+PERFDB_DEVICE = None    # (arch, CU count) the table was measured on: applied only on a matching device
 if os.environ.get("S2V_PERFDB", "1") != "0" and os.path.exists(PERFDB_PATH):
     import json as _json
     with open(PERFDB_PATH) as _f:
-        PERFDB = {k: (int(v["tile"]), int(v["splits"])) for k, v in _json.load(_f)["entries"].items()}
+        _db = _json.load(_f)
+    PERFDB = {k: (int(v["tile"]), int(v["splits"])) for k, v in _db["entries"].items()}
+    PERFDB_DEVICE = (_db.get("arch"), _db.get("cus"))
+_PERFDB_MATCH = {}
+
+
+def perfdb_applies(device) -> bool:
+    """The perf-db's forced tiles were timed on PERFDB_DEVICE (gfx950, 256 CUs): on another part the
+    planner's own model decides (the key has no architecture or CU count in it)."""
+    key = str(device)
+    if key not in _PERFDB_MATCH:
+        ok = False
+        if PERFDB and torch.device(device).type == "cuda":
+            pr = torch.cuda.get_device_properties(torch.device(device))
+            ok = (pr.gcnArchName.split(":")[0], pr.multi_processor_count) == PERFDB_DEVICE
+        _PERFDB_MATCH[key] = ok
+    return _PERFDB_MATCH[key]
 # tools/tune_perfdb.py: called as TUNE(ctx, key, relaunch, plan_of, yv, resv) for every launch conv_key()
 # covers; relaunch(tile, splits) runs the conv with that forced configuration, plan_of(tile, splits) is its
 # s2v_conv2d_plan (0, 0: the planner's own choice)
@@ -580,9 +603,10 @@ def _conv(ctx, x, cw, yv, out_step, act, alpha, resv, res_after, res_offset, nc_
     sh = cw.shift if shift is None else shift
     key = None
     if (PERFDB or TUNE is not None) and prec != PREC_F32 and not (force_tile or force_splits or x_split or cap or
-                                                                   _GROUPING):
+                                                                   _grouping()):
         key = conv_key(x, cw, yv, out_step, pool, prec)
-        force_tile, force_splits = PERFDB.get(key, (0, 0))
+        if TUNE is None and perfdb_applies(x.t.device):
+            force_tile, force_splits = PERFDB.get(key, (0, 0))
 
     def launch(ws, dry=False, st=_NOSTAMP, ft=None, fs=None):
         return S2V.conv2d_(x.v, yv, cw.wt, wsplit, wscale, cw.cout, [cw.kh, cw.kw], [cw.sh, cw.sw], [cw.ph, cw.pw],
@@ -606,16 +630,15 @@ def conv_group(ctx: Ctx, enabled: bool = True):
     if not enabled or CONV_HOOK is not None:
         yield
         return
-    global _GROUPING
     S2V.group_begin_()
-    _GROUPING = True
+    _TLS.grouping = True
     try:
         yield
     except BaseException:
         S2V.group_abort_()
         raise
     finally:
-        _GROUPING = False
+        _TLS.grouping = False
     global LAST_GROUP
     res = []
 
@@ -774,7 +797,7 @@ def _run_conv(ctx, launch, x, cw, yv, pool, in_scale=None, nc_scale=None, pix_ad
                       in_scale=in_scale is not None, nc_scale=nc_scale is not None, pix_add=pix_add is not None,
                       res=resv is not None, res_is_y=resv is not None and resv.data_ptr() == yv.data_ptr())
     flops = _conv_flops(x, cw, yv, pool)
-    if STAMP is not None and not _GROUPING:
+    if STAMP is not None and not _grouping():
         st = STAMP(info, flops) or _NOSTAMP
     if CONV_HOOK is None:
         go()
@@ -811,7 +834,8 @@ def modulated_conv2d(ctx: Ctx, x: NHWC, cw: ConvW, y: NHWC, s: torch.Tensor, d: 
     key, force_tile = None, 0
     if (PERFDB or TUNE is not None) and prec != PREC_F32 and not (force_splits or x_split):
         key = conv_key(x, cw, yv, 1, False, prec) + f"|mod{int(d is not None)}{int(d2s)}"
-        force_tile, force_splits = PERFDB.get(key, (0, 0))
+        if TUNE is None and perfdb_applies(x.t.device):
+            force_tile, force_splits = PERFDB.get(key, (0, 0))
 
     def launch(ws, dry=False, st=_NOSTAMP, ft=None, fs=None):
         return S2V.modulated_conv2d_(x.v, yv, cw.wt, s, d, wbuf, cw.cout, [cw.kh, cw.kw], [cw.ph, cw.pw], cw.in_mode,
@@ -1164,6 +1188,45 @@ def fft_tables(h: int, w: int, device):
         assert t.numel() == 2 * wf * w + 4 * h * h + 2 * w * wf
         _FFT_TABLES[key] = t.to(device)
     return _FFT_TABLES[key]
+
+
+def ffc_fused_ok() -> bool:
+    """The fused LNet FFC kernels (s2v_ffc_*) cover the split-precision arithmetic; exact f32 runs the
+    separate st1 / rfft2 / fu / irfft2 / st2 / instnorm launches."""
+    return PRECISION in ("f16x3", "bf16x3")
+
+
+def ffc_spec_fwd(ctx: Ctx, xg: NHWC, cw: ConvW, tables: torch.Tensor, t1: NHWC, spec: torch.Tensor):
+    """t1 = relu(bn1(x_g conv1)), spec = rfftn(t1, ortho) in one launch (s2v_ffc_spec_fwd): ffc.py:98-104,
+    :158-160 (SpectralTransform.conv1 + FourierUnit's rfftn)."""
+    prec = prec_code()
+    xs, flag = _range(ctx, cw, xg, prec)
+    S2V.ffc_spec_fwd_(xg.v, cw.wt_x3(ctx, prec), cw.split_scale(prec), xs, cw.scale, cw.shift, tables, t1.v, spec,
+                      flag, prec)
+    return t1, spec
+
+
+def ffc_spec_inv(ctx: Ctx, spec: torch.Tensor, cw: ConvW, tables: torch.Tensor, t1: NHWC, u: NHWC):
+    """u = irfftn(relu(bn_fu(spec conv_fu)), ortho) + t1 in one launch (s2v_ffc_spec_inv): ffc.py:106-126,
+    :162 (FourierUnit conv + irfftn, SpectralTransform's x + fu(x))."""
+    prec = prec_code()
+    b, f, c2 = spec.shape
+    xs, flag = _range(ctx, cw, NHWC(spec.view(b, f, 1, c2)), prec)
+    S2V.ffc_spec_inv_(spec, cw.wt_x3(ctx, prec), cw.split_scale(prec), xs, cw.scale, cw.shift, tables, t1.v, u.v, flag,
+                      prec)
+    return u
+
+
+def ffc_norm(ctx: Ctx, y: NHWC, u: NHWC, cw: ConvW, out: NHWC, gamma=None, beta=None, *, act=ACT_NONE, alpha=0.0,
+             res: NHWC | None = None, eps=1e-5, pad_out: NHWC | None = None):
+    """out = act(IN([y_l | y_g + u conv2]) (1 + gamma) + beta) (+ res) (s2v_ffc_norm): SpectralTransform.conv2
+    (ffc.py:164), FFC's out_xg sum (ffc.py:225-229) and ADAIN + LeakyReLU (base_blocks.py:143-157, :376-386)
+    in one launch; ``pad_out`` also receives F.pad(out, 1, 'reflect')."""
+    prec = prec_code()
+    xs, flag = _range(ctx, cw, u, prec)
+    S2V.ffc_norm_(y.v, u.v, cw.wt_x3(ctx, prec), cw.split_scale(prec), xs, gamma, beta, eps, act, alpha,
+                  None if res is None else res.v, out.v, None if pad_out is None else pad_out.v, flag, prec)
+    return out
 
 
 def rfft2(ctx: Ctx, x: NHWC, tables: torch.Tensor, spec: torch.Tensor):

@@ -101,6 +101,20 @@ def test_lipsync_engines_plan(dry):
     d.forward(ctx, src, coeff)
 
 
+def test_lnet_fused_ffc_plan(dry, monkeypatch):
+    """LNet's 54 FFCs (3 levels x 9 blocks x 2) through the fused spectral / norm kernels (csrc/ffc.hip,
+    S2V_LNET_FUSED=1) in f16x3: two spectral launches and one norm per FFC, no separate st1 / fu / st2 / FFT /
+    InstanceNorm launches."""
+    from s2v_amd.engine import lnet
+    monkeypatch.setattr(lnet, "FUSED", True)
+    eng = lnet.LNetEngine(synth_sd("lnet"), "cpu")
+    mel, face, _ = (torch.from_numpy(a) for a in synth.lipsync_inputs("dry", 2, 96))
+    x6 = ops.NHWC(face.permute(0, 2, 3, 1).contiguous())
+    eng.forward(ops.Ctx("cpu"), mel, x6, ops.NHWC.empty(2, 96, 96, 3, "cpu"))
+    assert dry.calls.get("ffc_spec_fwd_") == 54 and dry.calls.get("ffc_spec_inv_") == 54
+    assert dry.calls.get("ffc_norm_") == 54 and "rfft2_" not in dry.calls and "instnorm_" not in dry.calls
+
+
 def test_parsenet_plan(dry):
     from helpers import parsenet_sd
     from s2v_amd.engine.parsenet import ParseNetEngine
@@ -142,6 +156,10 @@ def test_perfdb_table_and_lookup(dry, monkeypatch):
                 return fn(*a)
             return rec
     monkeypatch.setattr(ops, "S2V", Rec())
+    # the table applies only on the device it was measured on (arch + CU count)
+    assert db["arch"] == "gfx950" and db["cus"] == 256
+    assert not ops.perfdb_applies("cpu")
+    monkeypatch.setattr(ops, "perfdb_applies", lambda dev: True)
     prev = ops.set_precision("f16x3")
     try:
         ctx = ops.Ctx("cpu")

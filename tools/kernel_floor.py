@@ -42,6 +42,7 @@ def graph_us(fn, n):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=200)
+    ap.add_argument("--case", type=int, default=-1, help="run only conv case i (PMC passes)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     ctx = ops.Ctx(dev)
@@ -49,14 +50,25 @@ def main():
     print(f"fill 256 floats: {graph_us(lambda: ops.fill(ctx, t, 1.0), a.n):.2f} us per dependent launch", flush=True)
     big = torch.empty(1 << 24, device=dev)
     print(f"fill 64 MB: {graph_us(lambda: ops.fill(ctx, big, 1.0), 20):.2f} us per launch", flush=True)
-    cw = ConvW(torch.randn(64, 32, 1, 1) / 6, None, dev)
-    x = NHWC(torch.randn(1, 8, 8, 32, device=dev))
-    y = NHWC.empty(1, 8, 8, 64, dev)
-    for prec in ("f16x3",):
-        ops.set_precision(prec)
-        us = graph_us(lambda: ops.conv2d(ctx, x, cw, y), a.n)
-        print(f"1x1 conv 64 px x 32 -> 64 ({prec}, one 64x64 block, one K slice): {us:.2f} us per dependent launch",
-              flush=True)
+    ops.set_precision("f16x3")
+    # 1x1 convs on the 64x64 tile (force_tile 5, no split-K): fixed cost per launch (1 block, 1 K-slice), the
+    # cost per K-slice, and the dependence on the block count (LNet's FourierUnit / st1 / st2 shapes)
+    cases = ((64, 32, 64), (64, 192, 64), (64, 768, 64), (4992, 32, 192), (4992, 192, 192),
+             (4992, 768, 192), (36864, 32, 96), (36864, 96, 96), (2304, 768, 384))
+    for i, (m, cin, cout) in enumerate(cases):
+        if a.case >= 0 and i != a.case:
+            continue
+        cw = ConvW(torch.randn(cout, cin, 1, 1) / cin ** 0.5, None, dev)
+        x = NHWC(torch.randn(1, m, 1, cin, device=dev))
+        y = NHWC.empty(1, m, 1, cout, dev)
+        ops.conv2d(ctx, x, cw, y, force_tile=5, force_splits=1)
+        us = graph_us(lambda: ops.conv2d(ctx, x, cw, y, force_tile=5, force_splits=1), a.n)
+        blocks = -(-m // 64) * -(-cout // 64)
+        print(f"1x1 conv M={m:6d} K={cin:4d} N={cout:4d} 64x64 tile ({blocks:5d} blocks, {cin // 32:3d} K-slices): "
+              f"{us:7.2f} us per dependent launch", flush=True)
+        # the same conv alternating with a tiny fill (a different kernel between two conv launches)
+        us2 = graph_us(lambda: (ops.fill(ctx, t, 1.0), ops.conv2d(ctx, x, cw, y, force_tile=5, force_splits=1)), a.n // 2)
+        print(f"    alternating with fill: {us2:7.2f} us per (fill + conv)", flush=True)
 
 
 if __name__ == "__main__":

@@ -34,7 +34,10 @@ def main():
     ap.add_argument("--only", default="", help="comma list of shape names")
     ap.add_argument("--pad", default="reflect", choices=("reflect", "zero", "valid"),
                     help="3x3 convs: reflect padding (the model), zero padding, or a pre-padded (h+2) input")
+    ap.add_argument("--graph", action="store_true", help="time the launches as one captured HIP graph")
+    ap.add_argument("--prec", default="f16x3")
     a = ap.parse_args()
+    ops.set_precision(a.prec)
     dev = torch.device("cuda")
     ctx = ops.Ctx(dev)
     total = {}
@@ -58,10 +61,25 @@ def main():
                     res.append(f"t{t}s{sp}: -")
                     continue
                 torch.cuda.synchronize()
+                g = None
+                if a.graph:
+                    st = torch.cuda.Stream()
+                    st.wait_stream(torch.cuda.current_stream())
+                    with torch.cuda.stream(st):
+                        g = torch.cuda.CUDAGraph()
+                        with torch.cuda.graph(g, stream=st):
+                            for _ in range(a.iters):
+                                ops.conv2d(ctx, x, cw, y, **kw)
+                    torch.cuda.current_stream().wait_stream(st)
+                    g.replay()
+                    torch.cuda.synchronize()
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
-                for _ in range(a.iters):
-                    ops.conv2d(ctx, x, cw, y, **kw)
+                if g is not None:
+                    g.replay()
+                else:
+                    for _ in range(a.iters):
+                        ops.conv2d(ctx, x, cw, y, **kw)
                 e.record()
                 torch.cuda.synchronize()
                 us = s.elapsed_time(e) * 1e3 / a.iters

@@ -138,7 +138,9 @@ def main():
             entries[k] = {"tile": b["tile"], "splits": b["splits"], "us": round(b["us"], 2),
                           "planner_us": round(v["planner"]["us"], 2), "planner": v["planner"]["symbol"][10:],
                           "planner_splits": v["planner"]["splits"], "symbol": b["symbol"][10:]}
+    props = torch.cuda.get_device_properties(dev)
     out = {"device": torch.cuda.get_device_name(dev), "workloads": wls,
+           "arch": props.gcnArchName.split(":")[0], "cus": props.multi_processor_count,
            "how": f"tools/tune_perfdb.py: each candidate a HIP graph of {REPS} launches, best of {ROUNDS} replays; "
                   f"kept when < {GAIN} x the planner's choice",
            "entries": entries}
