@@ -28,6 +28,10 @@ FUSED_TORGB = os.environ.get("S2V_ENET_FUSED_TORGB", "1") == "1"
 # (ops.modulated_conv2d d2s: the bilinear taps folded into 4 parity-class filters, written depth-to-space)
 # plus the four border lines recomputed exactly; S2V_ENET_POLY_UP=0: upsample pass + conv
 POLY_UP = os.environ.get("S2V_ENET_POLY_UP", "1") == "1"
+# the first StyleConv (the 4-channel RGB input carried as 4, 100^2 -> 200^2) polyphase too: its K = 36 gather
+# then runs over the 100^2 input with the four parity classes as 4 x 256 output columns.  Measured slower on
+# MI355X (r05, lipsync 24.6-24.7 vs 24.1-24.2 ms, profiles/r05_ab_lnet_pair.txt): off by default
+POLY_UP4 = os.environ.get("S2V_ENET_POLY_UP4", "0") == "1"
 # the style encoder's split-precision convs (launched beside LNet) as persistent blocks on half the
 # device's CUs (s2v_conv_params.grid_cap, ops.half_chip_blocks): the CUs they leave free take LNet's
 # latency-bound kernels as soon as they are launched instead of after the encoder's 100-200 us tiles
@@ -79,7 +83,7 @@ class StyleLayer:
         self.noise_w = None if is_rgb else float(sd[p + "weight"].float().reshape(-1)[0])
         self.device = device
         self.conv4 = self.wsq4 = None
-        if upsample and self.k == 3 and self.cin % 32 == 0:
+        if upsample and self.k == 3 and (self.cin % 32 == 0 or (POLY_UP4 and self.cin == 4)):
             self.conv4 = ConvW(fold_up2_conv3(w), bias.repeat(4), device, padding=1)
             self.wsq4 = self.wsq.repeat(4, 1).contiguous()
 

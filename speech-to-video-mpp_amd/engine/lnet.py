@@ -43,8 +43,17 @@ SPEC_SPLITS = int(os.environ.get("S2V_LNET_SPEC_SPLITS", "1"))
 ENC_ORDER = os.environ.get("S2V_LNET_ENC_ORDER", "mra")
 # the FFC's spectral branch and norm as three fused kernels (ops.ffc_spec_fwd / ffc_spec_inv / ffc_norm,
 # csrc/ffc.hip) instead of st1 -> rfft2 -> fu -> irfft2 -> st2 -> instnorm (split-precision arithmetic only;
-# S2V_LNET_FUSED=1; default off: measured slower on MI355X, r05 — LNet B=16 13.2 vs 10.05 ms)
-FUSED = os.environ.get("S2V_LNET_FUSED", "0") == "1"
+# S2V_LNET_FUSED=0: the separate launches).  S2V_LNET_FUSED_LEVELS: the decoder levels (h) that take it; on
+# MI355X (r05, tools/ffc_micro.py, B = 16) the fused kernels win at 24^2 only: each block streams its whole
+# image (the channel slices of an image all read the same A rows), which at 12^2 / 48^2 costs more than
+# the launches it saves
+FUSED = os.environ.get("S2V_LNET_FUSED", "1") == "1"
+FUSED_LEVELS = tuple(int(v) for v in os.environ.get("S2V_LNET_FUSED_LEVELS", "24").split(",") if v)
+# S2V_LNET_PAIR=1: conv_to_l and l2g (both read the reflect-padded block input) as ONE grouped launch
+# (ops.conv_group) on the calling stream, the spectral chain on a single side stream
+PAIR = os.environ.get("S2V_LNET_PAIR", "1") == "1"
+# with PAIR: the grouped conv launch on the side stream and the spectral chain on the calling stream
+PAIR_SIDE = os.environ.get("S2V_LNET_PAIR_SIDE", "0") == "1"
 # split-K forced on the FFC's conv_to_l / l2g at the 12^2 level (0 = the planner's choice)
 C2L_SPLITS = int(os.environ.get("S2V_LNET_C2L_SPLITS", "0"))
 L2G_SPLITS = int(os.environ.get("S2V_LNET_L2G_SPLITS", "0"))
@@ -171,7 +180,31 @@ class FFCLama:
         self.device = device
 
     def fused(self) -> bool:
-        return FUSED and not GROUP and ops.ffc_fused_ok()
+        return FUSED and not GROUP and self.h in FUSED_LEVELS and ops.ffc_fused_ok()
+
+    @staticmethod
+    def _run_products(ctx, branches, c2l, l2g, spectral, grouped):
+        """conv_to_l, l2g and the spectral chain: concurrent branches (``branches``), or serial; with
+        ``grouped`` (PAIR) the two convs as one grouped launch on the calling stream beside the spectral
+        chain on one side stream."""
+        if grouped:
+            def pair(c):
+                with ops.conv_group(c):
+                    c2l(c)
+                    l2g(c)
+            if branches is None:
+                pair(ctx)
+                spectral(ctx)
+            elif PAIR_SIDE:
+                branches.run(ctx, spectral, pair)
+            else:
+                branches.run(ctx, pair, spectral)
+        elif branches is None:
+            c2l(ctx)
+            l2g(ctx)
+            spectral(ctx)
+        else:
+            branches.run(ctx, c2l, l2g, spectral)
 
     def pre_norm(self, ctx, x: NHWC, y: NHWC, branches=None, xpad: NHWC | None = None):
         """y <- [l2l(x_l)+g2l(x_g) | l2g(x_l) + spectral(x_g)] (before ADAIN).
@@ -225,13 +258,10 @@ class FFCLama:
             ops.conv2d(ctx, NHWC(spec.view(b, self.F, 1, 2 * cc)), self.fu, spec2, act=ops.ACT_RELU,
                        force_splits=SPEC_SPLITS)
             ops.irfft2(ctx, spec2.t.view(b, self.F, 2 * cc), self.fft, u, res=t1)
-        elif branches is None:
-            ops.conv2d(ctx, xr, self.conv_to_l, y.slice(0, cl), force_splits=fs_c2l)
-            l2g(ctx)
-            spectral(ctx)
         else:
-            branches.run(ctx, lambda c: ops.conv2d(c, xr, self.conv_to_l, y.slice(0, cl), force_splits=fs_c2l), l2g,
-                         spectral)
+            self._run_products(ctx, branches,
+                               lambda c: ops.conv2d(c, xr, self.conv_to_l, y.slice(0, cl), force_splits=fs_c2l), l2g,
+                               spectral, PAIR and not fs_c2l and not fs_l2g)
         ops.conv2d(ctx, u, self.st2, yg, res=yg, force_splits=SPEC_SPLITS)
         return None
 
@@ -262,12 +292,7 @@ class FFCLama:
             ops.ffc_spec_fwd(c, x.slice(cl, cg), self.st1, self.fft, t1, spec)   # st1 + rfftn (ffc.py:98-104, :158)
             ops.ffc_spec_inv(c, spec, self.fu, self.fft, t1, u)                  # fu + irfftn + x (ffc.py:106-126)
 
-        if branches is None:
-            c2l(ctx)
-            l2g(ctx)
-            spectral(ctx)
-        else:
-            branches.run(ctx, c2l, l2g, spectral)
+        self._run_products(ctx, branches, c2l, l2g, spectral, PAIR and not fs_c2l and not fs_l2g)
         return u
 
     def norm(self, ctx, bank: AdainBank, params, y: NHWC, out: NHWC, res: NHWC | None = None,

@@ -618,7 +618,7 @@ def test_torgb_up2_fused(ctx, n, h, w, cin):
     assert ((to_nchw(y) - ref).abs() <= 2e-6 * (bound + 1) + 1e-6).all()
 
 
-@pytest.mark.parametrize("n,cin,h,w,cout", [(2, 64, 9, 7, 32), (3, 32, 12, 16, 128)])
+@pytest.mark.parametrize("n,cin,h,w,cout", [(2, 64, 9, 7, 32), (3, 32, 12, 16, 128), (2, 4, 10, 12, 64)])
 def test_modulated_conv_d2s_polyphase(ctx, prec, n, cin, h, w, cout):
     """x2-bilinear-upsample + modulated 3x3 conv as one depth-to-space conv over the un-upsampled
     input with the four folded parity-class filters (engine.enet.fold_up2_conv3, s2v_conv_params
