@@ -107,12 +107,15 @@ def test_lnet_fused_ffc_plan(dry, monkeypatch):
     InstanceNorm launches."""
     from s2v_amd.engine import lnet
     monkeypatch.setattr(lnet, "FUSED", True)
+    monkeypatch.setattr(lnet, "FUSED_LEVELS", (12, 24, 48))
     eng = lnet.LNetEngine(synth_sd("lnet"), "cpu")
     mel, face, _ = (torch.from_numpy(a) for a in synth.lipsync_inputs("dry", 2, 96))
     x6 = ops.NHWC(face.permute(0, 2, 3, 1).contiguous())
     eng.forward(ops.Ctx("cpu"), mel, x6, ops.NHWC.empty(2, 96, 96, 3, "cpu"))
     assert dry.calls.get("ffc_spec_fwd_") == 54 and dry.calls.get("ffc_spec_inv_") == 54
     assert dry.calls.get("ffc_norm_") == 54 and "rfft2_" not in dry.calls and "instnorm_" not in dry.calls
+    # PAIR (the default): conv_to_l and l2g of every FFC as one grouped launch
+    assert dry.calls.get("group_end_", 0) >= 54 if lnet.PAIR else True     # (+ the grouped polyphase up convs)
 
 
 def test_parsenet_plan(dry):

@@ -30,6 +30,7 @@ def _engine():
 @pytest.mark.parametrize("b", [2, 16])
 def test_ffc_fused_matches_separate(monkeypatch, prec, level, b):
     lnet, eng = _engine()
+    monkeypatch.setattr(lnet, "FUSED_LEVELS", (12, 24, 48))
     lv = eng.levels[level]
     f1, f2 = lv["blocks"][3]
     h, c = f1.h, f1.c
@@ -76,7 +77,7 @@ def test_ffc_fused_off_in_f32(monkeypatch):
         assert not f1.fused()
     finally:
         ops.set_precision(prev)
-    assert f1.fused() == (lnet.FUSED and ops.PRECISION in ("f16x3", "bf16x3"))
+    assert f1.fused() == (lnet.FUSED and f1.h in lnet.FUSED_LEVELS and ops.PRECISION in ("f16x3", "bf16x3"))
 
 
 def test_lnet_fused_path_matches_reference(monkeypatch, golden):
@@ -86,6 +87,7 @@ def test_lnet_fused_path_matches_reference(monkeypatch, golden):
     from s2v_amd.engine import lnet
     from test_models_gpu import BAR, TOL, within
     monkeypatch.setattr(lnet, "FUSED", True)
+    monkeypatch.setattr(lnet, "FUSED_LEVELS", (12, 24, 48))
     prev = ops.set_precision("f16x3")
     try:
         net = models.LNet()
