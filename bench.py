@@ -92,6 +92,9 @@ def parse():
     ap.add_argument("--precision", choices=("f16x3", "bf16x3", "f32"), default="f16x3",
                     help="conv arithmetic (s2v_amd.ops.set_precision)")
     ap.add_argument("--no-alt", action="store_true", help="skip the timing of the other conv arithmetic")
+    ap.add_argument("--dump-stamps", default="",
+                    help="write every stamped launch of the timed replays (raw s_memrealtime ticks, per symbol, "
+                         "replay and launch slot, with its FLOPs) to this JSON file (tools/stamp_vs_trace.py)")
     return ap.parse_args()
 
 
@@ -269,6 +272,20 @@ class Stamper:
                 buf[..., 1] = 0
             L["c0"] = int(L["ctr"].item())
 
+    def raw(self):
+        """{symbol: [[replay, slot, s0, s1, flops], ...]} of the timed replays, in replay / slot order."""
+        torch.cuda.synchronize()
+        out = {}
+        for L in self.lanes.values():
+            c1 = int(L["ctr"].item())
+            for sym, buf in L["buf"].items():
+                b = buf.cpu()
+                for r in range(L["c0"] + 1, c1 + 1):
+                    for slot, (s0, s1) in enumerate(b[r % self.reps].tolist()):
+                        if s0 != -1 and s1 > 0:
+                            out.setdefault(sym, []).append([r, slot, s0, s1, L["flops"][sym][slot]])
+        return out
+
     def launches(self):
         """{symbol: [(duration us, flops), ...]} of every stamped launch of the timed replays."""
         torch.cuda.synchronize()
@@ -291,7 +308,7 @@ def _peak(sym):
         else FP32_MFMA_PEAK_TFLOPS
 
 
-PMC_ROUND = "r04"     # only this round's PMC passes describe the current build
+PMC_ROUND = "r05"     # only this round's PMC passes describe the current build
 
 
 def pmc_traffic(workload, sym, grid=None):
@@ -1021,6 +1038,9 @@ def worker(args):
                 kern[pre["kernel"].replace("conv_igemm_x3<", "conv_igemm_x3_persist<")] = ks[pre["kernel"]] + 4
             stamper = Stamper(kern, args.warmup + args.steps + 2 * args.lanes + 4, dev)
     elapsed = timed(args.precision, stamper)
+    if args.dump_stamps and stamper is not None:
+        with open(args.dump_stamps, "w") as f:
+            json.dump({"clock_hz": Stamper.CLOCK_HZ, "kernel": pre["kernel"], "launches": stamper.raw()}, f)
     if cuda:
         ops.check_all_ranges(args.workload)     # f16x3 range guard: raises if a timed launch overflowed
     units = wl.units_per_step(world) * args.steps
