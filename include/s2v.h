@@ -353,6 +353,10 @@ int s2v_irfft2(const float *spec, int n, int h, int w, int c, int scs, const flo
  * be NULL); x_scale: the f16x3 activation pre-scale of the conv's input (power of two, 1 = none); tables:
  * s2v_fft_tables for (h, h); flag (may be NULL): set to 1 when an accumulator is not finite (the f16x3 range
  * guard).  prec: S2V_PREC_F16X3 or S2V_PREC_BF16X3 (the exact-f32 arithmetic uses the separate kernels). */
+/* Self-check of the split-fp32 f16 operand split (conv_x3_impl.hpp split4): both variants (X3_F16_MIX 1 / 0)
+ * on x (n % 4 == 0 floats); *mismatch (device int, zeroed by the caller) += the float4s whose halves differ. */
+int s2v_f16_split_check(const float *x, long long n, int *mismatch, s2v_stream_t stream);
+
 int s2v_ffc_channels(int h);
 int s2v_ffc_spec_fwd(const float *x_g, int xcs, int n, int h, const void *w1, int w1_kpad, float wt_scale, float x_scale,
                      const float *scale, const float *shift, const float *tables, float *t1, float *spec, int *flag,

@@ -94,6 +94,7 @@ _SIGS = {
     "s2v_fft_tables_floats": (_c_size, [_c_int, _c_int]),
     "s2v_rfft2": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_int, _vp]),
     "s2v_irfft2": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_int, _vp, _c_int, _vp]),
+    "s2v_f16_split_check": (_c_int, [_vp, _c_ll, _vp, _vp]),
     "s2v_ffc_channels": (_c_int, [_c_int]),
     "s2v_ffc_spec_fwd": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_float, _c_float, _vp, _vp, _vp, _vp, _vp,
                                   _vp, _c_int, _vp]),

@@ -264,3 +264,26 @@ extern "C" int s2v_split_act(const float *x, long long pixels, int c, int xcs, i
         split_act_kernel<1><<<(unsigned)b, 256, 0, (hipStream_t)stream>>>(x, pixels, c, xcs, (char *)out, ocs);
     return check_launch("split_act");
 }
+
+// Both f16 split variants of conv_x3_impl.hpp (X3_F16_MIX 1: v_fma_mix residuals; 0: widen + subtract +
+// pack) on the same inputs: counts the float4s whose hi or lo halves differ (a self-check of the variant
+// the library is not built with; they must be bit-identical).
+__global__ __launch_bounds__(256) void f16_split_check_kernel(const float *__restrict__ x, long long n4,
+                                                              int *__restrict__ mismatch) {
+    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+        const f4 v = ((const f4 *)x)[i];
+        u32x2 h1, l1, h0, l0;
+        split4<1, 1>(v, h1, l1);
+        split4<1, 0>(v, h0, l0);
+        if (h1.x != h0.x || h1.y != h0.y || l1.x != l0.x || l1.y != l0.y) atomicAdd(mismatch, 1);
+    }
+}
+
+extern "C" int s2v_f16_split_check(const float *x, long long n, int *mismatch, s2v_stream_t stream) {
+    S2V_REQUIRE(x && mismatch && n > 0 && n % 4 == 0 && ((uintptr_t)x % 16) == 0,
+                "f16_split_check: n %% 4 == 0 floats, 16-byte aligned");
+    const long long n4 = n / 4;
+    const unsigned grid = (unsigned)std::min<long long>((n4 + 255) / 256, 4096);
+    f16_split_check_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(x, n4, mismatch);
+    return check_launch("f16_split_check");
+}

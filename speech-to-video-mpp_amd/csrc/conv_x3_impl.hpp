@@ -37,9 +37,14 @@ typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 // f16 lo halves by v_fma_mix (1): one VALU per half, written into the halves of one register; 0: widen the
-// hi halves (v_cvt_f32_f16), subtract, pack (as the bf16 path does).  0 was tried in r04 to close the
-// 3.5 % gap to the bf16x3 kernels and failed the modulated depth-to-space test's f16x3 bound (1.2e-4):
-// kept at 1
+// hi halves (v_cvt_f32_f16), subtract, pack (as the bf16 path does).  0 failed the modulated depth-to-space
+// test's f16x3 bound in r04 (1.2e-4).  Cause (r05, from the ISA of split4<1> built with 0): the compiler
+// folded "widen the packed hi halves" into a second conversion of the fp32 inputs — v_cvt_f16_f32 +
+// v_cvt_f32_f16 per value beside the v_cvt_pk_f16_f32 that produced the stored hi — so the lo halves were
+// residuals against a separately rounded copy of hi, not against the hi that is stored: whenever the two
+// conversions round differently, hi + lo misses the input by one f16 ulp.  The hi register now goes
+// through an empty asm, which the compiler cannot see through, so the widening reads the stored halves;
+// s2v_f16_split_check asserts both variants bit-identical (tests/test_ops_gpu.py).
 #ifndef X3_F16_MIX
 #define X3_F16_MIX 1
 #endif
@@ -78,14 +83,15 @@ __device__ __forceinline__ unsigned f16_residual2(unsigned h, float a, float b) 
 }
 
 // 4 fp32 -> 4 hi halves (8 bytes) + 4 lo halves (8 bytes)
-template <int ELT>
+template <int ELT, int MIX = X3_F16_MIX>
 __device__ __forceinline__ void split4(const f4 &v, u32x2 &hi, u32x2 &lo) {
     hi.x = pack2<ELT>(v.x, v.y);
     hi.y = pack2<ELT>(v.z, v.w);
-    if constexpr (ELT == 1 && X3_F16_MIX) {
+    if constexpr (ELT == 1 && MIX) {
         lo.x = f16_residual2(hi.x, v.x, v.y);
         lo.y = f16_residual2(hi.y, v.z, v.w);
     } else {
+        if constexpr (ELT == 1) asm volatile("" : "+v"(hi.x), "+v"(hi.y));   // widen THESE halves (see X3_F16_MIX)
         float h0, h1, h2, h3;
         unpack2<ELT>(hi.x, h0, h1);
         unpack2<ELT>(hi.y, h2, h3);

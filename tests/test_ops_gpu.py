@@ -923,3 +923,25 @@ def test_conv1x1_partial_slice_buffer_path(ctx, prec, cin, cout, tile):
     err = (to_nchw(y) - ref).abs()
     bound = conv_bound(xr, wt, 1, 0, 1)
     assert (err <= REL[prec] * (bound + 1) + 1e-5).all(), f"max err {err.max():.3e}"
+
+
+def test_f16_split_variants_bit_identical():
+    """the widen-subtract-pack f16 split (X3_F16_MIX=0) and the v_fma_mix split the
+    library uses (1) give bit-identical hi / lo halves (s2v_f16_split_check runs both on the same inputs):
+    normals over 14 decades down into the f16-subnormal lo range, and random fp32 bit patterns inside the
+    f16 range.  (The r04 failure of 0 was the compiler re-converting the inputs for the widening instead of
+    widening the stored hi halves; conv_x3_impl.hpp X3_F16_MIX.)"""
+    from s2v_amd import _lib
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(3)
+    parts = [torch.randn(1 << 18, generator=g) * 10.0 ** e for e in range(-9, 5)]
+    bits = torch.randint(0, 2 ** 31 - 1, (1 << 20,), generator=g, dtype=torch.int64).to(torch.int32).view(torch.float32)
+    bits = bits[torch.isfinite(bits) & (bits.abs() < 6.0e4)]
+    x = torch.cat(parts + [bits, -bits])
+    x = x[x.abs() < 6.0e4]
+    x = x[: x.numel() // 4 * 4].contiguous().to(DEV)
+    m = torch.zeros(1, dtype=torch.int32, device=DEV)
+    rc = lib.s2v_f16_split_check(x.data_ptr(), x.numel(), m.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    assert rc == 0, lib.s2v_last_error()
+    torch.cuda.synchronize()
+    assert int(m.item()) == 0, f"{int(m.item())} of {x.numel() // 4} float4s differ"
