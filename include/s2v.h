@@ -247,6 +247,15 @@ int s2v_adain_params(const float *hid, int batch, int hid_ns, int nhidden, const
 int s2v_modconv_demod(const float *s, int batch, int s_ns, int cin, const float *wsq, int cout,
                       float eps, float post, float *d, int d_ns, s2v_stream_t stream);
 
+/* Every demodulated layer of a StyleGAN2 decoder in one launch (stylegan2_clean_arch.py:81-83,
+ * gpen_model.py:225-247): for r < nrows, with (s_off, cin, w_off, -) = rows[4r..4r+3] (16-byte
+ * aligned int32 table),
+ *   d[b][r] = rsqrt(sum_{i<cin} s[b][s_off + i]^2 * wsq[w_off + (r - r0) * cin + i] + eps) * post
+ * i.e. w_off already points at row r's squared-weight row. */
+int s2v_modconv_demod_rows(const float *s, int batch, int s_ns, const int *rows, int nrows,
+                           const float *wsq, float eps, float post, float *d, int d_ns,
+                           s2v_stream_t stream);
+
 /* Bilinear resize (F.interpolate mode='bilinear', align_corners=False, no antialias) between
  * arbitrary strided 4-D views; scale_h/scale_w as torch's area_pixel_compute_scale.
  * Element (n,c,y,x) at base + n*sn + c*sc + y*sy + x*sx (strides in elements).

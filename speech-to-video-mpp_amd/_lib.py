@@ -71,6 +71,8 @@ _SIGS = {
     "s2v_instnorm_ws_bytes": (_c_size, [_c_int, _c_int, _c_int, _c_int]),
     "s2v_adain_params": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _c_int, _vp, _c_int, _vp]),
     "s2v_modconv_demod": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_float, _c_float, _vp, _c_int, _vp]),
+    "s2v_modconv_demod_rows": (_c_int, [_vp, _c_int, _c_int, _vp, _c_int, _vp, _c_float, _c_float, _vp, _c_int,
+                                        _vp]),
     "s2v_torgb_up2": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp, _c_int, _vp, _vp,
                                _c_int, _vp, _c_int, _vp]),
     "s2v_resize": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_ll, _c_ll, _c_ll, _c_ll, _vp, _c_int, _c_int,

@@ -669,27 +669,38 @@ __global__ __launch_bounds__(256) void adain_heads2(const float *__restrict__ hi
 }
 
 // One wave per output channel o; lanes stride over cin (coalesced rows of wsq), each lane keeps
-// the partial sums of up to 16 samples so a wsq row is read once for the whole batch chunk.
+// the partial sums of up to 16 samples so a wsq row is read once for the whole batch chunk.  The
+// loads of a 256-wide chunk of the row (4 per lane) are issued together: the first version walked
+// the row 64 values at a time with every load behind the previous FMA (18 us for a 512 x 512 layer,
+// all latency, profiles/r05_hbm_enhance.json).
 constexpr int DEMOD_NB = 16;
-__global__ __launch_bounds__(256) void demod_kernel(const float *__restrict__ s, int batch, int s_ns, int cin,
-                                                    const float *__restrict__ wsq, int cout, float eps, float post,
-                                                    float *__restrict__ d, int d_ns) {
-    const int lane = threadIdx.x & 63;
-    const int o = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (o >= cout) return;
-    const float *wr = wsq + (long long)o * cin;
+__device__ __forceinline__ void demod_row(const float *__restrict__ s, int batch, int s_ns, int cin,
+                                          const float *__restrict__ wr, float eps, float post,
+                                          float *__restrict__ d, int d_ns, int o, int lane) {
     for (int b0 = 0; b0 < batch; b0 += DEMOD_NB) {
         const int nb = min(DEMOD_NB, batch - b0);
         float acc[DEMOD_NB];
 #pragma unroll
         for (int j = 0; j < DEMOD_NB; ++j) acc[j] = 0.f;
-        for (int i = lane; i < cin; i += 64) {
-            const float w = wr[i];
+        for (int i0 = 0; i0 < cin; i0 += 256) {
+            float w[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int i = i0 + u * 64 + lane;
+                w[u] = i < cin ? wr[i] : 0.f;
+            }
 #pragma unroll
             for (int j = 0; j < DEMOD_NB; ++j) {
                 if (j < nb) {
-                    const float v = s[(long long)(b0 + j) * s_ns + i];
-                    acc[j] = fmaf(v * v, w, acc[j]);
+                    const float *sr = s + (long long)(b0 + j) * s_ns;
+                    float v[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int i = i0 + u * 64 + lane;
+                        v[u] = i < cin ? sr[i] : 0.f;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) acc[j] = fmaf(v[u] * v[u], w[u], acc[j]);
                 }
             }
         }
@@ -701,6 +712,27 @@ __global__ __launch_bounds__(256) void demod_kernel(const float *__restrict__ s,
             if (lane == 0 && j < nb) d[(long long)(b0 + j) * d_ns + o] = rsqrtf(v + eps) * post;
         }
     }
+}
+
+__global__ __launch_bounds__(256) void demod_kernel(const float *__restrict__ s, int batch, int s_ns, int cin,
+                                                    const float *__restrict__ wsq, int cout, float eps, float post,
+                                                    float *__restrict__ d, int d_ns) {
+    const int o = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (o >= cout) return;
+    demod_row(s, batch, s_ns, cin, wsq + (long long)o * cin, eps, post, d, d_ns, o, threadIdx.x & 63);
+}
+
+// Every demodulated layer of a StyleGAN2 decoder in one launch: output row r of the concatenated
+// demodulation vector (row r of layer l is channel r - r0_l of l) reads its modulation s at column
+// rows[r].x of the style bank, rows[r].y input channels, and its squared-weight row at wsq + rows[r].z.
+__global__ __launch_bounds__(256) void demod_rows_kernel(const float *__restrict__ s, int batch, int s_ns,
+                                                         const int4 *__restrict__ rows, int nrows,
+                                                         const float *__restrict__ wsq, float eps, float post,
+                                                         float *__restrict__ d, int d_ns) {
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= nrows) return;
+    const int4 t = rows[r];
+    demod_row(s + t.x, batch, s_ns, t.y, wsq + (unsigned)t.z, eps, post, d, d_ns, r, threadIdx.x & 63);
 }
 
 }  // namespace s2v
@@ -871,4 +903,14 @@ extern "C" int s2v_modconv_demod(const float *s, int batch, int s_ns, int cin, c
     demod_kernel<<<cdiv(cout, 4), 256, 0, (hipStream_t)stream>>>(s, batch, s_ns, cin, wsq, cout, eps, post, d,
                                                                  d_ns);
     return check_launch("demod");
+}
+
+extern "C" int s2v_modconv_demod_rows(const float *s, int batch, int s_ns, const int *rows, int nrows,
+                                      const float *wsq, float eps, float post, float *d, int d_ns,
+                                      s2v_stream_t stream) {
+    S2V_REQUIRE(s && rows && wsq && d && batch > 0 && nrows > 0 && d_ns >= nrows && ((uintptr_t)rows % 16) == 0,
+                "modconv_demod_rows: bad args");
+    demod_rows_kernel<<<cdiv(nrows, 4), 256, 0, (hipStream_t)stream>>>(s, batch, s_ns, (const int4 *)rows, nrows,
+                                                                       wsq, eps, post, d, d_ns);
+    return check_launch("demod_rows");
 }

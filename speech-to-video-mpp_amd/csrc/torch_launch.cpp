@@ -596,6 +596,24 @@ void modconv_demod_(const Tensor &s, const Tensor &wsq, const Tensor &d, double 
           "s2v_modconv_demod");
 }
 
+void modconv_demod_rows_(const Tensor &s, const Tensor &rows, const Tensor &wsq, const Tensor &d, double eps,
+                         double post, int64_t s_reach) {
+    const c10::DeviceGuard guard(s.device());
+    const at::Device dev = s.device();
+    const int64_t batch = d.size(0), nrows = rows.size(0);
+    same_dev(rows, dev, "demod rows");
+    TORCH_CHECK(rows.scalar_type() == at::kInt && rows.is_contiguous() && rows.dim() == 2 && rows.size(1) == 4,
+                "demod rows: int32 [nrows, 4]");
+    // s_reach: the table's largest s_off + cin (ops.DemodRows checks the table against wsq on the host)
+    const int64_t sns = rows_view(s, dev, batch, std::max<int64_t>(s_reach, 2), "demod s");
+    vec(wsq, dev, wsq.numel(), "demod wsq");
+    const int64_t dns = rows_view(d, dev, batch, nrows, "demod d");
+    check(s2v_modconv_demod_rows(s.data_ptr<float>(), (int)batch, (int)sns, rows.data_ptr<int>(), (int)nrows,
+                                 wsq.data_ptr<float>(), (float)eps, (float)post, d.data_ptr<float>(), (int)dns,
+                                 stream()),
+          "s2v_modconv_demod_rows");
+}
+
 void row_layernorm_(const Tensor &x, const Tensor &weight, const Tensor &bias, double eps, const Tensor &y) {
     const c10::DeviceGuard guard(x.device());
     const at::Device dev = x.device();
@@ -1013,6 +1031,8 @@ TORCH_LIBRARY_FRAGMENT(s2v, m) {
           "Tensor(a!) y, Tensor(b!)? pad_out, Tensor? ws) -> int");
     m.def("adain_params_(Tensor hid, int nhidden, Tensor w2t, Tensor bias, Tensor seg, Tensor(a!) out) -> ()");
     m.def("modconv_demod_(Tensor s, Tensor wsq, Tensor(a!) d, float eps, float post) -> ()");
+    m.def("modconv_demod_rows_(Tensor s, Tensor rows, Tensor wsq, Tensor(a!) d, float eps, float post, "
+          "int s_reach) -> ()");
     m.def("row_layernorm_(Tensor x, Tensor weight, Tensor bias, float eps, Tensor(a!) y) -> ()");
     m.def("attention_(Tensor q, Tensor k, Tensor v, Tensor(a!) out, int batch, int heads, int tokens, int dim_head, "
           "float scale) -> ()");
@@ -1054,6 +1074,7 @@ TORCH_LIBRARY_IMPL(s2v, CUDA, m) {
     m.impl("instnorm_", &instnorm_);
     m.impl("adain_params_", &adain_params_);
     m.impl("modconv_demod_", &modconv_demod_);
+    m.impl("modconv_demod_rows_", &modconv_demod_rows_);
     m.impl("row_layernorm_", &row_layernorm_);
     m.impl("attention_", &attention_);
     m.impl("resize_", &resize_);

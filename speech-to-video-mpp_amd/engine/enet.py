@@ -128,6 +128,7 @@ class ENetEngine:
             o += l.cin + pad
         self.mod = ConvW(torch.cat(ws, 0), torch.cat(bs, 0), dev)
         self.mod_offs = offs
+        self._demod = {}
         self.noise_seed = 0x5EED
 
     def _side(self, ctx):
@@ -135,7 +136,26 @@ class ENetEngine:
         side = ctx.streams(("enet", id(self)), 1)
         return None if side is None else side[0]
 
-    def _poly_styleconv(self, ctx, L, cur: NHWC, s, idx, noises, ctr):
+    def _demod_table(self, poly):
+        """The four StyleConvs' demodulations (base_blocks.py:492-494) as one ops.DemodRows table; a
+        polyphase layer contributes its four parity-class blocks (wsq4)."""
+        if poly not in self._demod:
+            ls = [(self.mod_offs[j], self.layers[j].wsq4 if poly and self.layers[j].conv4 is not None
+                   else self.layers[j].wsq) for j in (0, 1, 3, 4)]
+            t = ops.DemodRows(ls, self.device)
+            t.width = [w.shape[0] for _, w in ls]
+            self._demod[poly] = t
+        return self._demod[poly]
+
+    def _demods(self, ctx, s2):
+        """[B, nrows] demodulation vectors of the four StyleConvs, one launch (instead of one per layer
+        in the tail): slot j of the table is columns [r0[j], + width[j])."""
+        t = self._demod_table(POLY_UP)
+        dall = ops.empty((s2.shape[0], t.nrows), self.device)
+        ops.modconv_demod_rows(ctx, s2, t, dall, eps=1e-8, post=math.sqrt(2.0))
+        return t, dall
+
+    def _poly_styleconv(self, ctx, L, cur: NHWC, s, d4, idx, noises, ctr):
         """StyleConv(sample_mode='upsample') (base_blocks.py:500-533): F.interpolate(x, 2, bilinear) then
         the modulated 3x3 conv + noise + bias + LeakyReLU, as one depth-to-space conv over ``cur`` with
         the folded parity-class filters (L.conv4).  The fold assumes every upsampled row / column is an
@@ -145,8 +165,6 @@ class ENetEngine:
         in."""
         dev, b = self.device, cur.n
         h2, w2 = 2 * cur.h, 2 * cur.w
-        d4 = torch.empty((b, L.conv4.cout), device=dev)
-        ops.modconv_demod(ctx, s, L.wsq4, d4, eps=1e-8, post=math.sqrt(2.0))
         d = d4[:, : L.cout]                                      # the class-0 block: the layer's own demod
         noise = None
         if L.noise_w:
@@ -212,9 +230,11 @@ class ENetEngine:
             with ops.x3_grid_cap(sctx, style_grid(dev)), ops.side_stream(sst, ctx.keep):
                 style = self.style_code(sctx, face[:, 3:])
                 ops.conv2d(sctx, style, self.mod, svec)
+                dtab, dall = self._demods(sctx, svec.t.view(b, -1))   # off the tail: beside LNet
         else:
             style = self.style_code(ctx, face[:, 3:])
             ops.conv2d(ctx, style, self.mod, svec)
+            dtab, dall = self._demods(ctx, svec.t.view(b, -1))
         s2 = svec.t.view(b, -1)
         # LNet input: cat(inp, gt) -> bilinear 96x96 (ENet.py:103-104)
         x6 = NHWC.empty(b, 96, 96, 6, dev)
@@ -238,15 +258,16 @@ class ENetEngine:
             for li in range(2):
                 L = self.layers[3 * st + li]
                 off = self.mod_offs[3 * st + li]
+                r0, wd = dtab.r0[2 * st + li], dtab.width[2 * st + li]
                 if POLY_UP and L.conv4 is not None:
-                    cur = self._poly_styleconv(ctx, L, cur, s2[:, off: off + L.cin], 2 * st + li, noises, ctr)
+                    cur = self._poly_styleconv(ctx, L, cur, s2[:, off: off + L.cin], dall[:, r0: r0 + wd],
+                                               2 * st + li, noises, ctr)
                     continue
                 x = cur
                 if L.upsample:
                     x = NHWC.empty(b, 2 * cur.h, 2 * cur.w, cur.c, dev)
                     ops.resize_nhwc(ctx, cur, x, scale_factor=2)
-                d = torch.empty((b, L.cout), device=dev)
-                ops.modconv_demod(ctx, s2[:, off: off + L.cin], L.wsq, d, eps=1e-8, post=math.sqrt(2.0))
+                d = dall[:, r0: r0 + L.cout]
                 y = NHWC.empty(b, x.h, x.w, L.cout, dev)
                 noise = None
                 if L.noise_w:

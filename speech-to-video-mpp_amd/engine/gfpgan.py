@@ -83,6 +83,12 @@ class GFPGANEngine:
         self.style_b = torch.cat(bs).contiguous().to(dev)
         self.style_seg = torch.cat(segs).contiguous().to(dev)
         self.style_total = off
+        # every demodulated layer's d (style_conv1 + style_convs) from one launch right after the style
+        # GEMV (stylegan2_clean_arch.py:81-83 per layer in the reference): layer L's d is columns
+        # [demod_r0[L], + L.cout) of the [B, nrows] output
+        dl = [self.conv1] + self.convs
+        self.demod = ops.DemodRows([(self.style_off[id(L)], L.wsq) for L in dl], dev)
+        self.demod_r0 = {id(L): r for L, r in zip(dl, self.demod.r0)}
         self.noise_bufs = [sd[f"{d}noises.noise{i}"].float().reshape(-1).to(dev) for i in range(2 * nd + 1)]
         self._noise_cache = {}
         self.noise_seed = 0x6F9A
@@ -113,15 +119,15 @@ class GFPGANEngine:
         o = self.style_off[id(L)]
         return sall[:, o: o + L.cin]
 
-    def _style_conv(self, ctx, L, x: NHWC, sall, noise):
+    def _style_conv(self, ctx, L, x: NHWC, sall, dall, noise):
         b, dev = x.n, self.device
         s = self._style(L, sall)
         if L.upsample:
             xu = NHWC.empty(b, 2 * x.h, 2 * x.w, x.c, dev)
             ops.resize_nhwc(ctx, x, xu, scale_factor=2)
             x = xu
-        d = torch.empty((b, L.cout), device=dev)
-        ops.modconv_demod(ctx, s, L.wsq, d, eps=1e-8, post=math.sqrt(2.0))
+        r0 = self.demod_r0[id(L)]
+        d = dall[:, r0: r0 + L.cout]
         y = NHWC.empty(b, x.h, x.w, L.cout, dev)
         ops.conv2d(ctx, x, L.conv, y, in_scale=s, nc_scale=d, act=ops.ACT_LRELU, alpha=LRELU,
                    pix_add=noise if L.noise_w else None, pix_w=L.noise_w or 0.0)
@@ -170,6 +176,8 @@ class GFPGANEngine:
 
         sall = ops.empty((b, self.style_total), dev)
         ops.adain_params(ctx, style.t.view(b, -1), nsf, self.style_w2t, self.style_b, self.style_seg, sall)
+        dall = ops.empty((b, self.demod.nrows), dev)
+        ops.modconv_demod_rows(ctx, sall, self.demod, dall, eps=1e-8, post=math.sqrt(2.0))
         nl = 2 * self.levels + 1
         if noises is not None:
             noise = [None if t is None else t.reshape(b, -1).contiguous() for t in noises]
@@ -184,19 +192,19 @@ class GFPGANEngine:
         else:
             noise = self._stored_noise(b)
         cur = NHWC(self.const.expand(b, -1, -1, -1).contiguous())
-        cur = self._style_conv(ctx, self.conv1, cur, sall, noise[0])
+        cur = self._style_conv(ctx, self.conv1, cur, sall, dall, noise[0])
         skip = NHWC.empty(b, cur.h, cur.w, 3, dev)
         s = self._style(self.rgb1, sall)
         ops.conv2d(ctx, cur, self.rgb1.conv, skip, in_scale=s)
         i = 1
         for lvl in range(self.levels):
-            cur = self._style_conv(ctx, self.convs[2 * lvl], cur, sall, noise[2 * lvl + 1])
+            cur = self._style_conv(ctx, self.convs[2 * lvl], cur, sall, dall, noise[2 * lvl + 1])
             if i < 2 * len(conds):
                 scale, shift = conds[(i - 1) // 2]
                 half = cur.c // 2 if self.sft_half else 0
                 part = cur.slice(half, cur.c - half)
                 ops.eltwise(ctx, part, part, mul=scale, add=shift)
-            cur = self._style_conv(ctx, self.convs[2 * lvl + 1], cur, sall, noise[2 * lvl + 2])
+            cur = self._style_conv(ctx, self.convs[2 * lvl + 1], cur, sall, dall, noise[2 * lvl + 2])
             R = self.rgbs[lvl]
             rgb = NHWC.empty(b, cur.h, cur.w, 3, dev)
             ops.resize_nhwc(ctx, skip, rgb, scale_factor=2)

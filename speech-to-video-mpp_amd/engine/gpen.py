@@ -98,13 +98,18 @@ class GPENEngine:
             bs += [L.mod_b, torch.zeros(pad)]
             off += L.cin + pad
         self.mod = ConvW(torch.cat(ws), torch.cat(bs), dev)
+        # every StyledConv's demodulation from one launch after the modulation GEMM (gpen_model.py:225-247
+        # per layer in the reference): layer L's d is columns [demod_r0[L], + L.cout) of the output
+        dl = [self.conv1] + self.convs
+        self.demod = ops.DemodRows([(L.mod_off, L.wsq) for L in dl], dev)
+        for L, r in zip(dl, self.demod.r0):
+            L.demod_r0 = r
 
-    def _styled(self, ctx, L, x: NHWC, svec, out: NHWC, noise: NHWC):
+    def _styled(self, ctx, L, x: NHWC, svec, dall, out: NHWC, noise: NHWC):
         """StyledConv with isconcat: out [.., 2C] <- (lrelu(sqrt2 (demod conv + b)), lrelu(sqrt2 (w e + b)))."""
         b, dev = x.n, self.device
         s = svec[:, L.mod_off: L.mod_off + L.cin]
-        d = torch.empty((b, L.cout), device=dev)
-        ops.modconv_demod(ctx, s, L.wsq, d, eps=1e-8, post=SQ2)
+        d = dall[:, L.demod_r0: L.demod_r0 + L.cout]
         C = L.cout
         if L.upsample:
             oh, ow = L.conv.out_hw(x.h, x.w)
@@ -150,10 +155,12 @@ class GPENEngine:
         svec = NHWC.empty(b, 1, 1, self.mod.cout, dev)
         ops.conv2d(ctx, lat, self.mod, svec)
         sv = svec.t.view(b, -1)
+        dall = ops.empty((b, self.demod.nrows), dev)
+        ops.modconv_demod_rows(ctx, sv, self.demod, dall, eps=1e-8, post=SQ2)
         noise = [f for f in feats[::-1] for _ in range(2)][1:]      # FullGenerator.forward (:619-621)
         cur_in = NHWC(self.const.expand(b, -1, -1, -1).contiguous())
         cat = NHWC.empty(b, 4, 4, 2 * self.conv1.cout, dev)
-        self._styled(ctx, self.conv1, cur_in, sv, cat, noise[0])
+        self._styled(ctx, self.conv1, cur_in, sv, dall, cat, noise[0])
         skip = NHWC.empty(b, 4, 4, 3, dev)
         s = sv[:, self.rgb1.mod_off: self.rgb1.mod_off + self.rgb1.cin]
         ops.conv2d(ctx, cat, self.rgb1.conv, skip, in_scale=s, shift=self.rgb1.bias)
@@ -161,9 +168,9 @@ class GPENEngine:
             L1, L2, R = self.convs[2 * lvl], self.convs[2 * lvl + 1], self.rgbs[lvl]
             h = 2 * cat.h
             a = NHWC.empty(b, h, h, 2 * L1.cout, dev)
-            self._styled(ctx, L1, cat, sv, a, noise[2 * lvl + 1])
+            self._styled(ctx, L1, cat, sv, dall, a, noise[2 * lvl + 1])
             cat = NHWC.empty(b, h, h, 2 * L2.cout, dev)
-            self._styled(ctx, L2, a, sv, cat, noise[2 * lvl + 2])
+            self._styled(ctx, L2, a, sv, dall, cat, noise[2 * lvl + 2])
             rgb = NHWC.empty(b, h, h, 3, dev)
             ops.fir2d(ctx, skip, R.up_k, rgb, up=2, pad0=(2, 2))     # Upsample pad (2, 1)
             s = sv[:, R.mod_off: R.mod_off + R.cin]

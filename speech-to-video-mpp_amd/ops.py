@@ -986,6 +986,32 @@ def modconv_demod(ctx: Ctx, s: torch.Tensor, wsq: torch.Tensor, out: torch.Tenso
     return out
 
 
+class DemodRows:
+    """The demodulated layers of one StyleGAN2 decoder as one row table (``s2v::modconv_demod_rows_``):
+    ``layers`` = [(s_off, wsq [cout, cin])...] in row order; layer l's demodulation vector is columns
+    ``self.r0[l] : self.r0[l] + cout_l`` of the [B, nrows] output."""
+
+    def __init__(self, layers, device):
+        rows, ws, r0, w_off, reach = [], [], [], 0, 0
+        for s_off, wsq in layers:
+            cout, cin = wsq.shape
+            r0.append(len(rows))
+            rows += [(s_off, cin, w_off + o * cin, 0) for o in range(cout)]
+            ws.append(wsq.reshape(-1).float().cpu())
+            w_off += cout * cin
+            reach = max(reach, s_off + cin)
+        assert w_off < 2 ** 31, "demod table: squared weights past int32 offsets"
+        self.rows = torch.tensor(rows, dtype=torch.int32).to(device)
+        self.wsq = torch.cat(ws).contiguous().to(device)
+        self.r0, self.nrows, self.s_reach = r0, len(rows), reach
+
+
+def modconv_demod_rows(ctx: Ctx, s: torch.Tensor, table: DemodRows, out: torch.Tensor, *, eps=1e-8, post=1.0):
+    """s: [B, >= table.s_reach] style bank (unit column stride), out: [B, >= table.nrows]."""
+    S2V.modconv_demod_rows_(s, table.rows, table.wsq, out, eps, post, table.s_reach)
+    return out
+
+
 def torch_bilinear_scale(in_size: int, out_size: int, scale_factor=None) -> float:
     """area_pixel_compute_scale (align_corners=False) as PyTorch computes it (float32)."""
     if scale_factor is not None and scale_factor > 0:

@@ -437,6 +437,29 @@ def test_adain_params_and_demod(ctx, b, nh, L, total, contig):
     assert ((d.double().cpu() - ref).abs() / ref).max() < 1e-5
 
 
+@pytest.mark.parametrize("b", [1, 4, 19])
+def test_demod_rows_segmented(ctx, b):
+    """ops.DemodRows: several layers' demodulations in one launch (ragged cin: one partial 64-lane
+    chunk, a 256-wide chunk plus a tail, 1024; batch past the 16-sample chunk) against per-layer fp64."""
+    shapes = [(24, 40), (33, 300), (16, 1024), (8, 512), (5, 7)]
+    offs, o = [], 0
+    for _, cin in shapes:
+        offs.append(o)
+        o += cin + 3
+    s = rnd(b, o + 5, seed=31).float().to(DEV)
+    ws = [rnd(co, ci, seed=32 + i, lo=0, hi=1).float() for i, (co, ci) in enumerate(shapes)]
+    t = ops.DemodRows(list(zip(offs, ws)), DEV)
+    d = torch.full((b, t.nrows + 6), -1.0, device=DEV)
+    ops.modconv_demod_rows(ctx, s, t, d, eps=1e-8, post=math.sqrt(2))
+    sd = s.double().cpu()
+    for r0, off, w in zip(t.r0, offs, ws):
+        ci = w.shape[1]
+        ref = torch.rsqrt((sd[:, off: off + ci] ** 2) @ w.double().t() + 1e-8) * math.sqrt(2)
+        got = d[:, r0: r0 + w.shape[0]].double().cpu()
+        assert ((got - ref).abs() / ref).max() < 1e-5
+    assert (d[:, t.nrows:] == -1).all()
+
+
 @pytest.mark.parametrize("shape", [((2, 3, 384, 384), (96, 96), None), ((2, 5, 64, 64), None, 0.5),
                                    ((1, 4, 50, 50), None, 2), ((1, 3, 256, 256), (256, 256), None),
                                    ((2, 6, 100, 90), (37, 53), None), ((2, 8, 40, 36), None, 0.5),
