@@ -27,6 +27,8 @@ template <int ELT>   // LDS-DMA kernels on split-layout inputs (conv_glds.hip): 
 void launch_conv_glds(int cfg, const ConvArgs &a, dim3 grid, hipStream_t s);
 template <int ELT>   // grouped x3 launches (conv_x3_impl.hpp conv_igemm_x3_group): 0 or an error
 int launch_conv_x3_group(int cfg, const ConvGroup &g, dim3 grid, hipStream_t s);
+template <int ELT>   // narrow-N register-direct-A kernel (conv_x3_nar.hip)
+int launch_conv_x3_nar(const ConvArgs &a, dim3 grid, hipStream_t s);
 
 template <int BM, int BN, int AR, int BR, int BKN>
 __device__ __forceinline__ void store_ab(float *As, float *Bs, int tid, const f4 (&ra)[AR],
@@ -874,6 +876,7 @@ struct X3Cfg {
     TileCfg t;
     float tflops;
     int bpc;
+    int kind = 0;    // 1: conv_x3_nar (register-direct A fragments, conv_x3_nar.hip)
 };
 static const X3Cfg kX3Tiles[] = {
     {{256, 256, 2, 8, 1, 1}, 400.f, 1}, {{128, 128, 2, 8, 1, 1}, 330.f, 2}, {{64, 128, 2, 8, 1, 1}, 260.f, 3},
@@ -887,7 +890,10 @@ static const X3Cfg kX3Tiles[] = {
     // deep-stage 4-wave tiles (r05): 2 or 4 K-slices per LDS stage, so a latency-bound small-grid conv (LNet's
     // 12^2 - 48^2 layers: one block per CU, K loops of 6 - 72 slices) waits on half / a quarter as many
     // load round trips; one block per CU by LDS.  Forced-only until measured (tools/lnet_convs.py --tiles)
-    {{64, 64, 2, 4, 4, 1}, 0.f, 1},     {{128, 64, 2, 4, 2, 1}, 0.f, 1},   {{128, 32, 4, 4, 2, 1}, 0.f, 1}};
+    {{64, 64, 2, 4, 4, 1}, 0.f, 1},     {{128, 64, 2, 4, 2, 1}, 0.f, 1},   {{128, 32, 4, 4, 2, 1}, 0.f, 1},
+    // 256 x 64 with A fragments loaded by each lane straight into registers, B alone through LDS
+    // (conv_x3_nar.hip): direct zero-padded convs, cin % 32 == 0, no pooled epilogue, 2^31-byte offsets
+    {{256, 64, 4, 4, 1, 1}, 0.f, 2, 1}};
 constexpr int kNumX3 = sizeof(kX3Tiles) / sizeof(kX3Tiles[0]);
 
 static const TileCfg &tile_cfg(const s2v_conv_params *p, int tile);
@@ -962,6 +968,7 @@ static bool tiled_x3(const s2v_conv_params *p) {
 static bool uses_x3(const s2v_conv_params *p) { return tiled_x3(p) && !p->b_kn; }
 
 static int a_mode(const s2v_conv_params *p);
+static bool nar_ok(const s2v_conv_params *p);
 
 
 static const TileCfg &tile_cfg(const s2v_conv_params *p, int tile) {
@@ -1014,6 +1021,7 @@ static Plan make_plan_x3(const s2v_conv_params *p, int M, Plan pl) {
     for (int i = 0; i < kNumX3; ++i) {
         const X3Cfg &c = kX3Tiles[i];
         if (c.tflops <= 0.f) continue;                          // forced-only configurations
+        if (c.kind == 1 && !nar_ok(p)) continue;
         if (p->b_kn && c.t.nw != 4) continue;
         if (c.t.bm >= 256 && c.t.bn >= 128 && am != 0 && am != 3) continue;   // generic gathers spill there
         // the 256 / 512-row narrow-N tiles on per-row gathers: measured slower than 128x64 (256x64, r02)
@@ -1161,6 +1169,10 @@ static int validate(const s2v_conv_params *p, int &M, int &K) {
                 "conv2d: bad force_tile %d", p->force_tile);
     S2V_REQUIRE(!(tiled_x3(p) && p->b_kn && p->force_tile > 0 && kX3Tiles[p->force_tile - 1].t.nw != 4),
                 "conv2d: b_kn operands need a 4-wave split-bf16 tile (force_tile 4..6)");
+    S2V_REQUIRE(!(tiled_x3(p) && p->force_tile > 0 && kX3Tiles[p->force_tile - 1].kind == 1 && !nar_ok(p)),
+                "conv2d: force_tile %d (conv_x3_nar) needs a direct zero-padded conv, cin %% 32 == 0, <= 32 taps, no "
+                "pooling, packed weights over whole 64-row slabs, 2^31-byte offsets and, with in_scale, "
+                "oh * ow %% 256 == 0", p->force_tile);
     if (tiled_x3(p) && p->force_tile > 0) {
         // a forced tile must not read weight rows past the packed [npad] rows (the planner never
         // picks such a tile: the kernels load whole BN-row slabs of B without a row guard)
@@ -1310,6 +1322,15 @@ static int x3_amode(const s2v_conv_params *p, const TileCfg &t) {
     // never AMODE 0 for a partial 1x1, which assumes whole 32-channel K-slices)
     if (x_extent_bytes(p) >= (1LL << 31) || (long long)p->npad * p->kpad * 4 >= (1LL << 31)) return a_mode(p);
     return 4;
+}
+
+// conv_x3_nar's conditions: the AMODE 4 addressing (direct zero-padded conv, whole 32-channel slices,
+// <= 32 taps, 2^31-byte offsets), packed weights covering every 64-row B slab, no pooled epilogue, and
+// with an input modulation every 256-row tile inside one image (its s[n, c] loads are per tile)
+static bool nar_ok(const s2v_conv_params *p) {
+    return tiled_x3(p) && !p->b_kn && !p->x_split && a_mode(p) == 0 && p->cin % 32 == 0 && !p->out_pool &&
+           p->kh * p->kw <= 32 && x_extent_bytes(p) < (1LL << 31) && (long long)p->npad * p->kpad * 4 < (1LL << 31) &&
+           (long long)cdiv(p->cout, 64) * 64 <= p->npad && (!p->in_scale || (p->oh * p->ow) % 256 == 0);
 }
 
 // Persistent blocks of a launch under s2v_conv_params.grid_cap: the 256x256 buffer-load split-precision
@@ -1551,7 +1572,7 @@ extern "C" int s2v_conv2d_plan(const s2v_conv_params *p, int *out6) {
     }
     const TileCfg &t = tile_cfg(p, pl.tile);
     out6[0] = t.bm; out6[1] = t.bn; out6[2] = t.wm;
-    out6[3] = tiled_x3(p) ? x3_amode(p, t) : a_mode(p);
+    out6[3] = tiled_x3(p) ? (kX3Tiles[pl.tile].kind == 1 ? 6 : x3_amode(p, t)) : a_mode(p);
     out6[4] = p->b_kn != 0;
     out6[5] = pl.splits;
     out6[6] = tiled_x3(p) ? p->prec : 0;
@@ -1639,6 +1660,11 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
     dim3 grid(cdiv(M, t.bm), cdiv(p->cout, t.bn), batch * pl.splits);
     if (tiled_x3(p)) {
         if (!bkn) a.wt = (const float *)p->wt_x3;
+        if (kX3Tiles[pl.tile].kind == 1) {         // conv_x3_nar (nar_ok checked by the planner / validate)
+            a.x_bytes = (unsigned)x_extent_bytes(p);
+            a.w_bytes = (unsigned)((long long)p->npad * p->kpad * 4);
+            rc = p->prec == S2V_PREC_BF16X3 ? launch_conv_x3_nar<0>(a, grid, s) : launch_conv_x3_nar<1>(a, grid, s);
+        } else {
         const int am = x3_amode(p, t);
         if (am == 4) {
             a.x_bytes = (unsigned)x_extent_bytes(p);
@@ -1653,6 +1679,7 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
         }
         rc = p->prec == S2V_PREC_BF16X3 ? launch_conv_x3<0>(pl.tile, a, am, bkn, grid, s)
                                         : launch_conv_x3<1>(pl.tile, a, am, bkn, grid, s);
+        }
         if (rc) return rc;
     } else switch (pl.tile) {
         case 0: launch_tile<128, 128, 2>(a, amode, bkn, grid, s); break;

@@ -133,7 +133,46 @@ CONV_CASES = [
     (2, 32, 9, 10, 48, 3, 1, 1, 1, "up2", "zero", 11, 0),
     (2, 64, 20, 18, 32, 3, 1, 1, 1, "direct", "zero", 12, 0),
     (1, 128, 13, 17, 24, 3, 2, 1, 1, "direct", "zero", 12, 4),
+    # conv_x3_nar (force_tile 16: register-direct A fragments, 256x64): ragged M, N < 64, several N
+    # tiles, stride 2, split-K, 1x1
+    (2, 64, 23, 29, 64, 3, 1, 1, 1, "direct", "zero", 16, 0),
+    (1, 96, 19, 21, 40, 3, 1, 1, 1, "direct", "zero", 16, 3),
+    (2, 32, 17, 15, 130, 3, 2, 1, 1, "direct", "zero", 16, 0),
+    (2, 64, 11, 13, 96, 1, 1, 0, 1, "direct", "zero", 16, 2),
 ]
+
+
+@pytest.mark.parametrize("shape", [(4, 64, 32, 48, 64, 3, 1), (2, 128, 32, 40, 48, 3, 1), (2, 64, 64, 64, 64, 3, 2),
+                                   (3, 32, 16, 96, 64, 1, 1)])
+def test_conv_nar_bit_identical_to_lds_tile(ctx, prec, shape):
+    """conv_x3_nar (A fragments straight to registers) against the LDS-staged 256x64 4-wave tile
+    (force_tile 11): same K order, same split, same MFMA order per slice -> bit-identical outputs, with
+    the StyleGAN2 input modulation (in_scale, per image: tiles inside one image and tiles straddling two),
+    a pre-activation, the demodulation / noise / residual epilogue."""
+    if prec == "f32":
+        pytest.skip("split precisions only")
+    n, cin, h, w, cout, k, st = shape
+    wt = rnd(cout, cin, k, k, seed=41) / math.sqrt(cin * k * k)
+    cw = ConvW(wt.float(), rnd(cout, seed=42).float(), DEV, stride=st, padding=k // 2)
+    x = nhwc(rnd(n, cin, h, w, seed=43).float())
+    oh, ow = (h + 2 * (k // 2) - k) // st + 1, (w + 2 * (k // 2) - k) // st + 1
+    s = rnd(n, cin, seed=44, lo=0.5, hi=1.5).float().to(DEV)
+    d = rnd(n, cout, seed=45, lo=0.5, hi=1.5).float().to(DEV)
+    noise = rnd(n, oh * ow, seed=46).float().to(DEV)
+    res = nhwc(rnd(n, cout, oh, ow, seed=47).float())
+    for kw in (dict(), dict(in_scale=s, nc_scale=d, pix_add=noise, pix_w=0.3, act=ops.ACT_LRELU, alpha=0.2),
+               dict(pre_act=ops.ACT_LRELU, pre_alpha=0.2, res=res, act=ops.ACT_TANH), dict(force_splits=2)):
+        outs = []
+        for tile in (11, 16):
+            y = NHWC.empty(n, oh, ow, cout, DEV)
+            ops.conv2d(ctx, x, cw, y, force_tile=tile, **kw)
+            outs.append(y.t.clone())
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0], outs[1]), f"{kw.keys()}: max diff {(outs[0] - outs[1]).abs().max():.3e}"
+    xs = nhwc(rnd(n, cin, 10, 10, seed=48).float())
+    with pytest.raises(Exception, match="conv_x3_nar"):
+        ops.conv2d(ctx, xs, cw, NHWC.empty(n, (10 + 2 * (k // 2) - k) // st + 1, (10 + 2 * (k // 2) - k) // st + 1,
+                                           cout, DEV), force_tile=16, in_scale=s)
 
 
 @pytest.fixture

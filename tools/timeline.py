@@ -68,7 +68,7 @@ def main():
                           f"ends {(max(big) - lo) / 1e3:8.1f} us")
 
 
-if __name__ == "__main__" and "--lnet" not in sys.argv and "--ffc" not in sys.argv:
+if __name__ == "__main__" and not {"--lnet", "--ffc", "--seq"} & set(sys.argv):
     main()
 
 
@@ -114,3 +114,40 @@ def lnet_ffc(path, k=4):
 
 if __name__ == "__main__" and "--ffc" in sys.argv:
     lnet_ffc(sys.argv[1])
+
+
+def step_sequence(path, marker, nth=2):
+    """Every kernel of one graph-replayed step (from the ``nth``-last launch of ``marker`` to the next),
+    in start order: start offset, duration, idle gap before it, grid (when the trace has it), name;
+    then the step's kernel time grouped by kernel name.  Usage: timeline.py db --seq MARKER"""
+    db = sqlite3.connect(path)
+    cols = [r[1] for r in db.execute("pragma table_info(kernels)")]
+    s = "start" if "start" in cols else "start_ns"
+    e = "end" if "end" in cols else "end_ns"
+    gcols = [c for c in ("grid_size_x", "grid_size_y", "grid_size_z", "grid_x", "grid_y", "grid_z") if c in cols]
+    sel = ", ".join(["name", s, e] + gcols)
+    ks = list(db.execute(f"select {sel} from kernels order by {s}"))
+    mk = [i for i, k in enumerate(ks) if k[0].startswith(marker) or marker in k[0].split("(")[0]]
+    if len(mk) < nth + 1:
+        print(f"{len(mk)} launches of {marker!r} in the trace")
+        return
+    i0, i1 = mk[-nth - 1], mk[-nth]
+    seg = ks[i0:i1]
+    t0, prev = seg[0][1], seg[0][1]
+    per = defaultdict(lambda: [0, 0.0])
+    print(f"step: {(ks[i1][1] - t0) / 1e3:.1f} us, {len(seg)} kernels (columns: offset, duration, gap, grid, name)")
+    for k in seg:
+        n, a, b = k[0], k[1], k[2]
+        g = "x".join(str(v) for v in k[3:]) if gcols else ""
+        print(f"  {(a - t0) / 1e3:9.1f} {(b - a) / 1e3:8.1f} {(a - prev) / 1e3:7.1f} {g:>16s}  {n.split('(')[0][:80]}")
+        prev = max(prev, b)
+        p = per[n.split("(")[0][:80]]
+        p[0] += 1
+        p[1] += (b - a) / 1e3
+    print("by kernel:")
+    for n, (c, t) in sorted(per.items(), key=lambda kv: -kv[1][1]):
+        print(f"  {t:9.1f} us {c:5d}  {n}")
+
+
+if __name__ == "__main__" and "--seq" in sys.argv:
+    step_sequence(sys.argv[1], sys.argv[sys.argv.index("--seq") + 1])
