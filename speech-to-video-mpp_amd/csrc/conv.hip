@@ -27,8 +27,10 @@ template <int ELT>   // LDS-DMA kernels on split-layout inputs (conv_glds.hip): 
 void launch_conv_glds(int cfg, const ConvArgs &a, dim3 grid, hipStream_t s);
 template <int ELT>   // grouped x3 launches (conv_x3_impl.hpp conv_igemm_x3_group): 0 or an error
 int launch_conv_x3_group(int cfg, const ConvGroup &g, dim3 grid, hipStream_t s);
-template <int ELT>   // narrow-N register-direct-A kernel (conv_x3_nar.hip)
-int launch_conv_x3_nar(const ConvArgs &a, dim3 grid, hipStream_t s);
+template <int ELT>   // narrow-N register-direct-A kernel (conv_x3_nar.hip); breg: B fragments direct too
+int launch_conv_x3_nar(const ConvArgs &a, bool breg, dim3 grid, hipStream_t s);
+template <int ELT>   // 3x3 spatial-patch kernel with the input halo staged once per channel slice (conv_x3_halo.hip)
+int launch_conv_x3_halo(const ConvArgs &a, dim3 grid, hipStream_t s);
 
 template <int BM, int BN, int AR, int BR, int BKN>
 __device__ __forceinline__ void store_ab(float *As, float *Bs, int tid, const f4 (&ra)[AR],
@@ -876,7 +878,7 @@ struct X3Cfg {
     TileCfg t;
     float tflops;
     int bpc;
-    int kind = 0;    // 1: conv_x3_nar (register-direct A fragments, conv_x3_nar.hip)
+    int kind = 0;    // 1 / 2: conv_x3_nar (register-direct A / A and B fragments), 3: conv_x3_halo
 };
 static const X3Cfg kX3Tiles[] = {
     {{256, 256, 2, 8, 1, 1}, 400.f, 1}, {{128, 128, 2, 8, 1, 1}, 330.f, 2}, {{64, 128, 2, 8, 1, 1}, 260.f, 3},
@@ -893,7 +895,12 @@ static const X3Cfg kX3Tiles[] = {
     {{64, 64, 2, 4, 4, 1}, 0.f, 1},     {{128, 64, 2, 4, 2, 1}, 0.f, 1},   {{128, 32, 4, 4, 2, 1}, 0.f, 1},
     // 256 x 64 with A fragments loaded by each lane straight into registers, B alone through LDS
     // (conv_x3_nar.hip): direct zero-padded convs, cin % 32 == 0, no pooled epilogue, 2^31-byte offsets
-    {{256, 64, 4, 4, 1, 1}, 0.f, 2, 1}};
+    {{256, 64, 4, 4, 1, 1}, 0.f, 2, 1},
+    // ... with the B fragments loaded by every wave into registers too: no LDS, no barrier per slice
+    {{256, 64, 4, 4, 1, 1}, 0.f, 2, 2},
+    // 4 x 64 output patches, 64 channels, the 6 x 66 input halo per channel slice staged once
+    // (conv_x3_halo.hip): 3x3 stride-1 zero-padded convs with oh % 4 == 0, ow % 64 == 0
+    {{256, 64, 4, 4, 1, 1}, 0.f, 2, 3}};
 constexpr int kNumX3 = sizeof(kX3Tiles) / sizeof(kX3Tiles[0]);
 
 static const TileCfg &tile_cfg(const s2v_conv_params *p, int tile);
@@ -902,6 +909,7 @@ constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 struct Plan {
     int tile;   // index into kTiles, or -1 for the direct small-N kernel
     int splits, tps, ktiles;
+    int kslab = 1;   // split-K granularity in K-slices (9 for conv_x3_halo: whole channel slices)
 };
 
 // 16-byte epilogue stores are possible (store_epilogue4's vec): aligned rows and per-channel vectors
@@ -969,6 +977,8 @@ static bool uses_x3(const s2v_conv_params *p) { return tiled_x3(p) && !p->b_kn; 
 
 static int a_mode(const s2v_conv_params *p);
 static bool nar_ok(const s2v_conv_params *p);
+static bool x3_kind_ok(const s2v_conv_params *p, int kind);
+static bool halo_ok(const s2v_conv_params *p);
 
 
 static const TileCfg &tile_cfg(const s2v_conv_params *p, int tile) {
@@ -976,6 +986,14 @@ static const TileCfg &tile_cfg(const s2v_conv_params *p, int tile) {
 }
 
 static void finish_plan(Plan &pl, int splits) {
+    if (pl.kslab > 1) {                  // splits over whole groups of kslab K-slices (conv_x3_halo: 9 taps)
+        const int groups = pl.ktiles / pl.kslab;
+        if (splits > groups) splits = groups;
+        if (splits < 1) splits = 1;
+        pl.tps = (groups + splits - 1) / splits * pl.kslab;
+        pl.splits = (pl.ktiles + pl.tps - 1) / pl.tps;
+        return;
+    }
     if (splits > pl.ktiles) splits = pl.ktiles;
     if (splits < 1) splits = 1;
     pl.tps = (pl.ktiles + splits - 1) / splits;
@@ -990,6 +1008,7 @@ static Plan make_plan_x3(const s2v_conv_params *p, int M, Plan pl) {
     const int cus = plan_cus();
     if (p->force_tile > 0) {
         pl.tile = p->force_tile - 1;
+        if (kX3Tiles[pl.tile].kind == 3) pl.kslab = 9;
         const TileCfg &t = kX3Tiles[pl.tile].t;
         const long long blocks = (long long)cdiv(M, t.bm) * cdiv(p->cout, t.bn) * batch;
         int splits = p->force_splits;
@@ -1000,6 +1019,23 @@ static Plan make_plan_x3(const s2v_conv_params *p, int M, Plan pl) {
         }
         finish_plan(pl, splits);
         return pl;
+    }
+    // 3x3 stride-1 layers of <= 128 output channels over 64-wide rows (the enhancers' and DNet's 128^2 -
+    // 512^2 layers): the halo-staged spatial patch kernel, measured 20-30 % faster than every implicit-GEMM
+    // tile on them (4x512^2 64 -> 64: 356 vs 444 us, 128 -> 64: 547 vs 697, 4x256^2 128 -> 128: 292 vs 381,
+    // profiles/r05_halo_sweep.txt), whenever the grid fills the chip without split-K
+    if (halo_ok(p) && p->cout <= 128) {
+        const int batch = p->batch > 0 ? p->batch : 1;
+        const long long blocks = (long long)(M / 256) * cdiv(p->cout, 64) * batch;
+        if (blocks >= 2LL * plan_cus()) {
+            for (int i = 0; i < kNumX3; ++i)
+                if (kX3Tiles[i].kind == 3) {
+                    pl.tile = i;
+                    pl.kslab = 9;
+                    finish_plan(pl, 1);
+                    return pl;
+                }
+        }
     }
     if (pl.ktiles <= 4 && !p->b_kn && tune_value(S2V_TUNE_SMALLK_TILE)) {
         // K <= 128 (image-input layers): the launch is output-write / gather bound, the throughput
@@ -1021,7 +1057,7 @@ static Plan make_plan_x3(const s2v_conv_params *p, int M, Plan pl) {
     for (int i = 0; i < kNumX3; ++i) {
         const X3Cfg &c = kX3Tiles[i];
         if (c.tflops <= 0.f) continue;                          // forced-only configurations
-        if (c.kind == 1 && !nar_ok(p)) continue;
+        if (!x3_kind_ok(p, c.kind)) continue;
         if (p->b_kn && c.t.nw != 4) continue;
         if (c.t.bm >= 256 && c.t.bn >= 128 && am != 0 && am != 3) continue;   // generic gathers spill there
         // the 256 / 512-row narrow-N tiles on per-row gathers: measured slower than 128x64 (256x64, r02)
@@ -1047,6 +1083,7 @@ static Plan make_plan_x3(const s2v_conv_params *p, int M, Plan pl) {
         }
     }
     pl.tile = bt;
+    if (kX3Tiles[bt].kind == 3) pl.kslab = 9;
     finish_plan(pl, bs);
     return pl;
 }
@@ -1169,10 +1206,11 @@ static int validate(const s2v_conv_params *p, int &M, int &K) {
                 "conv2d: bad force_tile %d", p->force_tile);
     S2V_REQUIRE(!(tiled_x3(p) && p->b_kn && p->force_tile > 0 && kX3Tiles[p->force_tile - 1].t.nw != 4),
                 "conv2d: b_kn operands need a 4-wave split-bf16 tile (force_tile 4..6)");
-    S2V_REQUIRE(!(tiled_x3(p) && p->force_tile > 0 && kX3Tiles[p->force_tile - 1].kind == 1 && !nar_ok(p)),
-                "conv2d: force_tile %d (conv_x3_nar) needs a direct zero-padded conv, cin %% 32 == 0, <= 32 taps, no "
-                "pooling, packed weights over whole 64-row slabs, 2^31-byte offsets and, with in_scale, "
-                "oh * ow %% 256 == 0", p->force_tile);
+    S2V_REQUIRE(!(tiled_x3(p) && p->force_tile > 0 && !x3_kind_ok(p, kX3Tiles[p->force_tile - 1].kind)),
+                "conv2d: force_tile %d (conv_x3_nar / conv_x3_halo) needs a direct zero-padded conv, cin %% 32 == 0, "
+                "<= 32 taps, no pooling, packed weights over whole 64-row slabs, 2^31-byte offsets and, with "
+                "in_scale, oh * ow %% 256 == 0; conv_x3_halo also 3x3 stride 1 pad 1, oh %% 4 == 0, ow %% 64 == 0",
+                p->force_tile);
     if (tiled_x3(p) && p->force_tile > 0) {
         // a forced tile must not read weight rows past the packed [npad] rows (the planner never
         // picks such a tile: the kernels load whole BN-row slabs of B without a row guard)
@@ -1331,6 +1369,16 @@ static bool nar_ok(const s2v_conv_params *p) {
     return tiled_x3(p) && !p->b_kn && !p->x_split && a_mode(p) == 0 && p->cin % 32 == 0 && !p->out_pool &&
            p->kh * p->kw <= 32 && x_extent_bytes(p) < (1LL << 31) && (long long)p->npad * p->kpad * 4 < (1LL << 31) &&
            (long long)cdiv(p->cout, 64) * 64 <= p->npad && (!p->in_scale || (p->oh * p->ow) % 256 == 0);
+}
+
+// conv_x3_halo's conditions (and nar_ok's addressing / weight conditions)
+static bool halo_ok(const s2v_conv_params *p) {
+    return nar_ok(p) && p->kh == 3 && p->kw == 3 && p->sh == 1 && p->sw == 1 && p->dh == 1 && p->dw == 1 &&
+           p->ph == 1 && p->pw == 1 && p->oh % 4 == 0 && p->ow % 64 == 0;
+}
+
+static bool x3_kind_ok(const s2v_conv_params *p, int kind) {
+    return kind == 0 || (kind == 3 ? halo_ok(p) : nar_ok(p));
 }
 
 // Persistent blocks of a launch under s2v_conv_params.grid_cap: the 256x256 buffer-load split-precision
@@ -1572,7 +1620,7 @@ extern "C" int s2v_conv2d_plan(const s2v_conv_params *p, int *out6) {
     }
     const TileCfg &t = tile_cfg(p, pl.tile);
     out6[0] = t.bm; out6[1] = t.bn; out6[2] = t.wm;
-    out6[3] = tiled_x3(p) ? (kX3Tiles[pl.tile].kind == 1 ? 6 : x3_amode(p, t)) : a_mode(p);
+    out6[3] = tiled_x3(p) ? (kX3Tiles[pl.tile].kind >= 1 ? 5 + kX3Tiles[pl.tile].kind : x3_amode(p, t)) : a_mode(p);
     out6[4] = p->b_kn != 0;
     out6[5] = pl.splits;
     out6[6] = tiled_x3(p) ? p->prec : 0;
@@ -1660,10 +1708,16 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
     dim3 grid(cdiv(M, t.bm), cdiv(p->cout, t.bn), batch * pl.splits);
     if (tiled_x3(p)) {
         if (!bkn) a.wt = (const float *)p->wt_x3;
-        if (kX3Tiles[pl.tile].kind == 1) {         // conv_x3_nar (nar_ok checked by the planner / validate)
+        if (kX3Tiles[pl.tile].kind >= 1) {         // conv_x3_nar / _halo (conditions: planner / validate)
             a.x_bytes = (unsigned)x_extent_bytes(p);
             a.w_bytes = (unsigned)((long long)p->npad * p->kpad * 4);
-            rc = p->prec == S2V_PREC_BF16X3 ? launch_conv_x3_nar<0>(a, grid, s) : launch_conv_x3_nar<1>(a, grid, s);
+            const int kind = kX3Tiles[pl.tile].kind;
+            if (kind == 3)
+                rc = p->prec == S2V_PREC_BF16X3 ? launch_conv_x3_halo<0>(a, grid, s)
+                                                : launch_conv_x3_halo<1>(a, grid, s);
+            else
+                rc = p->prec == S2V_PREC_BF16X3 ? launch_conv_x3_nar<0>(a, kind == 2, grid, s)
+                                                : launch_conv_x3_nar<1>(a, kind == 2, grid, s);
         } else {
         const int am = x3_amode(p, t);
         if (am == 4) {

@@ -391,9 +391,24 @@ __device__ __forceinline__ void load_b(const ConvArgs &a, const float *__restric
 // register indices), then every thread walks the chunk row by row (consecutive threads ->
 // consecutive output channels: coalesced stores).  Split-K launches write raw partial sums to the
 // workspace instead.
+// ``base(c0)``: the GEMM row (output pixel m) of chunk row 0 — a chunk's CH rows are consecutive m;
+// ``rows(c0)``: how many of them exist.  epilogue_tile_fn is the linear tile (rows m0, m0 + 1, ...);
+// the spatial halo tile (conv_x3_halo.hip) maps each 64-row chunk to one output row segment.
+template <int BM, int BN, int NW, int CH, class Stage, class Base, class Rows>
+__device__ __forceinline__ void epilogue_tile_map(const ConvArgs &a, float *Cs, int tid, int n0, int bz, int bidx,
+                                                  Stage stage, Base base, Rows rows);
+
 template <int BM, int BN, int NW, int CH, class Stage>
 __device__ __forceinline__ void epilogue_tile_fn(const ConvArgs &a, float *Cs, int tid, int m0, int n0, int bz,
                                                  int bidx, Stage stage) {
+    const int mlim = min(BM, a.M - m0);
+    epilogue_tile_map<BM, BN, NW, CH>(a, Cs, tid, n0, bz, bidx, stage, [&](int c0) { return m0 + c0; },
+                                      [&](int c0) { return min(CH, mlim - c0); });
+}
+
+template <int BM, int BN, int NW, int CH, class Stage, class Base, class Rows>
+__device__ __forceinline__ void epilogue_tile_map(const ConvArgs &a, float *Cs, int tid, int n0, int bz, int bidx,
+                                                  Stage stage, Base base, Rows rows) {
     constexpr int NT = 64 * NW;
     constexpr int LDC = BN + 4;
     static_assert(CH % 16 == 0 && BM % CH == 0, "epilogue chunk");
@@ -403,7 +418,6 @@ __device__ __forceinline__ void epilogue_tile_fn(const ConvArgs &a, float *Cs, i
     const int cn = tid % TPR;
     const int n = n0 + cn;
     const bool live = n < a.cout;
-    const int mlim = min(BM, a.M - m0);
     const bool simple = !e.nc_scale && !e.pix_add && (!e.res || e.res_simple);
     const float sc = (live && e.scale) ? e.scale[n] : 1.f;
     const float sh = (live && e.shift) ? e.shift[n] : 0.f;
@@ -413,7 +427,8 @@ __device__ __forceinline__ void epilogue_tile_fn(const ConvArgs &a, float *Cs, i
         __syncthreads();   // operand stages (first chunk) / the previous chunk are no longer read
         stage(Cs, c0);
         __syncthreads();
-        const int clim = min(CH, mlim - c0);
+        const int clim = rows(c0);
+        const int cb = base(c0);
         if (!live || clim <= 0) continue;
         if (a.pool) {
             // 2x2 average of the activated outputs (ResBlock: lrelu(conv1) then bilinear x0.5 ==
@@ -424,7 +439,7 @@ __device__ __forceinline__ void epilogue_tile_fn(const ConvArgs &a, float *Cs, i
                 float v = 0.f;
 #pragma unroll
                 for (int d = 0; d < 4; ++d) v += fast_act(Cs[(4 * rq + d) * LDC + cn] * sc + sh, e.act, slope);
-                yb[(long long)((m0 + c0) / 4 + rq) * a.ycs] = 0.25f * v;
+                yb[(long long)(cb / 4 + rq) * a.ycs] = 0.25f * v;
             }
             continue;
         }
@@ -432,7 +447,7 @@ __device__ __forceinline__ void epilogue_tile_fn(const ConvArgs &a, float *Cs, i
             float *w = a.ws + (long long)bz * a.M * a.cout;
 #pragma unroll 1
             for (int rr = tid / TPR; rr < clim; rr += RSTEP)
-                w[(long long)(m0 + c0 + rr) * a.cout + n] = Cs[rr * LDC + cn];
+                w[(long long)(cb + rr) * a.cout + n] = Cs[rr * LDC + cn];
         } else if (simple) {
             float *__restrict__ yb = a.y + (long long)bidx * a.y_bs + out_col(a, n);
             const float *rsrc = e.res ? e.res + (long long)bidx * a.res_bs + n : nullptr;
@@ -445,7 +460,7 @@ __device__ __forceinline__ void epilogue_tile_fn(const ConvArgs &a, float *Cs, i
                 float rv[4];
                 if (rr0 + 3 * RSTEP < clim) {
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) rv[q] = rsrc[(long long)(m0 + c0 + rr0 + q * RSTEP) * e.res_cs];
+                    for (int q = 0; q < 4; ++q) rv[q] = rsrc[(long long)(cb + rr0 + q * RSTEP) * e.res_cs];
                 }
 #pragma unroll 1
                 for (; rr0 + 3 * RSTEP < clim; rr0 += 4 * RSTEP) {
@@ -454,11 +469,11 @@ __device__ __forceinline__ void epilogue_tile_fn(const ConvArgs &a, float *Cs, i
                     if (more) {
 #pragma unroll
                         for (int q = 0; q < 4; ++q)
-                            rn[q] = rsrc[(long long)(m0 + c0 + rr0 + (4 + q) * RSTEP) * e.res_cs];
+                            rn[q] = rsrc[(long long)(cb + rr0 + (4 + q) * RSTEP) * e.res_cs];
                     }
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
-                        const long long m = m0 + c0 + rr0 + q * RSTEP;
+                        const long long m = cb + rr0 + q * RSTEP;
                         float v = Cs[(rr0 + q * RSTEP) * LDC + cn] * sc + sh;
                         if (!e.res_after) v += rv[q];
                         v = fast_act(v, e.act, slope);
@@ -473,7 +488,7 @@ __device__ __forceinline__ void epilogue_tile_fn(const ConvArgs &a, float *Cs, i
             }
 #pragma unroll 1
             for (int rr = rr0; rr < clim; rr += RSTEP) {
-                const long long m = m0 + c0 + rr;
+                const long long m = cb + rr;
                 float v = Cs[rr * LDC + cn] * sc + sh;
                 float rv = 0.f;
                 if (rsrc) {
@@ -490,7 +505,7 @@ __device__ __forceinline__ void epilogue_tile_fn(const ConvArgs &a, float *Cs, i
             // element (store_epilogue), which made the epilogue as long as the main loop of a 64-channel tile
             const int hw = a.oh * a.ow;
             const int rr0 = tid / TPR;
-            int m = m0 + c0 + rr0;
+            int m = cb + rr0;
             int img = m / hw, rem = m - img * hw;
             float *__restrict__ yb = a.y + (long long)bidx * a.y_bs + out_col(a, n);
             const float *pix = e.pix_add ? e.pix_add + (long long)bidx * a.oh * a.ow * a.n : nullptr;
@@ -513,7 +528,7 @@ __device__ __forceinline__ void epilogue_tile_fn(const ConvArgs &a, float *Cs, i
             }
         } else {
 #pragma unroll 1
-            for (int rr = tid / TPR; rr < clim; rr += RSTEP) store_epilogue(a, bidx, m0 + c0 + rr, n, Cs[rr * LDC + cn]);
+            for (int rr = tid / TPR; rr < clim; rr += RSTEP) store_epilogue(a, bidx, cb + rr, n, Cs[rr * LDC + cn]);
         }
     }
 }

@@ -35,7 +35,9 @@ namespace s2v {
 #define NAR_ABL 0
 #endif
 
-template <int ELT>
+// BREG = 1: B fragments also straight to registers (every wave loads its own; the four waves' loads of
+// a slice hit the same lines): no LDS and no barrier in the main loop
+template <int ELT, int BREG>
 __global__ __launch_bounds__(256, 2) void conv_x3_nar(ConvArgs a) {
     launch_stamp(a, false);
     constexpr int BM = 256, BN = 64, NW = 4, TM16 = 4, TN16 = 4, RS = 32, BR = 2;
@@ -114,16 +116,31 @@ __global__ __launch_bounds__(256, 2) void conv_x3_nar(ConvArgs a) {
     ld.init(kt0, kperm, taps, nsl, a.kw);
     // one slice's operands in registers: B staging (two 16-byte slots), A fragments (8 channels of 4 rows)
     struct Ops {
-        u32x4 b[BR];
+        u32x4 b[BREG ? 1 : BR];
+        u32x4 bh[BREG ? TN16 : 1], bl[BREG ? TN16 : 1];   // BREG: the next slice's B fragments
         f4 v[2 * TM16];
         f4 s0, s1;       // modulation of the slice's channels (one-image tiles), loaded with the slice
         int cs;
     };
-    auto issue = [&](Ops &o) {
+    // BREG: this lane's B fragment rows n0 + 16 j + l16, hi slot kg and lo slot kg + 4 of the slice
+    int bfr[BREG ? TN16 : 1];
+#pragma unroll
+    for (int j = 0; j < (BREG ? TN16 : 1); ++j) bfr[j] = ((n0 + 16 * j + l16) * a.kpad) * 4 + kg * 16;
+    auto issue_b = [&](Ops &o) {
         const int kt = ld.kt(nsl);
 #pragma unroll
-        for (int j = 0; j < BR; ++j)
-            o.b[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wrs, boff[j], kt * 128, 0));
+        for (int j = 0; j < TN16; ++j) {
+            o.bh[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wrs, bfr[j], kt * 128, 0));
+            o.bl[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wrs, bfr[j] + 64, kt * 128, 0));
+        }
+    };
+    auto issue = [&](Ops &o) {
+        const int kt = ld.kt(nsl);
+        if constexpr (!BREG) {
+#pragma unroll
+            for (int j = 0; j < BR; ++j)
+                o.b[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wrs, boff[j], kt * 128, 0));
+        }
         const int toff = NAR_ABL == 1 ? 0 : ((ld.ky * a.dh * a.w + ld.kx * a.dw) * a.xcs + ld.cs * 32) * 4;
 #pragma unroll
         for (int i = 0; i < TM16; ++i) {
@@ -203,20 +220,58 @@ __global__ __launch_bounds__(256, 2) void conv_x3_nar(ConvArgs a) {
         // g + 1 is loaded first, so its LDS store waits for those two loads only.  A second register set
         // (two slices in flight) does not fit 256 VGPRs at two waves per SIMD without the compiler
         // merging the sets (r05).
-        Ops o;
-        issue(o);
-        store_b(smem, o);
-        __syncthreads();
+        if constexpr (BREG) {
+            // step g: B(g + 1) loads go out first (the split's in-order waits on A(g) leave them in
+            // flight), then A(g + 1); the MFMAs use B(g) held since the previous step
+            Ops o;
+            u32x4 bh[TN16], bl[TN16];
+            issue_b(o);
+            issue(o);
+#pragma unroll
+            for (int j = 0; j < TN16; ++j) {
+                bh[j] = o.bh[j];
+                bl[j] = o.bl[j];
+            }
 #pragma unroll 1
-        for (int g = 0; g < n; ++g) {
-            u32x4 ah[TM16], al[TM16];
-            split_a(o, ah, al);
-            __builtin_amdgcn_sched_barrier(0);
-            issue(o);                                          // past the last slice: re-loads it, unused
-            __builtin_amdgcn_sched_barrier(0);
-            mma(smem + (g & 1) * BSUB, ah, al);
-            store_b(smem + ((g + 1) & 1) * BSUB, o);
+            for (int g = 0; g < n; ++g) {
+                issue_b(o);                                    // slice g + 1 (past the end: re-load, unused)
+                u32x4 ah[TM16], al[TM16];
+                split_a(o, ah, al);
+                __builtin_amdgcn_sched_barrier(0);
+                issue(o);
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+                for (int j = 0; j < TN16; ++j)
+#pragma unroll
+                    for (int i = 0; i < TM16; ++i) {
+                        acc[i][j] = mfma16x16<ELT>(al[i], bh[j], acc[i][j]);
+                        acc[i][j] = mfma16x16<ELT>(ah[i], bl[j], acc[i][j]);
+                        acc[i][j] = mfma16x16<ELT>(ah[i], bh[j], acc[i][j]);
+                    }
+                __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+                for (int j = 0; j < TN16; ++j) {
+                    bh[j] = o.bh[j];
+                    bl[j] = o.bl[j];
+                }
+            }
+        } else {
+            Ops o;
+            issue(o);
+            store_b(smem, o);
             __syncthreads();
+#pragma unroll 1
+            for (int g = 0; g < n; ++g) {
+                u32x4 ah[TM16], al[TM16];
+                split_a(o, ah, al);
+                __builtin_amdgcn_sched_barrier(0);
+                issue(o);                                      // past the last slice: re-loads it, unused
+                __builtin_amdgcn_sched_barrier(0);
+                mma(smem + (g & 1) * BSUB, ah, al);
+                store_b(smem + ((g + 1) & 1) * BSUB, o);
+                __syncthreads();
+            }
         }
     }
     if (a.nonfinite) {                         // range guard: any non-finite accumulator flags the launch
@@ -246,12 +301,13 @@ __global__ __launch_bounds__(256, 2) void conv_x3_nar(ConvArgs a) {
 }
 
 template <int ELT>
-int launch_conv_x3_nar(const ConvArgs &a, dim3 grid, hipStream_t s) {
-    conv_x3_nar<ELT><<<grid, 256, 0, s>>>(a);
+int launch_conv_x3_nar(const ConvArgs &a, bool breg, dim3 grid, hipStream_t s) {
+    if (breg) conv_x3_nar<ELT, 1><<<grid, 256, 0, s>>>(a);
+    else conv_x3_nar<ELT, 0><<<grid, 256, 0, s>>>(a);
     return 0;
 }
 
-template int launch_conv_x3_nar<0>(const ConvArgs &, dim3, hipStream_t);
-template int launch_conv_x3_nar<1>(const ConvArgs &, dim3, hipStream_t);
+template int launch_conv_x3_nar<0>(const ConvArgs &, bool, dim3, hipStream_t);
+template int launch_conv_x3_nar<1>(const ConvArgs &, bool, dim3, hipStream_t);
 
 }  // namespace s2v

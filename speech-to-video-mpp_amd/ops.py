@@ -875,8 +875,10 @@ def plan_symbol(plan) -> str:
     persist = plan[10] if len(plan) > 10 else 0
     if avec == 5:
         return f"void s2v::conv_glds_x3<{bm}, {bn}, {wm}, {ks}, {x3 - 1}>(s2v::ConvArgs)"
-    if avec == 6:
-        return f"void s2v::conv_x3_nar<{x3 - 1}>(s2v::ConvArgs)"
+    if avec in (6, 7):
+        return f"void s2v::conv_x3_nar<{x3 - 1}, {avec - 6}>(s2v::ConvArgs)"
+    if avec == 8:
+        return f"void s2v::conv_x3_halo<{x3 - 1}>(s2v::ConvArgs)"
     if bm == 0:
         if wm < 0:
             if bkn >= 2000:

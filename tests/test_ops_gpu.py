@@ -133,9 +133,11 @@ CONV_CASES = [
     (2, 32, 9, 10, 48, 3, 1, 1, 1, "up2", "zero", 11, 0),
     (2, 64, 20, 18, 32, 3, 1, 1, 1, "direct", "zero", 12, 0),
     (1, 128, 13, 17, 24, 3, 2, 1, 1, "direct", "zero", 12, 4),
-    # conv_x3_nar (force_tile 16: register-direct A fragments, 256x64): ragged M, N < 64, several N
-    # tiles, stride 2, split-K, 1x1
+    # conv_x3_nar (force_tile 16: register-direct A fragments, 256x64; 17: B fragments too): ragged M,
+    # N < 64, several N tiles, stride 2, split-K, 1x1
     (2, 64, 23, 29, 64, 3, 1, 1, 1, "direct", "zero", 16, 0),
+    (2, 64, 23, 29, 64, 3, 1, 1, 1, "direct", "zero", 17, 2),
+    (2, 32, 17, 15, 130, 3, 2, 1, 1, "direct", "zero", 17, 0),
     (1, 96, 19, 21, 40, 3, 1, 1, 1, "direct", "zero", 16, 3),
     (2, 32, 17, 15, 130, 3, 2, 1, 1, "direct", "zero", 16, 0),
     (2, 64, 11, 13, 96, 1, 1, 0, 1, "direct", "zero", 16, 2),
@@ -145,8 +147,8 @@ CONV_CASES = [
 @pytest.mark.parametrize("shape", [(4, 64, 32, 48, 64, 3, 1), (2, 128, 32, 40, 48, 3, 1), (2, 64, 64, 64, 64, 3, 2),
                                    (3, 32, 16, 96, 64, 1, 1)])
 def test_conv_nar_bit_identical_to_lds_tile(ctx, prec, shape):
-    """conv_x3_nar (A fragments straight to registers) against the LDS-staged 256x64 4-wave tile
-    (force_tile 11): same K order, same split, same MFMA order per slice -> bit-identical outputs, with
+    """conv_x3_nar (A fragments straight to registers; force_tile 17: B too) against the LDS-staged
+    256x64 4-wave tile (force_tile 11): same K order, same split, same MFMA order per slice -> bit-identical outputs, with
     the StyleGAN2 input modulation (in_scale, per image: tiles inside one image and tiles straddling two),
     a pre-activation, the demodulation / noise / residual epilogue."""
     if prec == "f32":
@@ -163,16 +165,53 @@ def test_conv_nar_bit_identical_to_lds_tile(ctx, prec, shape):
     for kw in (dict(), dict(in_scale=s, nc_scale=d, pix_add=noise, pix_w=0.3, act=ops.ACT_LRELU, alpha=0.2),
                dict(pre_act=ops.ACT_LRELU, pre_alpha=0.2, res=res, act=ops.ACT_TANH), dict(force_splits=2)):
         outs = []
-        for tile in (11, 16):
+        for tile in (11, 16, 17):
             y = NHWC.empty(n, oh, ow, cout, DEV)
             ops.conv2d(ctx, x, cw, y, force_tile=tile, **kw)
             outs.append(y.t.clone())
         torch.cuda.synchronize()
-        assert torch.equal(outs[0], outs[1]), f"{kw.keys()}: max diff {(outs[0] - outs[1]).abs().max():.3e}"
+        for o in outs[1:]:
+            assert torch.equal(outs[0], o), f"{kw.keys()}: max diff {(outs[0] - o).abs().max():.3e}"
     xs = nhwc(rnd(n, cin, 10, 10, seed=48).float())
     with pytest.raises(Exception, match="conv_x3_nar"):
         ops.conv2d(ctx, xs, cw, NHWC.empty(n, (10 + 2 * (k // 2) - k) // st + 1, (10 + 2 * (k // 2) - k) // st + 1,
                                            cout, DEV), force_tile=16, in_scale=s)
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 8, 128, 64), (1, 96, 4, 64, 40), (2, 32, 12, 64, 130), (4, 128, 16, 64, 64)])
+def test_conv_halo_bit_identical_to_lds_tile(ctx, prec, shape):
+    """conv_x3_halo (force_tile 18: 4 x 64 output patches, the input halo split once per channel slice)
+    against the LDS-staged 256x64 tile (force_tile 11): same K order (taps fastest within a channel
+    slice), same MFMA order -> bit-identical, with modulation, pre-activation, demod / noise / residual
+    epilogues; halo split-K (whole channel slices) against the unsplit launch at the split bound; a
+    shape the kernel cannot take is refused when forced."""
+    if prec == "f32":
+        pytest.skip("split precisions only")
+    n, cin, h, w, cout = shape
+    wt = rnd(cout, cin, 3, 3, seed=51) / math.sqrt(cin * 9)
+    cw = ConvW(wt.float(), rnd(cout, seed=52).float(), DEV, padding=1)
+    x = nhwc(rnd(n, cin, h, w, seed=53).float())
+    s = rnd(n, cin, seed=54, lo=0.5, hi=1.5).float().to(DEV)
+    d = rnd(n, cout, seed=55, lo=0.5, hi=1.5).float().to(DEV)
+    noise = rnd(n, h * w, seed=56).float().to(DEV)
+    res = nhwc(rnd(n, cout, h, w, seed=57).float())
+    for kw in (dict(), dict(in_scale=s, nc_scale=d, pix_add=noise, pix_w=0.3, act=ops.ACT_LRELU, alpha=0.2),
+               dict(pre_act=ops.ACT_LRELU, pre_alpha=0.2, res=res, act=ops.ACT_TANH)):
+        outs = []
+        for tile in (11, 18):
+            y = NHWC.empty(n, h, w, cout, DEV)
+            ops.conv2d(ctx, x, cw, y, force_tile=tile, **kw)
+            outs.append(y.t.clone())
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0], outs[1]), f"{kw.keys()}: max diff {(outs[0] - outs[1]).abs().max():.3e}"
+    if cin >= 64:
+        ysp = NHWC.empty(n, h, w, cout, DEV)
+        ops.conv2d(ctx, x, cw, ysp, force_tile=18, force_splits=2)
+        y1 = NHWC.empty(n, h, w, cout, DEV)
+        ops.conv2d(ctx, x, cw, y1, force_tile=18)
+        assert (ysp.t - y1.t).abs().max() <= 1e-5 * (y1.t.abs().max() + 1)
+    with pytest.raises(Exception, match="conv_x3_halo"):
+        ops.conv2d(ctx, nhwc(rnd(n, cin, 6, 64, seed=58).float()), cw, NHWC.empty(n, 6, 64, cout, DEV), force_tile=18)
 
 
 @pytest.fixture
