@@ -30,7 +30,7 @@ int launch_conv_x3_group(int cfg, const ConvGroup &g, dim3 grid, hipStream_t s);
 template <int ELT>   // narrow-N register-direct-A kernel (conv_x3_nar.hip); breg: B fragments direct too
 int launch_conv_x3_nar(const ConvArgs &a, bool breg, dim3 grid, hipStream_t s);
 template <int ELT>   // 3x3 spatial-patch kernel with the input halo staged once per channel slice (conv_x3_halo.hip)
-int launch_conv_x3_halo(const ConvArgs &a, dim3 grid, hipStream_t s);
+int launch_conv_x3_halo(const ConvArgs &a, int th, dim3 grid, hipStream_t s);
 
 template <int BM, int BN, int AR, int BR, int BKN>
 __device__ __forceinline__ void store_ab(float *As, float *Bs, int tid, const f4 (&ra)[AR],
@@ -878,7 +878,7 @@ struct X3Cfg {
     TileCfg t;
     float tflops;
     int bpc;
-    int kind = 0;    // 1 / 2: conv_x3_nar (register-direct A / A and B fragments), 3: conv_x3_halo
+    int kind = 0;    // 1 / 2: conv_x3_nar (register-direct A / A and B fragments), 3 / 4: conv_x3_halo (4 / 8 rows)
 };
 static const X3Cfg kX3Tiles[] = {
     {{256, 256, 2, 8, 1, 1}, 400.f, 1}, {{128, 128, 2, 8, 1, 1}, 330.f, 2}, {{64, 128, 2, 8, 1, 1}, 260.f, 3},
@@ -900,7 +900,9 @@ static const X3Cfg kX3Tiles[] = {
     {{256, 64, 4, 4, 1, 1}, 0.f, 2, 2},
     // 4 x 64 output patches, 64 channels, the 6 x 66 input halo per channel slice staged once
     // (conv_x3_halo.hip): 3x3 stride-1 zero-padded convs with oh % 4 == 0, ow % 64 == 0
-    {{256, 64, 4, 4, 1, 1}, 0.f, 2, 3}};
+    {{256, 64, 4, 4, 1, 1}, 0.f, 2, 3},
+    // ... 8 x 64 patches, one 512-thread block per CU (oh % 8 == 0)
+    {{512, 64, 8, 8, 1, 1}, 0.f, 1, 4}};
 constexpr int kNumX3 = sizeof(kX3Tiles) / sizeof(kX3Tiles[0]);
 
 static const TileCfg &tile_cfg(const s2v_conv_params *p, int tile);
@@ -1008,7 +1010,7 @@ static Plan make_plan_x3(const s2v_conv_params *p, int M, Plan pl) {
     const int cus = plan_cus();
     if (p->force_tile > 0) {
         pl.tile = p->force_tile - 1;
-        if (kX3Tiles[pl.tile].kind == 3) pl.kslab = 9;
+        if (kX3Tiles[pl.tile].kind >= 3) pl.kslab = 9;
         const TileCfg &t = kX3Tiles[pl.tile].t;
         const long long blocks = (long long)cdiv(M, t.bm) * cdiv(p->cout, t.bn) * batch;
         int splits = p->force_splits;
@@ -1083,7 +1085,7 @@ static Plan make_plan_x3(const s2v_conv_params *p, int M, Plan pl) {
         }
     }
     pl.tile = bt;
-    if (kX3Tiles[bt].kind == 3) pl.kslab = 9;
+    if (kX3Tiles[bt].kind >= 3) pl.kslab = 9;
     finish_plan(pl, bs);
     return pl;
 }
@@ -1378,6 +1380,7 @@ static bool halo_ok(const s2v_conv_params *p) {
 }
 
 static bool x3_kind_ok(const s2v_conv_params *p, int kind) {
+    if (kind == 4) return halo_ok(p) && p->oh % 8 == 0;
     return kind == 0 || (kind == 3 ? halo_ok(p) : nar_ok(p));
 }
 
@@ -1621,6 +1624,7 @@ extern "C" int s2v_conv2d_plan(const s2v_conv_params *p, int *out6) {
     const TileCfg &t = tile_cfg(p, pl.tile);
     out6[0] = t.bm; out6[1] = t.bn; out6[2] = t.wm;
     out6[3] = tiled_x3(p) ? (kX3Tiles[pl.tile].kind >= 1 ? 5 + kX3Tiles[pl.tile].kind : x3_amode(p, t)) : a_mode(p);
+    if (tiled_x3(p) && kX3Tiles[pl.tile].kind == 4) out6[3] = 8;   // conv_x3_halo<ELT, 8>: bm 512 tells it apart
     out6[4] = p->b_kn != 0;
     out6[5] = pl.splits;
     out6[6] = tiled_x3(p) ? p->prec : 0;
@@ -1712,9 +1716,9 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
             a.x_bytes = (unsigned)x_extent_bytes(p);
             a.w_bytes = (unsigned)((long long)p->npad * p->kpad * 4);
             const int kind = kX3Tiles[pl.tile].kind;
-            if (kind == 3)
-                rc = p->prec == S2V_PREC_BF16X3 ? launch_conv_x3_halo<0>(a, grid, s)
-                                                : launch_conv_x3_halo<1>(a, grid, s);
+            if (kind >= 3)
+                rc = p->prec == S2V_PREC_BF16X3 ? launch_conv_x3_halo<0>(a, kind == 4 ? 8 : 4, grid, s)
+                                                : launch_conv_x3_halo<1>(a, kind == 4 ? 8 : 4, grid, s);
             else
                 rc = p->prec == S2V_PREC_BF16X3 ? launch_conv_x3_nar<0>(a, kind == 2, grid, s)
                                                 : launch_conv_x3_nar<1>(a, kind == 2, grid, s);

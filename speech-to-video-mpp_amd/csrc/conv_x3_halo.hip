@@ -22,13 +22,16 @@
 
 namespace s2v {
 
-template <int ELT>
-__global__ __launch_bounds__(256, 2) void conv_x3_halo(ConvArgs a) {
+// TH output rows per patch, one wave each (4: 256 threads, two blocks per CU; 8: 512 threads, one block
+// per CU with the B slices and the halo's edge rows amortised over twice the outputs)
+template <int ELT, int TH>
+__global__ __launch_bounds__(64 * TH, TH == 4 ? 2 : 1) void conv_x3_halo(ConvArgs a) {
     launch_stamp(a, false);
-    constexpr int TH = 4, TW = 64, BN = 64, TM16 = TW / 16, TN16 = BN / 16, RS = 32, BR = 2;
+    constexpr int NT = 64 * TH;
+    constexpr int TW = 64, BN = 64, TM16 = TW / 16, TN16 = BN / 16, RS = NT / 8, BR = BN / RS;
     constexpr int HW_ = TW + 2, HPX = (TH + 2) * HW_;   // halo row width, pixels
     constexpr int ITEMS = HPX * 4;                      // (pixel, 8-channel group) items per slice
-    constexpr int NIT = (ITEMS + 255) / 256;
+    constexpr int NIT = (ITEMS + NT - 1) / NT;
     constexpr int HALO = HPX * 128;                     // split hi | lo halo of one 32-channel slice
     constexpr int BSUB = BN * 128;
     constexpr int CH = 64;
@@ -70,12 +73,12 @@ __global__ __launch_bounds__(256, 2) void conv_x3_halo(ConvArgs a) {
     const __amdgpu_buffer_rsrc_t srs =
         __builtin_amdgcn_make_buffer_rsrc((void *)sc_base, 0, a.in_scale ? a.cin * 4 : 0, 0x00020000);
 
-    // halo items of this thread: item q = tid + 256 j -> pixel q >> 2, channel group q & 3 (= tid & 3)
+    // halo items of this thread: item q = tid + NT j -> pixel q >> 2, channel group q & 3 (= tid & 3)
     int hoff[NIT];        // byte offset of the item's 8 channels at channel slice 0, or -1 (zeros)
     int hlds[NIT];        // LDS byte offset of its hi slot, or -1 (no item)
 #pragma unroll
     for (int j = 0; j < NIT; ++j) {
-        const int q = tid + 256 * j;
+        const int q = tid + NT * j;
         hoff[j] = -1;
         hlds[j] = -1;
         if (q < ITEMS) {
@@ -219,7 +222,7 @@ __global__ __launch_bounds__(256, 2) void conv_x3_halo(ConvArgs a) {
     }
     // chunk c0 = wave row c0 / 64 of the patch: 64 consecutive output pixels
     const long long mrow0 = ((long long)img * a.oh + y0) * a.ow + x0;
-    epilogue_tile_map<TH * TW, BN, 4, CH>(
+    epilogue_tile_map<TH * TW, BN, TH, CH>(
         a, (float *)smem, tid, n0, bz, bidx,
         [&](float *Cs, int c0) {
             constexpr int LDC = BN + 4;
@@ -237,12 +240,13 @@ __global__ __launch_bounds__(256, 2) void conv_x3_halo(ConvArgs a) {
 }
 
 template <int ELT>
-int launch_conv_x3_halo(const ConvArgs &a, dim3 grid, hipStream_t s) {
-    conv_x3_halo<ELT><<<grid, 256, 0, s>>>(a);
+int launch_conv_x3_halo(const ConvArgs &a, int th, dim3 grid, hipStream_t s) {
+    if (th == 8) conv_x3_halo<ELT, 8><<<grid, 512, 0, s>>>(a);
+    else conv_x3_halo<ELT, 4><<<grid, 256, 0, s>>>(a);
     return 0;
 }
 
-template int launch_conv_x3_halo<0>(const ConvArgs &, dim3, hipStream_t);
-template int launch_conv_x3_halo<1>(const ConvArgs &, dim3, hipStream_t);
+template int launch_conv_x3_halo<0>(const ConvArgs &, int, dim3, hipStream_t);
+template int launch_conv_x3_halo<1>(const ConvArgs &, int, dim3, hipStream_t);
 
 }  // namespace s2v

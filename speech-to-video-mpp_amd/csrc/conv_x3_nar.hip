@@ -18,13 +18,12 @@
 // modulation s[n, c] of its channels) are in flight while the current one is multiplied.  Epilogue: conv_impl.hpp epilogue_tile_fn (every fused
 // epilogue, split-K partials, the range guard's non-finite flag).
 //
-// Measured on MI355X (r05, tools/gpu_s24.sh / s26 / s27, graph-timed, f16x3): parity bit-identical to
+// Measured on MI355X (r05, profiles/r05_nar_sweep.txt, graph-timed, f16x3): parity bit-identical to
 // the LDS tile; speed within +-5 % of the best LDS tile (4x512^2 64 -> 64: 441 vs 433 us for 128x64,
-// 128 -> 64: 712 vs 672 us; 4x256^2 256 -> 64: 347 vs 360 us).  So the LDS round trip is not what holds
-// these layers at 0.2 of the x3 peak: three waves per SIMD (168 VGPRs, spills) were slower, and with the
-// A loads made L1-resident (NAR_ABL=1) the launch was only 3 % faster — not operand traffic or load
-// latency either.  PMC (tools/gpu_s25.sh): 48 % of wave cycles waiting, ~4 non-MFMA VALU and ~2 SALU
-// per MFMA.  Kept forced-only (force_tile 16) as the measured alternative.
+// 128 -> 64: 712 vs 672 us; 4x256^2 256 -> 64: 347 vs 360 us): the LDS round trip is not what holds these
+// layers at 0.2 of the x3 peak.  With BREG = 1 (six more wave-loads per K-slice, no LDS, no barrier) the
+// launches are 1.4-1.5x slower: the bound is the L2 -> CU operand stream, which conv_x3_halo.hip cuts
+// (the input loaded once per channel slice instead of once per tap).  Kept forced-only (force_tile 16 / 17).
 #include "conv_x3_impl.hpp"
 
 namespace s2v {
