@@ -202,7 +202,7 @@ def live_roofline(forward, workload="lipsync"):
     if rep["n"] == d["launches"] and rep["ms"] > 0:
         d = dict(d, ms=rep["ms"])
     achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12
-    peak = X3_PEAK_TFLOPS if "conv_igemm_x3" in dom else FP32_MFMA_PEAK_TFLOPS
+    peak = _peak(dom)
     total_ms = sum(v["ms"] for v in per.values())
     total_flops = sum(v["flops"] for v in per.values())
     # HBM bytes per launch of the same symbol from the PMC passes of this workload (tools/gpu_profile.sh:
@@ -303,9 +303,11 @@ class Stamper:
         return out
 
 
+X3_KERNELS = ("conv_igemm_x3", "conv_glds_x3", "conv_x3_nar", "conv_x3_halo")   # split-precision families
+
+
 def _peak(sym):
-    return X3_PEAK_TFLOPS if ("conv_igemm_x3" in sym or "conv_glds_x3" in sym) \
-        else FP32_MFMA_PEAK_TFLOPS
+    return X3_PEAK_TFLOPS if any(k in sym for k in X3_KERNELS) else FP32_MFMA_PEAK_TFLOPS
 
 
 PMC_ROUND = "r05"     # only this round's PMC passes describe the current build

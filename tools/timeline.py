@@ -62,10 +62,11 @@ def main():
                 # the two branches' ends: LNet's last FourierUnit transform, the style encoder's last
                 # 256x256-tile conv (LNet has none)
                 fft = [b for n, a, b in step if "fft2" in n and a < hi]
-                big = [b for n, a, b in step if n.startswith("void s2v::conv_igemm_x3<256, 256") and a < hi]
+                big = [b for n, a, b in step if (n.startswith("void s2v::conv_igemm_x3<256, 256") or
+                                                  n.startswith("void s2v::conv_igemm_x3_persist<")) and a < hi]
                 if fft and big:
                     print(f"    LNet last FFT ends {(max(fft) - lo) / 1e3:8.1f} us, style encoder's last 256x256 conv "
-                          f"ends {(max(big) - lo) / 1e3:8.1f} us")
+                          f"(persistent or full-grid) ends {(max(big) - lo) / 1e3:8.1f} us")
 
 
 if __name__ == "__main__" and not {"--lnet", "--ffc", "--seq"} & set(sys.argv):
@@ -73,19 +74,27 @@ if __name__ == "__main__" and not {"--lnet", "--ffc", "--seq"} & set(sys.argv):
 
 
 def lnet_levels(path):
-    """LNet forward: wall time per decoder level (first rfft2 .. last irfft2 of that size) of the last
-    forward in the trace, with busy time and kernel count, and the encoder part before the decoder."""
+    """LNet forward: wall time per decoder level (first .. last FourierUnit transform of that size: the
+    separate rfft2 / irfft2 kernels, or the fused ffc_spec_fwd / ffc_spec_inv at a fused level) of the
+    last forward in the trace, with busy time and kernel count."""
     ks = load(path)
     hs = (12, 24, 48)
-    last = {h: max(i for i, (n, a, b) in enumerate(ks) if n.startswith(f"void s2v::irfft2_mf<{h},")) for h in hs}
-    first = {}
+
+    def fwd(n, h):
+        return n.startswith(f"void s2v::rfft2_mf<{h},") or n.startswith(f"void s2v::ffc_spec_fwd<{h},")
+
+    def inv(n, h):
+        return n.startswith(f"void s2v::irfft2_mf<{h},") or n.startswith(f"void s2v::ffc_spec_inv<{h},")
     for h in hs:
-        # the last forward's first rfft of this size: walk back 18 rffts from the end
-        idx = [i for i, (n, a, b) in enumerate(ks) if n.startswith(f"void s2v::rfft2_mf<{h},") and i <= last[h]]
-        first[h] = idx[-18]
-    for h in hs:
-        seg = [(a, b) for n, a, b in ks[first[h]: last[h] + 1]]
-        lo, hi = ks[first[h]][1], max(b for a, b in seg)
+        inv_i = [i for i, (n, a, b) in enumerate(ks) if inv(n, h)]
+        fwd_i = [i for i, (n, a, b) in enumerate(ks) if fwd(n, h)]
+        if not inv_i or len(fwd_i) < 18:
+            print(f"level {h}: {len(fwd_i)} forward transforms in the trace")
+            continue
+        last = inv_i[-1]
+        first = [i for i in fwd_i if i <= last][-18]       # the last forward's 18 FFCs of this size
+        seg = [(a, b) for n, a, b in ks[first: last + 1]]
+        lo, hi = ks[first][1], max(b for a, b in seg)
         print(f"level {h:2d}x{h:<2d}: wall {(hi - lo) / 1e3:8.1f} us  busy {busy(seg) / 1e3:8.1f}  "
               f"kernels {len(seg)}  per FFC {(hi - lo) / 18e3:6.1f} us")
 
