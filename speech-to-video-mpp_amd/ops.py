@@ -118,8 +118,9 @@ def _grouping() -> bool:
 # tools/tune_perfdb.py (every conv launch of the LNet / ENet / DNet forwards, each candidate tile and
 # split factor graph-timed against the planner's own choice), keyed by conv_key().  Only entries that
 # beat the planner by more than 3 % are kept; every other launch stays with the planner.
-# S2V_PERFDB=0 ignores the table.
-PERFDB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "perfdb_mi355x.json")
+# S2V_PERFDB=0 ignores the table; S2V_PERFDB_PATH reads another one (A/B of tuned tables).
+PERFDB_PATH = os.environ.get("S2V_PERFDB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                                "perfdb_mi355x.json")
 PERFDB = {}
 PERFDB_DEVICE = None    # (arch, CU count) the table was measured on: applied only on a matching device
 if os.environ.get("S2V_PERFDB", "1") != "0" and os.path.exists(PERFDB_PATH):

@@ -4,7 +4,7 @@
 Runs one eager forward of each bench.py workload named on the command line with ops.TUNE set: every
 conv launch ops.conv_key() covers (split precision, no forced configuration, no conv group, no grid
 cap) whose planner choice is a one-block-per-tile ``conv_igemm_x3`` tile is timed against every other
-tile (force_tile 1..11) and split-K factor, each candidate as a HIP graph of REPS back-to-back launches
+tile (force_tile 1..11, or --tiles) and split-K factor, each candidate as a HIP graph of REPS back-to-back launches
 (its splitk_reduce launch included), best of ROUNDS replays.  Keys seen before are not re-measured.
 The output is restored after the candidates ran (in-place residuals), so the forward continues on the
 planner's result.  A key is written to the table only when its best candidate beats the planner's
@@ -105,7 +105,12 @@ def main():
     ap.add_argument("--out", default=ops.PERFDB_PATH)
     ap.add_argument("--raw", default="", help="also write every measured key (planner, best) here")
     ap.add_argument("--merge", action="store_true", help="keep the entries of --out for keys not measured here")
+    ap.add_argument("--tiles", default="", help="comma list of force_tile values (default 1..11); r05: 1..15 adds "
+                    "the deep-stage 4-wave tiles")
     a = ap.parse_args()
+    global TILES
+    if a.tiles:
+        TILES = [int(t) for t in a.tiles.split(",")]
     sys.argv = [sys.argv[0]]
     bargs = bench.parse()
     dev = torch.device("cuda", 0)
