@@ -30,7 +30,7 @@ int launch_conv_x3_group(int cfg, const ConvGroup &g, dim3 grid, hipStream_t s);
 template <int ELT>   // narrow-N register-direct-A kernel (conv_x3_nar.hip); breg: B fragments direct too
 int launch_conv_x3_nar(const ConvArgs &a, bool breg, dim3 grid, hipStream_t s);
 template <int ELT>   // 3x3 spatial-patch kernel with the input halo staged once per channel slice (conv_x3_halo.hip)
-int launch_conv_x3_halo(const ConvArgs &a, int th, dim3 grid, hipStream_t s);
+int launch_conv_x3_halo(const ConvArgs &a, int th, int wn, dim3 grid, hipStream_t s);
 
 template <int BM, int BN, int AR, int BR, int BKN>
 __device__ __forceinline__ void store_ab(float *As, float *Bs, int tid, const f4 (&ra)[AR],
@@ -902,7 +902,9 @@ static const X3Cfg kX3Tiles[] = {
     // (conv_x3_halo.hip): 3x3 stride-1 zero-padded convs with oh % 4 == 0, ow % 64 == 0
     {{256, 64, 4, 4, 1, 1}, 0.f, 2, 3},
     // ... 8 x 64 patches, one 512-thread block per CU (oh % 8 == 0)
-    {{512, 64, 8, 8, 1, 1}, 0.f, 1, 4}};
+    {{512, 64, 8, 8, 1, 1}, 0.f, 1, 4},
+    // ... 4 x 64 patches x 128 output channels (two 64-channel wave columns), one 512-thread block per CU
+    {{256, 128, 4, 8, 1, 1}, 0.f, 1, 5}};
 constexpr int kNumX3 = sizeof(kX3Tiles) / sizeof(kX3Tiles[0]);
 
 static const TileCfg &tile_cfg(const s2v_conv_params *p, int tile);
@@ -1029,9 +1031,12 @@ static Plan make_plan_x3(const s2v_conv_params *p, int M, Plan pl) {
     if (halo_ok(p) && p->cout <= 128) {
         const int batch = p->batch > 0 ? p->batch : 1;
         const long long blocks = (long long)(M / 256) * cdiv(p->cout, 64) * batch;
+        // 65..128 output channels: one block per 128 columns (two 64-channel wave columns share the halo):
+        // 4x256^2 128 -> 128 279 vs 291 us (profiles/r05_halo_sweep.txt); <= 64: the 4-wave 64-column block
+        const int kind = p->cout > 64 && x3_kind_ok(p, 5) ? 5 : 3;
         if (blocks >= 2LL * plan_cus()) {
             for (int i = 0; i < kNumX3; ++i)
-                if (kX3Tiles[i].kind == 3) {
+                if (kX3Tiles[i].kind == kind) {
                     pl.tile = i;
                     pl.kslab = 9;
                     finish_plan(pl, 1);
@@ -1381,6 +1386,7 @@ static bool halo_ok(const s2v_conv_params *p) {
 
 static bool x3_kind_ok(const s2v_conv_params *p, int kind) {
     if (kind == 4) return halo_ok(p) && p->oh % 8 == 0;
+    if (kind == 5) return halo_ok(p) && (long long)cdiv(p->cout, 128) * 128 <= p->npad;
     return kind == 0 || (kind == 3 ? halo_ok(p) : nar_ok(p));
 }
 
@@ -1624,7 +1630,7 @@ extern "C" int s2v_conv2d_plan(const s2v_conv_params *p, int *out6) {
     const TileCfg &t = tile_cfg(p, pl.tile);
     out6[0] = t.bm; out6[1] = t.bn; out6[2] = t.wm;
     out6[3] = tiled_x3(p) ? (kX3Tiles[pl.tile].kind >= 1 ? 5 + kX3Tiles[pl.tile].kind : x3_amode(p, t)) : a_mode(p);
-    if (tiled_x3(p) && kX3Tiles[pl.tile].kind == 4) out6[3] = 8;   // conv_x3_halo<ELT, 8>: bm 512 tells it apart
+    if (tiled_x3(p) && kX3Tiles[pl.tile].kind >= 4) out6[3] = 8;   // conv_x3_halo<ELT, TH, WN>: bm / bn tell them apart
     out6[4] = p->b_kn != 0;
     out6[5] = pl.splits;
     out6[6] = tiled_x3(p) ? p->prec : 0;
@@ -1717,8 +1723,9 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
             a.w_bytes = (unsigned)((long long)p->npad * p->kpad * 4);
             const int kind = kX3Tiles[pl.tile].kind;
             if (kind >= 3)
-                rc = p->prec == S2V_PREC_BF16X3 ? launch_conv_x3_halo<0>(a, kind == 4 ? 8 : 4, grid, s)
-                                                : launch_conv_x3_halo<1>(a, kind == 4 ? 8 : 4, grid, s);
+                rc = p->prec == S2V_PREC_BF16X3
+                         ? launch_conv_x3_halo<0>(a, kind == 4 ? 8 : 4, kind == 5 ? 2 : 1, grid, s)
+                         : launch_conv_x3_halo<1>(a, kind == 4 ? 8 : 4, kind == 5 ? 2 : 1, grid, s);
             else
                 rc = p->prec == S2V_PREC_BF16X3 ? launch_conv_x3_nar<0>(a, kind == 2, grid, s)
                                                 : launch_conv_x3_nar<1>(a, kind == 2, grid, s);

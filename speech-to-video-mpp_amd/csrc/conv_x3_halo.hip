@@ -22,13 +22,14 @@
 
 namespace s2v {
 
-// TH output rows per patch, one wave each (4: 256 threads, two blocks per CU; 8: 512 threads, one block
-// per CU with the B slices and the halo's edge rows amortised over twice the outputs)
-template <int ELT, int TH>
-__global__ __launch_bounds__(64 * TH, TH == 4 ? 2 : 1) void conv_x3_halo(ConvArgs a) {
+// TH output rows per patch, WN waves per row each owning 64 of the BN = 64 WN output channels
+// (TH 4 / WN 1: 256 threads, two blocks per CU; TH 8 / WN 1 and TH 4 / WN 2: 512 threads, one block per
+// CU, the halo's edge rows resp. the halo itself amortised over twice the outputs)
+template <int ELT, int TH, int WN>
+__global__ __launch_bounds__(64 * TH * WN, TH * WN == 4 ? 2 : 1) void conv_x3_halo(ConvArgs a) {
     launch_stamp(a, false);
-    constexpr int NT = 64 * TH;
-    constexpr int TW = 64, BN = 64, TM16 = TW / 16, TN16 = BN / 16, RS = NT / 8, BR = BN / RS;
+    constexpr int NT = 64 * TH * WN;
+    constexpr int TW = 64, BN = 64 * WN, TM16 = TW / 16, TN16 = 4, RS = NT / 8, BR = BN / RS;
     constexpr int HW_ = TW + 2, HPX = (TH + 2) * HW_;   // halo row width, pixels
     constexpr int ITEMS = HPX * 4;                      // (pixel, 8-channel group) items per slice
     constexpr int NIT = (ITEMS + NT - 1) / NT;
@@ -43,6 +44,7 @@ __global__ __launch_bounds__(64 * TH, TH == 4 ? 2 : 1) void conv_x3_halo(ConvArg
     char *bst = smem + HALO;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave / WN, wc = wave - wr * WN;          // patch row, 64-channel column group
     const int l16 = lane & 15, kg = lane >> 4;
     const int total = gridDim.x * gridDim.y * gridDim.z;
     const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
@@ -157,12 +159,12 @@ __global__ __launch_bounds__(64 * TH, TH == 4 ? 2 : 1) void conv_x3_halo(ConvArg
         u32x4 bh[TN16], bl[TN16];
 #pragma unroll
         for (int j = 0; j < TN16; ++j) {
-            const char *p = Bs + (j * 16 + l16) * 128;
+            const char *p = Bs + (wc * 64 + j * 16 + l16) * 128;
             const int hs = (kg ^ swz(l16)) << 4;
             bh[j] = *(const u32x4 *)(p + hs);
             bl[j] = *(const u32x4 *)(p + (hs ^ 64));
         }
-        const int pbase = (wave + ky) * HW_ + kx + l16;
+        const int pbase = (wr + ky) * HW_ + kx + l16;
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < TM16; ++i) {
@@ -222,31 +224,32 @@ __global__ __launch_bounds__(64 * TH, TH == 4 ? 2 : 1) void conv_x3_halo(ConvArg
     }
     // chunk c0 = wave row c0 / 64 of the patch: 64 consecutive output pixels
     const long long mrow0 = ((long long)img * a.oh + y0) * a.ow + x0;
-    epilogue_tile_map<TH * TW, BN, TH, CH>(
+    epilogue_tile_map<TH * TW, BN, TH * WN, CH>(
         a, (float *)smem, tid, n0, bz, bidx,
         [&](float *Cs, int c0) {
             constexpr int LDC = BN + 4;
-            if (wave * 64 != c0) return;
+            if (wr * 64 != c0) return;
 #pragma unroll
             for (int i = 0; i < TM16; ++i)
 #pragma unroll
                 for (int j = 0; j < TN16; ++j)
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
-                        Cs[(i * 16 + 4 * kg + r) * LDC + j * 16 + l16] = acc[i][j][r] * a.acc_scale;
+                        Cs[(i * 16 + 4 * kg + r) * LDC + wc * 64 + j * 16 + l16] = acc[i][j][r] * a.acc_scale;
         },
         [&](int c0) { return (int)(mrow0 + (long long)(c0 / 64) * a.ow); }, [&](int) { return CH; });
     launch_stamp(a, true);
 }
 
 template <int ELT>
-int launch_conv_x3_halo(const ConvArgs &a, int th, dim3 grid, hipStream_t s) {
-    if (th == 8) conv_x3_halo<ELT, 8><<<grid, 512, 0, s>>>(a);
-    else conv_x3_halo<ELT, 4><<<grid, 256, 0, s>>>(a);
+int launch_conv_x3_halo(const ConvArgs &a, int th, int wn, dim3 grid, hipStream_t s) {
+    if (wn == 2) conv_x3_halo<ELT, 4, 2><<<grid, 512, 0, s>>>(a);
+    else if (th == 8) conv_x3_halo<ELT, 8, 1><<<grid, 512, 0, s>>>(a);
+    else conv_x3_halo<ELT, 4, 1><<<grid, 256, 0, s>>>(a);
     return 0;
 }
 
-template int launch_conv_x3_halo<0>(const ConvArgs &, int, dim3, hipStream_t);
-template int launch_conv_x3_halo<1>(const ConvArgs &, int, dim3, hipStream_t);
+template int launch_conv_x3_halo<0>(const ConvArgs &, int, int, dim3, hipStream_t);
+template int launch_conv_x3_halo<1>(const ConvArgs &, int, int, dim3, hipStream_t);
 
 }  // namespace s2v

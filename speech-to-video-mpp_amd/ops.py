@@ -879,7 +879,7 @@ def plan_symbol(plan) -> str:
     if avec in (6, 7):
         return f"void s2v::conv_x3_nar<{x3 - 1}, {avec - 6}>(s2v::ConvArgs)"
     if avec == 8:
-        return f"void s2v::conv_x3_halo<{x3 - 1}, {bm // 64}>(s2v::ConvArgs)"
+        return f"void s2v::conv_x3_halo<{x3 - 1}, {bm // 64}, {bn // 64}>(s2v::ConvArgs)"
     if bm == 0:
         if wm < 0:
             if bkn >= 2000:

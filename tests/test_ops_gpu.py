@@ -180,8 +180,8 @@ def test_conv_nar_bit_identical_to_lds_tile(ctx, prec, shape):
 
 @pytest.mark.parametrize("shape", [(2, 64, 8, 128, 64), (1, 96, 4, 64, 40), (2, 32, 12, 64, 130), (4, 128, 16, 64, 64)])
 def test_conv_halo_bit_identical_to_lds_tile(ctx, prec, shape):
-    """conv_x3_halo (force_tile 18 / 19: 4 x 64 / 8 x 64 output patches, the input halo split once per
-    channel slice)
+    """conv_x3_halo (force_tile 18 / 19 / 20: 4 x 64 / 8 x 64 output patches, 20 with 128 output channels
+    per block; the input halo split once per channel slice)
     against the LDS-staged 256x64 tile (force_tile 11): same K order (taps fastest within a channel
     slice), same MFMA order -> bit-identical, with modulation, pre-activation, demod / noise / residual
     epilogues; halo split-K (whole channel slices) against the unsplit launch at the split bound; a
@@ -199,7 +199,7 @@ def test_conv_halo_bit_identical_to_lds_tile(ctx, prec, shape):
     for kw in (dict(), dict(in_scale=s, nc_scale=d, pix_add=noise, pix_w=0.3, act=ops.ACT_LRELU, alpha=0.2),
                dict(pre_act=ops.ACT_LRELU, pre_alpha=0.2, res=res, act=ops.ACT_TANH)):
         outs = []
-        for tile in (11, 18) + ((19,) if h % 8 == 0 else ()):
+        for tile in (11, 18, 20) + ((19,) if h % 8 == 0 else ()):
             y = NHWC.empty(n, h, w, cout, DEV)
             ops.conv2d(ctx, x, cw, y, force_tile=tile, **kw)
             outs.append(y.t.clone())
