@@ -289,3 +289,47 @@ def test_torch_custom_ops_registered_hip_only():
         torch_ops.fused.fused_bias_act(torch.zeros(2, 3), torch.zeros(3), torch.zeros(0), 3, 0, 0.2, 1.0)
     with pytest.raises(NotImplementedError):
         torch_ops.upfirdn2d(torch.zeros(1, 2, 4, 4), torch.ones(2, 2))
+
+
+def _plan(n, h, w, cin, cout, k=3, stride=1, pad=1, force_tile=0, in_scale=False):
+    """s2v_conv2d_plan of an f16x3 direct conv (host-only: fake aligned pointers, nothing launched)."""
+    lib = _lib.load()
+    p = _lib.ConvParams()
+    p.x, p.y, p.wt_x3, p.wt = 1 << 20, 2 << 20, 3 << 20, 4 << 20
+    p.n, p.h, p.w, p.cin, p.xcs = n, h, w, cin, cin
+    p.kh = p.kw = k
+    p.sh = p.sw = stride
+    p.ph = p.pw = pad
+    p.dh = p.dw = 1
+    p.oh, p.ow = (h + 2 * pad - k) // stride + 1, (w + 2 * pad - k) // stride + 1
+    p.cout, p.ycs = cout, cout
+    p.kpad = (k * k * cin + 31) // 32 * 32
+    p.npad = (cout + 127) // 128 * 128 if cout <= 128 else (cout + 255) // 256 * 256
+    p.prec = 2                                  # S2V_PREC_F16X3
+    p.force_tile = force_tile
+    if in_scale:
+        p.in_scale, p.in_scale_ns = 5 << 20, cin
+    out = (ctypes.c_int * 11)()
+    rc = lib.s2v_conv2d_plan(ctypes.byref(p), out)
+    return rc, list(out)
+
+
+def test_planner_gives_narrow_3x3_layers_to_the_halo_kernel():
+    """conv.hip make_plan_x3 (no GPU needed): 3x3 stride-1 layers of <= 64 / <= 128 output channels over
+    64-wide rows with a chip-filling grid take conv_x3_halo<ELT, 4, 1> / <ELT, 4, 2> (plan A mode 8);
+    ragged rows, wide layers, strided convs and small grids keep the implicit-GEMM tiles; forcing the
+    halo tile where it cannot run is an error."""
+    from s2v_amd import ops
+    rc, pl = _plan(4, 512, 512, 128, 64, in_scale=True)
+    assert rc == 0 and pl[3] == 8 and (pl[0], pl[1]) == (256, 64), pl
+    assert ops.plan_symbol(pl) == "void s2v::conv_x3_halo<1, 4, 1>(s2v::ConvArgs)"
+    rc, pl = _plan(4, 256, 256, 128, 128)
+    assert rc == 0 and pl[3] == 8 and (pl[0], pl[1]) == (256, 128), pl
+    assert ops.plan_symbol(pl) == "void s2v::conv_x3_halo<1, 4, 2>(s2v::ConvArgs)"
+    for args in ((4, 200, 200, 64, 64), (16, 256, 256, 256, 256), (1, 64, 64, 64, 64)):
+        rc, pl = _plan(*args)
+        assert rc == 0 and pl[3] != 8, (args, pl)
+    rc, pl = _plan(4, 256, 256, 64, 64, stride=2)
+    assert rc == 0 and pl[3] != 8
+    rc, _ = _plan(4, 200, 200, 64, 64, force_tile=18)
+    assert rc != 0 and b"conv_x3_halo" in _lib.load().s2v_last_error()
