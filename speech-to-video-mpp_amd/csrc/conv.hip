@@ -983,6 +983,7 @@ static int a_mode(const s2v_conv_params *p);
 static bool nar_ok(const s2v_conv_params *p);
 static bool x3_kind_ok(const s2v_conv_params *p, int kind);
 static bool halo_ok(const s2v_conv_params *p);
+static double halo_fill(const s2v_conv_params *p, int th);
 
 
 static const TileCfg &tile_cfg(const s2v_conv_params *p, int tile) {
@@ -1028,13 +1029,18 @@ static Plan make_plan_x3(const s2v_conv_params *p, int M, Plan pl) {
     // 512^2 layers): the halo-staged spatial patch kernel, measured 20-30 % faster than every implicit-GEMM
     // tile on them (4x512^2 64 -> 64: 356 vs 444 us, 128 -> 64: 547 vs 697, 4x256^2 128 -> 128: 292 vs 381,
     // profiles/r05_halo_sweep.txt), whenever the grid fills the chip without split-K
-    if (halo_ok(p) && p->cout <= 128) {
+    // (<= 32 output channels stay on the 32-column tiles: half of a 64-column halo block would be idle,
+    // 4x512^2 64 -> 32: 320 us against 277 us on 128x32)
+    if (halo_ok(p) && p->cout > 32 && p->cout <= 128 && halo_fill(p, 4) >= 0.85) {
         const int batch = p->batch > 0 ? p->batch : 1;
-        const long long blocks = (long long)(M / 256) * cdiv(p->cout, 64) * batch;
+        const long long blocks = (long long)p->n * cdiv(p->oh, 4) * cdiv(p->ow, 64) * cdiv(p->cout, 64) * batch;
         // 65..128 output channels: one block per 128 columns (two 64-channel wave columns share the halo):
         // 4x256^2 128 -> 128 279 vs 291 us (profiles/r05_halo_sweep.txt); <= 64: the 4-wave 64-column block
         const int kind = p->cout > 64 && x3_kind_ok(p, 5) ? 5 : 3;
-        if (blocks >= 2LL * plan_cus()) {
+        // ... but large 65..128-channel layers stay on 512x128: 16x400^2 128 -> 128 2189 us there against
+        // 2595 / 2418 us on the halo blocks (profiles/r05_halo_sweep.txt)
+        const bool big_n128 = p->cout > 64 && (long long)p->n * p->oh * p->ow >= (1LL << 20);
+        if (blocks >= 2LL * plan_cus() && !big_n128) {
             for (int i = 0; i < kNumX3; ++i)
                 if (kX3Tiles[i].kind == kind) {
                     pl.tile = i;
@@ -1380,8 +1386,16 @@ static bool nar_ok(const s2v_conv_params *p) {
 
 // conv_x3_halo's conditions (and nar_ok's addressing / weight conditions)
 static bool halo_ok(const s2v_conv_params *p) {
-    return nar_ok(p) && p->kh == 3 && p->kw == 3 && p->sh == 1 && p->sw == 1 && p->dh == 1 && p->dw == 1 &&
-           p->ph == 1 && p->pw == 1 && p->oh % 4 == 0 && p->ow % 64 == 0;
+    // the nar_ok conditions without its in_scale one (a halo patch never straddles two images)
+    return tiled_x3(p) && !p->b_kn && !p->x_split && a_mode(p) == 0 && p->cin % 32 == 0 && !p->out_pool &&
+           x_extent_bytes(p) < (1LL << 31) && (long long)p->npad * p->kpad * 4 < (1LL << 31) &&
+           (long long)cdiv(p->cout, 64) * 64 <= p->npad && p->kh == 3 && p->kw == 3 && p->sh == 1 &&
+           p->sw == 1 && p->dh == 1 && p->dw == 1 && p->ph == 1 && p->pw == 1;
+}
+
+// output pixels / patch-grid pixels of conv_x3_halo's TH x 64 patches (ragged images run part-empty patches)
+static double halo_fill(const s2v_conv_params *p, int th) {
+    return (double)p->oh * p->ow / ((double)cdiv(p->oh, th) * th * cdiv(p->ow, 64) * 64);
 }
 
 static bool x3_kind_ok(const s2v_conv_params *p, int kind) {
@@ -1716,6 +1730,10 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
     const bool bkn = p->b_kn != 0;
     const TileCfg &t = tile_cfg(p, pl.tile);
     dim3 grid(cdiv(M, t.bm), cdiv(p->cout, t.bn), batch * pl.splits);
+    if (tiled_x3(p) && kX3Tiles[pl.tile].kind >= 3) {   // conv_x3_halo: one block per (image, patch)
+        const int th = kX3Tiles[pl.tile].kind == 4 ? 8 : 4;
+        grid.x = (unsigned)((long long)p->n * cdiv(p->oh, th) * cdiv(p->ow, 64));
+    }
     if (tiled_x3(p)) {
         if (!bkn) a.wt = (const float *)p->wt_x3;
         if (kX3Tiles[pl.tile].kind >= 1) {         // conv_x3_nar / _halo (conditions: planner / validate)

@@ -14,8 +14,8 @@
 // The next channel slice's halo is loaded into registers during the first taps.
 //
 // Conditions (conv.hip halo_ok): 3x3, stride 1, dilation 1, zero padding 1, direct input, cin % 32 == 0,
-// oh % 4 == 0 and ow % 64 == 0, packed weights over whole 64-row slabs, 2^31-byte offsets, no pooled
-// epilogue.  Same products and the same per-slice MFMA order as conv_igemm_x3, but the K order is
+// packed weights over whole 64-row slabs, 2^31-byte offsets, no pooled epilogue; ragged images run
+// partly empty last patches (the planner requires >= 85 % of the patch grid to be image).  Same products and the same per-slice MFMA order as conv_igemm_x3, but the K order is
 // channel-slice major over taps in the natural order (conv_x3_impl's kperm order is the same: tap
 // fastest), so results equal the LDS tiles bit for bit (tests/test_ops_gpu.py).
 #include "conv_x3_impl.hpp"
@@ -58,7 +58,8 @@ __global__ __launch_bounds__(64 * TH * WN, TH * WN == 4 ? 2 : 1) void conv_x3_ha
         mt = t % gridDim.x;
         bz = t / gridDim.x;
     }
-    const int ntx = a.ow / TW, nty = a.oh / TH;
+    const int ntx = (a.ow + TW - 1) / TW, nty = (a.oh + TH - 1) / TH;   // ragged last patches: rows / columns
+                                                                          // past the image are not stored
     const int img = mt / (ntx * nty), rr = mt - img * (ntx * nty);
     const int y0 = (rr / ntx) * TH, x0 = (rr % ntx) * TW;
     const int n0 = nt * BN;
@@ -237,7 +238,8 @@ __global__ __launch_bounds__(64 * TH * WN, TH * WN == 4 ? 2 : 1) void conv_x3_ha
                     for (int r = 0; r < 4; ++r)
                         Cs[(i * 16 + 4 * kg + r) * LDC + wc * 64 + j * 16 + l16] = acc[i][j][r] * a.acc_scale;
         },
-        [&](int c0) { return (int)(mrow0 + (long long)(c0 / 64) * a.ow); }, [&](int) { return CH; });
+        [&](int c0) { return (int)(mrow0 + (long long)(c0 / 64) * a.ow); },
+        [&](int c0) { return y0 + c0 / 64 < a.oh ? min(CH, a.ow - x0) : 0; });
     launch_stamp(a, true);
 }
 

@@ -316,9 +316,9 @@ def _plan(n, h, w, cin, cout, k=3, stride=1, pad=1, force_tile=0, in_scale=False
 
 def test_planner_gives_narrow_3x3_layers_to_the_halo_kernel():
     """conv.hip make_plan_x3 (no GPU needed): 3x3 stride-1 layers of <= 64 / <= 128 output channels over
-    64-wide rows with a chip-filling grid take conv_x3_halo<ELT, 4, 1> / <ELT, 4, 2> (plan A mode 8);
-    ragged rows, wide layers, strided convs and small grids keep the implicit-GEMM tiles; forcing the
-    halo tile where it cannot run is an error."""
+    a patch grid that is >= 85 % image and a chip-filling grid take conv_x3_halo<ELT, 4, 1> / <ELT, 4, 2>
+    (plan A mode 8); emptier patch grids, wide layers, strided convs and small grids keep the
+    implicit-GEMM tiles; forcing the halo tile where it cannot run is an error."""
     from s2v_amd import ops
     rc, pl = _plan(4, 512, 512, 128, 64, in_scale=True)
     assert rc == 0 and pl[3] == 8 and (pl[0], pl[1]) == (256, 64), pl
@@ -326,10 +326,13 @@ def test_planner_gives_narrow_3x3_layers_to_the_halo_kernel():
     rc, pl = _plan(4, 256, 256, 128, 128)
     assert rc == 0 and pl[3] == 8 and (pl[0], pl[1]) == (256, 128), pl
     assert ops.plan_symbol(pl) == "void s2v::conv_x3_halo<1, 4, 2>(s2v::ConvArgs)"
-    for args in ((4, 200, 200, 64, 64), (16, 256, 256, 256, 256), (1, 64, 64, 64, 64)):
+    for args in ((4, 200, 200, 64, 64), (16, 256, 256, 256, 256), (1, 64, 64, 64, 64), (4, 512, 512, 64, 32),
+                 (16, 400, 400, 128, 128)):
         rc, pl = _plan(*args)
         assert rc == 0 and pl[3] != 8, (args, pl)
     rc, pl = _plan(4, 256, 256, 64, 64, stride=2)
     assert rc == 0 and pl[3] != 8
-    rc, _ = _plan(4, 200, 200, 64, 64, force_tile=18)
+    rc, pl = _plan(4, 200, 192, 64, 64)                 # ragged rows, 97 % of the patch grid: halo
+    assert rc == 0 and pl[3] == 8, pl
+    rc, _ = _plan(4, 256, 256, 64, 64, stride=2, force_tile=18)
     assert rc != 0 and b"conv_x3_halo" in _lib.load().s2v_last_error()

@@ -178,14 +178,15 @@ def test_conv_nar_bit_identical_to_lds_tile(ctx, prec, shape):
                                            cout, DEV), force_tile=16, in_scale=s)
 
 
-@pytest.mark.parametrize("shape", [(2, 64, 8, 128, 64), (1, 96, 4, 64, 40), (2, 32, 12, 64, 130), (4, 128, 16, 64, 64)])
+@pytest.mark.parametrize("shape", [(2, 64, 8, 128, 64), (1, 96, 4, 64, 40), (2, 32, 12, 64, 130), (4, 128, 16, 64, 64),
+                                   (2, 64, 10, 100, 64), (1, 32, 7, 70, 96)])
 def test_conv_halo_bit_identical_to_lds_tile(ctx, prec, shape):
     """conv_x3_halo (force_tile 18 / 19 / 20: 4 x 64 / 8 x 64 output patches, 20 with 128 output channels
     per block; the input halo split once per channel slice)
     against the LDS-staged 256x64 tile (force_tile 11): same K order (taps fastest within a channel
     slice), same MFMA order -> bit-identical, with modulation, pre-activation, demod / noise / residual
-    epilogues; halo split-K (whole channel slices) against the unsplit launch at the split bound; a
-    shape the kernel cannot take is refused when forced."""
+    epilogues; ragged images (partly empty last patches); halo split-K (whole channel slices) against
+    the unsplit launch at the split bound; a strided conv is refused when forced."""
     if prec == "f32":
         pytest.skip("split precisions only")
     n, cin, h, w, cout = shape
@@ -212,8 +213,9 @@ def test_conv_halo_bit_identical_to_lds_tile(ctx, prec, shape):
         y1 = NHWC.empty(n, h, w, cout, DEV)
         ops.conv2d(ctx, x, cw, y1, force_tile=18)
         assert (ysp.t - y1.t).abs().max() <= 1e-5 * (y1.t.abs().max() + 1)
+    cw2 = ConvW(wt.float(), None, DEV, stride=2, padding=1)
     with pytest.raises(Exception, match="conv_x3_halo"):
-        ops.conv2d(ctx, nhwc(rnd(n, cin, 6, 64, seed=58).float()), cw, NHWC.empty(n, 6, 64, cout, DEV), force_tile=18)
+        ops.conv2d(ctx, nhwc(rnd(n, cin, 8, 64, seed=58).float()), cw2, NHWC.empty(n, 4, 32, cout, DEV), force_tile=18)
 
 
 @pytest.fixture
