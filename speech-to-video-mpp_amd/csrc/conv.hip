@@ -1039,7 +1039,7 @@ static Plan make_plan_x3(const s2v_conv_params *p, int M, Plan pl) {
         const int kind = p->cout > 64 && x3_kind_ok(p, 5) ? 5 : 3;
         // ... but large 65..128-channel layers stay on 512x128: 16x400^2 128 -> 128 2189 us there against
         // 2595 / 2418 us on the halo blocks (profiles/r05_halo_sweep.txt)
-        const bool big_n128 = p->cout > 64 && (long long)p->n * p->oh * p->ow >= (1LL << 20);
+        const bool big_n128 = p->cout > 64 && (long long)p->n * p->oh * p->ow * batch >= (1LL << 20);
         if (blocks >= 2LL * plan_cus() && !big_n128) {
             for (int i = 0; i < kNumX3; ++i)
                 if (kX3Tiles[i].kind == kind) {

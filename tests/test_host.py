@@ -291,7 +291,7 @@ def test_torch_custom_ops_registered_hip_only():
         torch_ops.upfirdn2d(torch.zeros(1, 2, 4, 4), torch.ones(2, 2))
 
 
-def _plan(n, h, w, cin, cout, k=3, stride=1, pad=1, force_tile=0, in_scale=False):
+def _plan(n, h, w, cin, cout, k=3, stride=1, pad=1, force_tile=0, in_scale=False, batch=0):
     """s2v_conv2d_plan of an f16x3 direct conv (host-only: fake aligned pointers, nothing launched)."""
     lib = _lib.load()
     p = _lib.ConvParams()
@@ -307,6 +307,8 @@ def _plan(n, h, w, cin, cout, k=3, stride=1, pad=1, force_tile=0, in_scale=False
     p.npad = (cout + 127) // 128 * 128 if cout <= 128 else (cout + 255) // 256 * 256
     p.prec = 2                                  # S2V_PREC_F16X3
     p.force_tile = force_tile
+    if batch:                                   # per-sample weights (modulated convs): n images per member
+        p.batch, p.x_bs, p.y_bs, p.w_bs = batch, n * h * w * cin, n * p.oh * p.ow * cout, p.npad * p.kpad
     if in_scale:
         p.in_scale, p.in_scale_ns = 5 << 20, cin
     out = (ctypes.c_int * 11)()
@@ -332,6 +334,8 @@ def test_planner_gives_narrow_3x3_layers_to_the_halo_kernel():
         assert rc == 0 and pl[3] != 8, (args, pl)
     rc, pl = _plan(4, 256, 256, 64, 64, stride=2)
     assert rc == 0 and pl[3] != 8
+    rc, pl = _plan(1, 400, 400, 128, 128, batch=16)     # ENet's 400^2 StyleConv (per-sample weights): 512x128
+    assert rc == 0 and pl[3] != 8, pl
     rc, pl = _plan(4, 200, 192, 64, 64)                 # ragged rows, 97 % of the patch grid: halo
     assert rc == 0 and pl[3] == 8, pl
     rc, _ = _plan(4, 256, 256, 64, 64, stride=2, force_tile=18)
