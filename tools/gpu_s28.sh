@@ -1,5 +1,5 @@
 # full GPU suite + smoke on the current tree
-O=gpurun_out/s28; mkdir -p $O
+O=gpurun_out/${OUT:-s28}; mkdir -p $O
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/tests.log 2>&1; rc=$?
 tail -3 $O/tests.log
 [ $rc -eq 0 ] || { grep -E "FAILED|Error" $O/tests.log | head -20; exit 1; }

@@ -1,6 +1,6 @@
 # r05 final measurements of the current tree: bench lines (driver defaults + each workload), kernel stats,
 # FETCH/WRITE PMC and HBM tables, the lipsync phase timeline, the GPEN native ops' bandwidth
-O=gpurun_out/s30; mkdir -p $O
+O=gpurun_out/${OUT:-s30}; mkdir -p $O
 for w in lipsync lnet dnet pipeline enhance; do
   extra=""; [ $w != lipsync ] && extra="--no-cpu-baseline"
   timeout -k 10 420 python -u bench.py --workload $w $extra > $O/bench_$w.log 2>&1 || { echo "bench $w failed"; tail -5 $O/bench_$w.log; exit 1; }
