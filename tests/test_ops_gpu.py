@@ -141,6 +141,17 @@ CONV_CASES = [
     (1, 96, 19, 21, 40, 3, 1, 1, 1, "direct", "zero", 16, 3),
     (2, 32, 17, 15, 130, 3, 2, 1, 1, "direct", "zero", 16, 0),
     (2, 64, 11, 13, 96, 1, 1, 0, 1, "direct", "zero", 16, 2),
+    # conv_x3_halo (force_tile 18: 4 x 64 patches x 64 channels; 20: x 128 channels): every epilogue
+    # variant of the test (incl. the output slice of a wider tensor), ragged patches, split-K
+    (2, 64, 12, 64, 64, 3, 1, 1, 1, "direct", "zero", 18, 0),
+    (1, 96, 9, 70, 100, 3, 1, 1, 1, "direct", "zero", 20, 2),
+    (2, 32, 5, 130, 40, 3, 1, 1, 1, "direct", "zero", 18, 0),
+    # 1x1 Cout <= 4 heads (conv_small_cpar, LDS weights; 2 / 4 / 8 lanes per pixel, 4 / 8 float4s
+    # per lane)
+    (2, 64, 17, 19, 3, 1, 1, 0, 1, "direct", "zero", 0, 0),
+    (1, 128, 9, 33, 2, 1, 1, 0, 1, "direct", "zero", 0, 0),
+    (2, 32, 7, 11, 4, 1, 1, 0, 1, "direct", "zero", 0, 0),
+    (1, 256, 5, 9, 1, 1, 1, 0, 1, "direct", "zero", 0, 0),
 ]
 
 
