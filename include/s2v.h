@@ -542,6 +542,31 @@ int s2v_u8_div255_f64_border(const unsigned char *x, int h, int w, int border, d
 int s2v_face_blend(const unsigned char *base, const float *full_mask, const unsigned char *full_img,
                    const double *mask_sharp, unsigned char *out, long long pixels, s2v_stream_t stream);
 
+/* ---- GFPGANer.enhance restore composition (third_part/GFPGAN/gfpgan/utils.py:97-143, inference.py:300-301;
+ * facexlib 0.2.5 FaceRestoreHelper, requirements.txt:5, not vendored) ------------------------------- */
+
+/* s2v_warp_affine with BORDER_CONSTANT value border[ch] (host array of c values, saturated to the
+ * image type; NULL = 0): align_warp_face's cv2.warpAffine(img, affine, (512, 512),
+ * borderValue=(135, 133, 132)).  xis == 0 warps one source image with each of the n matrices. */
+int s2v_warp_affine_border(const void *x, int n, int h, int w, int c, long long xrs, long long xis, int dtype,
+                           const double *M, void *y, int oh, int ow, long long yrs, long long yis,
+                           const double *border, s2v_stream_t stream);
+/* basicsr tensor2img(x, rgb2bgr=True, min_max=(-1, 1)) (gfpgan/utils.py:121): fp32 NCHW RGB
+ * [n][3][h][w] -> uint8 HWC BGR, round((clamp(x, -1, 1) + 1) / 2 * 255) half to even. */
+int s2v_tensor2img_u8(const float *x, int n, int h, int w, unsigned char *y, s2v_stream_t stream);
+/* paste_faces_to_input_image's square mask (upscale 1): erosion [H][W] fp32 = cv2.erode(warpAffine(
+ * ones(S, S) fp32, M), ones((2, 2))) with M the device fp64 2x3 inverse affine (warpAffine inverts it
+ * again, as OpenCV does); *area (device fp64) = the sum of the erosion (zeroed first). */
+int s2v_restore_mask(const double *M, int S, int H, int W, float *erosion, double *area, s2v_stream_t stream);
+/* cv2.erode(x, ones((k, k), uint8)) on an fp32 [h][w] image (anchor k / 2, border never wins);
+ * ws: h * w floats, distinct from x and y. */
+int s2v_erode_rect_f32(const float *x, int h, int w, int k, float *y, float *ws, s2v_stream_t stream);
+/* out = soft * (erosion * warpAffine(face uint8 [S][S][3], M)) + (1 - soft) * base in fp32 on HWC
+ * [H][W][3] frames; base / out uint8 (0) or the fp32 accumulator of several faces (1; in place
+ * allowed), uint8 out truncates (astype(uint8)). */
+int s2v_restore_paste(const unsigned char *face, int S, const double *M, const float *soft, const float *erosion,
+                      const void *base, int base_f32, void *out, int out_f32, int H, int W, s2v_stream_t stream);
+
 /* ---- 3DMM coefficient regression front end (facing.py:100-130) ---------------- */
 
 /* face3d util/preprocess.py resize_n_crop_img (:147-167) as align_img (:186-216) calls it, then the

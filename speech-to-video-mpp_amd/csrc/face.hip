@@ -206,39 +206,47 @@ __device__ __forceinline__ WarpCoord warp_coord(const double *iM, int x, int y) 
     return c;
 }
 
+// taps outside the source read the border value bv (BORDER_CONSTANT, remapBilinear's cval)
 template <typename T>
-__device__ __forceinline__ T tap(const T *img, long long rs, int c, int h, int w, int yy, int xx, int ch) {
-    return (yy >= 0 && yy < h && xx >= 0 && xx < w) ? img[(long long)yy * rs + (long long)xx * c + ch] : T(0);
+__device__ __forceinline__ T tap(const T *img, long long rs, int c, int h, int w, int yy, int xx, int ch, T bv = T(0)) {
+    return (yy >= 0 && yy < h && xx >= 0 && xx < w) ? img[(long long)yy * rs + (long long)xx * c + ch] : bv;
 }
 
 // uint8: 15-bit integer weights w = (32 - fy or fy) * (32 - fx or fx) * 32, (sum + 2^14) >> 15
 __device__ __forceinline__ unsigned char warp_u8(const unsigned char *img, long long rs, int c, int h, int w,
-                                                 const WarpCoord &q, int ch) {
+                                                 const WarpCoord &q, int ch, unsigned char bv = 0) {
     const int w00 = (32 - q.fy) * (32 - q.fx) * 32, w01 = (32 - q.fy) * q.fx * 32;
     const int w10 = q.fy * (32 - q.fx) * 32, w11 = q.fy * q.fx * 32;
-    const int s = tap(img, rs, c, h, w, q.sy, q.sx, ch) * w00 + tap(img, rs, c, h, w, q.sy, q.sx + 1, ch) * w01 +
-                  tap(img, rs, c, h, w, q.sy + 1, q.sx, ch) * w10 + tap(img, rs, c, h, w, q.sy + 1, q.sx + 1, ch) * w11;
+    const int s = tap(img, rs, c, h, w, q.sy, q.sx, ch, bv) * w00 + tap(img, rs, c, h, w, q.sy, q.sx + 1, ch, bv) * w01 +
+                  tap(img, rs, c, h, w, q.sy + 1, q.sx, ch, bv) * w10 +
+                  tap(img, rs, c, h, w, q.sy + 1, q.sx + 1, ch, bv) * w11;
     return (unsigned char)((s + (1 << 14)) >> 15);
 }
 
 // float: the (1 - t, t) products of initInterTab2D (exact), summed in tap order in T
 template <typename T>
-__device__ __forceinline__ T warp_fp(const T *img, long long rs, int c, int h, int w, const WarpCoord &q, int ch) {
+__device__ __forceinline__ T warp_fp(const T *img, long long rs, int c, int h, int w, const WarpCoord &q, int ch,
+                                     T bv = T(0)) {
     const float tx = (float)q.fx / 32.f, ty = (float)q.fy / 32.f;
     const T w00 = (T)((1.f - ty) * (1.f - tx)), w01 = (T)((1.f - ty) * tx);
     const T w10 = (T)(ty * (1.f - tx)), w11 = (T)(ty * tx);
-    T s = tap(img, rs, c, h, w, q.sy, q.sx, ch) * w00;
-    s = s + tap(img, rs, c, h, w, q.sy, q.sx + 1, ch) * w01;
-    s = s + tap(img, rs, c, h, w, q.sy + 1, q.sx, ch) * w10;
-    s = s + tap(img, rs, c, h, w, q.sy + 1, q.sx + 1, ch) * w11;
+    T s = tap(img, rs, c, h, w, q.sy, q.sx, ch, bv) * w00;
+    s = s + tap(img, rs, c, h, w, q.sy, q.sx + 1, ch, bv) * w01;
+    s = s + tap(img, rs, c, h, w, q.sy + 1, q.sx, ch, bv) * w10;
+    s = s + tap(img, rs, c, h, w, q.sy + 1, q.sx + 1, ch, bv) * w11;
     return s;
 }
+
+// BORDER_CONSTANT value per channel (cv::Scalar saturated to the image type)
+struct WarpBorder {
+    double v[4];
+};
 
 template <typename T>
 __global__ __launch_bounds__(256) void warp_affine_kernel(const T *__restrict__ x, int h, int w, int c, long long xrs,
                                                           long long xis, const double *__restrict__ M, int n,
                                                           T *__restrict__ y, int oh, int ow, long long yrs,
-                                                          long long yis) {
+                                                          long long yis, WarpBorder bd) {
     const long long total = (long long)n * oh * ow;
     for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
         const int X = (int)(e % ow);
@@ -251,8 +259,9 @@ __global__ __launch_bounds__(256) void warp_affine_kernel(const T *__restrict__ 
         const T *img = x + (long long)b * xis;
         T *o = y + (long long)b * yis + (long long)Y * yrs + (long long)X * c;
         for (int ch = 0; ch < c; ++ch) {
-            if constexpr (sizeof(T) == 1) o[ch] = warp_u8((const unsigned char *)img, xrs, c, h, w, q, ch);
-            else o[ch] = warp_fp(img, xrs, c, h, w, q, ch);
+            const T bv = (T)bd.v[ch < 4 ? ch : 3];
+            if constexpr (sizeof(T) == 1) o[ch] = warp_u8((const unsigned char *)img, xrs, c, h, w, q, ch, bv);
+            else o[ch] = warp_fp(img, xrs, c, h, w, q, ch, bv);
         }
     }
 }
@@ -426,6 +435,119 @@ __global__ __launch_bounds__(256) void blend_plain_kernel(const unsigned char *_
     }
 }
 
+// ------------------------------------------------------------------------------ GFPGANer restore
+// basicsr tensor2img(output, rgb2bgr=True, min_max=(-1, 1)) as GFPGANer.enhance calls it
+// (gfpgan/utils.py:120-121): clamp(-1, 1), (x + 1) / 2, RGB -> BGR, (x * 255.).round() (half to
+// even), astype(uint8); NCHW fp32 -> HWC uint8
+__global__ __launch_bounds__(256) void tensor2img_u8_kernel(const float *__restrict__ x, long long hw, int n,
+                                                            unsigned char *__restrict__ y) {
+    const long long total = (long long)n * hw;
+    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+        const long long b = e / hw, p = e - b * hw;
+        const float *s = x + b * 3 * hw + p;
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+            float v = fminf(fmaxf(s[(2 - ch) * hw], -1.f), 1.f);
+            v = (v + 1.f) / 2.f;
+            y[e * 3 + ch] = (unsigned char)(int)rintf(v * 255.f);
+        }
+    }
+}
+
+// facexlib paste_faces_to_input_image (square parse map, upscale 1): inv_mask = warpAffine(ones(S, S)
+// fp32, inverse_affine) is the sum of the bilinear weights of the taps inside the crop (exact in fp32);
+// inv_mask_erosion = cv2.erode(inv_mask, ones((2, 2))) (anchor (1, 1): the min over rows y-1..y and
+// columns x-1..x inside the frame); area += the block's sum of the erosion (fp64)
+__global__ __launch_bounds__(256) void restore_mask_kernel(const double *__restrict__ M, int S, int H, int W,
+                                                           float *__restrict__ E, double *__restrict__ area) {
+    __shared__ double part[4];
+    double iM[6];
+    invert_affine(M, iM);
+    double acc = 0.0;
+    const long long total = (long long)H * W;
+    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+        const int X = (int)(e % W), Y = (int)(e / W);
+        float m = INFINITY;
+        for (int dy = -1; dy <= 0; ++dy) {
+            const int yy = Y + dy;
+            if (yy < 0) continue;
+            for (int dx = -1; dx <= 0; ++dx) {
+                const int xx = X + dx;
+                if (xx < 0) continue;
+                const WarpCoord q = warp_coord(iM, xx, yy);
+                const float tx = (float)q.fx / 32.f, ty = (float)q.fy / 32.f;
+                const bool x0 = q.sx >= 0 && q.sx < S, x1 = q.sx + 1 >= 0 && q.sx + 1 < S;
+                const bool y0 = q.sy >= 0 && q.sy < S, y1 = q.sy + 1 >= 0 && q.sy + 1 < S;
+                float v = (y0 && x0) ? (1.f - ty) * (1.f - tx) : 0.f;
+                v = v + ((y0 && x1) ? (1.f - ty) * tx : 0.f);
+                v = v + ((y1 && x0) ? ty * (1.f - tx) : 0.f);
+                v = v + ((y1 && x1) ? ty * tx : 0.f);
+                m = fminf(m, v);
+            }
+        }
+        E[e] = m;
+        acc += (double)m;
+    }
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(area, (part[0] + part[1]) + (part[2] + part[3]));
+}
+
+// cv2.erode with a k x k rectangle of ones (anchor (k / 2, k / 2)) as OpenCV's separable morphology:
+// min over columns x - k/2 .. x - k/2 + k - 1 inside the frame (the constant border never wins), then
+// the same over rows
+__global__ __launch_bounds__(256) void erode_row_kernel(const float *__restrict__ x, int h, int w, int k,
+                                                        float *__restrict__ y) {
+    const long long total = (long long)h * w;
+    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+        const int X = (int)(e % w);
+        const float *row = x + (e - X);
+        const int a = max(X - k / 2, 0), b = min(X - k / 2 + k, w);
+        float m = INFINITY;
+        for (int t = a; t < b; ++t) m = fminf(m, row[t]);
+        y[e] = m;
+    }
+}
+
+__global__ __launch_bounds__(256) void erode_col_kernel(const float *__restrict__ x, int h, int w, int k,
+                                                        float *__restrict__ y) {
+    const long long total = (long long)h * w;
+    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+        const int X = (int)(e % w), Y = (int)(e / w);
+        const int a = max(Y - k / 2, 0), b = min(Y - k / 2 + k, h);
+        float m = INFINITY;
+        for (int t = a; t < b; ++t) m = fminf(m, x[(long long)t * w + X]);
+        y[e] = m;
+    }
+}
+
+// upsample_img = inv_soft_mask * pasted_face + (1 - inv_soft_mask) * upsample_img with pasted_face =
+// inv_mask_erosion * warpAffine(restored_face uint8, inverse_affine) (BORDER_CONSTANT 0), fp32; TO
+// uint8 is the final astype(uint8) (truncation)
+template <typename TB, typename TO>
+__global__ __launch_bounds__(256) void restore_paste_kernel(const unsigned char *__restrict__ face, int S,
+                                                            const double *__restrict__ M,
+                                                            const float *__restrict__ soft,
+                                                            const float *__restrict__ E, const TB *base,
+                                                            TO *out, int H, int W) {
+    double iM[6];
+    invert_affine(M, iM);
+    const long long total = (long long)H * W;
+    for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+        const int X = (int)(e % W), Y = (int)(e / W);
+        const WarpCoord q = warp_coord(iM, X, Y);
+        const float sm = soft[e], em = E[e], ism = 1.f - sm;
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+            const float pasted = em * (float)warp_u8(face, (long long)S * 3, 3, S, S, q, ch);
+            const float v = sm * pasted + ism * (float)base[e * 3 + ch];
+            if constexpr (sizeof(TO) == 1) out[e * 3 + ch] = (unsigned char)(int)v;
+            else out[e * 3 + ch] = v;
+        }
+    }
+}
+
 }  // namespace
 }  // namespace s2v
 
@@ -508,17 +630,36 @@ extern "C" int s2v_warp_affine(const void *x, int n, int h, int w, int c, long l
     S2V_REQUIRE(xrs >= (long long)w * c && yrs >= (long long)ow * c && (n == 1 || (xis >= xrs * h && yis >= yrs * oh)),
                 "warp_affine: row / image pitches smaller than the rows / images");
     S2V_REQUIRE(h < 32767 && w < 32767, "warp_affine: source larger than OpenCV's int16 coordinates");
+    return s2v_warp_affine_border(x, n, h, w, c, xrs, xis, dtype, M, y, oh, ow, yrs, yis, nullptr, stream);
+}
+
+extern "C" int s2v_warp_affine_border(const void *x, int n, int h, int w, int c, long long xrs, long long xis,
+                                      int dtype, const double *M, void *y, int oh, int ow, long long yrs,
+                                      long long yis, const double *border, s2v_stream_t stream) {
+    S2V_REQUIRE(x && y && M && n > 0 && h > 0 && w > 0 && c > 0 && oh > 0 && ow > 0, "warp_affine: bad args");
+    S2V_REQUIRE(dtype >= 0 && dtype <= 2, "warp_affine: dtype must be 0 (uint8), 1 (fp32) or 2 (fp64)");
+    // xis == 0: n warps of one source image (align_warp_face's faces of one frame)
+    S2V_REQUIRE(xrs >= (long long)w * c && yrs >= (long long)ow * c &&
+                    (n == 1 || ((xis == 0 || xis >= xrs * h) && yis >= yrs * oh)),
+                "warp_affine: row / image pitches smaller than the rows / images");
+    S2V_REQUIRE(h < 32767 && w < 32767, "warp_affine: source larger than OpenCV's int16 coordinates");
+    WarpBorder bd = {{0., 0., 0., 0.}};
+    for (int i = 0; border && i < 4; ++i) {
+        double v = border[i < c ? i : c - 1];
+        if (dtype == 0) v = v <= 0. ? 0. : (v >= 255. ? 255. : rint(v));   // saturate_cast<uchar>
+        bd.v[i] = v;
+    }
     const unsigned g = grid_1d((long long)n * oh * ow);
     hipStream_t s = (hipStream_t)stream;
     if (dtype == 0)
         warp_affine_kernel<unsigned char><<<g, 256, 0, s>>>((const unsigned char *)x, h, w, c, xrs, xis, M, n,
-                                                            (unsigned char *)y, oh, ow, yrs, yis);
+                                                            (unsigned char *)y, oh, ow, yrs, yis, bd);
     else if (dtype == 1)
         warp_affine_kernel<float><<<g, 256, 0, s>>>((const float *)x, h, w, c, xrs, xis, M, n, (float *)y, oh, ow, yrs,
-                                                    yis);
+                                                    yis, bd);
     else
         warp_affine_kernel<double><<<g, 256, 0, s>>>((const double *)x, h, w, c, xrs, xis, M, n, (double *)y, oh, ow,
-                                                     yrs, yis);
+                                                     yrs, yis, bd);
     return check_launch("warp_affine");
 }
 
@@ -611,4 +752,51 @@ extern "C" int s2v_face_blend(const unsigned char *base, const float *full_mask,
     else
         blend_sr_kernel<<<g, 256, 0, (hipStream_t)stream>>>(base, full_mask, full_img, out, pixels);
     return check_launch("face_blend");
+}
+
+extern "C" int s2v_tensor2img_u8(const float *x, int n, int h, int w, unsigned char *y, s2v_stream_t stream) {
+    S2V_REQUIRE(x && y && n > 0 && h > 0 && w > 0, "tensor2img_u8: bad args");
+    const long long hw = (long long)h * w;
+    tensor2img_u8_kernel<<<grid_1d(n * hw), 256, 0, (hipStream_t)stream>>>(x, hw, n, y);
+    return check_launch("tensor2img_u8");
+}
+
+extern "C" int s2v_restore_mask(const double *M, int S, int H, int W, float *erosion, double *area,
+                                s2v_stream_t stream) {
+    S2V_REQUIRE(M && erosion && area && S > 0 && H > 0 && W > 0, "restore_mask: bad args");
+    hipStream_t s = (hipStream_t)stream;
+    if (hipMemsetAsync(area, 0, sizeof(double), s) != hipSuccess) return check_launch("restore_mask");
+    restore_mask_kernel<<<grid_1d((long long)H * W), 256, 0, s>>>(M, S, H, W, erosion, area);
+    return check_launch("restore_mask");
+}
+
+extern "C" int s2v_erode_rect_f32(const float *x, int h, int w, int k, float *y, float *ws, s2v_stream_t stream) {
+    S2V_REQUIRE(x && y && ws && h > 0 && w > 0 && k > 0 && ws != x && ws != y, "erode_rect_f32: bad args");
+    const unsigned g = grid_1d((long long)h * w);
+    hipStream_t s = (hipStream_t)stream;
+    erode_row_kernel<<<g, 256, 0, s>>>(x, h, w, k, ws);
+    erode_col_kernel<<<g, 256, 0, s>>>(ws, h, w, k, y);
+    return check_launch("erode_rect_f32");
+}
+
+extern "C" int s2v_restore_paste(const unsigned char *face, int S, const double *M, const float *soft,
+                                 const float *erosion, const void *base, int base_f32, void *out, int out_f32, int H,
+                                 int W, s2v_stream_t stream) {
+    S2V_REQUIRE(face && M && soft && erosion && base && out && S > 0 && H > 0 && W > 0, "restore_paste: bad args");
+    S2V_REQUIRE(base != out || (base_f32 && out_f32), "restore_paste: in place only on the fp32 accumulator");
+    const unsigned g = grid_1d((long long)H * W);
+    hipStream_t s = (hipStream_t)stream;
+    if (!base_f32 && !out_f32)
+        restore_paste_kernel<unsigned char, unsigned char><<<g, 256, 0, s>>>(
+            face, S, M, soft, erosion, (const unsigned char *)base, (unsigned char *)out, H, W);
+    else if (!base_f32)
+        restore_paste_kernel<unsigned char, float><<<g, 256, 0, s>>>(face, S, M, soft, erosion,
+                                                                     (const unsigned char *)base, (float *)out, H, W);
+    else if (out_f32)
+        restore_paste_kernel<float, float><<<g, 256, 0, s>>>(face, S, M, soft, erosion, (const float *)base,
+                                                             (float *)out, H, W);
+    else
+        restore_paste_kernel<float, unsigned char><<<g, 256, 0, s>>>(face, S, M, soft, erosion, (const float *)base,
+                                                                     (unsigned char *)out, H, W);
+    return check_launch("restore_paste");
 }
