@@ -233,9 +233,14 @@ def reference_hook(enh):
 
 def run(face: str, audio_path: str, max_frames: int = 8, batch: int = 16, box_frac: float = 0.6,
         ckpt_dir: str | None = None, enhance: bool = False, device: str = "cuda", ref_enhance: bool = False,
-        ref_hook=None):
+        ref_hook=None, restore: bool = True, restorer=None, enhancer=None):
     """-> dict(frames uint8 [n,H,W,3] device, preds uint8 [n,3,384,384], meta).  ``ref_enhance``:
-    Step 5 with FaceEnhancement-512 (``ref_hook``: any callable on uint8 [b,3,h,w] references)."""
+    Step 5 with FaceEnhancement-512 (``ref_hook``: any callable on uint8 [b,3,h,w] references).
+    ``enhance``: the per-frame tail of inference.py:296-330 on the pasted frames -> ``enhanced``
+    uint8 [n,2H,2W,3]: GFPGANer.enhance(ff, only_center_face=True) (``restore``; restore.GFPGANer,
+    :300-301), the FaceParse mouth mask + 10-level Laplacian blend (post.MouthBlend, :302-313), then
+    FaceEnhancement-2048 with SR x2 on the 2x frame (:326-327).  ``restorer`` / ``enhancer``: given
+    objects (else built from ``ckpt_dir`` as the reference builds them)."""
     from . import audio, pipeline, post, synth
     dev = torch.device(device)
     t0 = time.time()
@@ -272,17 +277,31 @@ def run(face: str, audio_path: str, max_frames: int = 8, batch: int = 16, box_fr
     enhanced = None
     if enhance:
         from . import face as faces
-        enh = faces.FaceEnhancement(base_dir=ckpt_dir or "checkpoints", in_size=2048, channel_multiplier=2, narrow=1,
-                                    sr_scale=2, sr_model=None, model="GPEN-BFR-2048", use_sr=True, device=device)
+        base = ckpt_dir or "checkpoints"
+        enh = enhancer or faces.FaceEnhancement(base_dir=base, in_size=2048, channel_multiplier=2, narrow=1,
+                                                sr_scale=2, sr_model=None, model="GPEN-BFR-2048", use_sr=True,
+                                                device=device)                       # inference.py:228-231
+        if restore and restorer is None:
+            from .restore import GFPGANer
+            restorer = GFPGANer(model_path=os.path.join(base, "GFPGANv1.4.pth"), upscale=1, arch="clean",
+                                channel_multiplier=2, bg_upsampler=None, device=device, base_dir=base)   # :255-256
+        mouth = post.MouthBlend(enh.faceparser)
+        box = (y1, y2, x1, x2)
         enhanced = []
         for i in range(n):
+            pp = out[i]
+            if restore:
+                _, _, restored_img = restorer.enhance(pp, has_aligned=False, only_center_face=True,
+                                                      paste_back=True)                  # inference.py:300-301
+                pp = mouth.run(restored_img, pp, box)                                   # :302-313
             big = post.resize_linear(frames[i], (2 * W, 2 * H))                      # tmp_xf (inference.py:326)
-            enhanced.append(enh.process_device(out[i], big, face_enhance=True, possion_blending=True)[0])
+            enhanced.append(enh.process_device(pp, big, bbox=box, face_enhance=True, possion_blending=True)[0])
         enhanced = torch.stack(enhanced)
     torch.cuda.synchronize(dev)
     meta = {"frames": n, "frame_hw": [int(H), int(W)], "fps": fps, "video": src_kind, "weights": wkind,
             "mel_cols": int(mel.shape[1]), "mel_windows": int(chunks.shape[0]), "wav_samples_16k": int(len(wav)),
             "box": [y1, y2, x1, x2], "semantic": skind, "ref_enhance": ref_hook is not None,
+            "restore": bool(enhance and restore),
             "seconds": round(time.time() - t0, 3)}
     return {"frames": out, "preds": preds, "enhanced": enhanced, "meta": meta}
 
@@ -297,10 +316,11 @@ def main(argv=None):
     ap.add_argument("--box_frac", type=float, default=0.6)
     ap.add_argument("--checkpoints", default=None)
     ap.add_argument("--enhance", action="store_true")
+    ap.add_argument("--no_restore", action="store_true", help="with --enhance: skip GFPGANer + the mouth blend")
     ap.add_argument("--ref_enhance", action="store_true", help="Step 5: FaceEnhancement-512 on the references")
     a = ap.parse_args(argv)
     r = run(a.face, a.audio, a.max_frames, a.LNet_batch_size, a.box_frac, a.checkpoints, a.enhance,
-            ref_enhance=a.ref_enhance)
+            ref_enhance=a.ref_enhance, restore=not a.no_restore)
     os.makedirs(os.path.dirname(os.path.abspath(a.outfile)), exist_ok=True)
     arrays = {"frames": r["frames"].cpu().numpy(), "preds": r["preds"].cpu().numpy()}
     if r["enhanced"] is not None:
