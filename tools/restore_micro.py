@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-phase timing of GFPGANer.enhance (s2v_amd.restore; gfpgan/utils.py:97-143) on one synthetic
-frame with synthetic weights: RetinaFace-R50 detect_faces on the frame (its candidates with a low
-threshold, as the network is random), then the composition with a fixed centre face (LMEDS fit,
+frame with synthetic weights: the RetinaFace-R50 network and detect_faces(img, 0.97) on the frame
+(random weights: the candidate count, hence the host NMS, is not a real frame's), then the composition with a fixed centre face (LMEDS fit,
 gray-border warp, GFPGANv1Clean, tensor2img, paste-back).  ms per call, best of --iters.
 
     python tools/restore_micro.py [--h 720 --w 1280] [--iters 10]"""
@@ -63,7 +63,9 @@ def main():
     r = restore.GFPGANer(upscale=1, device=dev, net=g.eval(), face_det=_Rows(rows))
     fh = r.face_helper
     res = {}
-    res["detect_faces (RetinaFace-R50 + decode + NMS)"] = best_ms(lambda: det.detect_faces(img, 0.5), a.iters)
+    res["RetinaFace-R50 network (head maps)"] = best_ms(lambda: det.det.head_maps(img), a.iters)
+    k = len(det.detect_faces(img, 0.97))
+    res[f"detect_faces(img, 0.97) ({k} faces kept)"] = best_ms(lambda: det.detect_faces(img, 0.97), a.iters)
 
     def align():
         fh.clean_all()
