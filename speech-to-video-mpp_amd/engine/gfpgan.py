@@ -14,6 +14,7 @@ Mapping onto the kernels:
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -22,6 +23,9 @@ from ..ops import NHWC, ConvW
 from .enet import StyleLayer
 
 LRELU = 0.2
+# ToRGB and its bilinear x2 skip upsample as one pass (ops.torgb_up2, as ENet's); S2V_GFPGAN_FUSED_TORGB=0:
+# resize + small conv with the residual
+FUSED_TORGB = os.environ.get("S2V_GFPGAN_FUSED_TORGB", "1") == "1"
 
 
 class GFPGANEngine:
@@ -193,9 +197,10 @@ class GFPGANEngine:
             noise = self._stored_noise(b)
         cur = NHWC(self.const.expand(b, -1, -1, -1).contiguous())
         cur = self._style_conv(ctx, self.conv1, cur, sall, dall, noise[0])
-        skip = NHWC.empty(b, cur.h, cur.w, 3, dev)
+        skip = NHWC.empty(b, cur.h, cur.w, 4, dev)             # RGB + a 4th channel the fused ToRGB carries
+        ops.fill(ctx, skip.t)
         s = self._style(self.rgb1, sall)
-        ops.conv2d(ctx, cur, self.rgb1.conv, skip, in_scale=s)
+        ops.conv2d(ctx, cur, self.rgb1.conv, skip.slice(0, 3), in_scale=s)
         i = 1
         for lvl in range(self.levels):
             cur = self._style_conv(ctx, self.convs[2 * lvl], cur, sall, dall, noise[2 * lvl + 1])
@@ -206,11 +211,14 @@ class GFPGANEngine:
                 ops.eltwise(ctx, part, part, mul=scale, add=shift)
             cur = self._style_conv(ctx, self.convs[2 * lvl + 1], cur, sall, dall, noise[2 * lvl + 2])
             R = self.rgbs[lvl]
-            rgb = NHWC.empty(b, cur.h, cur.w, 3, dev)
-            ops.resize_nhwc(ctx, skip, rgb, scale_factor=2)
+            rgb = NHWC.empty(b, cur.h, cur.w, 4, dev)
             s = self._style(R, sall)
-            ops.conv2d(ctx, cur, R.conv, rgb, in_scale=s, res=rgb)
+            if FUSED_TORGB and R.cin % 32 == 0 and (cur.h * cur.w) % 32 == 0:
+                ops.torgb_up2(ctx, cur, R.conv, s, skip, rgb)       # ToRGB + bilinear x2 skip (stylegan2_clean_arch.py:157-176)
+            else:
+                ops.resize_nhwc(ctx, skip, rgb, scale_factor=2)
+                ops.conv2d(ctx, cur, R.conv, rgb.slice(0, 3), in_scale=s, res=rgb.slice(0, 3))
             skip = rgb
             i += 2
-        ops.nhwc_to_nchw(ctx, skip, out)
+        ops.nhwc_to_nchw(ctx, skip.slice(0, 3), out)
         return out, rgbs
