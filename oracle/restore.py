@@ -48,6 +48,23 @@ def get_center_face(det_faces, h=0, w=0, center=None):
     return det_faces[idx], idx
 
 
+def get_largest_face(det_faces, h, w):
+    """facexlib face_restoration_helper.get_largest_face: largest box area, boxes clipped to the image."""
+    def get_location(val, length):
+        if val < 0:
+            return 0
+        if val > length:
+            return length
+        return val
+    areas = []
+    for f in det_faces:
+        left, right = get_location(f[0], w), get_location(f[2], w)
+        top, bottom = get_location(f[1], h), get_location(f[3], h)
+        areas.append((right - left) * (bottom - top))
+    idx = areas.index(max(areas))
+    return det_faces[idx], idx
+
+
 def landmarks_5(bboxes, h, w, only_center_face=False, eye_dist_threshold=None):
     """FaceRestoreHelper.get_face_landmarks_5's selection (template_3points=False, no resize, no
     pad_blur) on detect_faces' rows -> (det_faces, all_landmarks_5)."""

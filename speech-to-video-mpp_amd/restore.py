@@ -72,6 +72,15 @@ class RetinaFaceDetector:
         return np.concatenate((bounding_boxes[keep, :], landms[keep]), axis=1)
 
 
+def get_largest_face(det_faces, h, w):
+    """facexlib get_largest_face: the face with the largest box area after clipping the box to the image."""
+    def clip(v, n):
+        return 0 if v < 0 else (n if v > n else v)
+    areas = [(clip(f[2], w) - clip(f[0], w)) * (clip(f[3], h) - clip(f[1], h)) for f in det_faces]
+    idx = areas.index(max(areas))
+    return det_faces[idx], idx
+
+
 def get_center_face(det_faces, h=0, w=0, center=None):
     """facexlib get_center_face: the face whose box centre is nearest the image centre."""
     center = np.array(center) if center is not None else np.array([w / 2, h / 2])
@@ -221,9 +230,9 @@ class FaceRestoreHelper:
         if len(self.det_faces) == 0:
             return 0
         if only_keep_largest:
-            areas = [(f[2] - f[0]) * (f[3] - f[1]) for f in self.det_faces]
-            idx = areas.index(max(areas))
-            self.det_faces, self.all_landmarks_5 = [self.det_faces[idx]], [self.all_landmarks_5[idx]]
+            h, w = self.input_img.shape[:2]
+            det, idx = get_largest_face(self.det_faces, h, w)
+            self.det_faces, self.all_landmarks_5 = [det], [self.all_landmarks_5[idx]]
         elif only_center_face:
             h, w = self.input_img.shape[:2]
             det, idx = get_center_face(self.det_faces, h, w)

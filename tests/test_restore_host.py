@@ -106,3 +106,12 @@ def test_paste_restatement_keeps_the_frame_outside_the_face():
     assert trace[0]["area"] == 63 * 63 and trace[0]["w_edge"] == 3
     assert np.array_equal(out[:50], img[:50]) and np.array_equal(out[:, 145:], img[:, 145:])
     assert np.array_equal(out[80:100, 90:110], face[20:40, 20:40])
+
+
+def test_largest_face_clips_boxes_to_the_image():
+    """A box hanging off the frame loses the area outside it (facexlib get_largest_face)."""
+    from s2v_amd import restore
+    dets = [np.array([-300, -300, 60, 60, 0.99]), np.array([100, 50, 190, 150, 0.98])]
+    for fn in (restore.get_largest_face, OR.get_largest_face):
+        det, idx = fn(dets, 200, 220)
+        assert idx == 1 and det is dets[1]
