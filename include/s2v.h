@@ -554,18 +554,24 @@ int s2v_warp_affine_border(const void *x, int n, int h, int w, int c, long long 
 /* basicsr tensor2img(x, rgb2bgr=True, min_max=(-1, 1)) (gfpgan/utils.py:121): fp32 NCHW RGB
  * [n][3][h][w] -> uint8 HWC BGR, round((clamp(x, -1, 1) + 1) / 2 * 255) half to even. */
 int s2v_tensor2img_u8(const float *x, int n, int h, int w, unsigned char *y, s2v_stream_t stream);
-/* paste_faces_to_input_image's square mask (upscale 1): erosion [H][W] fp32 = cv2.erode(warpAffine(
- * ones(S, S) fp32, M), ones((2, 2))) with M the device fp64 2x3 inverse affine (warpAffine inverts it
- * again, as OpenCV does); *area (device fp64) = the sum of the erosion (zeroed first). */
-int s2v_restore_mask(const double *M, int S, int H, int W, float *erosion, double *area, s2v_stream_t stream);
+/* paste_faces_to_input_image's square mask (upscale 1) on the frame window [y0, y0+wh) x [x0, x0+ww)
+ * of an H x W frame: erosion [wh][ww] fp32 = cv2.erode(warpAffine(ones(S, S) fp32, M), ones((2, 2)))
+ * (frame coordinates) with M the device fp64 2x3 inverse affine (warpAffine inverts it again, as OpenCV
+ * does); area[0] (device fp64) = the sum of the erosion over the window, in a fixed order; area holds
+ * 1 + 512 doubles (area[1..] are the per-block partials).  A window holding the warped crop's whole
+ * footprint gives the frame's sum. */
+int s2v_restore_mask(const double *M, int S, int H, int W, int y0, int x0, int wh, int ww, float *erosion,
+                     double *area, s2v_stream_t stream);
 /* cv2.erode(x, ones((k, k), uint8)) on an fp32 [h][w] image (anchor k / 2, border never wins);
  * ws: h * w floats, distinct from x and y. */
 int s2v_erode_rect_f32(const float *x, int h, int w, int k, float *y, float *ws, s2v_stream_t stream);
 /* out = soft * (erosion * warpAffine(face uint8 [S][S][3], M)) + (1 - soft) * base in fp32 on HWC
- * [H][W][3] frames; base / out uint8 (0) or the fp32 accumulator of several faces (1; in place
- * allowed), uint8 out truncates (astype(uint8)). */
+ * [H][W][3] frames, soft / erosion [wh][ww] covering the frame window [y0, +wh) x [x0, +ww) (0 outside);
+ * base / out uint8 (0) or the fp32 accumulator of several faces (1; in place allowed), uint8 out
+ * truncates (astype(uint8)). */
 int s2v_restore_paste(const unsigned char *face, int S, const double *M, const float *soft, const float *erosion,
-                      const void *base, int base_f32, void *out, int out_f32, int H, int W, s2v_stream_t stream);
+                      int y0, int x0, int wh, int ww, const void *base, int base_f32, void *out, int out_f32, int H,
+                      int W, s2v_stream_t stream);
 
 /* ---- 3DMM coefficient regression front end (facing.py:100-130) ---------------- */
 

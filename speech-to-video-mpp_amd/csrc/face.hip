@@ -457,16 +457,21 @@ __global__ __launch_bounds__(256) void tensor2img_u8_kernel(const float *__restr
 // facexlib paste_faces_to_input_image (square parse map, upscale 1): inv_mask = warpAffine(ones(S, S)
 // fp32, inverse_affine) is the sum of the bilinear weights of the taps inside the crop (exact in fp32);
 // inv_mask_erosion = cv2.erode(inv_mask, ones((2, 2))) (anchor (1, 1): the min over rows y-1..y and
-// columns x-1..x inside the frame); area += the block's sum of the erosion (fp64)
-__global__ __launch_bounds__(256) void restore_mask_kernel(const double *__restrict__ M, int S, int H, int W,
-                                                           float *__restrict__ E, double *__restrict__ area) {
+// columns x-1..x inside the frame), over the frame window [y0, y0 + wh) x [x0, x0 + ww) (E is [wh][ww]);
+// part[block] = the block's fp64 sum of the erosion (one store per block: a single-address atomic from
+// ~8k blocks serialised to ~100 us at 1080p)
+constexpr int RESTORE_PARTS = 512;
+
+__global__ __launch_bounds__(256) void restore_mask_kernel(const double *__restrict__ M, int S, int y0, int x0,
+                                                           int wh, int ww, float *__restrict__ E,
+                                                           double *__restrict__ parts) {
     __shared__ double part[4];
     double iM[6];
     invert_affine(M, iM);
     double acc = 0.0;
-    const long long total = (long long)H * W;
+    const long long total = (long long)wh * ww;
     for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
-        const int X = (int)(e % W), Y = (int)(e / W);
+        const int X = x0 + (int)(e % ww), Y = y0 + (int)(e / ww);
         float m = INFINITY;
         for (int dy = -1; dy <= 0; ++dy) {
             const int yy = Y + dy;
@@ -491,7 +496,19 @@ __global__ __launch_bounds__(256) void restore_mask_kernel(const double *__restr
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
     __syncthreads();
-    if (threadIdx.x == 0) atomicAdd(area, (part[0] + part[1]) + (part[2] + part[3]));
+    if (threadIdx.x == 0) parts[blockIdx.x] = (part[0] + part[1]) + (part[2] + part[3]);
+}
+
+// area = the block partials summed in a fixed order (deterministic)
+__global__ __launch_bounds__(256) void restore_area_kernel(const double *__restrict__ parts, int n,
+                                                           double *__restrict__ area) {
+    __shared__ double part[4];
+    double acc = 0.0;
+    for (int i = threadIdx.x; i < n; i += 256) acc += parts[i];
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) area[0] = (part[0] + part[1]) + (part[2] + part[3]);
 }
 
 // cv2.erode with a k x k rectangle of ones (anchor (k / 2, k / 2)) as OpenCV's separable morphology:
@@ -524,20 +541,32 @@ __global__ __launch_bounds__(256) void erode_col_kernel(const float *__restrict_
 
 // upsample_img = inv_soft_mask * pasted_face + (1 - inv_soft_mask) * upsample_img with pasted_face =
 // inv_mask_erosion * warpAffine(restored_face uint8, inverse_affine) (BORDER_CONSTANT 0), fp32; TO
-// uint8 is the final astype(uint8) (truncation)
+// uint8 is the final astype(uint8) (truncation).  soft / E cover the window [y0, +wh) x [x0, +ww) and are
+// 0 outside it, where the blend is the base itself (0 * 0 + 1 * base)
 template <typename TB, typename TO>
 __global__ __launch_bounds__(256) void restore_paste_kernel(const unsigned char *__restrict__ face, int S,
                                                             const double *__restrict__ M,
                                                             const float *__restrict__ soft,
-                                                            const float *__restrict__ E, const TB *base,
-                                                            TO *out, int H, int W) {
+                                                            const float *__restrict__ E, int y0, int x0, int wh,
+                                                            int ww, const TB *base, TO *out, int H, int W) {
     double iM[6];
     invert_affine(M, iM);
     const long long total = (long long)H * W;
     for (long long e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
         const int X = (int)(e % W), Y = (int)(e / W);
+        const int wy = Y - y0, wx = X - x0;
+        if (wy < 0 || wy >= wh || wx < 0 || wx >= ww) {
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) {
+                const float v = (float)base[e * 3 + ch];
+                if constexpr (sizeof(TO) == 1) out[e * 3 + ch] = (unsigned char)(int)v;
+                else out[e * 3 + ch] = v;
+            }
+            continue;
+        }
+        const long long we = (long long)wy * ww + wx;
         const WarpCoord q = warp_coord(iM, X, Y);
-        const float sm = soft[e], em = E[e], ism = 1.f - sm;
+        const float sm = soft[we], em = E[we], ism = 1.f - sm;
 #pragma unroll
         for (int ch = 0; ch < 3; ++ch) {
             const float pasted = em * (float)warp_u8(face, (long long)S * 3, 3, S, S, q, ch);
@@ -761,12 +790,16 @@ extern "C" int s2v_tensor2img_u8(const float *x, int n, int h, int w, unsigned c
     return check_launch("tensor2img_u8");
 }
 
-extern "C" int s2v_restore_mask(const double *M, int S, int H, int W, float *erosion, double *area,
-                                s2v_stream_t stream) {
+extern "C" int s2v_restore_mask(const double *M, int S, int H, int W, int y0, int x0, int wh, int ww,
+                                float *erosion, double *area, s2v_stream_t stream) {
     S2V_REQUIRE(M && erosion && area && S > 0 && H > 0 && W > 0, "restore_mask: bad args");
+    S2V_REQUIRE(y0 >= 0 && x0 >= 0 && wh > 0 && ww > 0 && y0 + wh <= H && x0 + ww <= W,
+                "restore_mask: window outside the frame");
     hipStream_t s = (hipStream_t)stream;
-    if (hipMemsetAsync(area, 0, sizeof(double), s) != hipSuccess) return check_launch("restore_mask");
-    restore_mask_kernel<<<grid_1d((long long)H * W), 256, 0, s>>>(M, S, H, W, erosion, area);
+    long long nb = ((long long)wh * ww + 255) / 256;
+    const int blocks = (int)(nb < RESTORE_PARTS ? nb : RESTORE_PARTS);
+    restore_mask_kernel<<<blocks, 256, 0, s>>>(M, S, y0, x0, wh, ww, erosion, area + 1);
+    restore_area_kernel<<<1, 256, 0, s>>>(area + 1, blocks, area);
     return check_launch("restore_mask");
 }
 
@@ -780,23 +813,25 @@ extern "C" int s2v_erode_rect_f32(const float *x, int h, int w, int k, float *y,
 }
 
 extern "C" int s2v_restore_paste(const unsigned char *face, int S, const double *M, const float *soft,
-                                 const float *erosion, const void *base, int base_f32, void *out, int out_f32, int H,
-                                 int W, s2v_stream_t stream) {
+                                 const float *erosion, int y0, int x0, int wh, int ww, const void *base, int base_f32,
+                                 void *out, int out_f32, int H, int W, s2v_stream_t stream) {
     S2V_REQUIRE(face && M && soft && erosion && base && out && S > 0 && H > 0 && W > 0, "restore_paste: bad args");
+    S2V_REQUIRE(y0 >= 0 && x0 >= 0 && wh >= 0 && ww >= 0 && y0 + wh <= H && x0 + ww <= W,
+                "restore_paste: window outside the frame");
     S2V_REQUIRE(base != out || (base_f32 && out_f32), "restore_paste: in place only on the fp32 accumulator");
     const unsigned g = grid_1d((long long)H * W);
     hipStream_t s = (hipStream_t)stream;
     if (!base_f32 && !out_f32)
         restore_paste_kernel<unsigned char, unsigned char><<<g, 256, 0, s>>>(
-            face, S, M, soft, erosion, (const unsigned char *)base, (unsigned char *)out, H, W);
+            face, S, M, soft, erosion, y0, x0, wh, ww, (const unsigned char *)base, (unsigned char *)out, H, W);
     else if (!base_f32)
-        restore_paste_kernel<unsigned char, float><<<g, 256, 0, s>>>(face, S, M, soft, erosion,
+        restore_paste_kernel<unsigned char, float><<<g, 256, 0, s>>>(face, S, M, soft, erosion, y0, x0, wh, ww,
                                                                      (const unsigned char *)base, (float *)out, H, W);
     else if (out_f32)
-        restore_paste_kernel<float, float><<<g, 256, 0, s>>>(face, S, M, soft, erosion, (const float *)base,
-                                                             (float *)out, H, W);
+        restore_paste_kernel<float, float><<<g, 256, 0, s>>>(face, S, M, soft, erosion, y0, x0, wh, ww,
+                                                             (const float *)base, (float *)out, H, W);
     else
-        restore_paste_kernel<float, unsigned char><<<g, 256, 0, s>>>(face, S, M, soft, erosion, (const float *)base,
-                                                                     (unsigned char *)out, H, W);
+        restore_paste_kernel<float, unsigned char><<<g, 256, 0, s>>>(face, S, M, soft, erosion, y0, x0, wh, ww,
+                                                                     (const float *)base, (unsigned char *)out, H, W);
     return check_launch("restore_paste");
 }

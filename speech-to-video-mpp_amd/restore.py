@@ -283,11 +283,7 @@ class FaceRestoreHelper:
             return img.clone()                      # cv2.resize to the same size copies; astype(uint8)
         dev = self.device
         ctx = faces._ctx(dev)
-        E = torch.empty((h, w), dtype=torch.float32, device=dev)
-        C = torch.empty_like(E)
-        soft = torch.empty_like(E)
-        tmp = torch.empty_like(E)
-        area = torch.empty(1, dtype=torch.float64, device=dev)
+        area = torch.empty(1 + 512, dtype=torch.float64, device=dev)     # result + the block partials
         acc = None
         out = torch.empty((h, w, 3), dtype=torch.uint8, device=dev)
         S = self.face_size[0]
@@ -295,23 +291,40 @@ class FaceRestoreHelper:
         for i, (face, inv) in enumerate(zip(self.restored_faces, self.inverse_affine_matrices)):
             face = post.to_device(face, dev).contiguous()
             md = faces._mats(inv, dev)
-            check(ctx.lib.s2v_restore_mask(md.data_ptr(), S, h, w, E.data_ptr(), area.data_ptr(), ctx.stream),
-                  "s2v_restore_mask")
-            total_face_area = np.float32(area.item())          # np.sum(inv_mask_erosion) (fp32)
-            w_edge = int(total_face_area ** 0.5) // 20
-            k = w_edge * 2
-            check(ctx.lib.s2v_erode_rect_f32(E.data_ptr(), h, w, k if k > 0 else 3, C.data_ptr(), tmp.data_ptr(),
-                                             ctx.stream), "s2v_erode_rect_f32")
-            if k + 1 == 1:
-                soft.copy_(C)
-            else:
-                taps = gaussian_taps_auto(k + 1, dev)
-                need = ctx.lib.s2v_gaussian_blur_ws_bytes(h, w, 1)
-                ws, wsb = ctx.ws.get(need)
-                check(ctx.lib.s2v_gaussian_blur(C.data_ptr(), 1, h, w, 0, taps.data_ptr(), k + 1, soft.data_ptr(), 1,
-                                                1, ws, wsb, ctx.stream), "s2v_gaussian_blur")
+            # the masks are computed on a window: the warped crop's footprint (where inv_mask can be
+            # non-zero) padded by the largest erosion + blur reach its area allows (k = 2 w_edge <=
+            # sqrt(area) / 10 <= sqrt(footprint) / 10).  Outside it every mask is 0 and the blend is the
+            # base itself, and the window's own borders see only zeros, so the result equals the
+            # full-frame computation bit for bit.
+            fy, fx, fh, fw = faces.paste_window(inv, S, h, w)
+            y0 = x0 = wh = ww = 0
+            total_face_area, w_edge = np.float32(0.0), 0
+            soft = E = None
+            if fh > 0 and fw > 0:
+                pad = int(math.ceil(math.sqrt(fh * fw) / 10.0)) + 2
+                y0, x0 = max(0, fy - pad), max(0, fx - pad)
+                wh, ww = min(h, fy + fh + pad) - y0, min(w, fx + fw + pad) - x0
+                E = torch.empty((wh, ww), dtype=torch.float32, device=dev)
+                C, soft, tmp = torch.empty_like(E), torch.empty_like(E), torch.empty_like(E)
+                check(ctx.lib.s2v_restore_mask(md.data_ptr(), S, h, w, y0, x0, wh, ww, E.data_ptr(), area.data_ptr(),
+                                               ctx.stream), "s2v_restore_mask")
+                total_face_area = np.float32(area[0].item())   # np.sum(inv_mask_erosion) (fp32)
+                w_edge = int(total_face_area ** 0.5) // 20
+                k = w_edge * 2
+                assert k <= pad, (k, pad)
+                check(ctx.lib.s2v_erode_rect_f32(E.data_ptr(), wh, ww, k if k > 0 else 3, C.data_ptr(),
+                                                 tmp.data_ptr(), ctx.stream), "s2v_erode_rect_f32")
+                if k + 1 == 1:
+                    soft.copy_(C)
+                else:
+                    taps = gaussian_taps_auto(k + 1, dev)
+                    need = ctx.lib.s2v_gaussian_blur_ws_bytes(wh, ww, 1)
+                    ws, wsb = ctx.ws.get(need)
+                    check(ctx.lib.s2v_gaussian_blur(C.data_ptr(), 1, wh, ww, 0, taps.data_ptr(), k + 1,
+                                                    soft.data_ptr(), 1, 1, ws, wsb, ctx.stream), "s2v_gaussian_blur")
             if trace is not None:
-                trace.append(dict(erosion=E.clone(), area=total_face_area, w_edge=w_edge, soft=soft.clone()))
+                trace.append(dict(window=(y0, x0, wh, ww), erosion=None if E is None else E.clone(),
+                                  area=total_face_area, w_edge=w_edge, soft=None if soft is None else soft.clone()))
             base, base_f32 = (img, 0) if acc is None else (acc, 1)
             if i == last:
                 dst, dst_f32 = out, 0
@@ -319,7 +332,9 @@ class FaceRestoreHelper:
                 if acc is None:
                     acc = torch.empty((h, w, 3), dtype=torch.float32, device=dev)
                 dst, dst_f32 = acc, 1
-            check(ctx.lib.s2v_restore_paste(face.data_ptr(), S, md.data_ptr(), soft.data_ptr(), E.data_ptr(),
+            sp = soft.data_ptr() if soft is not None else area.data_ptr()      # unread with an empty window
+            ep = E.data_ptr() if E is not None else area.data_ptr()
+            check(ctx.lib.s2v_restore_paste(face.data_ptr(), S, md.data_ptr(), sp, ep, y0, x0, wh, ww,
                                             base.data_ptr(), base_f32, dst.data_ptr(), dst_f32, h, w, ctx.stream),
                   "s2v_restore_paste")
         return out

@@ -79,15 +79,16 @@ def test_restore_mask_erosion_and_area(mi):
     H, W, S = 260, 300, 512
     inv = INVS[mi]
     E = torch.empty((H, W), device=DEV)
-    area = torch.empty(1, dtype=torch.float64, device=DEV)
+    area = torch.empty(1 + 512, dtype=torch.float64, device=DEV)
     ctx = _ctx()
     md = face._mats(inv, DEV)
-    _lib.check(ctx.lib.s2v_restore_mask(md.data_ptr(), S, H, W, E.data_ptr(), area.data_ptr(), ctx.stream), "mask")
+    _lib.check(ctx.lib.s2v_restore_mask(md.data_ptr(), S, H, W, 0, 0, H, W, E.data_ptr(), area.data_ptr(),
+                                        ctx.stream), "mask")
     exp = OR.erode(OF.warp_affine(np.ones((S, S), np.float32), inv, (W, H)), 2)
     got = E.cpu().numpy()
     assert np.array_equal(got, exp), np.abs(got - exp).max()
     ref = float(np.sum(exp))
-    assert ref > 100 and abs(area.item() - ref) <= 1e-6 * ref
+    assert ref > 100 and abs(area[0].item() - ref) <= 1e-6 * ref
 
 
 @pytest.mark.parametrize("k", [1, 3, 4, 10, 31])
@@ -111,10 +112,11 @@ class _NoDetector:
         raise AssertionError("not used")
 
 
-@pytest.mark.parametrize("nfaces", [1, 2])
+@pytest.mark.parametrize("nfaces", [1, 2, 3])
 def test_paste_faces_to_input_image_bit_exact(nfaces):
-    """paste_faces_to_input_image on given restored faces / inverse affines: one face (uint8 -> uint8)
-    and two overlapping faces (the second blends onto the fp32 result of the first)."""
+    """paste_faces_to_input_image on given restored faces / inverse affines: one face (uint8 -> uint8),
+    two overlapping faces (the second blends onto the fp32 result of the first) and a third whose crop
+    covers the whole frame (mask window clipped to the frame: the blur's reflect-101 edges)."""
     img = rng_u8(5, (260, 300, 3))
     restored = [rng_u8(6 + i, (512, 512, 3)) for i in range(nfaces)]
     inv = INVS[:nfaces]
@@ -128,7 +130,11 @@ def test_paste_faces_to_input_image_bit_exact(nfaces):
     exp = OR.paste_faces(img, restored, inv, (512, 512), otrace)
     for a, b in zip(trace, otrace):
         assert a["w_edge"] == b["w_edge"] > 0
-        assert np.array_equal(a["soft"].cpu().numpy(), b["soft"])
+        y0, x0, wh, ww = a["window"]
+        for key in ("soft", "erosion"):                  # the windowed masks, zero elsewhere, = the full frame's
+            full = np.zeros_like(b[key])
+            full[y0: y0 + wh, x0: x0 + ww] = a[key].cpu().numpy()
+            assert np.array_equal(full, b[key]), key
     assert np.array_equal(got, exp), int((got != exp).sum())
     assert not np.array_equal(got, img)
 

@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--h", type=int, default=720)
     ap.add_argument("--w", type=int, default=1280)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--no-detect", action="store_true", help="skip the RetinaFace timing (profiling runs)")
     a = ap.parse_args()
     from helpers import GFPGAN_KW, synth_sd
     from oracle import restore as OR
@@ -63,9 +64,10 @@ def main():
     r = restore.GFPGANer(upscale=1, device=dev, net=g.eval(), face_det=_Rows(rows))
     fh = r.face_helper
     res = {}
-    res["RetinaFace-R50 network (head maps)"] = best_ms(lambda: det.det.head_maps(img), a.iters)
-    k = len(det.detect_faces(img, 0.97))
-    res[f"detect_faces(img, 0.97) ({k} faces kept)"] = best_ms(lambda: det.detect_faces(img, 0.97), a.iters)
+    if not a.no_detect:
+        res["RetinaFace-R50 network (head maps)"] = best_ms(lambda: det.det.head_maps(img), a.iters)
+        k = len(det.detect_faces(img, 0.97))
+        res[f"detect_faces(img, 0.97) ({k} faces kept)"] = best_ms(lambda: det.detect_faces(img, 0.97), a.iters)
 
     def align():
         fh.clean_all()
