@@ -62,6 +62,11 @@ FP32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 matrix 157.3 TF (
 # fp32 MAC, so their ceiling in algorithmic (fp32-equivalent) FLOP/s is a third of that peak
 X3_PEAK_TFLOPS = 2500.0 / 3
 REF_GFLOP_PER_FRAME = 407.46       # ENet+LNet algorithmic GFLOP/frame (2*MAC)
+# ENet's StyleConv NoiseInjection strength in the timed lipsync / pipeline / clip weights (non-zero,
+# as in a trained checkpoint): every step draws four N(0,1) noise planes (base_blocks.py:528-531)
+NOISE_W = 0.1
+NOISE_DESC = (f"on: NoiseInjection weight {NOISE_W} on all four StyleConvs, fresh N(0,1) planes drawn "
+              "on the device every step and added in the conv epilogues")
 
 
 ARITH = {"f16x3": "f16x3: fp32 tensors, conv products as split-fp32 hi*hi+hi*lo+lo*hi on f16 MFMA "
@@ -462,7 +467,10 @@ class LipSync(Workload):
         from s2v_amd import models, synth
         from s2v_amd.models import arch
         self.batch = args.batch or 16
-        self.sd = synth.synth_torch_state_dict(arch.ENetParams(lnet=arch.LNetParams()))
+        # StyleConv noise ON: NoiseInjection weight 0.1 on every StyleConv (real checkpoints carry
+        # non-zero strengths; base_blocks.py:528-531 draws fresh N(0,1) noise per call), so every timed
+        # step draws its noise planes and adds them in the conv epilogues
+        self.sd = synth.synth_torch_state_dict(arch.ENetParams(lnet=arch.LNetParams()), noise_weight=NOISE_W)
         self.model = models.ENet()
         self.model.load_state_dict(self.sd)
         self.model.eval()
@@ -472,7 +480,7 @@ class LipSync(Workload):
         self.fn_lane = lambda lane, m, f, g: self.model(m, f, g, lane=lane)  # noqa: E731
         self.config = {"workload": f"ENet(+LNet) forward, B={self.batch} synthetic {args.size}x{args.size} crops "
                                    f"+ [1,80,16] mel windows -> 384x384 (models/ENet.py:82-139)",
-                       "crop": args.size}
+                       "crop": args.size, "styleconv_noise": NOISE_DESC}
 
     def forward(self):
         return self.fn(*self.inputs)
@@ -481,7 +489,11 @@ class LipSync(Workload):
         from oracle import nets
         torch.set_num_threads(threads)
         mel, face, gt = make_inputs(2, self.size, "cpu", 1234)
-        n, el = _timed_cpu(lambda: nets.enet_forward(self.sd, mel, face, gt), 2, seconds, 8)
+
+        def fwd():             # fresh StyleConv noise per call, as the timed GPU step draws it
+            noises = [torch.randn(2, 1, s, s) for s in (200, 200, 400, 400)]
+            return nets.enet_forward(self.sd, mel, face, gt, noises=noises)
+        n, el = _timed_cpu(fwd, 2, seconds, 8)
         return {"value": round(n / el, 4), "unit": "frames/s", "cores": threads, "kind": "port",
                 "sample": f"{n} frames (2-frame batches) of the same ENet(+LNet) {self.size}x{self.size} workload "
                           f"in {el:.1f}s, torch CPU fp32, {threads} threads"}
@@ -581,7 +593,7 @@ class Pipeline(Workload):
         from s2v_amd.models import arch
         self.batch = args.batch or 16
         self.sd_d = synth.synth_torch_state_dict(arch.DNetParams())
-        self.sd_e = synth.synth_torch_state_dict(arch.ENetParams(lnet=arch.LNetParams()))
+        self.sd_e = synth.synth_torch_state_dict(arch.ENetParams(lnet=arch.LNetParams()), noise_weight=NOISE_W)
         dnet, enet = models.DNet(), models.ENet()
         dnet.load_state_dict(self.sd_d)
         enet.load_state_dict(self.sd_e)
@@ -614,7 +626,7 @@ class Pipeline(Workload):
         self.fn_lane = lambda lane, m, s, c: self.pipe.run_batch(m, s, c, self.outs[lane], lane=lane)  # noqa: E731
         self.config = {"workload": f"DNet -> uint8 ref -> ENet(+LNet) -> uint8, B={b} frames per step "
                                    "(inference.py:259-288, facing.py:176-191), 256x256 DNet/ENet crops",
-                       "host_precompute": self.host}
+                       "host_precompute": self.host, "styleconv_noise": NOISE_DESC}
 
     def forward(self):
         return self.fn(*self.inputs)
@@ -893,7 +905,8 @@ class Clip(Pipeline):
         self.config = {"workload": f"run_sharded over a {n}-frame clip (40 ms of 16 kHz audio per frame): broadcast "
                                    "wav/semantic/expression, mel + 16-column windows, coefficient windows, "
                                    "DNet -> uint8 ref -> ENet(+LNet) -> uint8 384x384 per rank, gather to rank 0 "
-                                   "(inference.py:204-288, facing.py:176-191)", "clip_frames": n}
+                                   "(inference.py:204-288, facing.py:176-191)", "clip_frames": n,
+                       "styleconv_noise": NOISE_DESC}
 
     def units_per_step(self, world):
         # the clip's mel windows (inference.py:209-222: 997 for 40 s); only rank 0 holds the frames

@@ -93,7 +93,9 @@ typedef struct s2v_conv_params {
      * is written at y + ((n*out_full_h + oy*out_step)*out_full_w + ox*out_step)*ycs — one parity
      * class of a polyphase transposed conv.  No pix_add; res only in place (res == y). */
     int out_step; int out_full_h, out_full_w;
-    /* arithmetic of the implicit-GEMM kernels (the Cout <= 4 VALU and K <= 64 kernels are always fp32):
+    /* arithmetic of the implicit-GEMM kernels and of the Cout <= 4 heads with a 5x5 / 7x7 stride-1 filter over
+     * 32 / 64 channels (conv_head_x3: the filter column in N, the row in K; S2V_HEAD_X3=0 turns it off); the
+     * other Cout <= 4 VALU kernels and the K <= 64 kernels are always fp32:
      *   S2V_PREC_F32     v_mfma_f32_32x32x2_f32, exact fp32 products (reads ``wt``);
      *   S2V_PREC_BF16X3  split-fp32 on v_mfma_f32_32x32x16_bf16: a*b ~ ah*bh + ah*bl + al*bh with
      *                    ah = bf16(a), al = bf16(a - ah); <= 3*2^-16 relative error per product, any range;
@@ -303,6 +305,11 @@ int s2v_attention(const float *q, const float *k, const float *v, int batch, int
 int s2v_flow_warp(const float *flow, int n, int fh, int fw, int flow_cs, const float *src, int c, int h,
                   int w, long long ssn, long long ssc, long long ssy, long long ssx, float *y, int ycs,
                   s2v_stream_t stream);
+/* The same warp written beside a copy of its source: y[p, 0:c) = src[p], y[p, c:2c) = warp(src)[p]
+ * (EditingNet's torch.cat([input_image, warp_image], 1), DNet.py:114-115) in one pass; ycs >= 2c. */
+int s2v_flow_warp_cat(const float *flow, int n, int fh, int fw, int flow_cs, const float *src, int c, int h,
+                      int w, long long ssn, long long ssc, long long ssy, long long ssx, float *y, int ycs,
+                      s2v_stream_t stream);
 
 /* Mel spectrogram (futils/audio.py:45-51, :20-23, :57-61, :92-123 + hparams.py:21-61):
  * preemphasis(0.97) -> STFT(n_fft 800, hop 200, periodic Hann, center=True, zero or reflect
@@ -329,6 +336,18 @@ int s2v_fused_bias_act(const float *x, const float *b, const float *ref, float *
 int s2v_upfirdn2d(const float *x, int major, int in_h, int in_w, int minor, const float *k, int kh, int kw,
                   int up_x, int up_y, int down_x, int down_y, int pad_x0, int pad_x1, int pad_y0, int pad_y1,
                   float *y, int out_h, int out_w, s2v_stream_t stream);
+/* The same two ops over the element types of the reference's AT_DISPATCH_FLOATING_TYPES_AND_HALF
+ * (fused_bias_act_kernel.cu:79, upfirdn2d_kernel.cu:225).  Every pointer (bias, refer, kernel
+ * included) holds `dtype` elements.  Arithmetic: S2V_DT_F64 in double throughout (alpha / scale
+ * taken as double); S2V_DT_F16 loads halves, computes in fp32 and rounds once on the store (the
+ * reference's CUDA path rounds after every operation; its CPU fallback computes each op in fp32);
+ * S2V_DT_F32 is s2v_fused_bias_act / s2v_upfirdn2d. */
+enum { S2V_DT_F32 = 0, S2V_DT_F16 = 1, S2V_DT_F64 = 2 };
+int s2v_fused_bias_act_dt(int dtype, const void *x, const void *b, const void *ref, void *y, long long size, int c,
+                          long long step_b, int act, int grad, double alpha, double scale, s2v_stream_t stream);
+int s2v_upfirdn2d_dt(int dtype, const void *x, int major, int in_h, int in_w, int minor, const void *k, int kh,
+                     int kw, int up_x, int up_y, int down_x, int down_y, int pad_x0, int pad_x1, int pad_y0,
+                     int pad_y1, void *y, int out_h, int out_w, s2v_stream_t stream);
 
 /* FourierUnit transforms (models/ffc.py:93-126): torch.fft.rfftn / irfftn over (H, W),
  * norm='ortho', as separable 1-D passes staged in LDS (one block per sample x 4 channels).

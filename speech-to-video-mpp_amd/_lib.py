@@ -85,12 +85,18 @@ _SIGS = {
                                _c_ll, _c_float, _vp, _c_int, _c_ll, _vp]),
     "s2v_flow_warp": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_ll, _c_ll,
                                _c_ll, _c_ll, _vp, _c_int, _vp]),
+    "s2v_flow_warp_cat": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_ll, _c_ll,
+                                   _c_ll, _c_ll, _vp, _c_int, _vp]),
     "s2v_melspectrogram": (_c_int, [_vp, _c_ll, _vp, _c_int, _vp, _c_ll, _vp]),
     "s2v_mel_chunks": (_c_int, [_vp, _c_ll, _vp, _c_int, _c_int, _vp, _vp]),
     "s2v_fused_bias_act": (_c_int, [_vp, _vp, _vp, _vp, _c_ll, _c_int, _c_ll, _c_int, _c_int, _c_float, _c_float,
                                     _vp]),
     "s2v_upfirdn2d": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_int,
                                _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _vp]),
+    "s2v_fused_bias_act_dt": (_c_int, [_c_int, _vp, _vp, _vp, _vp, _c_ll, _c_int, _c_ll, _c_int, _c_int,
+                                       ctypes.c_double, ctypes.c_double, _vp]),
+    "s2v_upfirdn2d_dt": (_c_int, [_c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int,
+                                  _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _vp]),
     "s2v_fir2d": (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_int,
                            _c_int, _vp, _c_int, _c_int, _c_int, _c_float, _vp, _c_int, _c_float, _c_float, _vp]),
     "s2v_fft_tables_floats": (_c_size, [_c_int, _c_int]),

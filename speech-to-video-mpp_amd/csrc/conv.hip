@@ -841,6 +841,34 @@ static int halo_ks(const s2v_conv_params *p) {
     return p->kh;
 }
 
+// Split-precision heads (conv_head.hip): Cout <= 4, a square 5x5 / 7x7 stride-1 filter over 32 / 64
+// channels, direct input with zero or reflect padding, no prologue scaling, one shared filter
+// (S2V_HEAD_X3=0: the fp32 VALU kernels instead)
+int launch_conv_head_x3(const ConvArgs &a, int prec, int co, int ks, int ncs, int th, hipStream_t s);
+static bool head_x3_on() {
+    static const int on = [] { const char *e = getenv("S2V_HEAD_X3"); return e ? atoi(e) : 1; }();
+    return on != 0;
+}
+static bool head_x3_ok(const s2v_conv_params *p) {
+    const int batch = p->batch > 0 ? p->batch : 1;
+    if (!head_x3_on() || p->prec == S2V_PREC_F32 || p->x_split || p->force_tile || !p->wt_x3 || ((uintptr_t)p->wt_x3 % 16))
+        return false;
+    if (p->cout > 4 || p->kh != p->kw || (p->kh != 7 && p->kh != 5) || (p->cin != 32 && p->cin != 64)) return false;
+    if (p->in_mode != S2V_IN_DIRECT || p->sh != 1 || p->sw != 1 || p->dh != 1 || p->dw != 1) return false;
+    if (p->in_scale || p->pre_act || p->w_bs || batch != 1 || p->b_kn || p->out_step > 1 || p->out_pool || p->d2s_cout)
+        return false;
+    if (p->ph >= p->kh || p->pw >= p->kw || p->xcs % 4 || ((uintptr_t)p->x % 16)) return false;
+    if (p->pad_mode == S2V_PAD_REFLECT && (p->ph >= p->h || p->pw >= p->w)) return false;
+    return true;
+}
+// output rows per conv_head_x3 block: 16, halved while the grid is under two blocks per CU (>= 4)
+static int head_rows(const s2v_conv_params *p) {
+    const long long strips = cdiv(p->ow, 64 - p->kw + 1);
+    int th = 16;
+    while (th > 4 && (long long)p->n * strips * cdiv(p->oh, th) < 2LL * device_cus()) th /= 2;
+    return th;
+}
+
 // channel splits of the halo kernel: about three blocks per CU, at least 8 channels per split
 static int halo_splits(const s2v_conv_params *p, int &per) {
     const long long blocks = (long long)p->n * cdiv(p->ow, 128) * cdiv(p->oh, 8);
@@ -1143,6 +1171,12 @@ static Plan make_plan(const s2v_conv_params *p_in, int M, int K) {
     Plan pl{};
     pl.ktiles = (K + 31) / 32;
     if (p->x_split) return make_plan_glds(p, M, pl);
+    if (head_x3_ok(p)) {
+        pl.tile = -3;
+        pl.splits = 1;
+        pl.tps = pl.ktiles;
+        return pl;
+    }
     if (use_direct(p) && !p->force_tile) {
         pl.tile = -1;
         pl.splits = 1;
@@ -1623,6 +1657,11 @@ extern "C" int s2v_conv2d_plan(const s2v_conv_params *p, int *out6) {
         out6[4] = p->cin == 4 && p->kh == p->kw && (p->kh == 1 || p->kh == 3) ? 2000 + p->kh * p->kw : 0;
         return 0;
     }
+    if (pl.tile == -3) {                                // conv_head_x3<prec - 1, CO, KS, cin / 32>
+        out6[0] = 0; out6[1] = p->cout; out6[2] = p->cin / 32; out6[3] = 0;
+        out6[4] = 3000 + p->kh; out6[5] = 1; out6[6] = p->prec;
+        return 0;
+    }
     if (pl.tile < 0 && halo_ks(p)) {
         out6[0] = 0; out6[1] = p->cout < 4 ? p->cout : 4;
         out6[2] = 0; out6[3] = 0;
@@ -1678,6 +1717,17 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
         else if (qpt == 1) conv_smallk<1, 1><<<grid, 256, lds, s>>>(a, batch, tppx, iters, vec);
         else conv_smallk<2, 1><<<grid, 256, lds, s>>>(a, batch, tppx, iters, vec);
         return check_launch("conv_smallk");
+    }
+    if (pl.tile == -3) {
+        a.wt = (const float *)p->wt_x3;
+        a.acc_scale = p->wt_scale > 0.f ? 1.f / p->wt_scale : 1.f;
+        if (p->x_scale > 0.f && p->x_scale != 1.f) {
+            a.x_scale = p->x_scale;
+            a.acc_scale /= p->x_scale;
+        }
+        rc = launch_conv_head_x3(a, p->prec, p->cout, p->kh, p->cin / 32, head_rows(p), s);
+        if (rc) return rc;
+        return check_launch("conv_head_x3");
     }
     if (pl.tile < 0 && halo_ks(p)) {
         if (pl.splits > 1) {

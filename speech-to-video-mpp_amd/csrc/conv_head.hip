@@ -1,0 +1,193 @@
+// Wide-filter small-Cout output heads on the split-precision MFMA: DNet's 7x7 64 -> 3 tanh output conv
+// (models/DNet.py:77-86, FinalBlock2d base_blocks.py:444-457, 16 x 256^2) and LNet's 7x7 64 -> 3
+// sigmoid head (models/LNet.py:77, 16 x 96^2).
+//
+// A Cout <= 4 conv is a GEMM with N = Cout: as an implicit GEMM it wastes the MFMA's N dimension, and
+// as a direct VALU conv (conv_halo_small) it is bound by fp32 FMA issue and by re-staging the input
+// in 4-channel chunks (each 256-byte NHWC pixel read 16 bytes at a time: 13x the input in fetched
+// lines at the DNet head).  Here the filter column kx moves into N and the row ky into K:
+//
+//   P[p, (o, kx)] = sum_{ky, c} x[oy - ph + ky, x0 + p, c] * W[o, ky, kx, c]     (N = Cout * KS <= 32)
+//   y[oy, x0 + q, o] = sum_kx P[q + kx, (o, kx)]                                 (shift-sum over kx)
+//
+// One block owns a strip of TW = 64 - KS + 1 output columns (64 input columns, four 16-row MFMA
+// blocks, one per wave) and a band of output rows.  The KS input rows an output row reads live in an
+// LDS ring, each staged ONCE per block as split hi | lo halves (the whole 32-channel slice of a pixel
+// is one 128-byte row: every fetched line is used whole); an output row stages one new input row,
+// prefetched into registers under the previous row's MFMAs.  The filter (K = KS * cin, N = 32) stays
+// in VGPRs for the whole block as pre-split fragments (224 VGPRs at KS = 7, cin = 64), so the row
+// loop reads only LDS.  Products are split-fp32 (hi*hi + hi*lo + lo*hi on 16x16x32 MFMAs, fp32
+// accumulate) exactly as the implicit-GEMM kernels (conv_x3_impl.hpp), and so are the activation
+// pre-scale (x_scale), the weight pre-scale (acc_scale) and the non-finite flag of the range guard.
+#include "conv_x3_impl.hpp"
+
+namespace s2v {
+
+constexpr int kHeadM = 64;    // input columns of a strip (4 MFMA row blocks of 16)
+
+template <int ELT, int CO, int KS, int NCS>
+__global__ __launch_bounds__(256, 1) void conv_head_x3(ConvArgs a, int strips, int th) {
+    constexpr int TW = kHeadM - KS + 1;       // output columns per strip
+    constexpr int NSL = KS * NCS;             // K-slices: (ky, 32-channel slice)
+    constexpr int SLB = kHeadM * 128;         // bytes of one 32-channel slice of a staged row
+    constexpr int ROWB = NCS * SLB;           // bytes of one staged input row
+    constexpr int PLD = 33;                   // P row pitch (floats)
+    static_assert(CO * KS <= 32, "N = Cout * KS must fit two 16-column blocks");
+    __shared__ __attribute__((aligned(16))) char ring[KS * ROWB];
+    __shared__ float P[kHeadM * PLD];
+
+    launch_stamp(a, false);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int mb = tid >> 6;                  // the wave's 16-row block of the strip
+    int b = blockIdx.x;
+    const int strip = b % strips;
+    b /= strips;
+    const int bands = (a.oh + th - 1) / th;
+    const int band = b % bands, img = b / bands;
+    const int ox0 = strip * TW, oy0 = band * th;
+    const int oy1 = min(oy0 + th, a.oh);
+    const int base = oy0 - a.ph;              // input row of ring row 0
+    const bool refl = a.pad_mode == S2V_PAD_REFLECT;
+    const float *__restrict__ xb = a.x + (long long)img * a.h * a.w * a.xcs;
+
+    // ---- filter fragments: B[n][k], n = o * KS + kx (rows past CO * KS are zero), K-slice s = ky * NCS + cs
+    // holds W[o][(ky * KS + kx) * cin + 32 cs + k] = packed split row o, 32-k group (ky * KS + kx) * NCS + cs
+    const char *__restrict__ wtb = (const char *)a.wt;
+    u32x4 bh[NSL][2], bl[NSL][2];
+#pragma unroll
+    for (int s = 0; s < NSL; ++s) {
+        const int ky = s / NCS, cs = s - (s / NCS) * NCS;
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+            const int n = nb * 16 + (lane & 15);
+            const int o = n / KS, kx = n - (n / KS) * KS;
+            u32x4 h = {0u, 0u, 0u, 0u}, l = {0u, 0u, 0u, 0u};
+            if (o < CO) {
+                const char *p = wtb + ((long long)o * a.kpad + (long long)((ky * KS + kx) * NCS + cs) * 32) * 4 +
+                                16 * (lane >> 4);
+                h = *(const u32x4 *)p;
+                l = *(const u32x4 *)(p + 64);
+            }
+            bh[s][nb] = h;
+            bl[s][nb] = l;
+        }
+    }
+
+    // ---- input rows: thread t stages pixel t >> 2, channel octets (t & 3) + 4 j of every 32-channel slice
+    const int sp = tid >> 2, sq = tid & 3;
+    int gx = ox0 - a.pw + sp;
+    if (refl) gx = reflect_idx(gx, a.w);
+    const bool xok = (unsigned)gx < (unsigned)a.w;
+    f4 pre[NCS][2];
+    auto load_row = [&](int r) {              // ring row r = input row base + r
+        int gy = base + r;
+        if (refl) gy = reflect_idx(gy, a.h);
+        const bool ok = xok && (unsigned)gy < (unsigned)a.h;
+        const float *src = xb + ((long long)gy * a.w + gx) * a.xcs + 8 * sq;
+#pragma unroll
+        for (int cs = 0; cs < NCS; ++cs) {
+            f4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = {0.f, 0.f, 0.f, 0.f};
+            if (ok) {
+                v0 = *(const f4 *)(src + 32 * cs);
+                v1 = *(const f4 *)(src + 32 * cs + 4);
+            }
+            pre[cs][0] = v0;
+            pre[cs][1] = v1;
+        }
+    };
+    auto store_row = [&](int r) {
+        char *dst = ring + (r % KS) * ROWB;
+#pragma unroll
+        for (int cs = 0; cs < NCS; ++cs) {
+            f4 v0 = pre[cs][0] * a.x_scale, v1 = pre[cs][1] * a.x_scale;
+            u32x2 h0, l0, h1, l1;
+            split4<ELT>(v0, h0, l0);
+            split4<ELT>(v1, h1, l1);
+            const u32x4 hi = {h0.x, h0.y, h1.x, h1.y}, lo = {l0.x, l0.y, l1.x, l1.y};
+            const int off = cs * SLB + slot_off(sp, sq);
+            *(u32x4 *)(dst + off) = hi;
+            *(u32x4 *)(dst + (off ^ 64)) = lo;
+        }
+    };
+    for (int r = 0; r < KS; ++r) {
+        load_row(r);
+        store_row(r);
+    }
+    __syncthreads();
+
+    const int l16 = lane & 15;
+    const int arow = mb * 16 + l16;
+    const int aoff = slot_off(arow, lane >> 4);   // hi slot; the lo slot is aoff ^ 64 (ring rows are 128-B multiples)
+    bool bad = false;
+    for (int oy = oy0; oy < oy1; ++oy) {
+        const int rr = oy - oy0;              // ring row of ky = 0
+        const bool more = oy + 1 < oy1;
+        if (more) load_row(rr + KS);          // the next output row's new input row, under the MFMAs
+        floatx4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s = 0; s < NSL; ++s) {
+            const int ky = s / NCS, cs = s - (s / NCS) * NCS;
+            const int ro = ((rr + ky) % KS) * ROWB + cs * SLB;
+            const u32x4 ah = *(const u32x4 *)(ring + ro + aoff), al = *(const u32x4 *)(ring + ro + (aoff ^ 64));
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+                acc[nb] = mfma16x16<ELT>(al, bh[s][nb], acc[nb]);
+                acc[nb] = mfma16x16<ELT>(ah, bl[s][nb], acc[nb]);
+                acc[nb] = mfma16x16<ELT>(ah, bh[s][nb], acc[nb]);
+            }
+        }
+        __builtin_amdgcn_s_setprio(0);
+        // C layout: column lane & 15, rows 4 (lane >> 4) + r of the wave's 16-row block
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                P[(mb * 16 + 4 * (lane >> 4) + r) * PLD + nb * 16 + l16] = acc[nb][r] * a.acc_scale;
+        __syncthreads();                      // P complete; ring row rr no longer read
+        for (int i = tid; i < TW * CO; i += 256) {
+            const int q = i / CO, o = i - (i / CO) * CO;
+            const int ox = ox0 + q;
+            if (ox >= a.ow) continue;
+            float v = 0.f;
+#pragma unroll
+            for (int kx = 0; kx < KS; ++kx) v += P[(q + kx) * PLD + o * KS + kx];
+            bad |= !__builtin_isfinite(v);
+            store_epilogue(a, 0, (img * a.oh + oy) * a.ow + ox, o, v);
+        }
+        if (more) store_row(rr + KS);         // into the ring slot of row rr (ky = 0 of this output row)
+        __syncthreads();                      // P reads done; the new ring row visible
+    }
+    if (bad && a.nonfinite) __hip_atomic_store(a.nonfinite, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    launch_stamp(a, true);
+}
+
+template <int ELT, int CO>
+static int launch_head_co(const ConvArgs &a, int ks, int ncs, dim3 grid, int strips, int th, hipStream_t s) {
+    if (ks == 7 && ncs == 2) conv_head_x3<ELT, CO, 7, 2><<<grid, 256, 0, s>>>(a, strips, th);
+    else if (ks == 7 && ncs == 1) conv_head_x3<ELT, CO, 7, 1><<<grid, 256, 0, s>>>(a, strips, th);
+    else if (ks == 5 && ncs == 2) conv_head_x3<ELT, CO, 5, 2><<<grid, 256, 0, s>>>(a, strips, th);
+    else if (ks == 5 && ncs == 1) conv_head_x3<ELT, CO, 5, 1><<<grid, 256, 0, s>>>(a, strips, th);
+    else S2V_REQUIRE(false, "conv_head_x3: no kernel for a %dx%d filter over %d channels", ks, ks, 32 * ncs);
+    return 0;
+}
+
+// host launcher (conv.hip): prec 1 = bf16x3, 2 = f16x3
+int launch_conv_head_x3(const ConvArgs &a, int prec, int co, int ks, int ncs, int th, hipStream_t s) {
+    const int tw = kHeadM - ks + 1;
+    const int strips = (int)cdiv(a.ow, tw);
+    const int bands = (int)cdiv(a.oh, th);
+    const dim3 grid((unsigned)((long long)a.n * bands * strips));
+#define S2V_HEAD(ELT)                                                                         \
+    switch (co) {                                                                             \
+        case 1: return launch_head_co<ELT, 1>(a, ks, ncs, grid, strips, th, s);              \
+        case 2: return launch_head_co<ELT, 2>(a, ks, ncs, grid, strips, th, s);              \
+        case 3: return launch_head_co<ELT, 3>(a, ks, ncs, grid, strips, th, s);              \
+        default: return launch_head_co<ELT, 4>(a, ks, ncs, grid, strips, th, s);             \
+    }
+    if (prec == S2V_PREC_BF16X3) { S2V_HEAD(0) }
+    S2V_HEAD(1)
+#undef S2V_HEAD
+}
+
+}  // namespace s2v

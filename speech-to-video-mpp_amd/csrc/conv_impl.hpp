@@ -448,7 +448,7 @@ __device__ __forceinline__ void epilogue_tile_map(const ConvArgs &a, float *Cs, 
 #pragma unroll 1
             for (int rr = tid / TPR; rr < clim; rr += RSTEP)
                 w[(long long)(cb + rr) * a.cout + n] = Cs[rr * LDC + cn];
-        } else if (simple) {
+        } else if (simple && a.y_step <= 1) {
             float *__restrict__ yb = a.y + (long long)bidx * a.y_bs + out_col(a, n);
             const float *rsrc = e.res ? e.res + (long long)bidx * a.res_bs + n : nullptr;
             int rr0 = tid / TPR;
@@ -499,6 +499,62 @@ __device__ __forceinline__ void epilogue_tile_map(const ConvArgs &a, float *Cs, 
                 if (rsrc && e.res_after) v += rv;
                 yb[out_row(a, m)] = v;
             }
+        } else if (a.y_step > 1 && !e.nc_scale) {
+            // strided (polyphase transposed) / depth-to-space (polyphase x2 StyleConv) output: the output
+            // pixel of each row advances incrementally (one division per chunk instead of out_row's and
+            // pix_index's per element), and the noise plane / residual of four rows is loaded ahead of
+            // their stores
+            const int cls = a.d2s_c > 0 ? n / a.d2s_c : 0;
+            const int oc = a.d2s_c > 0 ? n - cls * a.d2s_c : n;
+            const int dy = cls >> 1, dx = cls & 1, ys = a.y_step;
+            const int hw = a.oh * a.ow;
+            int m = cb + tid / TPR;
+            int img = m / hw, rem = m - img * hw;
+            int oy = rem / a.ow, ox = rem - (rem / a.ow) * a.ow;
+            float *__restrict__ yb = a.y + (long long)bidx * a.y_bs + oc;
+            const float *pix = e.pix_add ? e.pix_add + (long long)bidx * a.y_h * a.y_w * a.n : nullptr;
+            const float *rsrc = e.res ? e.res + (long long)bidx * a.res_bs + oc : nullptr;   // in place (validate)
+            auto pixel = [&]() {
+                const long long q = ((long long)img * a.y_h + oy * ys + dy) * a.y_w + ox * ys + dx;
+                ox += RSTEP;
+                while (ox >= a.ow) {
+                    ox -= a.ow;
+                    if (++oy == a.oh) { oy = 0; ++img; }
+                }
+                return q;
+            };
+            int rr = tid / TPR;
+#pragma unroll 1
+            for (; rr + 3 * RSTEP < clim; rr += 4 * RSTEP) {
+                long long q[4];
+                float pv[4] = {0.f, 0.f, 0.f, 0.f}, rv[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) q[j] = pixel();
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if (pix) pv[j] = pix[q[j]];
+                    if (rsrc) rv[j] = rsrc[q[j] * a.ycs];
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    float v = Cs[(rr + j * RSTEP) * LDC + cn] * sc + sh + e.pix_w * pv[j];
+                    if (!e.res_after) v += rv[j];
+                    v = fast_act(v, e.act, slope);
+                    if (e.res_after) v += rv[j];
+                    yb[q[j] * a.ycs] = v;
+                }
+            }
+#pragma unroll 1
+            for (; rr < clim; rr += RSTEP) {
+                const long long q = pixel();
+                float v = Cs[rr * LDC + cn] * sc + sh;
+                if (pix) v += e.pix_w * pix[q];
+                float rv = rsrc ? rsrc[q * a.ycs] : 0.f;
+                if (!e.res_after) v += rv;
+                v = fast_act(v, e.act, slope);
+                if (e.res_after) v += rv;
+                yb[q * a.ycs] = v;
+            }
         } else if (a.y_step <= 1 && a.d2s_c <= 0 && (!e.res || e.res_simple)) {
             // per-(image, channel) scale and / or per-pixel add on a dense output (GPEN / GFPGAN StyledConv:
             // demod scale + noise): the row's image index advances incrementally instead of a division per
@@ -510,8 +566,30 @@ __device__ __forceinline__ void epilogue_tile_map(const ConvArgs &a, float *Cs, 
             float *__restrict__ yb = a.y + (long long)bidx * a.y_bs + out_col(a, n);
             const float *pix = e.pix_add ? e.pix_add + (long long)bidx * a.oh * a.ow * a.n : nullptr;
             const float *rsrc = e.res ? e.res + (long long)bidx * a.res_bs + n : nullptr;
+            int rr = rr0;
+            if (!e.nc_scale) {
+                // the noise plane (and residual) of four rows loaded ahead of their stores
 #pragma unroll 1
-            for (int rr = rr0; rr < clim; rr += RSTEP, m += RSTEP, rem += RSTEP) {
+                for (; rr + 3 * RSTEP < clim; rr += 4 * RSTEP, m += 4 * RSTEP) {
+                    float pv[4] = {0.f, 0.f, 0.f, 0.f}, rv[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        if (pix) pv[j] = pix[m + j * RSTEP];
+                        if (rsrc) rv[j] = rsrc[(long long)(m + j * RSTEP) * e.res_cs];
+                    }
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        float v = Cs[(rr + j * RSTEP) * LDC + cn] * sc + sh + e.pix_w * pv[j];
+                        if (!e.res_after) v += rv[j];
+                        v = fast_act(v, e.act, slope);
+                        if (e.res_after) v += rv[j];
+                        yb[(long long)(m + j * RSTEP) * a.ycs] = v;
+                    }
+                }
+                rem = m - img * hw;
+            }
+#pragma unroll 1
+            for (; rr < clim; rr += RSTEP, m += RSTEP, rem += RSTEP) {
                 while (rem >= hw) { rem -= hw; ++img; }
                 float v = Cs[rr * LDC + cn] * sc;
                 if (e.nc_scale) v *= e.nc_scale[(long long)img * e.nc_ns + n];

@@ -288,12 +288,21 @@ __device__ __forceinline__ void deform_at(const float *flow, int fh, int fw, int
     gy = (2.f * ((float)fy / (float)(fh - 1)) - 1.f) + 2.f * (f[1] / (float)(fh - 1));
 }
 
+// Blocks walk the pixels XCD-contiguously: block b runs on XCD b % 8, so logical block L is chosen
+// such that each XCD takes one contiguous eighth of the (image, row) range.  The bilinear taps of
+// neighbouring output rows share source lines; with the plain order every XCD's L2 fetched those
+// lines for its own interleaved rows (r05: 4.5-5.9x the algorithmic bytes in FETCH_SIZE).
+// CAT: y[p, 0:c) = src[p] and y[p, c:2c) = the warp (EditingNet's torch.cat([input_image, warp_image], 1), DNet.py:114-115, in
+// one pass: whole 2c-float pixels written, no separate NCHW -> NHWC copy).
+template <bool CAT>
 __global__ __launch_bounds__(256) void flow_warp_kernel(const float *__restrict__ flow, int n, int fh, int fw,
                                                         int fcs, const float *__restrict__ src, int c, int h, int w,
                                                         long long ssn, long long ssc, long long ssy, long long ssx,
                                                         float *__restrict__ y, int ycs) {
     const long long total = (long long)n * h * w;
-    const long long e = blockIdx.x * 256LL + threadIdx.x;
+    const int nb = (int)gridDim.x, per = nb >> 3, rem = nb & 7, xcd = blockIdx.x & 7, idx = blockIdx.x >> 3;
+    const int L = xcd < rem ? xcd * (per + 1) + idx : rem * (per + 1) + (xcd - rem) * per + idx;
+    const long long e = L * 256LL + threadIdx.x;
     if (e >= total) return;
     const int ox = (int)(e % w);
     const int oy = (int)((e / w) % h);
@@ -329,6 +338,10 @@ __global__ __launch_bounds__(256) void flow_warp_kernel(const float *__restrict_
     const bool vse = ix1 >= 0 && ix1 < w && iy1 >= 0 && iy1 < h;
     const float *sb = src + nn * ssn;
     float *yo = y + e * ycs;
+    if (CAT) {
+        for (int cc = 0; cc < c; ++cc) yo[cc] = sb[cc * ssc + oy * ssy + ox * ssx];
+        yo += c;
+    }
     for (int cc = 0; cc < c; ++cc) {
         const float *sc = sb + cc * ssc;
         float acc = 0.f;
@@ -408,54 +421,61 @@ __global__ __launch_bounds__(256) void mel_chunks_kernel(const float *__restrict
 }
 
 // ------------------------------------------------------------------ GPEN ops
-__global__ __launch_bounds__(256) void fused_bias_act_kernel(const float *__restrict__ x, const float *__restrict__ b,
-                                                             const float *__restrict__ ref, float *__restrict__ y,
-                                                             long long size, int c, long long step_b, int act, int grad,
-                                                             float alpha, float scale) {
-    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < size; i += (long long)gridDim.x * 256) {
-        float v = x[i];
-        if (b) v += b[(i / step_b) % c];
-        const float r = ref ? ref[i] : 0.f;
-        float o;
-        switch (act * 10 + grad) {
-            case 30: o = v > 0.f ? v : v * alpha; break;
-            case 31: o = r > 0.f ? v : v * alpha; break;
-            case 12:
-            case 32: o = 0.f; break;
-            default: o = v; break;
-        }
-        y[i] = o * scale;
+// Element type T of the reference's AT_DISPATCH_FLOATING_TYPES_AND_HALF (fused_bias_act_kernel.cu:79,
+// upfirdn2d_kernel.cu:225): float, double, half (_Float16).  Arithmetic runs in OpT: double for
+// double, fp32 for float and half (the half result is rounded once, on the store).
+template <typename T> struct OpT { using type = float; };
+template <> struct OpT<double> { using type = double; };
+template <typename T> struct alignas(4 * sizeof(T)) Vec4 { T v[4]; };
+
+template <typename T, typename A>
+__device__ __forceinline__ A bias_act(A v, A r, int mode, A alpha) {
+    switch (mode) {
+        case 30: return v > A(0) ? v : v * alpha;
+        case 31: return r > A(0) ? v : v * alpha;
+        case 12:
+        case 32: return A(0);
+        default: return v;
     }
 }
 
-// Row form (step_b % 4 == 0, 16-byte aligned; the GPEN call on [N, C, H, W] has step_b = H*W): a
-// block row walks one (n, c) plane with float4 loads / stores, the bias channel fixed per row — no
-// per-element 64-bit index division.
-__global__ __launch_bounds__(256) void fused_bias_act_rows(const float *__restrict__ x, const float *__restrict__ b,
-                                                           const float *__restrict__ ref, float *__restrict__ y,
+template <typename T>
+__global__ __launch_bounds__(256) void fused_bias_act_kernel(const T *__restrict__ x, const T *__restrict__ b,
+                                                             const T *__restrict__ ref, T *__restrict__ y,
+                                                             long long size, int c, long long step_b, int act, int grad,
+                                                             typename OpT<T>::type alpha, typename OpT<T>::type scale) {
+    using A = typename OpT<T>::type;
+    const int mode = act * 10 + grad;
+    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < size; i += (long long)gridDim.x * 256) {
+        A v = (A)x[i];
+        if (b) v += (A)b[(i / step_b) % c];
+        const A r = ref ? (A)ref[i] : A(0);
+        y[i] = (T)(bias_act<T, A>(v, r, mode, alpha) * scale);
+    }
+}
+
+// Row form (step_b % 4 == 0, 4-element aligned; the GPEN call on [N, C, H, W] has step_b = H*W): a
+// block row walks one (n, c) plane with 4-element vector loads / stores (16 B for float, 8 B for
+// half, 32 B for double), the bias channel fixed per row — no per-element 64-bit index division.
+template <typename T>
+__global__ __launch_bounds__(256) void fused_bias_act_rows(const T *__restrict__ x, const T *__restrict__ b,
+                                                           const T *__restrict__ ref, T *__restrict__ y,
                                                            long long rows, int c, long long step4, int act, int grad,
-                                                           float alpha, float scale) {
+                                                           typename OpT<T>::type alpha, typename OpT<T>::type scale) {
+    using A = typename OpT<T>::type;
+    const int mode = act * 10 + grad;
     for (long long r = blockIdx.y; r < rows; r += gridDim.y) {
-        const float bv = b ? b[r % c] : 0.f;
-        const float4 *xr = (const float4 *)x + r * step4;
-        const float4 *rr = ref ? (const float4 *)ref + r * step4 : nullptr;
-        float4 *yr = (float4 *)y + r * step4;
+        const A bv = b ? (A)b[r % c] : A(0);
+        const Vec4<T> *xr = (const Vec4<T> *)x + r * step4;
+        const Vec4<T> *rr = ref ? (const Vec4<T> *)ref + r * step4 : nullptr;
+        Vec4<T> *yr = (Vec4<T> *)y + r * step4;
         for (long long i = blockIdx.x * 256LL + threadIdx.x; i < step4; i += (long long)gridDim.x * 256) {
-            float4 v = xr[i];
-            v.x += bv; v.y += bv; v.z += bv; v.w += bv;
-            float4 o = v;
-            const int mode = act * 10 + grad;
-            if (mode == 30) {
-                o.x = v.x > 0.f ? v.x : v.x * alpha; o.y = v.y > 0.f ? v.y : v.y * alpha;
-                o.z = v.z > 0.f ? v.z : v.z * alpha; o.w = v.w > 0.f ? v.w : v.w * alpha;
-            } else if (mode == 31) {
-                const float4 q = rr[i];
-                o.x = q.x > 0.f ? v.x : v.x * alpha; o.y = q.y > 0.f ? v.y : v.y * alpha;
-                o.z = q.z > 0.f ? v.z : v.z * alpha; o.w = q.w > 0.f ? v.w : v.w * alpha;
-            } else if (mode == 12 || mode == 32) {
-                o = make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-            o.x *= scale; o.y *= scale; o.z *= scale; o.w *= scale;
+            const Vec4<T> v = xr[i];
+            Vec4<T> q{};
+            if (mode == 31) q = rr[i];
+            Vec4<T> o;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o.v[j] = (T)(bias_act<T, A>((A)v.v[j] + bv, (A)q.v[j], mode, alpha) * scale);
             yr[i] = o;
         }
     }
@@ -464,11 +484,12 @@ __global__ __launch_bounds__(256) void fused_bias_act_rows(const float *__restri
 // out = down( FIR( zero-pad( zero-insert-up(x) ), flip(k) ) ) per plane, [major][H][W][minor].
 // UP / DN / KS > 0 fix the factors and the square filter at compile time (the GPEN Upsample /
 // Downsample / Blur forms with the 4x4 kernel): shifts instead of divisions, unrolled taps.
-template <int UP = 0, int DN = 0, int KS = 0>
-__global__ __launch_bounds__(256) void upfirdn2d_kernel(const float *__restrict__ x, int major, int ih, int iw,
-                                                        int minor, const float *__restrict__ k, int kh_, int kw_,
+template <typename T, int UP = 0, int DN = 0, int KS = 0>
+__global__ __launch_bounds__(256) void upfirdn2d_kernel(const T *__restrict__ x, int major, int ih, int iw,
+                                                        int minor, const T *__restrict__ k, int kh_, int kw_,
                                                         int upx_, int upy_, int dnx_, int dny_, int px0, int py0,
-                                                        float *__restrict__ y, int oh, int ow) {
+                                                        T *__restrict__ y, int oh, int ow) {
+    using A = typename OpT<T>::type;
     const int upx = UP ? UP : upx_, upy = UP ? UP : upy_, dnx = DN ? DN : dnx_, dny = DN ? DN : dny_;
     const int kh = KS ? KS : kh_, kw = KS ? KS : kw_;
     const long long total = (long long)major * oh * ow * minor;
@@ -479,8 +500,8 @@ __global__ __launch_bounds__(256) void upfirdn2d_kernel(const float *__restrict_
         t /= ow;
         const int oy = (int)(t % oh);
         const int mj = (int)(t / oh);
-        const float *xb = x + (long long)mj * ih * iw * minor + mi;
-        float acc = 0.f;
+        const T *xb = x + (long long)mj * ih * iw * minor + mi;
+        A acc = A(0);
 #pragma unroll
         for (int i = 0; i < (KS ? KS : 1); ++i) {
             for (int ii = 0; ii < (KS ? 1 : kh); ++ii) {
@@ -497,29 +518,30 @@ __global__ __launch_bounds__(256) void upfirdn2d_kernel(const float *__restrict_
                         if (ux < 0 || ux % upx) continue;
                         const int ix = ux / upx;
                         if (ix >= iw) continue;
-                        acc = fmaf(xb[((long long)iy * iw + ix) * minor], k[(kh - 1 - ti) * kw + (kw - 1 - tj)], acc);
+                        acc = fma((A)xb[((long long)iy * iw + ix) * minor], (A)k[(kh - 1 - ti) * kw + (kw - 1 - tj)], acc);
                     }
                 }
             }
         }
-        y[e] = acc;
+        y[e] = (T)acc;
     }
 }
 
 // Plane form (minor == 1, the NCHW tensors GPEN passes as [N*C, H, W, 1]) with the 4x4 filter:
 // a block owns a 16 x 64 output tile of one plane, stages the input rows it touches in LDS with
 // coalesced row loads (zeros outside the image), and each thread computes 4 adjacent outputs.
-template <int UP, int DN>
-__global__ __launch_bounds__(256) void upfirdn2d_plane4(const float *__restrict__ x, int ih, int iw,
-                                                        const float *__restrict__ k, int px0, int py0,
-                                                        float *__restrict__ y, int oh, int ow, int tiles_x,
+template <typename T, int UP, int DN>
+__global__ __launch_bounds__(256) void upfirdn2d_plane4(const T *__restrict__ x, int ih, int iw,
+                                                        const T *__restrict__ k, int px0, int py0,
+                                                        T *__restrict__ y, int oh, int ow, int tiles_x,
                                                         int tiles_y) {
+    using A = typename OpT<T>::type;
     constexpr int TY = 16, TX = 64;
     // input rows / cols a tile touches: zero-inserted coordinates u = o*DN + t - p, t in [0, 4)
     constexpr int RH = ((TY - 1) * DN + 3) / UP + 2, RW = ((TX - 1) * DN + 3) / UP + 2;
-    __shared__ float tile[RH][RW + 1];
-    __shared__ float ks[16];
-    if (threadIdx.x < 16) ks[threadIdx.x] = k[15 - threadIdx.x];          // flipped
+    __shared__ A tile[RH][RW + 1];
+    __shared__ A ks[16];
+    if (threadIdx.x < 16) ks[threadIdx.x] = (A)k[15 - threadIdx.x];          // flipped
     int t = blockIdx.x;
     const int txi = t % tiles_x;
     t /= tiles_x;
@@ -530,17 +552,17 @@ __global__ __launch_bounds__(256) void upfirdn2d_plane4(const float *__restrict_
     const int uy0 = oy0 * DN - py0, ux0 = ox0 * DN - px0;
     const int iy0 = uy0 >= 0 ? uy0 / UP : -((-uy0 + UP - 1) / UP);
     const int ix0 = ux0 >= 0 ? ux0 / UP : -((-ux0 + UP - 1) / UP);
-    const float *xp = x + plane * ih * iw;
+    const T *xp = x + plane * ih * iw;
     for (int e = threadIdx.x; e < RH * RW; e += 256) {
         const int r = e / RW, cidx = e - r * RW;
         const int gy = iy0 + r, gx = ix0 + cidx;
-        tile[r][cidx] = ((unsigned)gy < (unsigned)ih && (unsigned)gx < (unsigned)iw) ? xp[(long long)gy * iw + gx] : 0.f;
+        tile[r][cidx] = ((unsigned)gy < (unsigned)ih && (unsigned)gx < (unsigned)iw) ? (A)xp[(long long)gy * iw + gx] : A(0);
     }
     __syncthreads();
     const int ry = threadIdx.x >> 4, rx = (threadIdx.x & 15) * 4;
     const int oy = oy0 + ry;
     if (oy >= oh) return;
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    A acc[4] = {A(0), A(0), A(0), A(0)};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int uy = oy * DN + i - py0;
@@ -553,14 +575,14 @@ __global__ __launch_bounds__(256) void upfirdn2d_plane4(const float *__restrict_
                 const int ux = (ox0 + rx + p) * DN + j - px0;
                 if (UP > 1 && (ux % UP + UP) % UP) continue;
                 const int lx = (ux >= 0 ? ux / UP : -((-ux + UP - 1) / UP)) - ix0;
-                acc[p] = fmaf(tile[ly][lx], ks[i * 4 + j], acc[p]);
+                acc[p] = fma(tile[ly][lx], ks[i * 4 + j], acc[p]);
             }
         }
     }
-    float *yp = y + plane * oh * ow + (long long)oy * ow;
+    T *yp = y + plane * oh * ow + (long long)oy * ow;
 #pragma unroll
     for (int p = 0; p < 4; ++p)
-        if (ox0 + rx + p < ow) yp[ox0 + rx + p] = acc[p];
+        if (ox0 + rx + p < ow) yp[ox0 + rx + p] = (T)acc[p];
 }
 
 // ------------------------------------------------------------------ noise
@@ -833,9 +855,20 @@ extern "C" int s2v_flow_warp(const float *flow, int n, int fh, int fw, int flow_
                              s2v_stream_t stream) {
     S2V_REQUIRE(flow && src && y && n > 0 && fh > 1 && fw > 1 && c > 0 && h > 0 && w > 0 && flow_cs >= 2 && ycs >= c,
                 "flow_warp: bad args");
-    flow_warp_kernel<<<cdiv((long long)n * h * w, 256), 256, 0, (hipStream_t)stream>>>(
+    flow_warp_kernel<false><<<cdiv((long long)n * h * w, 256), 256, 0, (hipStream_t)stream>>>(
         flow, n, fh, fw, flow_cs, src, c, h, w, ssn, ssc, ssy, ssx, y, ycs);
     return check_launch("flow_warp");
+}
+
+extern "C" int s2v_flow_warp_cat(const float *flow, int n, int fh, int fw, int flow_cs, const float *src, int c, int h,
+                                 int w, long long ssn, long long ssc, long long ssy, long long ssx, float *y, int ycs,
+                                 s2v_stream_t stream) {
+    S2V_REQUIRE(flow && src && y && n > 0 && fh > 1 && fw > 1 && c > 0 && h > 0 && w > 0 && flow_cs >= 2 &&
+                    ycs >= 2 * c,
+                "flow_warp_cat: bad args");
+    flow_warp_kernel<true><<<cdiv((long long)n * h * w, 256), 256, 0, (hipStream_t)stream>>>(
+        flow, n, fh, fw, flow_cs, src, c, h, w, ssn, ssc, ssy, ssx, y, ycs);
+    return check_launch("flow_warp_cat");
 }
 
 extern "C" int s2v_melspectrogram(const float *wav, long long n_samples, const float *tables, int pad_reflect,
@@ -856,30 +889,33 @@ extern "C" int s2v_mel_chunks(const float *mel, long long frames, const int *sta
     return check_launch("mel_chunks");
 }
 
-extern "C" int s2v_fused_bias_act(const float *x, const float *b, const float *ref, float *y, long long size, int c,
-                                  long long step_b, int act, int grad, float alpha, float scale,
-                                  s2v_stream_t stream) {
+template <typename T>
+static int fused_bias_act_t(const T *x, const T *b, const T *ref, T *y, long long size, int c, long long step_b, int act,
+                            int grad, double alpha, double scale, s2v_stream_t stream) {
+    using A = typename OpT<T>::type;
     S2V_REQUIRE(x && y && size >= 0, "fused_bias_act: bad args");
     S2V_REQUIRE(!b || (c > 0 && step_b > 0), "fused_bias_act: bias needs c > 0 and step_b > 0");
     if (size == 0) return 0;
-    const bool rows_ok = step_b % 4 == 0 && size % step_b == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0 &&
-                         (!ref || ((uintptr_t)ref & 15) == 0);
+    const uintptr_t al = 4 * sizeof(T) - 1;
+    const bool rows_ok = step_b > 0 && step_b % 4 == 0 && size % step_b == 0 && ((uintptr_t)x & al) == 0 &&
+                         ((uintptr_t)y & al) == 0 && (!ref || ((uintptr_t)ref & al) == 0);
     if (rows_ok) {
         const long long rows = size / step_b, step4 = step_b / 4;
         const unsigned gx = (unsigned)((step4 + 255) / 256 < 64 ? (step4 + 255) / 256 : 64);
         const unsigned gy = (unsigned)(rows < 65535 ? rows : 65535);
-        fused_bias_act_rows<<<dim3(gx, gy), 256, 0, (hipStream_t)stream>>>(x, b, ref, y, rows, b ? c : 1, step4, act,
-                                                                           grad, alpha, scale);
+        fused_bias_act_rows<T><<<dim3(gx, gy), 256, 0, (hipStream_t)stream>>>(x, b, ref, y, rows, b ? c : 1, step4, act,
+                                                                              grad, (A)alpha, (A)scale);
     } else {
-        fused_bias_act_kernel<<<grid_for(size), 256, 0, (hipStream_t)stream>>>(x, b, ref, y, size, c, step_b, act, grad,
-                                                                                 alpha, scale);
+        fused_bias_act_kernel<T><<<grid_for(size), 256, 0, (hipStream_t)stream>>>(x, b, ref, y, size, c, step_b, act,
+                                                                                    grad, (A)alpha, (A)scale);
     }
     return check_launch("fused_bias_act");
 }
 
-extern "C" int s2v_upfirdn2d(const float *x, int major, int in_h, int in_w, int minor, const float *k, int kh, int kw,
-                             int up_x, int up_y, int down_x, int down_y, int pad_x0, int pad_x1, int pad_y0,
-                             int pad_y1, float *y, int out_h, int out_w, s2v_stream_t stream) {
+template <typename T>
+static int upfirdn2d_t(const T *x, int major, int in_h, int in_w, int minor, const T *k, int kh, int kw, int up_x,
+                       int up_y, int down_x, int down_y, int pad_x0, int pad_x1, int pad_y0, int pad_y1, T *y, int out_h,
+                       int out_w, s2v_stream_t stream) {
     S2V_REQUIRE(x && k && y && major > 0 && in_h > 0 && in_w > 0 && minor > 0 && kh > 0 && kw > 0,
                 "upfirdn2d: bad args");
     S2V_REQUIRE(up_x >= 1 && up_y >= 1 && down_x >= 1 && down_y >= 1, "upfirdn2d: up/down must be >= 1");
@@ -894,15 +930,61 @@ extern "C" int s2v_upfirdn2d(const float *x, int major, int in_h, int in_w, int 
     if (k4 && minor == 1 && pad_x0 >= 0 && pad_y0 >= 0 && ((up_x == 1 && down_x <= 2) || (up_x == 2 && down_x == 1))) {
         const int tx = (out_w + 63) / 64, ty = (out_h + 15) / 16;
         const unsigned gp = (unsigned)((long long)major * tx * ty);
-        if (up_x == 2) upfirdn2d_plane4<2, 1><<<gp, 256, 0, st>>>(x, in_h, in_w, k, pad_x0, pad_y0, y, out_h, out_w, tx, ty);
-        else if (down_x == 2) upfirdn2d_plane4<1, 2><<<gp, 256, 0, st>>>(x, in_h, in_w, k, pad_x0, pad_y0, y, out_h, out_w, tx, ty);
-        else upfirdn2d_plane4<1, 1><<<gp, 256, 0, st>>>(x, in_h, in_w, k, pad_x0, pad_y0, y, out_h, out_w, tx, ty);
-    } else if (k4 && up_x == 1 && down_x == 1) upfirdn2d_kernel<1, 1, 4><<<g, 256, 0, st>>>(S2V_UFD_ARGS);
-    else if (k4 && up_x == 2 && down_x == 1) upfirdn2d_kernel<2, 1, 4><<<g, 256, 0, st>>>(S2V_UFD_ARGS);
-    else if (k4 && up_x == 1 && down_x == 2) upfirdn2d_kernel<1, 2, 4><<<g, 256, 0, st>>>(S2V_UFD_ARGS);
-    else upfirdn2d_kernel<><<<g, 256, 0, st>>>(S2V_UFD_ARGS);
+        if (up_x == 2) upfirdn2d_plane4<T, 2, 1><<<gp, 256, 0, st>>>(x, in_h, in_w, k, pad_x0, pad_y0, y, out_h, out_w, tx, ty);
+        else if (down_x == 2) upfirdn2d_plane4<T, 1, 2><<<gp, 256, 0, st>>>(x, in_h, in_w, k, pad_x0, pad_y0, y, out_h, out_w, tx, ty);
+        else upfirdn2d_plane4<T, 1, 1><<<gp, 256, 0, st>>>(x, in_h, in_w, k, pad_x0, pad_y0, y, out_h, out_w, tx, ty);
+    } else if (k4 && up_x == 1 && down_x == 1) upfirdn2d_kernel<T, 1, 1, 4><<<g, 256, 0, st>>>(S2V_UFD_ARGS);
+    else if (k4 && up_x == 2 && down_x == 1) upfirdn2d_kernel<T, 2, 1, 4><<<g, 256, 0, st>>>(S2V_UFD_ARGS);
+    else if (k4 && up_x == 1 && down_x == 2) upfirdn2d_kernel<T, 1, 2, 4><<<g, 256, 0, st>>>(S2V_UFD_ARGS);
+    else upfirdn2d_kernel<T><<<g, 256, 0, st>>>(S2V_UFD_ARGS);
 #undef S2V_UFD_ARGS
     return check_launch("upfirdn2d");
+}
+
+extern "C" int s2v_fused_bias_act(const float *x, const float *b, const float *ref, float *y, long long size, int c,
+                                  long long step_b, int act, int grad, float alpha, float scale,
+                                  s2v_stream_t stream) {
+    return fused_bias_act_t<float>(x, b, ref, y, size, c, step_b, act, grad, alpha, scale, stream);
+}
+
+extern "C" int s2v_upfirdn2d(const float *x, int major, int in_h, int in_w, int minor, const float *k, int kh, int kw,
+                             int up_x, int up_y, int down_x, int down_y, int pad_x0, int pad_x1, int pad_y0,
+                             int pad_y1, float *y, int out_h, int out_w, s2v_stream_t stream) {
+    return upfirdn2d_t<float>(x, major, in_h, in_w, minor, k, kh, kw, up_x, up_y, down_x, down_y, pad_x0, pad_x1,
+                              pad_y0, pad_y1, y, out_h, out_w, stream);
+}
+
+extern "C" int s2v_fused_bias_act_dt(int dtype, const void *x, const void *b, const void *ref, void *y, long long size,
+                                     int c, long long step_b, int act, int grad, double alpha, double scale,
+                                     s2v_stream_t stream) {
+    switch (dtype) {
+        case S2V_DT_F32:
+            return fused_bias_act_t<float>((const float *)x, (const float *)b, (const float *)ref, (float *)y, size, c,
+                                           step_b, act, grad, alpha, scale, stream);
+        case S2V_DT_F16:
+            return fused_bias_act_t<_Float16>((const _Float16 *)x, (const _Float16 *)b, (const _Float16 *)ref,
+                                              (_Float16 *)y, size, c, step_b, act, grad, alpha, scale, stream);
+        case S2V_DT_F64:
+            return fused_bias_act_t<double>((const double *)x, (const double *)b, (const double *)ref, (double *)y, size,
+                                            c, step_b, act, grad, alpha, scale, stream);
+    }
+    S2V_REQUIRE(false, "fused_bias_act: dtype %d is not one of S2V_DT_F32 / F16 / F64", dtype);
+    return S2V_E_INVALID;
+}
+
+extern "C" int s2v_upfirdn2d_dt(int dtype, const void *x, int major, int in_h, int in_w, int minor, const void *k,
+                                int kh, int kw, int up_x, int up_y, int down_x, int down_y, int pad_x0, int pad_x1,
+                                int pad_y0, int pad_y1, void *y, int out_h, int out_w, s2v_stream_t stream) {
+#define S2V_UFD_DT(T) upfirdn2d_t<T>((const T *)x, major, in_h, in_w, minor, (const T *)k, kh, kw, up_x, up_y, down_x, \
+                                     down_y, pad_x0, pad_x1, pad_y0, pad_y1, (T *)y, out_h, out_w, stream)
+    switch (dtype) {
+        case S2V_DT_F32: return S2V_UFD_DT(float);
+        case S2V_DT_F16: return S2V_UFD_DT(_Float16);
+        case S2V_DT_F64: return S2V_UFD_DT(double);
+    }
+#undef S2V_UFD_DT
+    S2V_REQUIRE(false, "upfirdn2d: dtype %d is not one of S2V_DT_F32 / F16 / F64", dtype);
+    return S2V_E_INVALID;
 }
 
 extern "C" int s2v_gaussian_noise(float *y, long long n, unsigned long long seed, unsigned long long offset,

@@ -727,6 +727,21 @@ void flow_warp_(const Tensor &flow, const Tensor &src, const Tensor &y) {
           "s2v_flow_warp");
 }
 
+// y NHWC view [N, H, W, 2C] <- [src | warp(src)] (s2v_flow_warp_cat)
+void flow_warp_cat_(const Tensor &flow, const Tensor &src, const Tensor &y) {
+    const c10::DeviceGuard guard(flow.device());
+    const at::Device dev = flow.device();
+    const NV fv = nhwc(flow, dev, "flow_warp_cat flow"), yv = nhwc(y, dev, "flow_warp_cat y");
+    f32(src, dev, "flow_warp_cat src");
+    TORCH_CHECK(src.dim() == 4 && src.size(0) == fv.n && fv.c >= 2, "flow_warp_cat: src [N, C, H, W], flow >= 2 channels");
+    TORCH_CHECK(yv.n == fv.n && yv.h == src.size(2) && yv.w == src.size(3) && yv.c == 2 * src.size(1),
+                "flow_warp_cat: y [N, H, W, 2C]");
+    check(s2v_flow_warp_cat(fv.p, fv.n, fv.h, fv.w, fv.cs, src.data_ptr<float>(), (int)src.size(1), (int)src.size(2),
+                            (int)src.size(3), src.stride(0), src.stride(1), src.stride(2), src.stride(3), yv.p, yv.cs,
+                            stream()),
+          "s2v_flow_warp_cat");
+}
+
 void fill_value_(const Tensor &y, double value) {
     const c10::DeviceGuard guard(y.device());
     f32(y, y.device(), "fill y");
@@ -1042,6 +1057,7 @@ TORCH_LIBRARY_FRAGMENT(s2v, m) {
     m.def("row_pack_(Tensor x, Tensor(a!) y, int kw, int pw) -> ()");
     m.def("torgb_up2_(Tensor x, Tensor wt, Tensor s, Tensor? bias, Tensor skip, Tensor(a!) y) -> ()");
     m.def("flow_warp_(Tensor flow, Tensor src, Tensor(a!) y) -> ()");
+    m.def("flow_warp_cat_(Tensor flow, Tensor src, Tensor(a!) y) -> ()");
     m.def("fill_value_(Tensor(a!) y, float value) -> ()");
     m.def("gaussian_noise_(Tensor(a!) y, int seed, int offset, Tensor? ctr, int shift) -> ()");
     m.def("counter_add_(Tensor(a!) ctr, int inc) -> ()");
@@ -1082,6 +1098,7 @@ TORCH_LIBRARY_IMPL(s2v, CUDA, m) {
     m.impl("row_pack_", &row_pack_);
     m.impl("torgb_up2_", &torgb_up2_);
     m.impl("flow_warp_", &flow_warp_);
+    m.impl("flow_warp_cat_", &flow_warp_cat_);
     m.impl("fill_value_", &fill_value_);
     m.impl("gaussian_noise_", &gaussian_noise_);
     m.impl("counter_add_", &counter_add_);

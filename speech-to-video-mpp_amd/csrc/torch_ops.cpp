@@ -34,13 +34,37 @@ void need_f32_dev(const at::Tensor &t, const char *name) {
 const float *fptr(const c10::optional<at::Tensor> &t) { return t && t->defined() ? t->data_ptr<float>() : nullptr; }
 
 // ---------------------------------------------------------------- GPEN native-op signatures
+// float32, float16 and float64, as the reference dispatches (AT_DISPATCH_FLOATING_TYPES_AND_HALF,
+// fused_bias_act_kernel.cu:79, upfirdn2d_kernel.cu:225); every tensor argument in the input's dtype
+// (the reference reads them with data_ptr<scalar_t>()).  Other dtypes raise.
+int dt_code(const at::Tensor &t, const char *name) {
+    TORCH_CHECK(t.is_cuda(), name, ": expected a HIP device tensor (the s2v ops have no CPU kernel)");
+    switch (t.scalar_type()) {
+        case at::kFloat: return S2V_DT_F32;
+        case at::kHalf: return S2V_DT_F16;
+        case at::kDouble: return S2V_DT_F64;
+        default: TORCH_CHECK(false, name, ": expected float32, float16 or float64, got ", t.scalar_type());
+    }
+    return -1;
+}
+
+void same_dtype(const at::Tensor &t, const at::Tensor &like, const char *name) {
+    TORCH_CHECK(t.is_cuda(), name, ": expected a HIP device tensor");
+    TORCH_CHECK(t.scalar_type() == like.scalar_type(), name, ": expected ", like.scalar_type(), " like the input, got ",
+                t.scalar_type());
+}
+
 at::Tensor fused_bias_act(const at::Tensor &input, const at::Tensor &bias, const at::Tensor &refer, int64_t act,
                           int64_t grad, double alpha, double scale) {
-    need_f32_dev(input, "fused_bias_act input");
-    need_f32_dev(bias, "fused_bias_act bias");
+    const int dt = dt_code(input, "fused_bias_act input");
     const at::Tensor x = input.contiguous();
-    const at::Tensor b = bias.contiguous();
+    const at::Tensor b = bias.numel() ? bias.contiguous() : bias;
     const at::Tensor r = refer.numel() ? refer.contiguous() : refer;
+    if (b.numel()) same_dtype(b, x, "fused_bias_act bias");
+    if (r.numel()) {
+        same_dtype(r, x, "fused_bias_act refer");
+        TORCH_CHECK(r.numel() == x.numel(), "fused_bias_act: refer has ", r.numel(), " elements, input ", x.numel());
+    }
     auto y = at::empty_like(x);
     int c = 1;
     int64_t step_b = 1;
@@ -48,18 +72,16 @@ at::Tensor fused_bias_act(const at::Tensor &input, const at::Tensor &bias, const
     for (int64_t i = 2; i < x.dim(); ++i) step_b *= x.size(i);
     TORCH_CHECK(b.numel() == 0 || b.numel() == c, "fused_bias_act: bias has ", b.numel(), " entries, input ", c,
                 " channels");
-    if (r.numel()) need_f32_dev(r, "fused_bias_act refer");
-    check(s2v_fused_bias_act(x.data_ptr<float>(), b.numel() ? b.data_ptr<float>() : nullptr,
-                             r.numel() ? r.data_ptr<float>() : nullptr, y.data_ptr<float>(), x.numel(), c, step_b,
-                             (int)act, (int)grad, (float)alpha, (float)scale, stream()),
+    check(s2v_fused_bias_act_dt(dt, x.data_ptr(), b.numel() ? b.data_ptr() : nullptr, r.numel() ? r.data_ptr() : nullptr,
+                                y.data_ptr(), x.numel(), c, step_b, (int)act, (int)grad, alpha, scale, stream()),
           "s2v_fused_bias_act");
     return y;
 }
 
 at::Tensor upfirdn2d(const at::Tensor &input, const at::Tensor &kernel, int64_t up_x, int64_t up_y, int64_t down_x,
                      int64_t down_y, int64_t pad_x0, int64_t pad_x1, int64_t pad_y0, int64_t pad_y1) {
-    need_f32_dev(input, "upfirdn2d input");
-    need_f32_dev(kernel, "upfirdn2d kernel");
+    const int dt = dt_code(input, "upfirdn2d input");
+    same_dtype(kernel, input, "upfirdn2d kernel");
     TORCH_CHECK(input.dim() == 4 && kernel.dim() == 2, "upfirdn2d: input [major, H, W, minor], kernel [kh, kw]");
     const at::Tensor x = input.contiguous(), k = kernel.contiguous();
     const int64_t major = x.size(0), in_h = x.size(1), in_w = x.size(2), minor = x.size(3);
@@ -68,9 +90,9 @@ at::Tensor upfirdn2d(const at::Tensor &input, const at::Tensor &kernel, int64_t 
     const int64_t out_w = (in_w * up_x + pad_x0 + pad_x1 - kw) / down_x + 1;
     TORCH_CHECK(out_h > 0 && out_w > 0, "upfirdn2d: empty output");
     auto y = at::empty({major, out_h, out_w, minor}, x.options());
-    check(s2v_upfirdn2d(x.data_ptr<float>(), (int)major, (int)in_h, (int)in_w, (int)minor, k.data_ptr<float>(), (int)kh,
-                        (int)kw, (int)up_x, (int)up_y, (int)down_x, (int)down_y, (int)pad_x0, (int)pad_x1, (int)pad_y0,
-                        (int)pad_y1, y.data_ptr<float>(), (int)out_h, (int)out_w, stream()),
+    check(s2v_upfirdn2d_dt(dt, x.data_ptr(), (int)major, (int)in_h, (int)in_w, (int)minor, k.data_ptr(), (int)kh, (int)kw,
+                           (int)up_x, (int)up_y, (int)down_x, (int)down_y, (int)pad_x0, (int)pad_x1, (int)pad_y0,
+                           (int)pad_y1, y.data_ptr(), (int)out_h, (int)out_w, stream()),
           "s2v_upfirdn2d");
     return y;
 }

@@ -140,8 +140,7 @@ class DNetEngine:
         ops.layernorm2d(ctx, hg, *self.flow_ln, t, act=ops.ACT_LRELU, alpha=LRELU)
         flow = self._conv(ctx, t, self.flow_conv)        # [B, H/4, W/4, 2]
         x6 = NHWC.empty(b, H, W, 6, dev)
-        ops.nchw_to_nhwc(ctx, img, x6.slice(0, 3))
-        ops.flow_warp(ctx, flow, img, x6.slice(3, 3))
+        ops.flow_warp_cat(ctx, flow, img, x6)            # [img | warp(img)] (DNet.py:89, :114-115)
         result = {"flow_field": torch.empty((b, 2, flow.h, flow.w), device=dev),
                   "warp_image": torch.empty((b, 3, H, W), device=dev)}
         ops.nhwc_to_nchw(ctx, flow, result["flow_field"])

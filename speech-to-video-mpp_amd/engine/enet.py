@@ -130,6 +130,7 @@ class ENetEngine:
         self.mod_offs = offs
         self._demod = {}
         self.noise_seed = 0x5EED
+        self.last_noises = [None] * 4
 
     def _side(self, ctx):
         """(stream, Ctx) of the calling lane for the style encoder branch (CUDA devices only)."""
@@ -173,6 +174,7 @@ class ENetEngine:
             else:
                 noise = torch.empty((b, h2, w2), device=dev)
                 ops.gaussian_noise(ctx, noise, self.noise_seed, idx << 36, ctr=ctr, shift=40)
+                self.last_noises[idx] = noise
         y = NHWC.empty(b, h2, w2, L.cout, dev)
         kw = dict(act=ops.ACT_LRELU, alpha=LRELU, pix_w=L.noise_w or 0.0)
         ops.modulated_conv2d(ctx, cur, L.conv4, y, s, d4, pix_add=noise, d2s=True, **kw)
@@ -252,6 +254,10 @@ class ENetEngine:
         ops.pad_reflect(ctx, lo, cur, (2, 2, 2, 2))
         skip = cur               # RGB + a finite pad channel: the x2 skip upsample takes the float4 path
         ctr = None
+        # the noise planes drawn by this forward ([B, H, W] per StyleConv, None where the layer has no
+        # noise or the caller passed it): kept referenced so that under a captured graph they stay
+        # the buffers every replay draws into (tests compare a replay against the oracle with them)
+        self.last_noises = [None] * 4
         if noises is None and any(L.noise_w for L in self.layers):
             ctr = ctx.noise(id(self)).bump(ctx)        # one draw per forward, also under graph replay
         for st in range(2):
@@ -276,6 +282,7 @@ class ENetEngine:
                     else:
                         noise = torch.empty((b, x.h, x.w), device=dev)
                         ops.gaussian_noise(ctx, noise, self.noise_seed, (2 * st + li) << 36, ctr=ctr, shift=40)
+                        self.last_noises[2 * st + li] = noise
                 ops.modulated_conv2d(ctx, x, L.conv, y, s2[:, off: off + L.cin], d, act=ops.ACT_LRELU, alpha=LRELU,
                                      pix_add=noise, pix_w=L.noise_w or 0.0)
                 cur = y

@@ -885,6 +885,8 @@ def plan_symbol(plan) -> str:
             if bkn >= 2000:
                 return f"void s2v::conv_smallk4<{-wm}, {bkn - 2000}>(s2v::ConvArgs, int, int, int, int)"
             return f"void s2v::conv_smallk<{-wm}, {avec}>(s2v::ConvArgs, int, int, int, int)"
+        if bkn >= 3000:
+            return f"void s2v::conv_head_x3<{x3 - 1}, {bn}, {bkn - 3000}, {wm}>(s2v::ConvArgs, int, int)"
         if bkn >= 1000:
             return f"void s2v::conv_halo_small<{bn}, {bkn - 1000}>(s2v::ConvArgs, int, int)"
         if wm:
@@ -1100,6 +1102,12 @@ def attention(ctx: Ctx, q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, out: 
 def flow_warp(ctx: Ctx, flow: NHWC, src: torch.Tensor, y: NHWC):
     """flow: NHWC view with >= 2 channels (x, y); src: NCHW-strided device tensor."""
     S2V.flow_warp_(flow.v, src, y.v)
+    return y
+
+
+def flow_warp_cat(ctx: Ctx, flow: NHWC, src: torch.Tensor, y: NHWC):
+    """y (2C channels) <- [src | warp(src)]: the copy and the warp in one pass (``s2v::flow_warp_cat_``)."""
+    S2V.flow_warp_cat_(flow.v, src, y.v)
     return y
 
 

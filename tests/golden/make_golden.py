@@ -188,6 +188,21 @@ def gen_ops():
     for name, (up, down, pad) in {"up2": (2, 1, (2, 1)), "blur22": (1, 1, (2, 2)),
                                   "blur11": (1, 1, (1, 1)), "down2": (1, 2, (1, 1))}.items():
         arrays[f"ufd_{name}"] = upfirdn2d(xi, k * (4 if up == 2 else 1), up=up, down=down, pad=pad).numpy()
+    # the other two dtypes the reference's ops dispatch (fused_bias_act_kernel.cu:79,
+    # upfirdn2d_kernel.cu:225), through the same CPU fallbacks: float64, and float16 with
+    # fp64 outputs of the half-rounded inputs beside the fallback's own half result
+    for dt, tag in ((torch.float64, "f64"), (torch.float16, "f16")):
+        xd, bd = x.to(dt), b.to(dt)
+        arrays[f"fba_{tag}_out"] = fused_leaky_relu(xd, bd, 0.2, 2 ** 0.5).numpy()
+        if dt == torch.float16:
+            arrays["fba_f16_exact"] = fused_leaky_relu(xd.double(), bd.double(), 0.2, 2 ** 0.5).numpy()
+        for name, (up, down, pad) in {"up2": (2, 1, (2, 1)), "blur22": (1, 1, (2, 2)),
+                                      "down2": (1, 2, (1, 1))}.items():
+            kd = (k * (4 if up == 2 else 1)).to(dt)
+            arrays[f"ufd_{name}_{tag}"] = upfirdn2d(xi.to(dt), kd, up=up, down=down, pad=pad).numpy()
+            if dt == torch.float16:
+                arrays[f"ufd_{name}_f16_exact"] = upfirdn2d(xi.to(dt).double(), kd.double(), up=up, down=down,
+                                                            pad=pad).numpy()
     flow = torch.from_numpy(synth.hash_array("golden.flow", (2, 2, 16, 16), -3.0, 3.0))
     src = torch.from_numpy(synth.hash_array("golden.flow.src", (2, 3, 64, 64)))
     deform = flow_util.convert_flow_to_deformation(flow)

@@ -692,6 +692,47 @@ def test_small_cout_conv(ctx, prec, cin, k, cout):
     assert ((to_nchw(y) - ref).abs() <= 2e-6 * (bound + 1) + 1e-6).all()
 
 
+@pytest.mark.parametrize("n,cin,h,w,k,cout,pad_mode,act", [
+    (2, 64, 13, 11, 7, 3, "zero", ops.ACT_NONE),           # one strip, one band, partial everything
+    (2, 64, 37, 130, 7, 3, "reflect", ops.ACT_TANH),      # DNet head form: 3 strips (58 + 58 + 14), 3 bands
+    (3, 64, 96, 96, 7, 4, "zero", ops.ACT_SIGMOID),       # LNet head form (Cout carried as 4)
+    (1, 32, 20, 64, 5, 4, "zero", ops.ACT_NONE),          # 5x5 over one 32-channel slice
+    (2, 32, 9, 61, 7, 1, "reflect", ops.ACT_NONE)])
+def test_conv_head_x3(ctx, prec, n, cin, h, w, k, cout, pad_mode, act):
+    """Cout <= 4 wide-filter heads (conv_head.hip: kx in N, ky in K, an LDS ring of split input rows)
+    in the split precisions; exact fp32 VALU (conv_halo_small / conv_small_cpar) in f32.  Against the
+    fp64 conv at the per-mode bound of the implicit-GEMM kernels (REL * sum|a*b|)."""
+    wt = rnd(cout, cin, k, k, seed=60) / math.sqrt(cin * k * k)
+    bias = rnd(cout, seed=61)
+    x = rnd(n, cin, h, w, seed=62, lo=-2.0, hi=2.0)
+    pm = ops.PAD_REFLECT if pad_mode == "reflect" else ops.PAD_ZERO
+    cw = ConvW(wt.float(), bias.float(), DEV, padding=k // 2, pad_mode=pm)
+    y = NHWC.empty(n, h, w, cout, DEV)
+    xd = nhwc(x.float())
+    syms = []
+
+    def hook(c, p, flops, launch):
+        syms.append(ops.plan_symbol(p.plan))
+        launch()
+    ops.CONV_HOOK = hook
+    try:
+        ops.conv2d(ctx, xd, cw, y, act=act, alpha=0.0)
+    finally:
+        ops.CONV_HOOK = None
+    if prec != "f32":
+        assert syms and syms[0].startswith("void s2v::conv_head_x3<"), syms
+    xp = F.pad(x, (k // 2,) * 4, mode="reflect") if pad_mode == "reflect" else x
+    ref = F.conv2d(xp, wt, bias, padding=0 if pad_mode == "reflect" else k // 2)
+    bound = conv_bound(xp, wt, 1, 0 if pad_mode == "reflect" else k // 2, 1)
+    tol = (2e-6 if prec == "f32" else REL[prec]) * (bound + 1) + 1e-6
+    got = to_nchw(y)
+    if act == ops.ACT_TANH:
+        ref = torch.tanh(ref)                             # |tanh'| <= 1
+    elif act == ops.ACT_SIGMOID:
+        ref, tol = torch.sigmoid(ref), tol / 4            # |sigmoid'| <= 1/4
+    assert ((got - ref).abs() <= tol).all(), (got - ref).abs().max()
+
+
 @pytest.mark.parametrize("n,hw,cin", [(2, (16, 8), 32), (2, (13, 11), 32), (3, (8, 16), 64), (2, (9, 7), 96)])
 def test_small_cout_per_sample_weights(ctx, n, hw, cin):
     """Per-sample (modulated) weights on the small-Cout kernel: LDS-staged weights need every block

@@ -70,6 +70,46 @@ def test_lipsync_b16_graph_replay_vs_oracle():
     within(lows[-1][idx], rl, TOL["f16x3"]["low"], "replayed b16 low")
 
 
+def test_lipsync_b16_noise_on_graph_replay_vs_oracle():
+    """The timed configuration with StyleConv noise ON (bench.py's lipsync weights: every
+    StyleConv's NoiseInjection weight 0.1, as real checkpoints carry non-zero strengths and
+    base_blocks.py:528-531 draws fresh noise per call): B=16 captured as bench.py captures it,
+    replayed 3 times.  Each replay draws fresh noise (outputs differ); the noise planes the last
+    replay drew are read back and fed to the oracle as explicit noise tensors, and frames 0, 1,
+    14, 15 of that replay must match it at the bounds of the noise-free test."""
+    from oracle import nets
+    from s2v_amd import models
+    from s2v_amd.models import arch
+    from s2v_amd.runtime import GraphRunner
+    if ops.PRECISION != "f16x3":
+        pytest.skip("the benchmarked arithmetic is f16x3")
+    sd = synth.synth_torch_state_dict(arch.ENetParams(lnet=arch.LNetParams()), noise_weight=0.1)
+    model = models.ENet()
+    model.load_state_dict(sd, strict=True)
+    model.eval()
+    mel, face, gt = synth.lipsync_inputs("enet.b16", 16, 256)
+    inputs = [torch.from_numpy(a).to(DEV) for a in (mel, face, gt)]
+    runner = GraphRunner(lambda m, f, g: model(m, f, g), inputs, warmup=1)
+    eng = model._engine(inputs[0].device)[0]
+    outs = []
+    for _ in range(3):
+        outs.append(runner.replay()[0].clone())
+    torch.cuda.synchronize()
+    assert (outs[1] - outs[2]).abs().max() > 1e-3, "every replay draws fresh noise"
+    assert all(n is not None for n in eng.last_noises)
+    idx = [0, 1, 14, 15]
+    noises = [n[idx].cpu().unsqueeze(1) for n in eng.last_noises]
+    assert [tuple(n.shape[2:]) for n in noises] == [(200, 200), (200, 200), (400, 400), (400, 400)]
+    for n in noises:                                   # N(0, 1) draws
+        assert abs(float(n.mean())) < 0.02 and 0.95 < float(n.std()) < 1.05
+    with torch.no_grad():
+        ro, _ = nets.enet_forward(sd, torch.from_numpy(mel[idx]), torch.from_numpy(face[idx]),
+                                  torch.from_numpy(gt[idx]), noises=noises)
+    got = outs[-1][idx]
+    within(clamp01(got), clamp01(ro), BAR, "replayed b16 noise-on clamped bar")
+    within(got, ro, TOL["f16x3"]["enet"], "replayed b16 noise-on out")
+
+
 def test_lnet_bench_capture_vs_oracle():
     """configs[1] as bench.py times it (bench.LNetOnly: the device bilinear resize of B=16 256x256
     crops to 96x96, then LNet.forward, captured by runtime.GraphRunner with warmup 1 and replayed):

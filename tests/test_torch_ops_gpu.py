@@ -172,6 +172,86 @@ def test_fused_bias_act_row_form():
     assert (got.cpu() - torch.where(xb > 0, xb, xb * 0.2) * 2 ** 0.5).abs().max() < 1e-5
 
 
+def _f16_bound(exact):
+    """Stated float16 tolerance: the drop-in computes in fp32 and rounds once, so it lies within half
+    an f16 ulp (<= 2^-11 |v|) of the exact result; allow 2^-10 |v| plus the subnormal spacing 2^-24."""
+    return 2.0 ** -10 * np.abs(exact) + 2.0 ** -24
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float16])
+def test_gpen_ops_half_and_double_match_reference_fallbacks(golden, dtype):
+    """The dtypes the reference dispatches (AT_DISPATCH_FLOATING_TYPES_AND_HALF:
+    fused_bias_act_kernel.cu:79, upfirdn2d_kernel.cu:225) through torch.ops.s2v, against the
+    reference's CPU fallbacks run in that dtype (tests/golden/make_golden.py gen_ops).
+    Tolerances: float64 1e-12 absolute (values are O(1)); float16 within one f16 ulp of the exact
+    (fp64) result on the half-rounded inputs, and within two ulps of the fallback's own half output
+    (it rounds after every torch op)."""
+    g = golden("ops")
+    tag = "f64" if dtype == torch.float64 else "f16"
+    x = torch.from_numpy(synth.hash_array("golden.fba.x", (2, 8, 5, 7))).to(DEV, dtype)
+    b = torch.from_numpy(synth.hash_array("golden.fba.b", (8,))).to(DEV, dtype)
+    outs = {"fba": torch_ops.fused_leaky_relu(x, b, 0.2, 2 ** 0.5)}
+    raw = torch_ops.fused.fused_bias_act(x, b, x.new_empty(0), 3, 0, 0.2, 2 ** 0.5)
+    assert raw.dtype == dtype and torch.equal(raw, outs["fba"])
+    xi = torch.from_numpy(synth.hash_array("golden.ufd.x", (2, 3, 9, 11))).to(DEV, dtype)
+    for name, (up, down, pad) in {"up2": (2, 1, (2, 1)), "blur22": (1, 1, (2, 2)), "down2": (1, 2, (1, 1))}.items():
+        outs[f"ufd_{name}"] = torch_ops.upfirdn2d(xi, _blur_kernel(up).to(dtype), up=up, down=down, pad=pad)
+    for key, got in outs.items():
+        assert got.dtype == dtype, key
+        got = got.cpu().double().numpy()
+        ref_key = f"fba_{tag}_out" if key == "fba" else f"{key}_{tag}"
+        ref = g[ref_key].astype(np.float64)
+        assert got.shape == ref.shape, key
+        if dtype == torch.float64:
+            assert np.abs(got - ref).max() < 1e-12, key
+        else:
+            exact = g["fba_f16_exact" if key == "fba" else f"{key}_f16_exact"]
+            assert (np.abs(got - exact) <= _f16_bound(exact)).all(), (key, np.abs(got - exact).max())
+            assert (np.abs(got - ref) <= 2 * _f16_bound(ref)).all(), (key, np.abs(got - ref).max())
+
+
+def test_gpen_ops_dtype_rules():
+    """float16 / float64 go through the row kernel (step_b % 4 == 0) and the generic kernels too;
+    a dtype the reference does not dispatch, or a kernel / bias of another dtype, raises."""
+    gen = torch.Generator().manual_seed(17)
+    for dt in (torch.float16, torch.float64):
+        x = torch.randn(2, 8, 8, 12, generator=gen).to(dt)
+        b = torch.randn(8, generator=gen).to(dt)
+        r = torch.randn(2, 8, 8, 12, generator=gen).to(dt)
+        xb = x.double() + b.double()[None, :, None, None]
+        for (act, grad), e in {(3, 0): torch.where(xb > 0, xb, xb * 0.2) * 1.5,
+                               (3, 1): torch.where(r.double() > 0, xb, xb * 0.2) * 1.5, (1, 0): xb * 1.5}.items():
+            got = torch_ops.fused.fused_bias_act(x.to(DEV), b.to(DEV), r.to(DEV) if grad else x.new_empty(0).to(DEV),
+                                                  act, grad, 0.2, 1.5).cpu().double()
+            tol = 1e-12 if dt == torch.float64 else torch.from_numpy(_f16_bound(e.numpy()))
+            assert ((got - e).abs() <= tol).all(), (dt, act, grad)
+        x5 = torch.randn(3, 5, 7, generator=gen).to(dt)                     # step_b = 7: element kernel
+        b5 = torch.randn(5, generator=gen).to(dt)
+        e5 = x5.double() + b5.double()[None, :, None]
+        e5 = torch.where(e5 > 0, e5, e5 * 0.2) * 2 ** 0.5
+        got5 = torch_ops.fused_leaky_relu(x5.to(DEV), b5.to(DEV)).cpu().double()
+        assert ((got5 - e5).abs() <= (1e-12 if dt == torch.float64 else torch.from_numpy(_f16_bound(e5.numpy())))).all()
+        xm = torch.randn(2, 7, 9, 3, generator=gen).to(dt)                  # minor > 1, 3x4 kernel: generic kernel
+        km = torch.randn(3, 4, generator=gen).to(dt)
+        from oracle.enhancers import upfirdn2d as ref_upfirdn2d
+        em = ref_upfirdn2d(xm.double().permute(0, 3, 1, 2), km.double(), up=2, down=1, pad=(2, 1)).permute(0, 2, 3, 1)
+        gm = torch_ops.upfirdn2d_op.upfirdn2d(xm.to(DEV), km.to(DEV), 2, 2, 1, 1, 2, 1, 2, 1).cpu().double()
+        assert gm.shape == em.shape
+        # fp32 accumulation of up to 12 half products before the single rounding
+        tol = 1e-12 if dt == torch.float64 else torch.from_numpy(_f16_bound(em.numpy())) + 1e-5
+        assert ((gm - em).abs() <= tol).all(), dt
+    with pytest.raises(RuntimeError):
+        torch_ops.fused.fused_bias_act(torch.ones(4, 4, dtype=torch.bfloat16, device=DEV),
+                                       torch.ones(4, dtype=torch.bfloat16, device=DEV), torch.empty(0, device=DEV),
+                                       3, 0, 0.2, 1.0)
+    with pytest.raises(RuntimeError):
+        torch_ops.fused.fused_bias_act(torch.ones(4, 4, dtype=torch.float16, device=DEV),
+                                       torch.ones(4, device=DEV), torch.empty(0, device=DEV), 3, 0, 0.2, 1.0)
+    with pytest.raises(RuntimeError):
+        torch_ops.upfirdn2d_op.upfirdn2d(torch.ones(1, 8, 8, 1, dtype=torch.float64, device=DEV),
+                                         torch.ones(4, 4, device=DEV), 1, 1, 1, 1, 1, 1, 1, 1)
+
+
 class _NoLaunchLib:
     """libs2v ctypes handle that refuses every kernel launch (host-only queries pass through)."""
     HOST = {"s2v_conv2d_plan", "s2v_conv2d_ws_bytes", "s2v_tune", "s2v_last_error", "s2v_device_cus", "s2v_version",
