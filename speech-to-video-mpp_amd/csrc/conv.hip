@@ -853,7 +853,8 @@ static bool head_x3_ok(const s2v_conv_params *p) {
     const int batch = p->batch > 0 ? p->batch : 1;
     if (!head_x3_on() || p->prec == S2V_PREC_F32 || p->x_split || p->force_tile || !p->wt_x3 || ((uintptr_t)p->wt_x3 % 16))
         return false;
-    if (p->cout > 4 || p->kh != p->kw || (p->kh != 7 && p->kh != 5) || (p->cin != 32 && p->cin != 64)) return false;
+    if (p->cout > 4 || p->kh != p->kw || (p->kh != 7 && p->kh != 5) || (p->cin != 32 && p->cin % 64) || p->cin > 512)
+        return false;
     if (p->in_mode != S2V_IN_DIRECT || p->sh != 1 || p->sw != 1 || p->dh != 1 || p->dw != 1) return false;
     if (p->in_scale || p->pre_act || p->w_bs || batch != 1 || p->b_kn || p->out_step > 1 || p->out_pool || p->d2s_cout)
         return false;
@@ -863,9 +864,10 @@ static bool head_x3_ok(const s2v_conv_params *p) {
 }
 // output rows per conv_head_x3 block: 16, halved while the grid is under two blocks per CU (>= 4)
 static int head_rows(const s2v_conv_params *p) {
-    const long long strips = cdiv(p->ow, 64 - p->kw + 1);
+    const long long strips = cdiv(p->ow, 32 - p->kw + 1);
     int th = 16;
-    while (th > 4 && (long long)p->n * strips * cdiv(p->oh, th) < 2LL * device_cus()) th /= 2;
+    const long long groups = p->cin > 64 ? p->cin / 64 : 1;
+    while (th > 4 && (long long)p->n * strips * groups * cdiv(p->oh, th) < 2LL * device_cus()) th /= 2;
     return th;
 }
 
@@ -1173,7 +1175,7 @@ static Plan make_plan(const s2v_conv_params *p_in, int M, int K) {
     if (p->x_split) return make_plan_glds(p, M, pl);
     if (head_x3_ok(p)) {
         pl.tile = -3;
-        pl.splits = 1;
+        pl.splits = p->cin > 64 ? p->cin / 64 : 1;     // 64-channel groups, folded by splitk_reduce
         pl.tps = pl.ktiles;
         return pl;
     }
@@ -1658,8 +1660,8 @@ extern "C" int s2v_conv2d_plan(const s2v_conv_params *p, int *out6) {
         return 0;
     }
     if (pl.tile == -3) {                                // conv_head_x3<prec - 1, CO, KS, cin / 32>
-        out6[0] = 0; out6[1] = p->cout; out6[2] = p->cin / 32; out6[3] = 0;
-        out6[4] = 3000 + p->kh; out6[5] = 1; out6[6] = p->prec;
+        out6[0] = 0; out6[1] = p->cout; out6[2] = p->cin == 32 ? 1 : 2; out6[3] = 0;
+        out6[4] = 3000 + p->kh; out6[5] = pl.splits; out6[6] = p->prec;
         return 0;
     }
     if (pl.tile < 0 && halo_ks(p)) {
@@ -1725,9 +1727,19 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
             a.x_scale = p->x_scale;
             a.acc_scale /= p->x_scale;
         }
-        rc = launch_conv_head_x3(a, p->prec, p->cout, p->kh, p->cin / 32, head_rows(p), s);
+        if (pl.splits > 1) {
+            const size_t need = (size_t)pl.splits * (size_t)M * p->cout * sizeof(float);
+            if (!p->ws || p->ws_bytes < need) {
+                set_error("conv2d: split workspace of %zu bytes required (have %zu)", need, p->ws_bytes);
+                return S2V_E_WORKSPACE;
+            }
+        }
+        rc = launch_conv_head_x3(a, p->prec, p->cout, p->kh, p->cin == 32 ? 1 : 2, head_rows(p), s);
         if (rc) return rc;
-        return check_launch("conv_head_x3");
+        rc = check_launch("conv_head_x3");
+        if (rc || pl.splits <= 1) return rc;
+        splitk_reduce<<<cdiv((long long)M * p->cout, 256), 256, 0, s>>>(a, 1, epi_vec4(p));
+        return check_launch("splitk_reduce");
     }
     if (pl.tile < 0 && halo_ks(p)) {
         if (pl.splits > 1) {
