@@ -1354,6 +1354,9 @@ static ConvArgs make_args(const s2v_conv_params *p, int M, int K, const Plan &pl
     a.stamp_stride = p->stamp_stride; a.stamp_reps = p->stamp_reps > 0 ? p->stamp_reps : 1;
     a.x_scale = 1.f;
     a.nonfinite = p->nonfinite;
+    static const bool vec4_on = [] { const char *e = getenv("S2V_EPI_VEC4"); return !e || atoi(e) != 0; }();
+    a.vec4 = vec4_on && epi_vec4(p) && (!p->nc_scale || (p->nc_scale_ns % 4 == 0 && ((uintptr_t)p->nc_scale % 16) == 0)) &&
+             (p->d2s_cout <= 0 || p->d2s_cout % 4 == 0);
     if (tiled_x3(p) && !p->b_kn && !p->x_split && p->x_scale > 0.f && p->x_scale != 1.f) {
         a.x_scale = p->x_scale;
         a.acc_scale /= p->x_scale;

@@ -44,6 +44,8 @@ struct ConvArgs {
     int stamp_slot, stamp_stride, stamp_reps;
     float x_scale;          // split-precision A operand pre-scale (power of two; 1 = none)
     int *nonfinite;         // set to 1 when an accumulator is non-finite (or null)
+    int vec4;               // the tile epilogues may write 4-channel quads (cout, ycs, y_bs multiples of 4, 16-byte
+                            // aligned y / scale / shift / res / nc_scale rows: conv.hip epi_vec4)
     int vgrid_x, vgrid_y, vgrid_z;   // x3 persistent launch: the tile grid gridDim.x blocks loop over
                                      // (s2v_conv_params.grid_cap); vgrid_x == 0: one block per tile
 };
@@ -422,6 +424,18 @@ __device__ __forceinline__ void epilogue_tile_map(const ConvArgs &a, float *Cs, 
     const float sc = (live && e.scale) ? e.scale[n] : 1.f;
     const float sh = (live && e.shift) ? e.shift[n] : 0.f;
     const float slope = e.act == S2V_ACT_RELU ? 0.f : (e.act == S2V_ACT_LRELU ? e.alpha : 1.f);
+    // 4-channel quads per thread (a.vec4): one LDS read, one 16-byte store and one address update per four
+    // outputs instead of per output (the per-element index / act VALU was ~40 % of the non-MFMA vector work
+    // of the 256x256 StyleConv launches, PMC profiles/r06_pmc_headline_conv.json)
+    constexpr int TQ = BN / 4 < NT ? BN / 4 : NT;    // threads per tile row
+    constexpr int RS4 = NT / TQ;
+    const bool vq = a.vec4 && !a.pool && a.splits <= 1 && BN % 4 == 0 && (BN / 4) % TQ == 0 &&
+                    (a.y_step > 1 ? !e.nc_scale : (!e.res || e.res_simple));
+    const int cq = tid % TQ, nq = n0 + 4 * cq;
+    const bool liveq = nq < a.cout;
+    f4 sc4 = {1.f, 1.f, 1.f, 1.f}, sh4 = {0.f, 0.f, 0.f, 0.f};
+    if (vq && liveq && e.scale) sc4 = *(const f4 *)(e.scale + nq);
+    if (vq && liveq && e.shift) sh4 = *(const f4 *)(e.shift + nq);
 #pragma unroll 1
     for (int c0 = 0; c0 < BM; c0 += CH) {
         __syncthreads();   // operand stages (first chunk) / the previous chunk are no longer read
@@ -429,6 +443,64 @@ __device__ __forceinline__ void epilogue_tile_map(const ConvArgs &a, float *Cs, 
         __syncthreads();
         const int clim = rows(c0);
         const int cb = base(c0);
+        if (vq) {
+            if (!liveq || clim <= 0) continue;
+            const int hw = a.oh * a.ow;
+            const int rr0 = tid / TQ;
+            int m = cb + rr0;
+            int img = m / hw, rem = m - img * hw;
+            auto act4 = [&](f4 v) {
+                v.x = fast_act(v.x, e.act, slope); v.y = fast_act(v.y, e.act, slope);
+                v.z = fast_act(v.z, e.act, slope); v.w = fast_act(v.w, e.act, slope);
+                return v;
+            };
+            if (a.y_step > 1) {
+                // strided / depth-to-space output: quads stay inside one parity class (d2s_c % 4 == 0)
+                const int cls = a.d2s_c > 0 ? nq / a.d2s_c : 0;
+                const int oc = a.d2s_c > 0 ? nq - cls * a.d2s_c : nq;
+                const int dy = cls >> 1, dx = cls & 1, ys = a.y_step;
+                int oy = rem / a.ow, ox = rem - (rem / a.ow) * a.ow;
+                float *__restrict__ yb = a.y + (long long)bidx * a.y_bs + oc;
+                const float *pix = e.pix_add ? e.pix_add + (long long)bidx * a.y_h * a.y_w * a.n : nullptr;
+                const float *rsrc = e.res ? e.res + (long long)bidx * a.res_bs + oc : nullptr;
+#pragma unroll 1
+                for (int rr = rr0; rr < clim; rr += RS4) {
+                    const long long q = ((long long)img * a.y_h + oy * ys + dy) * a.y_w + ox * ys + dx;
+                    ox += RS4;
+                    while (ox >= a.ow) {
+                        ox -= a.ow;
+                        if (++oy == a.oh) { oy = 0; ++img; }
+                    }
+                    f4 v = *(const f4 *)&Cs[rr * LDC + 4 * cq] * sc4 + sh4;
+                    if (pix) v += e.pix_w * pix[q];
+                    f4 rv = {0.f, 0.f, 0.f, 0.f};
+                    if (rsrc) rv = *(const f4 *)(rsrc + q * a.ycs);
+                    if (!e.res_after) v += rv;
+                    v = act4(v);
+                    if (e.res_after) v += rv;
+                    *(f4 *)(yb + q * a.ycs) = v;
+                }
+            } else {
+                float *__restrict__ yb = a.y + (long long)bidx * a.y_bs + nq;
+                const float *pix = e.pix_add ? e.pix_add + (long long)bidx * a.oh * a.ow * a.n : nullptr;
+                const float *rsrc = e.res ? e.res + (long long)bidx * a.res_bs + nq : nullptr;
+#pragma unroll 1
+                for (int rr = rr0; rr < clim; rr += RS4, m += RS4, rem += RS4) {
+                    while (rem >= hw) { rem -= hw; ++img; }
+                    f4 v = *(const f4 *)&Cs[rr * LDC + 4 * cq] * sc4;
+                    if (e.nc_scale) v *= *(const f4 *)(e.nc_scale + (long long)img * e.nc_ns + nq);
+                    v += sh4;
+                    if (pix) v += e.pix_w * pix[m];
+                    f4 rv = {0.f, 0.f, 0.f, 0.f};
+                    if (rsrc) rv = *(const f4 *)(rsrc + (long long)m * e.res_cs);
+                    if (!e.res_after) v += rv;
+                    v = act4(v);
+                    if (e.res_after) v += rv;
+                    *(f4 *)(yb + (long long)m * a.ycs) = v;
+                }
+            }
+            continue;
+        }
         if (!live || clim <= 0) continue;
         if (a.pool) {
             // 2x2 average of the activated outputs (ResBlock: lrelu(conv1) then bilinear x0.5 ==

@@ -39,6 +39,9 @@ POLY_UP4 = os.environ.get("S2V_ENET_POLY_UP4", "0") == "1"
 # 29.1 -> 26.1-26.5 ms (caps 192: 28.5, 160: 27.1, 112: 28.9, 96: 31.4, 64: 38.9; r03).
 # S2V_ENET_STYLE_GRID: an explicit block count (0: one block per tile).
 STYLE_GRID = os.environ.get("S2V_ENET_STYLE_GRID", "half")
+# where the style-encoder branch forks off the calling stream: 0 = before LNet (both from the start of
+# the step), h = before LNet's h x h decoder level (LNet's earlier levels then run on the whole chip)
+FORK_AT = int(os.environ.get("S2V_ENET_FORK_AT", "0"))
 
 
 def style_grid(device) -> int:
@@ -225,28 +228,38 @@ class ENetEngine:
         b = audio.shape[0]
         svec = NHWC.empty(b, 1, 1, self.mod.cout, dev)
         side = self._side(ctx) if OVERLAP else None
-        if side is not None:
+        enc = {}
+
+        def fork():
             sst, sctx = side
-            cur_st = torch.cuda.current_stream(dev)
-            sst.wait_stream(cur_st)
+            sst.wait_stream(torch.cuda.current_stream(dev))
             with ops.x3_grid_cap(sctx, style_grid(dev)), ops.side_stream(sst, ctx.keep):
-                style = self.style_code(sctx, face[:, 3:])
-                ops.conv2d(sctx, style, self.mod, svec)
-                dtab, dall = self._demods(sctx, svec.t.view(b, -1))   # off the tail: beside LNet
+                enc["style"] = self.style_code(sctx, face[:, 3:])
+                ops.conv2d(sctx, enc["style"], self.mod, svec)
+                enc["d"] = self._demods(sctx, svec.t.view(b, -1))   # off the tail: beside LNet
+        on_level = None
+        if side is not None:
+            if FORK_AT:
+                on_level = lambda h: fork() if h == FORK_AT and not enc else None  # noqa: E731
+            else:
+                fork()
         else:
-            style = self.style_code(ctx, face[:, 3:])
-            ops.conv2d(ctx, style, self.mod, svec)
-            dtab, dall = self._demods(ctx, svec.t.view(b, -1))
-        s2 = svec.t.view(b, -1)
+            enc["style"] = self.style_code(ctx, face[:, 3:])
+            ops.conv2d(ctx, enc["style"], self.mod, svec)
+            enc["d"] = self._demods(ctx, svec.t.view(b, -1))
         # LNet input: cat(inp, gt) -> bilinear 96x96 (ENet.py:103-104)
         x6 = NHWC.empty(b, 96, 96, 6, dev)
         ops.nchw_to_nhwc(ctx, face[:, :3], x6.slice(0, 3))
         ops.nchw_to_nhwc(ctx, gt, x6.slice(3, 3))
         lo = NHWC.empty(b, 96, 96, 4, dev)          # channel 3 = sigmoid(0): finite, zero weights
-        self.lnet.forward(ctx, audio, x6, lo, pad_rgb=True)
+        self.lnet.forward(ctx, audio, x6, lo, pad_rgb=True, on_level=on_level)
+        if side is not None and not enc:
+            fork()                                             # FORK_AT names no LNet level
         ops.nhwc_to_nchw(ctx, lo.slice(0, 3), low)
         if side is not None:
             torch.cuda.current_stream(dev).wait_stream(side[0])    # style code ready for the StyleConvs
+        style, (dtab, dall) = enc["style"], enc["d"]
+        s2 = svec.t.view(b, -1)
         if aux is not None:
             aux["style"] = style.t.view(b, -1)
         # F.pad(reflect, 2) -> StyleConv / ToRGB stages (ENet.py:119-129)

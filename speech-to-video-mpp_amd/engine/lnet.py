@@ -380,10 +380,11 @@ class LNetEngine:
         return None if side is None else Branches(self.device, side)
 
     def forward(self, ctx, audio: torch.Tensor, face6: NHWC, out: NHWC, logits: NHWC | None = None,
-                pad_rgb: bool = False):
+                pad_rgb: bool = False, on_level=None):
         """audio: [B,1,80,16] device tensor; face6: NHWC [B,96,96,6] = [masked | ref];
         out: NHWC [B,96,96,3] receives sigmoid(final conv) ([B,96,96,4] with a 4th constant channel
-        when ``pad_rgb``)."""
+        when ``pad_rgb``).  ``on_level(h)``: called on the calling stream before the decoder level of
+        h x h starts (ENet forks its style encoder there, engine/enet.py FORK_AT)."""
         dev = self.device
         b = face6.n
         # ---- visual encoder (LNet.py:30-43) and audio encoder (LNet.py:102-120): the masked-face
@@ -432,6 +433,8 @@ class LNetEngine:
         cur = cat
         for lv in self.levels:
             c = lv["c"]
+            if on_level is not None:
+                on_level(cur.h)
             ya = NHWC.empty(cur.n, cur.h, cur.w, c, dev)
             yb = NHWC.empty(cur.n, cur.h, cur.w, c, dev)
             # the ADAIN that ends each FFC also writes the reflect-padded copy the next FFC's 3x3
