@@ -39,6 +39,12 @@ POLY_UP4 = os.environ.get("S2V_ENET_POLY_UP4", "0") == "1"
 # 29.1 -> 26.1-26.5 ms (caps 192: 28.5, 160: 27.1, 112: 28.9, 96: 31.4, 64: 38.9; r03).
 # S2V_ENET_STYLE_GRID: an explicit block count (0: one block per tile).
 STYLE_GRID = os.environ.get("S2V_ENET_STYLE_GRID", "half")
+# the first StyleConv (3x3 over the 4-channel RGB input carried as 4, after the x2 upsample) as a row-tap
+# packed 3x1 conv (ConvW.make_rowpack + ops.row_pack: the (kx, c) taps become 12 of 32 packed channels) on
+# the buffer-load tiles instead of the per-element gather of a 4-channel input; its modulation is the
+# bank's segment laid out per packed channel (s'[kx * 4 + c] = s[c]).  Measured on MI355X (r06, same-box A/B,
+# 3 pairs): lipsync 23.50 (gather) vs 23.59 ms (packed) -- off by default (S2V_ENET_ROWPACK0=1 turns it on)
+ROWPACK0 = os.environ.get("S2V_ENET_ROWPACK0", "0") == "1"
 # where the style-encoder branch forks off the calling stream: 0 = before LNet (both from the start of
 # the step), h = before LNet's h x h decoder level (LNet's earlier levels then run on the whole chip)
 FORK_AT = int(os.environ.get("S2V_ENET_FORK_AT", "0"))
@@ -89,6 +95,11 @@ class StyleLayer:
         if upsample and self.k == 3 and (self.cin % 32 == 0 or (POLY_UP4 and self.cin == 4)):
             self.conv4 = ConvW(fold_up2_conv3(w), bias.repeat(4), device, padding=1)
             self.wsq4 = self.wsq.repeat(4, 1).contiguous()
+        self.rp = None                                       # row-packed form (ROWPACK0): packed channel count
+        if ROWPACK0 and self.conv4 is None and not is_rgb and self.k == 3 and self.cin * self.k <= 32:
+            self.conv.make_rowpack(device)
+            self.rp = self.conv.rowpack.cin
+            self.conv.rowpack.shift = self.conv.shift             # the layer bias in the packed conv's epilogue
 
 
 class ENetEngine:
@@ -125,10 +136,17 @@ class ENetEngine:
         offs, o, ws, bs = [], 0, [], []
         for l in self.layers:
             offs.append(o)
-            pad = (-l.cin) % 4
-            ws += [l.mod_w, torch.zeros(pad, l.mod_w.shape[1])]
-            bs += [l.mod_b, torch.zeros(pad)]
-            o += l.cin + pad
+            mw, mb = l.mod_w, l.mod_b
+            if l.rp is not None:
+                # s'[kx * cin + c] = s[c] for kx < k, zero up to the packed width (ConvW.make_rowpack's channel
+                # order); its first cin entries are s itself, which the demodulation reads
+                z = l.rp - l.k * l.cin
+                mw = torch.cat([mw] * l.k + [torch.zeros(z, mw.shape[1])])
+                mb = torch.cat([mb] * l.k + [torch.zeros(z)])
+            pad = (-mw.shape[0]) % 4
+            ws += [mw, torch.zeros(pad, l.mod_w.shape[1])]
+            bs += [mb, torch.zeros(pad)]
+            o += mw.shape[0] + pad
         self.mod = ConvW(torch.cat(ws, 0), torch.cat(bs, 0), dev)
         self.mod_offs = offs
         self._demod = {}
@@ -286,6 +304,11 @@ class ENetEngine:
                 if L.upsample:
                     x = NHWC.empty(b, 2 * cur.h, 2 * cur.w, cur.c, dev)
                     ops.resize_nhwc(ctx, cur, x, scale_factor=2)
+                conv, cin = L.conv, L.cin
+                if L.rp is not None:
+                    xp = NHWC.empty(b, x.h, x.w, L.rp, dev)
+                    ops.row_pack(ctx, x, xp, L.k, L.k // 2)
+                    x, conv, cin = xp, L.conv.rowpack, L.rp
                 d = dall[:, r0: r0 + L.cout]
                 y = NHWC.empty(b, x.h, x.w, L.cout, dev)
                 noise = None
@@ -296,7 +319,7 @@ class ENetEngine:
                         noise = torch.empty((b, x.h, x.w), device=dev)
                         ops.gaussian_noise(ctx, noise, self.noise_seed, (2 * st + li) << 36, ctr=ctr, shift=40)
                         self.last_noises[2 * st + li] = noise
-                ops.modulated_conv2d(ctx, x, L.conv, y, s2[:, off: off + L.cin], d, act=ops.ACT_LRELU, alpha=LRELU,
+                ops.modulated_conv2d(ctx, x, conv, y, s2[:, off: off + cin], d, act=ops.ACT_LRELU, alpha=LRELU,
                                      pix_add=noise, pix_w=L.noise_w or 0.0)
                 cur = y
             R = self.layers[3 * st + 2]
