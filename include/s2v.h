@@ -148,6 +148,14 @@ typedef struct s2v_conv_params {
      * y + ((n_*out_full_h + 2*oy + cls/2)*out_full_w + 2*ox + cls%2)*ycs + o, and pix_add is read
      * at that full-resolution pixel ([N, out_full_h, out_full_w]). */
     int d2s_cout;
+    /* enhancer epilogue folds (dense outputs only: out_step <= 1, no pool, no d2s), after act and res:
+     *  SFT (gfpganv1_clean_arch.py:98-106):   out[m][n] = v * post_mul[m][n - post_c0] + post_add[m][n - post_c0]
+     *      for n >= post_c0 (rows of pitch post_cs; post_mul and post_add share it);
+     *  second output (GPEN NoiseInjection concat half, gpen_model.py:292-302):
+     *      y[m][dup_off + n] = act(dup_a * dup_src[m][n] + dup_bias[n]) for n < cout (rows of pitch dup_cs;
+     *      dup_bias may be NULL); dup_off >= cout and dup_off + cout <= ycs. */
+    const float *post_mul, *post_add; int post_cs, post_c0;
+    const float *dup_src, *dup_bias; float dup_a; int dup_cs, dup_off;
 } s2v_conv_params;
 
 enum { S2V_PREC_F32 = 0, S2V_PREC_BF16X3 = 1, S2V_PREC_F16X3 = 2 };

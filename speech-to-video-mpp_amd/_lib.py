@@ -49,6 +49,8 @@ class ConvParams(ctypes.Structure):
         ("stamp_reps", _c_int),
         ("x_scale", _c_float), ("nonfinite", _vp),
         ("d2s_cout", _c_int),
+        ("post_mul", _vp), ("post_add", _vp), ("post_cs", _c_int), ("post_c0", _c_int),
+        ("dup_src", _vp), ("dup_bias", _vp), ("dup_a", _c_float), ("dup_cs", _c_int), ("dup_off", _c_int),
     ]
 
 

@@ -259,9 +259,22 @@ __device__ __forceinline__ void store_epilogue4(const ConvArgs &a, int bidx, int
     v.z = apply_act(v.z, e.act, e.alpha);
     v.w = apply_act(v.w, e.act, e.alpha);
     if (e.res && e.res_after) v += r;
+    if (e.post_mul && n >= e.post_c0) {       // SFT (post_c0 % 4 == 0 under vec: a quad is all in or out)
+        const long long q = (long long)m * e.post_cs + n - e.post_c0;
+        v = v * *(const f4 *)(e.post_mul + q) + *(const f4 *)(e.post_add + q);
+    }
     f4 *dst = (f4 *)(a.y + (long long)bidx * a.y_bs + (long long)m * a.ycs + n);
     if (nt) __builtin_nontemporal_store(v, dst);
     else *dst = v;
+    if (e.dup_src) {
+        f4 d = e.dup_a * *(const f4 *)(e.dup_src + (long long)m * e.dup_cs + n);
+        if (e.dup_bias) d += *(const f4 *)(e.dup_bias + n);
+        d.x = apply_act(d.x, e.act, e.alpha);
+        d.y = apply_act(d.y, e.act, e.alpha);
+        d.z = apply_act(d.z, e.act, e.alpha);
+        d.w = apply_act(d.w, e.act, e.alpha);
+        *(f4 *)(a.y + (long long)bidx * a.y_bs + (long long)m * a.ycs + e.dup_off + n) = d;
+    }
 }
 
 // Small-K direct convolution (K = kh*kw*cin <= 64: the 4-channel image-input layers and the
@@ -416,7 +429,7 @@ __global__ __launch_bounds__(256) void conv_smallk4(ConvArgs a, int batch, int t
         };
         // the epilogue's per-channel scale / shift are loaded once, before any store
         const Epi &ep = a.epi;
-        const bool plain = vec && !ep.nc_scale && !ep.res && !ep.pix_add && a.y_step <= 1;
+        const bool plain = vec && !ep.nc_scale && !ep.res && !ep.pix_add && a.y_step <= 1 && !ep.post_mul && !ep.dup_src;
         f4 esc[QPT], esh[QPT];
 #pragma unroll
         for (int q = 0; q < QPT; ++q) {
@@ -950,7 +963,11 @@ struct Plan {
 static int epi_vec4(const s2v_conv_params *p) {
     return p->cout % 4 == 0 && p->ycs % 4 == 0 && ((uintptr_t)p->y % 16) == 0 && p->y_bs % 4 == 0 &&
            (!p->res || (p->res_cs % 4 == 0 && ((uintptr_t)p->res % 16) == 0 && p->res_bs % 4 == 0)) &&
-           (!p->scale || ((uintptr_t)p->scale % 16) == 0) && (!p->shift || ((uintptr_t)p->shift % 16) == 0);
+           (!p->scale || ((uintptr_t)p->scale % 16) == 0) && (!p->shift || ((uintptr_t)p->shift % 16) == 0) &&
+           (!p->post_mul || (p->post_cs % 4 == 0 && p->post_c0 % 4 == 0 && ((uintptr_t)p->post_mul % 16) == 0 &&
+                             ((uintptr_t)p->post_add % 16) == 0)) &&
+           (!p->dup_src || (p->dup_cs % 4 == 0 && p->dup_off % 4 == 0 && ((uintptr_t)p->dup_src % 16) == 0 &&
+                            (!p->dup_bias || ((uintptr_t)p->dup_bias % 16) == 0)));
 }
 
 static bool use_direct(const s2v_conv_params *p) { return p->cout <= 4 && !p->b_kn; }
@@ -1315,6 +1332,16 @@ static int validate(const s2v_conv_params *p, int &M, int &K) {
         S2V_REQUIRE(p->x_split || (!(use_direct(p) && !p->force_tile) && !is_smallk(p)),
                     "conv2d: out_pool needs the implicit-GEMM path");
     }
+    if (p->post_mul || p->dup_src) {
+        S2V_REQUIRE(p->out_step <= 1 && !p->out_pool && p->d2s_cout <= 0 && p->batch <= 1 && p->cout > 4,
+                    "conv2d: post_mul / dup_src need a dense output (no strided / pooled / depth-to-space / batched) "
+                    "and cout > 4");
+        S2V_REQUIRE(!p->post_mul || (p->post_add && p->post_c0 >= 0 && p->post_c0 < p->cout &&
+                                     p->post_cs >= p->cout - p->post_c0),
+                    "conv2d: post_mul needs post_add, 0 <= post_c0 < cout and post_cs >= cout - post_c0");
+        S2V_REQUIRE(!p->dup_src || (p->dup_cs >= p->cout && p->dup_off >= p->cout && p->dup_off + p->cout <= p->ycs),
+                    "conv2d: dup_src needs dup_cs >= cout and cout <= dup_off <= ycs - cout");
+    }
     if (p->d2s_cout > 0)
         S2V_REQUIRE(p->out_step == 2 && p->cout == 4 * p->d2s_cout && !p->res && !p->out_pool && !p->nc_scale,
                     "conv2d: depth-to-space output needs out_step 2, cout == 4 * d2s_cout, no res / pool / nc_scale");
@@ -1344,6 +1371,8 @@ static ConvArgs make_args(const s2v_conv_params *p, int M, int K, const Plan &pl
     e.res_oy = p->res_oy; e.res_ox = p->res_ox; e.res_after = p->res_after_act;
     e.res_simple = (e.res_h == p->oh && e.res_w == p->ow && p->res_oy == 0 && p->res_ox == 0);
     e.act = p->act; e.alpha = p->alpha;
+    e.post_mul = p->post_mul; e.post_add = p->post_add; e.post_cs = p->post_cs; e.post_c0 = p->post_c0;
+    e.dup_src = p->dup_src; e.dup_bias = p->dup_bias; e.dup_a = p->dup_a; e.dup_cs = p->dup_cs; e.dup_off = p->dup_off;
     a.x_bs = p->x_bs; a.w_bs = p->w_bs; a.y_bs = p->y_bs; a.res_bs = p->res_bs;
     a.M = M; a.K = K; a.ktiles = pl.ktiles; a.splits = pl.splits; a.tps = pl.tps; a.ws = p->ws;
     a.y_step = p->out_step > 1 ? p->out_step : 1; a.y_h = p->out_full_h; a.y_w = p->out_full_w;
@@ -1446,7 +1475,8 @@ static bool x3_kind_ok(const s2v_conv_params *p, int kind) {
 // Persistent blocks of a launch under s2v_conv_params.grid_cap: the 256x256 buffer-load split-precision
 // tile only (conv_x3_impl.hpp x3_has_persist), when the tile grid exceeds the cap; 0 = one block per tile
 static int persist_blocks(const s2v_conv_params *p, const Plan &pl, int M) {
-    if (p->grid_cap <= 0 || !tiled_x3(p) || p->b_kn || p->x_split || pl.tile != 0) return 0;
+    // (not with the SFT / second-output extras: the persistent kernel is built without them)
+    if (p->grid_cap <= 0 || !tiled_x3(p) || p->b_kn || p->x_split || pl.tile != 0 || p->post_mul || p->dup_src) return 0;
     const TileCfg &t = kX3Tiles[0].t;
     if (x3_amode(p, t) != 4) return 0;
     const long long cap = p->grid_cap & ~7LL;
@@ -1472,7 +1502,8 @@ struct GroupPlan {
 
 static bool group_member_ok(const s2v_conv_params *p, int cfg) {
     return tiled_x3(p) && !p->b_kn && !p->x_split && p->grid_cap == 0 && p->force_tile == 0 && !p->out_pool &&
-           (p->batch <= 1) && x3_amode(p, kX3Tiles[cfg].t) == 4 && !p->in_scale && p->pre_act == S2V_ACT_NONE;
+           (p->batch <= 1) && x3_amode(p, kX3Tiles[cfg].t) == 4 && !p->in_scale && p->pre_act == S2V_ACT_NONE &&
+           !p->post_mul && !p->dup_src;       // the grouped kernel is built without the epilogue extras
 }
 
 static int group_plan(const s2v_conv_params *ps, int n, GroupPlan &gp) {
@@ -1533,7 +1564,7 @@ static int group_plan(const s2v_conv_params *ps, int n, GroupPlan &gp) {
         }
     }
     S2V_REQUIRE(gp.cfg >= 0, "conv2d_group: members need the split-precision buffer-load path (direct zero-padded "
-                "conv, cin %% 32 == 0, <= 32 taps, no in_scale / pre_act / pool / grid_cap / force_tile, batch 1)");
+                "conv, cin %% 32 == 0, <= 32 taps, no in_scale / pre_act / pool / grid_cap / force_tile / post / dup, batch 1)");
     for (int i = 0; i < n; ++i) {
         Plan &pl = gp.plan[i];
         pl.tile = gp.cfg;

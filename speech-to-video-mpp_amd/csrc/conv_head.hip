@@ -125,7 +125,7 @@ __global__ __launch_bounds__(kHeadT) void conv_head_x3(ConvArgs a, int strips, i
     // shift-sum outputs: thread t owns strip column t / CO, channel t % CO (TW * CO <= 512); the plain
     // epilogue (scale, shift, activation) inline with its two per-channel values loaded once per block
     const Epi &e = a.epi;
-    const bool plain = !e.nc_scale && !e.pix_add && !e.res;
+    const bool plain = !e.nc_scale && !e.pix_add && !e.res && !e.post_mul && !e.dup_src;
     float *__restrict__ wsp = a.splits > 1 ? a.ws + (long long)cg * a.M * a.cout : nullptr;
     const int oq = tid / CO, oo = tid - (tid / CO) * CO;
     const bool owner = tid < TW * CO && ox0 + oq < a.ow;

@@ -15,6 +15,11 @@ struct Epi {
     int res_cs, res_h, res_w, res_oy, res_ox, res_after, res_simple;
     int act;
     float alpha;
+    const float *post_mul, *post_add;   // SFT on channels >= post_c0 (s2v_conv_params)
+    int post_cs, post_c0;
+    const float *dup_src, *dup_bias;    // second output at channel offset dup_off
+    float dup_a;
+    int dup_cs, dup_off;
 };
 
 struct ConvArgs {
@@ -106,6 +111,9 @@ __device__ __forceinline__ long long pix_index(const ConvArgs &a, int bidx, int 
            (cls & 1);
 }
 
+// EXTRA = false: a kernel that never carries the SFT / second-output extras (host-checked), so their
+// registers are not allocated in it
+template <bool EXTRA = true>
 __device__ __forceinline__ void store_epilogue(const ConvArgs &a, int bidx, int m, int n, float v) {
     const Epi &e = a.epi;
     const int hw = a.oh * a.ow;
@@ -131,7 +139,16 @@ __device__ __forceinline__ void store_epilogue(const ConvArgs &a, int bidx, int 
     }
     v = apply_act(v, e.act, e.alpha);
     if (e.res && e.res_after) v += r;
+    if (EXTRA && e.post_mul && n >= e.post_c0) {
+        const long long q = (long long)m * e.post_cs + n - e.post_c0;
+        v = v * e.post_mul[q] + e.post_add[q];
+    }
     a.y[(long long)bidx * a.y_bs + out_row(a, m) + out_col(a, n)] = v;
+    if (EXTRA && e.dup_src) {
+        float d = e.dup_a * e.dup_src[(long long)m * e.dup_cs + n];
+        if (e.dup_bias) d += e.dup_bias[n];
+        a.y[(long long)bidx * a.y_bs + out_row(a, m) + e.dup_off + n] = apply_act(d, e.act, e.alpha);
+    }
 }
 
 // Map an output pixel + filter tap to an input pixel; false -> zero padding.
@@ -396,19 +413,20 @@ __device__ __forceinline__ void load_b(const ConvArgs &a, const float *__restric
 // ``base(c0)``: the GEMM row (output pixel m) of chunk row 0 — a chunk's CH rows are consecutive m;
 // ``rows(c0)``: how many of them exist.  epilogue_tile_fn is the linear tile (rows m0, m0 + 1, ...);
 // the spatial halo tile (conv_x3_halo.hip) maps each 64-row chunk to one output row segment.
-template <int BM, int BN, int NW, int CH, class Stage, class Base, class Rows>
+// EXTRA = false drops the SFT / second-output code (store_epilogue<EXTRA>).
+template <int BM, int BN, int NW, int CH, bool EXTRA = true, class Stage, class Base, class Rows>
 __device__ __forceinline__ void epilogue_tile_map(const ConvArgs &a, float *Cs, int tid, int n0, int bz, int bidx,
                                                   Stage stage, Base base, Rows rows);
 
-template <int BM, int BN, int NW, int CH, class Stage>
+template <int BM, int BN, int NW, int CH, bool EXTRA = true, class Stage>
 __device__ __forceinline__ void epilogue_tile_fn(const ConvArgs &a, float *Cs, int tid, int m0, int n0, int bz,
                                                  int bidx, Stage stage) {
     const int mlim = min(BM, a.M - m0);
-    epilogue_tile_map<BM, BN, NW, CH>(a, Cs, tid, n0, bz, bidx, stage, [&](int c0) { return m0 + c0; },
-                                      [&](int c0) { return min(CH, mlim - c0); });
+    epilogue_tile_map<BM, BN, NW, CH, EXTRA>(a, Cs, tid, n0, bz, bidx, stage, [&](int c0) { return m0 + c0; },
+                                             [&](int c0) { return min(CH, mlim - c0); });
 }
 
-template <int BM, int BN, int NW, int CH, class Stage, class Base, class Rows>
+template <int BM, int BN, int NW, int CH, bool EXTRA, class Stage, class Base, class Rows>
 __device__ __forceinline__ void epilogue_tile_map(const ConvArgs &a, float *Cs, int tid, int n0, int bz, int bidx,
                                                   Stage stage, Base base, Rows rows) {
     constexpr int NT = 64 * NW;
@@ -420,7 +438,8 @@ __device__ __forceinline__ void epilogue_tile_map(const ConvArgs &a, float *Cs, 
     const int cn = tid % TPR;
     const int n = n0 + cn;
     const bool live = n < a.cout;
-    const bool simple = !e.nc_scale && !e.pix_add && (!e.res || e.res_simple);
+    const bool extra = EXTRA && (e.post_mul || e.dup_src);
+    const bool simple = !e.nc_scale && !e.pix_add && (!e.res || e.res_simple) && !extra;
     const float sc = (live && e.scale) ? e.scale[n] : 1.f;
     const float sh = (live && e.shift) ? e.shift[n] : 0.f;
     const float slope = e.act == S2V_ACT_RELU ? 0.f : (e.act == S2V_ACT_LRELU ? e.alpha : 1.f);
@@ -430,12 +449,14 @@ __device__ __forceinline__ void epilogue_tile_map(const ConvArgs &a, float *Cs, 
     constexpr int TQ = BN / 4 < NT ? BN / 4 : NT;    // threads per tile row
     constexpr int RS4 = NT / TQ;
     const bool vq = a.vec4 && !a.pool && a.splits <= 1 && BN % 4 == 0 && (BN / 4) % TQ == 0 &&
-                    (a.y_step > 1 ? !e.nc_scale : (!e.res || e.res_simple));
+                    (a.y_step > 1 ? !e.nc_scale && !e.post_mul && !e.dup_src : (!e.res || e.res_simple));
     const int cq = tid % TQ, nq = n0 + 4 * cq;
     const bool liveq = nq < a.cout;
     f4 sc4 = {1.f, 1.f, 1.f, 1.f}, sh4 = {0.f, 0.f, 0.f, 0.f};
     if (vq && liveq && e.scale) sc4 = *(const f4 *)(e.scale + nq);
     if (vq && liveq && e.shift) sh4 = *(const f4 *)(e.shift + nq);
+    f4 dsb4 = {0.f, 0.f, 0.f, 0.f};
+    if (EXTRA && vq && liveq && e.dup_src && e.dup_bias) dsb4 = *(const f4 *)(e.dup_bias + nq);
 #pragma unroll 1
     for (int c0 = 0; c0 < BM; c0 += CH) {
         __syncthreads();   // operand stages (first chunk) / the previous chunk are no longer read
@@ -496,7 +517,15 @@ __device__ __forceinline__ void epilogue_tile_map(const ConvArgs &a, float *Cs, 
                     if (!e.res_after) v += rv;
                     v = act4(v);
                     if (e.res_after) v += rv;
+                    if (EXTRA && e.post_mul && nq >= e.post_c0) {
+                        const long long q = (long long)m * e.post_cs + nq - e.post_c0;
+                        v = v * *(const f4 *)(e.post_mul + q) + *(const f4 *)(e.post_add + q);
+                    }
                     *(f4 *)(yb + (long long)m * a.ycs) = v;
+                    if (EXTRA && e.dup_src) {
+                        f4 d = e.dup_a * *(const f4 *)(e.dup_src + (long long)m * e.dup_cs + nq) + dsb4;
+                        *(f4 *)(yb + (long long)m * a.ycs + e.dup_off) = act4(d);
+                    }
                 }
             }
             continue;
@@ -627,7 +656,7 @@ __device__ __forceinline__ void epilogue_tile_map(const ConvArgs &a, float *Cs, 
                 if (e.res_after) v += rv;
                 yb[q * a.ycs] = v;
             }
-        } else if (a.y_step <= 1 && a.d2s_c <= 0 && (!e.res || e.res_simple)) {
+        } else if (a.y_step <= 1 && a.d2s_c <= 0 && (!e.res || e.res_simple) && !extra) {
             // per-(image, channel) scale and / or per-pixel add on a dense output (GPEN / GFPGAN StyledConv:
             // demod scale + noise): the row's image index advances incrementally instead of a division per
             // element (store_epilogue), which made the epilogue as long as the main loop of a 64-channel tile
@@ -678,14 +707,14 @@ __device__ __forceinline__ void epilogue_tile_map(const ConvArgs &a, float *Cs, 
             }
         } else {
 #pragma unroll 1
-            for (int rr = tid / TPR; rr < clim; rr += RSTEP) store_epilogue(a, bidx, cb + rr, n, Cs[rr * LDC + cn]);
+            for (int rr = tid / TPR; rr < clim; rr += RSTEP) store_epilogue<EXTRA>(a, bidx, cb + rr, n, Cs[rr * LDC + cn]);
         }
     }
 }
 
 // 32x32 MFMA accumulators (C/D map: lane owns column li of each tile, rows (r&3) + 8(r>>2) + 4 lh)
 // held by NW waves laid out WAVES_M x NW/WAVES_M
-template <int BM, int BN, int WAVES_M, int TM, int TN, int NW = 4, int CH = BM>
+template <int BM, int BN, int WAVES_M, int TM, int TN, int NW = 4, int CH = BM, bool EXTRA = true>
 __device__ __forceinline__ void epilogue_tile(const ConvArgs &a, const floatx16 (&acc)[TM][TN], float *Cs, int tid,
                                               int m0, int n0, int bz, int bidx) {
     constexpr int WAVES_N = NW / WAVES_M;
@@ -694,7 +723,7 @@ __device__ __forceinline__ void epilogue_tile(const ConvArgs &a, const floatx16 
     const int lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WAVES_N, wn = wave % WAVES_N;
     const int li = lane & 31, lh = lane >> 5;
-    epilogue_tile_fn<BM, BN, NW, CH>(a, Cs, tid, m0, n0, bz, bidx, [&](float *C, int c0) {
+    epilogue_tile_fn<BM, BN, NW, CH, EXTRA>(a, Cs, tid, m0, n0, bz, bidx, [&](float *C, int c0) {
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
             const int r0 = wm * WTM + i * 32 - c0;

@@ -271,7 +271,9 @@ constexpr int x3_chunk(int bm, int bn, int smem) {
 // loop-invariant offsets plus a scalar K offset.  The host picks it when the x slab and the weights
 // fit 2^31 bytes and the filter has <= 32 taps.
 // One output tile: L is its linear index in the (gx, gy, total / (gx gy)) tile grid.
-template <int BM, int BN, int WAVES_M, int NW, int KS, int PF, int AMODE_, int BKN, int ELT>
+// EXTRA = false: the persistent and grouped forms, which the host never gives the SFT / second-output
+// extras (their registers pushed the persistent 256x256 tile from 6 to 21 spilled VGPRs)
+template <int BM, int BN, int WAVES_M, int NW, int KS, int PF, int AMODE_, int BKN, int ELT, bool EXTRA = true>
 __device__ __forceinline__ void conv_x3_tile(const ConvArgs &a, int L, int gx, int gy, int total) {
     constexpr bool BUF = AMODE_ == 4;
     constexpr int AMODE = BUF ? 0 : AMODE_;
@@ -655,7 +657,7 @@ __device__ __forceinline__ void conv_x3_tile(const ConvArgs &a, int L, int gx, i
                     for (int r = 0; r < 4; ++r) bad |= !__builtin_isfinite(acc4[i][j][r]);
             if (bad) __hip_atomic_store(a.nonfinite, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        epilogue_tile_fn<BM, BN, NW, CH>(a, (float *)smem, tid, m0, n0, bz, bidx, [&](float *Cs, int c0) {
+        epilogue_tile_fn<BM, BN, NW, CH, EXTRA>(a, (float *)smem, tid, m0, n0, bz, bidx, [&](float *Cs, int c0) {
             constexpr int LDC = BN + 4;
 #pragma unroll
             for (int i = 0; i < TM16; ++i) {
@@ -669,7 +671,7 @@ __device__ __forceinline__ void conv_x3_tile(const ConvArgs &a, int L, int gx, i
             }
         });
     } else {
-        epilogue_tile<BM, BN, WAVES_M, TM, TN, NW, CH>(a, acc, (float *)smem, tid, m0, n0, bz, bidx);
+        epilogue_tile<BM, BN, WAVES_M, TM, TN, NW, CH, EXTRA>(a, acc, (float *)smem, tid, m0, n0, bz, bidx);
     }
 }
 
@@ -694,7 +696,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3_persist(ConvArgs a) 
     const int total = a.vgrid_x * a.vgrid_y * a.vgrid_z;
 #pragma unroll 1
     for (int L = blockIdx.x; L < total; L += gridDim.x) {
-        conv_x3_tile<BM, BN, WAVES_M, NW, KS, PF, AMODE_, BKN, ELT>(a, L, a.vgrid_x, a.vgrid_y, total);
+        conv_x3_tile<BM, BN, WAVES_M, NW, KS, PF, AMODE_, BKN, ELT, false>(a, L, a.vgrid_x, a.vgrid_y, total);
         __syncthreads();     // the epilogue's LDS reads end before the next tile's operand stores
     }
     launch_stamp(a, true);
@@ -710,7 +712,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_igemm_x3_group(ConvGroup g) {
 #pragma unroll
     for (int i = 1; i < kConvGroupMax; ++i)
         if (i < g.n && L >= g.start[i]) p = i;
-    conv_x3_tile<BM, BN, WAVES_M, NW, KS, PF, 4, 0, ELT>(g.a[p], L - g.start[p], g.gx[p], g.gy[p],
+    conv_x3_tile<BM, BN, WAVES_M, NW, KS, PF, 4, 0, ELT, false>(g.a[p], L - g.start[p], g.gx[p], g.gy[p],
                                                          g.start[p + 1] - g.start[p]);
 }
 

@@ -287,13 +287,28 @@ std::vector<int64_t> conv2d_(const Tensor &x, const Tensor &y, const Tensor &wt,
                              int64_t act, double alpha, int64_t out_step, bool out_pool, bool x_split, const OptT &ws,
                              int64_t grid_cap, int64_t force_tile, int64_t force_splits, const OptT &stamps,
                              const OptT &stamp_ctr, at::IntArrayRef stamp_pos, double x_scale, const OptT &nonfinite,
-                             bool dry) {
+                             bool dry, const OptT &post_mul, const OptT &post_add, int64_t post_c0, const OptT &dup_src,
+                             const OptT &dup_bias, double dup_a, int64_t dup_off) {
     const c10::DeviceGuard guard(x.device());
     const at::Device dev = x.device();
     s2v_conv_params p{};
     conv_common(p, x, y, cout, kernel, stride, padding, dilation, in_mode, pad_mode, scale, shift, pix_add, pix_w, res,
                 res_offset, res_after_act, act, alpha, out_step, out_pool, x_split, false, prec, force_tile,
                 force_splits);
+    if (has(post_mul) || has(post_add)) {      // SFT fold: NHWC views of the output's pixels, cout - post_c0 channels
+        TORCH_CHECK(has(post_mul) && has(post_add), "conv: post_mul and post_add go together");
+        const NV mv = nhwc(*post_mul, dev, "conv post_mul"), av = nhwc(*post_add, dev, "conv post_add");
+        TORCH_CHECK(mv.n == p.n && mv.h == p.oh && mv.w == p.ow && mv.c == cout - post_c0 && av.n == mv.n &&
+                        av.h == mv.h && av.w == mv.w && av.c == mv.c && av.cs == mv.cs,
+                    "conv post_mul / post_add: [N, OH, OW, cout - post_c0] views of one pitch");
+        p.post_mul = mv.p; p.post_add = av.p; p.post_cs = mv.cs; p.post_c0 = (int)post_c0;
+    }
+    if (has(dup_src)) {                         // second output: act(dup_a * dup_src + dup_bias) at channel dup_off
+        const NV dv = nhwc(*dup_src, dev, "conv dup_src");
+        TORCH_CHECK(dv.n == p.n && dv.h == p.oh && dv.w == p.ow && dv.c == cout, "conv dup_src: [N, OH, OW, cout]");
+        p.dup_src = dv.p; p.dup_cs = dv.cs; p.dup_a = (float)dup_a; p.dup_off = (int)dup_off;
+        p.dup_bias = vec(dup_bias, dev, cout, "conv dup_bias");
+    }
     f32(wt, dev, "conv wt");
     TORCH_CHECK(wt.dim() == 2 && wt.is_contiguous() && wt.size(0) >= cout, "conv wt: packed [npad, kpad]");
     p.wt = wt.data_ptr<float>(); p.npad = (int)wt.size(0); p.kpad = (int)wt.size(1);
@@ -1024,7 +1039,8 @@ TORCH_LIBRARY_FRAGMENT(s2v, m) {
           "float pix_w, Tensor? res, int[2] res_offset, bool res_after_act, int act, float alpha, int out_step, "
           "bool out_pool, bool x_split, Tensor? ws, int grid_cap, int force_tile, int force_splits, "
           "Tensor(s!)? stamps, Tensor? stamp_ctr, int[3] stamp_pos, float x_scale, Tensor(f!)? nonfinite, "
-          "bool dry) -> int[]");
+          "bool dry, Tensor? post_mul=None, Tensor? post_add=None, int post_c0=0, Tensor? dup_src=None, "
+          "Tensor? dup_bias=None, float dup_a=0., int dup_off=0) -> int[]");
     m.def("modulated_conv2d_(Tensor x, Tensor(a!) y, Tensor wt, Tensor s, Tensor? d, Tensor(b!) wbuf, int cout, "
           "int[2] kernel, int[2] padding, int in_mode, int prec, bool x_split, Tensor? scale, Tensor? shift, "
           "Tensor? pix_add, "

@@ -23,6 +23,9 @@ from ..ops import NHWC, ConvW
 from .enet import StyleLayer
 
 LRELU = 0.2
+# SFT (gfpganv1_clean_arch.py:98-106: out[:, half:] = out[:, half:] * scale + shift) folded into the StyleConv's
+# epilogue (ops.conv2d post=); S2V_GFPGAN_FOLD_SFT=0: a separate elementwise pass
+FOLD_SFT = os.environ.get("S2V_GFPGAN_FOLD_SFT", "1") == "1"
 # ToRGB and its bilinear x2 skip upsample as one pass (ops.torgb_up2, as ENet's); S2V_GFPGAN_FUSED_TORGB=0:
 # resize + small conv with the residual
 FUSED_TORGB = os.environ.get("S2V_GFPGAN_FUSED_TORGB", "1") == "1"
@@ -123,7 +126,7 @@ class GFPGANEngine:
         o = self.style_off[id(L)]
         return sall[:, o: o + L.cin]
 
-    def _style_conv(self, ctx, L, x: NHWC, sall, dall, noise):
+    def _style_conv(self, ctx, L, x: NHWC, sall, dall, noise, post=None):
         b, dev = x.n, self.device
         s = self._style(L, sall)
         if L.upsample:
@@ -134,7 +137,7 @@ class GFPGANEngine:
         d = dall[:, r0: r0 + L.cout]
         y = NHWC.empty(b, x.h, x.w, L.cout, dev)
         ops.conv2d(ctx, x, L.conv, y, in_scale=s, nc_scale=d, act=ops.ACT_LRELU, alpha=LRELU,
-                   pix_add=noise if L.noise_w else None, pix_w=L.noise_w or 0.0)
+                   pix_add=noise if L.noise_w else None, pix_w=L.noise_w or 0.0, post=post)
         return y
 
     def forward(self, ctx, x: torch.Tensor, out: torch.Tensor, return_rgb=True, randomize_noise=True, noises=None):
@@ -203,12 +206,19 @@ class GFPGANEngine:
         ops.conv2d(ctx, cur, self.rgb1.conv, skip.slice(0, 3), in_scale=s)
         i = 1
         for lvl in range(self.levels):
-            cur = self._style_conv(ctx, self.convs[2 * lvl], cur, sall, dall, noise[2 * lvl + 1])
+            post = None
             if i < 2 * len(conds):
                 scale, shift = conds[(i - 1) // 2]
-                half = cur.c // 2 if self.sft_half else 0
-                part = cur.slice(half, cur.c - half)
-                ops.eltwise(ctx, part, part, mul=scale, add=shift)
+                c = self.convs[2 * lvl].cout
+                half = c // 2 if self.sft_half else 0
+                post = (scale, shift, half)
+            if FOLD_SFT:                                      # the SFT in the StyleConv's epilogue
+                cur = self._style_conv(ctx, self.convs[2 * lvl], cur, sall, dall, noise[2 * lvl + 1], post=post)
+            else:
+                cur = self._style_conv(ctx, self.convs[2 * lvl], cur, sall, dall, noise[2 * lvl + 1])
+                if post is not None:
+                    part = cur.slice(post[2], cur.c - post[2])
+                    ops.eltwise(ctx, part, part, mul=post[0], add=post[1])
             cur = self._style_conv(ctx, self.convs[2 * lvl + 1], cur, sall, dall, noise[2 * lvl + 2])
             R = self.rgbs[lvl]
             rgb = NHWC.empty(b, cur.h, cur.w, 4, dev)

@@ -19,6 +19,7 @@ sqrt(2) * lrelu(v + b) == lrelu(sqrt(2) v + sqrt(2) b)).  Per layer:
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -27,6 +28,11 @@ from ..ops import NHWC, ConvW
 
 LRELU = 0.2
 SQ2 = math.sqrt(2.0)
+# NoiseInjection's concat half (gpen_model.py:292-302): S2V_GPEN_FOLD_NOISE=1 writes it from the StyledConv's
+# epilogue as a second output (ops.conv2d dup=) on the non-upsampling layers.  Off by default: measured 0.4 %
+# slower on the enhance workload (the epilogue's extra dependent loads cost the conv more than the separate
+# pass costs, MI355X A/B r06)
+FOLD_NOISE = os.environ.get("S2V_GPEN_FOLD_NOISE", "0") == "1"
 
 
 class _StyledLayer:
@@ -116,6 +122,11 @@ class GPENEngine:
             t = NHWC.empty(b, oh, ow, C, dev)
             ops.conv2d(ctx, x, L.conv, t, in_scale=s, nc_scale=d)
             ops.fir2d(ctx, t, L.blur, out.slice(0, C), pad0=(1, 1), bias=L.bias_a, act=ops.ACT_LRELU, alpha=LRELU)
+        elif FOLD_NOISE:
+            # the concat half in the same epilogue: out[.., C + n] = lrelu(sqrt2 (w e + b)) of the encoder feature e
+            ops.conv2d(ctx, x, L.conv, out.slice(0, C), in_scale=s, nc_scale=d, shift=L.bias_a,
+                       act=ops.ACT_LRELU, alpha=LRELU, dup=(noise, L.bias_n, SQ2 * L.noise_w, C))
+            return out
         else:
             ops.conv2d(ctx, x, L.conv, out.slice(0, C), in_scale=s, nc_scale=d, shift=L.bias_a,
                        act=ops.ACT_LRELU, alpha=LRELU)

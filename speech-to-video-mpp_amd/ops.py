@@ -530,11 +530,19 @@ def _ptr(t):
 
 def conv2d(ctx: Ctx, x: NHWC, cw: ConvW, y: NHWC, *, act=ACT_NONE, alpha=0.0, res: NHWC | None = None,
            res_after=False, res_offset=(0, 0), nc_scale=None, in_scale=None, pre_act=ACT_NONE, pre_alpha=0.0,
-           pix_add=None, pix_w=0.0, scale=None, shift=None, force_tile=0, force_splits=0, pool=False):
+           pix_add=None, pix_w=0.0, scale=None, shift=None, force_tile=0, force_splits=0, pool=False, post=None,
+           dup=None):
     """Fused conv (s2v_conv_params, dispatched as ``s2v::conv2d_``).  nc_scale / in_scale: [N, C]
     device tensors.  A transposed ConvW with a polyphase plan (``cw.poly``) runs as one stride-1 conv
     per output parity class, each writing every second pixel of y.  ``pool``: y is the 2x2 average
-    pool of the activated conv output (half the conv's size)."""
+    pool of the activated conv output (half the conv's size).
+    ``post`` = (mul, add, c0): SFT on output channels >= c0 after the activation, y = v * mul + add with
+    mul / add NHWC views of y's pixels over cout - c0 channels (gfpganv1_clean_arch.py:98-106).
+    ``dup`` = (src, bias, a, off): a second output y.t[..., off + n] = act(a * src[..., n] + bias[n]) in
+    the same epilogue, src an NHWC view of y's pixels over cout channels (GPEN's noise-injection concat
+    half, gpen_model.py:292-302)."""
+    assert (post is None and dup is None) or (cw.rowpack is None and getattr(cw, "poly", None) is None), \
+        "conv: post / dup epilogues on plain (not row-packed, not polyphase) convs only"
     if cw.rowpack is not None:
         # small-channel wide-kernel conv: row-tap packed input, kh x 1 conv over the packed channels
         assert x.c == cw.cin, f"conv: input has {x.c} channels, weights expect {cw.cin}"
@@ -565,8 +573,19 @@ def conv2d(ctx: Ctx, x: NHWC, cw: ConvW, y: NHWC, *, act=ACT_NONE, alpha=0.0, re
     f = 2 if pool else 1
     assert (y.n, y.h * f, y.w * f, y.c) == (x.n, oh, ow, cw.cout), \
         f"conv: output view {(y.n, y.h, y.w, y.c)} != {(x.n, oh // f, ow // f, cw.cout)}"
+    extra = {}
+    if post is not None:
+        pm, pa, c0 = post
+        assert (pm.n, pm.h, pm.w, pm.c) == (y.n, y.h, y.w, cw.cout - c0) and (pa.n, pa.h, pa.w, pa.c) == (pm.n, pm.h,
+                                                                                                         pm.w, pm.c)
+        extra.update(post_mul=pm.v, post_add=pa.v, post_c0=int(c0))
+    if dup is not None:
+        ds, db, da, off = dup
+        assert (ds.n, ds.h, ds.w, ds.c) == (y.n, y.h, y.w, cw.cout)
+        assert y.coff == 0 and off >= cw.cout and off + cw.cout <= y.cs, "dup: second output inside y's pixel pitch"
+        extra.update(dup_src=ds.v, dup_bias=db, dup_a=float(da), dup_off=int(off))
     _conv(ctx, x, cw, y.v, 1, act, alpha, None if res is None else res.v, res_after, res_offset, nc_scale, in_scale,
-          pre_act, pre_alpha, pix_add, pix_w, scale, shift, force_tile, force_splits, pool=pool)
+          pre_act, pre_alpha, pix_add, pix_w, scale, shift, force_tile, force_splits, pool=pool, extra=extra)
     return y
 
 
@@ -588,7 +607,7 @@ def conv_key(x, cw, yv, out_step, pool, prec) -> str:
 
 
 def _conv(ctx, x, cw, yv, out_step, act, alpha, resv, res_after, res_offset, nc_scale, in_scale, pre_act, pre_alpha,
-          pix_add, pix_w, scale, shift, force_tile, force_splits, pool=False):
+          pix_add, pix_w, scale, shift, force_tile, force_splits, pool=False, extra=None):
     """One ``s2v::conv2d_`` launch: x an NHWC view, yv / resv torch views (out_step 2: a strided
     parity-class view of a wider tensor)."""
     prec = prec_code()
@@ -614,7 +633,7 @@ def _conv(ctx, x, cw, yv, out_step, act, alpha, resv, res_after, res_offset, nc_
                            [cw.dh, cw.dw], cw.in_mode, cw.pad_mode, prec, sc, sh, in_scale, nc_scale, pre_act, pre_alpha,
                            pix_add, pix_w, resv, list(res_offset), res_after, act, alpha, out_step, pool, x_split != 0,
                            ws, cap, force_tile if ft is None else ft, force_splits if fs is None else fs, st[0], st[1],
-                           st[2], xscale, flag, dry)
+                           st[2], xscale, flag, dry, **(extra or {}))
     if TUNE is not None and key is not None:
         TUNE(ctx, key, lambda ft, fs: _with_ws(ctx, lambda ws: launch(ws, False, _NOSTAMP, ft, fs)[0]),
              lambda ft, fs: launch(ctx.ws.tensor(), True, _NOSTAMP, ft, fs)[1:], yv, resv)

@@ -42,8 +42,13 @@ class _NoOps:
         schema = getattr(self.ns, name).default._schema
         args = schema.arguments
 
-        def fn(*a):
-            assert len(a) == len(args), f"{name}: {len(a)} args, schema has {len(args)}"
+        def fn(*a, **kw):
+            # positional arguments, then keywords; the rest must carry schema defaults
+            names = [arg.name for arg in args]
+            assert len(a) <= len(args) and all(k in names[len(a):] for k in kw), f"{name}: bad arguments {sorted(kw)}"
+            for arg in args[len(a):]:
+                assert arg.name in kw or arg.has_default_value(), f"{name}: missing {arg.name}"
+            a = tuple(a) + tuple(kw.get(arg.name) if arg.name in kw else arg.default_value for arg in args[len(a):])
             for v, arg in zip(a, args):
                 t = str(arg.type)
                 if t == "Tensor":
@@ -78,7 +83,7 @@ def test_gfpgan_plan(dry):
     for rn in (True, False):
         _, rgbs = eng.forward(ops.Ctx("cpu"), x, out, return_rgb=True, randomize_noise=rn)
     assert [r.shape[-1] for r in rgbs] == [8, 16, 32, 64, 128, 256, 512]
-    assert dry.calls.get("modulated_conv2d_", 0) + dry.calls["conv2d_"] > 120 and dry.calls["eltwise_"] == 2 * 14
+    assert dry.calls.get("modulated_conv2d_", 0) + dry.calls["conv2d_"] > 120 and dry.calls["eltwise_"] == 14   # the U-Net skip adds (SFT in the epilogues)
 
 
 def test_gpen_plan(dry):
@@ -86,7 +91,15 @@ def test_gpen_plan(dry):
     eng = GPENEngine(synth_sd("gpen"), "cpu")
     x = torch.zeros(2, 3, 512, 512)
     eng.forward(ops.Ctx("cpu"), x, torch.empty_like(x))
-    assert dry.calls["fir2d_"] == 7 + 7 + 7 and dry.calls["eltwise_"] == 15
+    assert dry.calls["fir2d_"] == 7 + 7 + 7 and dry.calls["eltwise_"] == 15  # the 15 noise-concat halves
+    from s2v_amd.engine import gpen
+    calls = dict(dry.calls)
+    gpen.FOLD_NOISE, prev = True, gpen.FOLD_NOISE
+    try:
+        eng.forward(ops.Ctx("cpu"), x, torch.empty_like(x))
+    finally:
+        gpen.FOLD_NOISE = prev
+    assert dry.calls["eltwise_"] - calls["eltwise_"] == 7     # folded: only the upsampling layers' halves
 
 
 def test_lipsync_engines_plan(dry):

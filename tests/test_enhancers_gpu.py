@@ -72,8 +72,12 @@ def test_gfpgan_matches_reference(prec, gfpgan, golden):
     print("gfpgan out max err", err)
 
 
-def test_gfpgan_batch_vs_oracle_and_noise(gfpgan):
+@pytest.mark.parametrize("fold", [True, False])
+def test_gfpgan_batch_vs_oracle_and_noise(gfpgan, fold, monkeypatch):
+    """Both SFT forms: in the StyleConv epilogue (engine/gfpgan.py FOLD_SFT) and as its own pass."""
     from oracle import enhancers
+    from s2v_amd.engine import gfpgan as eng
+    monkeypatch.setattr(eng, "FOLD_SFT", fold)
     x = torch.from_numpy(synth.face_inputs("gfpgan.b2", 2))
     img, _ = gfpgan(x.to(DEV), return_rgb=False, randomize_noise=False)
     with torch.no_grad():
@@ -109,8 +113,13 @@ def test_gpen2048_matches_reference(prec, golden):
     print(f"gpen2048 {prec} out max err {err:.2e} (|out| max {g['out_stats'][2]:.2f})")
 
 
-def test_gpen_batch_vs_oracle(gpen):
+@pytest.mark.parametrize("fold", [False, True])
+def test_gpen_batch_vs_oracle(gpen, fold, monkeypatch):
+    """Both noise-concat forms: a separate pass (the default) and the StyleConv epilogue's second output
+    (engine/gpen.py FOLD_NOISE)."""
     from oracle import enhancers
+    from s2v_amd.engine import gpen as eng
+    monkeypatch.setattr(eng, "FOLD_NOISE", fold)
     x = torch.from_numpy(synth.face_inputs("gpen.b2", 2))
     img, none = gpen(x.to(DEV))
     assert none is None

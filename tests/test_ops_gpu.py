@@ -1104,3 +1104,40 @@ def test_f16_split_variants_bit_identical():
     assert rc == 0, lib.s2v_last_error()
     torch.cuda.synchronize()
     assert int(m.item()) == 0, f"{int(m.item())} of {x.numel() // 4} float4s differ"
+
+
+@pytest.mark.parametrize("tile,splits", [(0, 0), (1, 0), (4, 0), (4, 3), (8, 0), (11, 0), (18, 0), (18, 2), (20, 0)])
+@pytest.mark.parametrize("nc", [False, True])
+def test_conv2d_post_and_dup_epilogue(ctx, prec, tile, splits, nc):
+    """The epilogue extras of the enhancers' StyleConvs, against fp64: ``post`` (GFPGAN's SFT on the
+    upper half of the channels after the activation, gfpganv1_clean_arch.py:98-106) and ``dup`` (GPEN's
+    noise-injection concat half as a second output beside the conv's, gpen_model.py:292-302), with and
+    without the per-(image, channel) demodulation scale, through the LDS tiles, split-K (the split-K fold's
+    epilogue) and the halo tile."""
+    if tile > 6 and prec == "f32":
+        pytest.skip("tiles 7-20 exist in the split-precision table only")
+    n, cin, h, w, cout = 2, 64, 8, 64, 256 if tile == 1 else 64       # (the 256x256 tile needs 256 channels)
+    c0 = cout // 2
+    wt = rnd(cout, cin, 3, 3, seed=71) / math.sqrt(cin * 9)
+    bias = rnd(cout, seed=72)
+    x = rnd(n, cin, h, w, seed=73)
+    d = rnd(n, cout, seed=74, lo=0.5, hi=1.5)
+    pm, pa = rnd(n, cout - c0, h, w, seed=75), rnd(n, cout - c0, h, w, seed=76)
+    ds, db = rnd(n, cout, h, w, seed=77), rnd(cout, seed=78)
+    cw = ConvW(wt.float(), bias.float(), DEV, padding=1)
+    full = NHWC.empty(n, h, w, 2 * cout, DEV)
+    y = full.slice(0, cout)
+    ops.conv2d(ctx, nhwc(x.float()), cw, y, act=ops.ACT_LRELU, alpha=0.2,
+               nc_scale=d.float().to(DEV) if nc else None, force_tile=tile, force_splits=splits,
+               post=(nhwc(pm.float()), nhwc(pa.float()), c0),
+               dup=(nhwc(ds.float()), db.float().to(DEV), 0.7, cout))
+    scale = d[:, :, None, None] if nc else torch.ones(1, cout, 1, 1, dtype=torch.float64)
+    v = F.leaky_relu(F.conv2d(x, wt, padding=1) * scale + bias[None, :, None, None], 0.2)
+    bound = conv_bound(x, wt, 1, 1, 1) * scale.abs()
+    v[:, c0:] = v[:, c0:] * pm + pa
+    bound[:, c0:] = bound[:, c0:] * pm.abs()
+    got = to_nchw(full)
+    err = (got[:, :cout] - v).abs()
+    assert (err <= REL[prec] * (bound + 1) + 1e-6).all(), f"main: max err {err.max():.3e}"
+    dref = F.leaky_relu(0.7 * ds + db[None, :, None, None], 0.2)
+    assert (got[:, cout:] - dref).abs().max() < 1e-6
