@@ -315,7 +315,7 @@ def _peak(sym):
     return X3_PEAK_TFLOPS if any(k in sym for k in X3_KERNELS) else FP32_MFMA_PEAK_TFLOPS
 
 
-PMC_ROUND = "r05"     # only this round's PMC passes describe the current build
+PMC_ROUND = "r06"     # only this round's PMC passes describe the current build
 
 
 def pmc_traffic(workload, sym, grid=None):

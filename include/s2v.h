@@ -585,10 +585,12 @@ int s2v_tensor2img_u8(const float *x, int n, int h, int w, unsigned char *y, s2v
  * of an H x W frame: erosion [wh][ww] fp32 = cv2.erode(warpAffine(ones(S, S) fp32, M), ones((2, 2)))
  * (frame coordinates) with M the device fp64 2x3 inverse affine (warpAffine inverts it again, as OpenCV
  * does); area[0] (device fp64) = the sum of the erosion over the window, in a fixed order; area holds
- * 1 + 512 doubles (area[1..] are the per-block partials).  A window holding the warped crop's whole
+ * 1 + s2v_restore_parts() doubles (area[1..] are the per-block partials).  A window holding the warped crop's whole
  * footprint gives the frame's sum. */
 int s2v_restore_mask(const double *M, int S, int H, int W, int y0, int x0, int wh, int ww, float *erosion,
                      double *area, s2v_stream_t stream);
+/* The per-block partial count of s2v_restore_mask: its area buffer holds 1 + s2v_restore_parts() doubles. */
+int s2v_restore_parts(void);
 /* cv2.erode(x, ones((k, k), uint8)) on an fp32 [h][w] image (anchor k / 2, border never wins);
  * ws: h * w floats, distinct from x and y. */
 int s2v_erode_rect_f32(const float *x, int h, int w, int k, float *y, float *ws, s2v_stream_t stream);

@@ -70,7 +70,9 @@ def landmarks_5(bboxes, h, w, only_center_face=False, eye_dist_threshold=None):
     pad_blur) on detect_faces' rows -> (det_faces, all_landmarks_5)."""
     det_faces, lms = [], []
     for bbox in bboxes:
-        eye_dist = np.linalg.norm([bbox[5] - bbox[7], bbox[6] - bbox[8]])
+        # facexlib 0.2.5's expression as published, index quirk included (bbox[5:7] / [7:9] are the eyes;
+        # it differences [6]-[8] and [7]-[9]); facexlib is not vendored, so this is restated, parity unpinned
+        eye_dist = np.linalg.norm([bbox[6] - bbox[8], bbox[7] - bbox[9]])
         if eye_dist_threshold is not None and eye_dist < eye_dist_threshold:
             continue
         lms.append(np.array([[bbox[i], bbox[i + 1]] for i in range(5, 15, 2)]))

@@ -161,6 +161,7 @@ _SIGS = {
                                         _c_int, _c_ll, _c_ll, _vp, _vp]),
     "s2v_tensor2img_u8": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _vp]),
     "s2v_restore_mask": (_c_int, [_vp] + [_c_int] * 7 + [_vp, _vp, _vp]),
+    "s2v_restore_parts": (_c_int, []),
     "s2v_erode_rect_f32": (_c_int, [_vp, _c_int, _c_int, _c_int, _vp, _vp, _vp]),
     "s2v_restore_paste": (_c_int, [_vp, _c_int, _vp, _vp, _vp] + [_c_int] * 4 + [_vp, _c_int, _vp, _c_int, _c_int,
                                                                              _c_int, _vp]),

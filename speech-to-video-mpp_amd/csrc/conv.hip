@@ -942,7 +942,7 @@ static const X3Cfg kX3Tiles[] = {
     // ... with the B fragments loaded by every wave into registers too: no LDS, no barrier per slice
     {{256, 64, 4, 4, 1, 1}, 0.f, 2, 2},
     // 4 x 64 output patches, 64 channels, the 6 x 66 input halo per channel slice staged once
-    // (conv_x3_halo.hip): 3x3 stride-1 zero-padded convs with oh % 4 == 0, ow % 64 == 0
+    // (conv_x3_halo.hip): 3x3 stride-1 zero-padded convs (ragged images: partly empty last patches)
     {{256, 64, 4, 4, 1, 1}, 0.f, 2, 3},
     // ... 8 x 64 patches, one 512-thread block per CU (oh % 8 == 0)
     {{512, 64, 8, 8, 1, 1}, 0.f, 1, 4},
@@ -1275,7 +1275,8 @@ static int validate(const s2v_conv_params *p, int &M, int &K) {
     S2V_REQUIRE(!(tiled_x3(p) && p->force_tile > 0 && !x3_kind_ok(p, kX3Tiles[p->force_tile - 1].kind)),
                 "conv2d: force_tile %d (conv_x3_nar / conv_x3_halo) needs a direct zero-padded conv, cin %% 32 == 0, "
                 "<= 32 taps, no pooling, packed weights over whole 64-row slabs, 2^31-byte offsets and, with "
-                "in_scale, oh * ow %% 256 == 0; conv_x3_halo also 3x3 stride 1 pad 1, oh %% 4 == 0, ow %% 64 == 0",
+                "in_scale, oh * ow %% 256 == 0; conv_x3_halo also 3x3 stride 1 pad 1 (ragged images run partly empty "
+                "patches), and its 8-row form oh %% 8 == 0",
                 p->force_tile);
     if (tiled_x3(p) && p->force_tile > 0) {
         // a forced tile must not read weight rows past the packed [npad] rows (the planner never

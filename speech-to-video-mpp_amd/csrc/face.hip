@@ -790,6 +790,8 @@ extern "C" int s2v_tensor2img_u8(const float *x, int n, int h, int w, unsigned c
     return check_launch("tensor2img_u8");
 }
 
+extern "C" int s2v_restore_parts(void) { return RESTORE_PARTS; }
+
 extern "C" int s2v_restore_mask(const double *M, int S, int H, int W, int y0, int x0, int wh, int ww,
                                 float *erosion, double *area, s2v_stream_t stream) {
     S2V_REQUIRE(M && erosion && area && S > 0 && H > 0 && W > 0, "restore_mask: bad args");

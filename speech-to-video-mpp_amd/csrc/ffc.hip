@@ -671,7 +671,9 @@ extern "C" int s2v_ffc_norm(const float *y, int ycs, int n, int h, const float *
                             int pad_cs, int *flag, int prec, s2v_stream_t stream) {
     const int c = s2v_ffc_channels(h), cc = (c - c / 4) / 2;
     S2V_REQUIRE(y && u && w2 && out && c > 0, "ffc_norm: bad args");
-    S2V_REQUIRE(ycs >= c && out_cs >= c && out_cs % 4 == 0 && ((uintptr_t)out % 16) == 0 &&
+    // y is read with float4 loads (and may be ``out`` itself: LNet normalises in place)
+    S2V_REQUIRE(ycs >= c && ycs % 4 == 0 && ((uintptr_t)y % 16) == 0 && out_cs >= c && out_cs % 4 == 0 &&
+                ((uintptr_t)out % 16) == 0 &&
                 (!res || (res_cs >= c && res_cs % 4 == 0 && ((uintptr_t)res % 16) == 0)) &&
                 (!pad || (pad_cs >= c && pad_cs % 4 == 0 && ((uintptr_t)pad % 16) == 0)) && ((uintptr_t)u % 16) == 0,
                 "ffc_norm: channel pitches / alignment");

@@ -1083,7 +1083,8 @@ TORCH_LIBRARY_FRAGMENT(s2v, m) {
           "Tensor tables, Tensor(a!) t1, Tensor(b!) spec, Tensor? flag, int prec) -> ()");
     m.def("ffc_spec_inv_(Tensor spec, Tensor wfu, float wt_scale, float x_scale, Tensor? scale, Tensor? shift, "
           "Tensor tables, Tensor t1, Tensor(a!) u, Tensor? flag, int prec) -> ()");
-    m.def("ffc_norm_(Tensor y, Tensor u, Tensor w2, float wt_scale, float x_scale, Tensor? gamma, Tensor? beta, "
+    // y may be the same tensor as out (LNet normalises in place), hence mutable
+    m.def("ffc_norm_(Tensor(c!) y, Tensor u, Tensor w2, float wt_scale, float x_scale, Tensor? gamma, Tensor? beta, "
           "float eps, int act, float alpha, Tensor? res, Tensor(a!) out, Tensor(b!)? pad_out, Tensor? flag, int prec) -> ()");
     m.def("eltwise_(Tensor x, Tensor? mul, Tensor? add, Tensor? bias, float a, int act, float alpha, float post, "
           "Tensor(a!) y) -> ()");

@@ -72,6 +72,14 @@ class RetinaFaceDetector:
         return np.concatenate((bounding_boxes[keep, :], landms[keep]), axis=1)
 
 
+def edge_boundary(area) -> bool:
+    """True when int(sqrt(area)) // 20 (facexlib's w_edge) could change with the last bits of an fp32
+    area: sqrt(area) within 1e-4 (relative) of a multiple of 20, where a device sum in another order than
+    numpy's pairwise np.sum may land on the other side."""
+    r = float(area) ** 0.5
+    return r >= 20.0 and abs(r - 20.0 * round(r / 20.0)) <= 1e-4 * r
+
+
 def get_largest_face(det_faces, h, w):
     """facexlib get_largest_face: the face with the largest box area after clipping the box to the image."""
     def clip(v, n):
@@ -222,7 +230,9 @@ class FaceRestoreHelper:
             raise NotImplementedError("get_face_landmarks_5: resize is not on the GFPGANer path")
         bboxes = self.face_det.detect_faces(self.input_img, CONF_THRESHOLD)
         for bbox in bboxes:
-            eye_dist = np.linalg.norm([bbox[5] - bbox[7], bbox[6] - bbox[8]])
+            # facexlib 0.2.5's expression as published, index quirk included (bbox[5:7] / [7:9] are the eyes;
+            # it differences [6]-[8] and [7]-[9]); facexlib is not vendored, so this is restated, parity unpinned
+            eye_dist = np.linalg.norm([bbox[6] - bbox[8], bbox[7] - bbox[9]])
             if eye_dist_threshold is not None and eye_dist < eye_dist_threshold:
                 continue
             self.all_landmarks_5.append(np.array([[bbox[i], bbox[i + 1]] for i in range(5, 15, 2)]))
@@ -283,7 +293,7 @@ class FaceRestoreHelper:
             return img.clone()                      # cv2.resize to the same size copies; astype(uint8)
         dev = self.device
         ctx = faces._ctx(dev)
-        area = torch.empty(1 + 512, dtype=torch.float64, device=dev)     # result + the block partials
+        area = torch.empty(1 + ctx.lib.s2v_restore_parts(), dtype=torch.float64, device=dev)   # result + partials
         acc = None
         out = torch.empty((h, w, 3), dtype=torch.uint8, device=dev)
         S = self.face_size[0]
@@ -309,6 +319,12 @@ class FaceRestoreHelper:
                 check(ctx.lib.s2v_restore_mask(md.data_ptr(), S, h, w, y0, x0, wh, ww, E.data_ptr(), area.data_ptr(),
                                                ctx.stream), "s2v_restore_mask")
                 total_face_area = np.float32(area[0].item())   # np.sum(inv_mask_erosion) (fp32)
+                if edge_boundary(total_face_area):
+                    # sqrt(area) within rounding of a multiple of 20: w_edge hangs on the last bits of the
+                    # sum, so take it as facexlib does, numpy's pairwise fp32 np.sum over the whole frame
+                    full = np.zeros((h, w), dtype=np.float32)
+                    full[y0: y0 + wh, x0: x0 + ww] = E.cpu().numpy()
+                    total_face_area = np.sum(full)
                 w_edge = int(total_face_area ** 0.5) // 20
                 k = w_edge * 2
                 assert k <= pad, (k, pad)

@@ -115,3 +115,12 @@ def test_largest_face_clips_boxes_to_the_image():
     for fn in (restore.get_largest_face, OR.get_largest_face):
         det, idx = fn(dets, 200, 220)
         assert idx == 1 and det is dets[1]
+
+
+def test_edge_boundary_guard():
+    """w_edge = int(sqrt(area)) // 20 flips at multiples of 20; near them the paste recomputes the area as
+    numpy's pairwise fp32 sum (facexlib's np.sum) instead of trusting the device sum's last bits."""
+    from s2v_amd.restore import edge_boundary
+    assert edge_boundary(np.float32(3600.0)) and edge_boundary(np.float32(3600.3)) and edge_boundary(np.float32(3599.8))
+    assert not edge_boundary(np.float32(3700.0)) and not edge_boundary(np.float32(63 * 63))
+    assert not edge_boundary(np.float32(0.0)) and not edge_boundary(np.float32(399.0))

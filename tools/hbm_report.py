@@ -36,6 +36,8 @@ _DNET = [
      "DNet 7x7 64->3 tanh head (DNet.py:77-86): in 16x256^2x64, out 16x256^2x3"),
     ("conv_halo_small<3, 7>", _b(16 * 256 * 256 * 64 * F, 16 * 256 * 256 * 3 * F),
      "DNet 7x7 64->3 tanh head, fp32 VALU form"),
+    ("conv_head_x3<1, 2, 7,", _b(16 * 64 * 64 * 256 * F, 16 * 64 * 64 * 2 * F),
+     "DNet 7x7 256->2 flow head (DNet.py:77-82), split-K over channel groups: in 16x64^2x256, out 16x64^2x2"),
     ("conv_halo_small<2, 7>", _b(16 * 64 * 64 * 256 * F, 16 * 64 * 64 * 2 * F),
      "DNet 7x7 256->2 flow head (DNet.py:77-82): in 16x64^2x256, out 16x64^2x2"),
     ("flow_warp_kernel<true>", _b(16 * 3 * 256 * 256 * F, 16 * 64 * 64 * 2 * F, 16 * 256 * 256 * 6 * F),
