@@ -28,8 +28,12 @@ namespace s2v {
 constexpr int kHeadM = 32;    // input columns of a strip (2 MFMA row blocks of 16)
 constexpr int kHeadT = kHeadM * 8;   // threads: 2 waves per row block (one per 16 filter columns)
 
-template <int ELT, int CO, int KS, int NCS>
+// RPI output rows per loop iteration (1 or 2): with 2, the KS + 1 ring rows of two output rows are each read
+// from LDS once and feed both rows' MFMA chains (six independent accumulators), and the P / barrier phase runs
+// once per two rows
+template <int ELT, int CO, int KS, int NCS, int RPI>
 __global__ __launch_bounds__(kHeadT) void conv_head_x3(ConvArgs a, int strips, int th) {
+    constexpr int RING = KS + RPI - 1;        // staged input rows
     constexpr int TW = kHeadM - KS + 1;       // output columns per strip
     constexpr int NSL = KS * NCS;             // K-slices: (ky, 32-channel slice)
     constexpr int SLB = kHeadM * 128;         // bytes of one 32-channel slice of a staged row
@@ -37,8 +41,8 @@ __global__ __launch_bounds__(kHeadT) void conv_head_x3(ConvArgs a, int strips, i
     constexpr int PLD = 33;                   // P row pitch (floats)
     static_assert(CO * KS <= 32, "N = Cout * KS must fit two 16-column blocks");
     static_assert(TW * CO <= kHeadT, "one shift-sum output per thread");
-    __shared__ __attribute__((aligned(16))) char ring[KS * ROWB];
-    __shared__ float P[kHeadM * PLD];
+    __shared__ __attribute__((aligned(16))) char ring[RING * ROWB];
+    __shared__ float P[RPI][kHeadM * PLD];
 
     launch_stamp(a, false);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -106,16 +110,16 @@ __global__ __launch_bounds__(kHeadT) void conv_head_x3(ConvArgs a, int strips, i
         split4<ELT>(v[0] * a.x_scale, h0, l0);
         split4<ELT>(v[1] * a.x_scale, h1, l1);
         const u32x4 hi = {h0.x, h0.y, h1.x, h1.y}, lo = {l0.x, l0.y, l1.x, l1.y};
-        const int off = (r % KS) * ROWB + scs * SLB + slot_off(sp, sq);
+        const int off = (r % RING) * ROWB + scs * SLB + slot_off(sp, sq);
         *(u32x4 *)(ring + off) = hi;
         *(u32x4 *)(ring + (off ^ 64)) = lo;
     };
-    {   // the first output row's KS input rows: all loads in flight at once
-        f4 v[KS][2];
+    {   // the first iteration's RING input rows: all loads in flight at once
+        f4 v[RING][2];
 #pragma unroll
-        for (int r = 0; r < KS; ++r) load_row(r, v[r]);
+        for (int r = 0; r < RING; ++r) load_row(r, v[r]);
 #pragma unroll
-        for (int r = 0; r < KS; ++r) store_row(r, v[r]);
+        for (int r = 0; r < RING; ++r) store_row(r, v[r]);
     }
     __syncthreads();
 
@@ -131,54 +135,90 @@ __global__ __launch_bounds__(kHeadT) void conv_head_x3(ConvArgs a, int strips, i
     const bool owner = tid < TW * CO && ox0 + oq < a.ow;
     const float esc = (owner && e.scale) ? e.scale[oo] : 1.f, esh = (owner && e.shift) ? e.shift[oo] : 0.f;
     float *__restrict__ yrow = a.y + (long long)img * a.oh * a.ow * a.ycs + (long long)(ox0 + oq) * a.ycs + oo;
-    for (int oy = oy0; oy < oy1; ++oy) {
-        const int rr = oy - oy0;              // ring row of ky = 0
-        const bool more = oy + 1 < oy1;
-        f4 nxt[2];
-        if (more) load_row(rr + KS, nxt);     // the next output row's new input row, under the MFMAs
-        // the three split products in separate accumulators: three independent MFMA chains
-        floatx4 acc[3] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    for (int oy = oy0; oy < oy1; oy += RPI) {
+        const int rr = oy - oy0;              // ring row of ky = 0 of the iteration's first output row
+        const bool more = oy + RPI < oy1;
+        f4 nxt[RPI][2];
+        if (more) {                           // the next iteration's new input rows, under the MFMAs
+#pragma unroll
+            for (int j = 0; j < RPI; ++j) load_row(rr + RING + j, nxt[j]);
+        }
+        // the three split products of each row in separate accumulators: 3 RPI independent MFMA chains
+        floatx4 acc[RPI][3];
+#pragma unroll
+        for (int j = 0; j < RPI; ++j)
+#pragma unroll
+            for (int q = 0; q < 3; ++q) acc[j][q] = floatx4{0.f, 0.f, 0.f, 0.f};
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int s = 0; s < NSL; ++s) {
-            const int ky = s / NCS, cs = s - (s / NCS) * NCS;
-            const int ro = ((rr + ky) % KS) * ROWB + cs * SLB;
-            const u32x4 ah = *(const u32x4 *)(ring + ro + aoff), al = *(const u32x4 *)(ring + ro + (aoff ^ 64));
-            acc[0] = mfma16x16<ELT>(al, bh[s], acc[0]);
-            acc[1] = mfma16x16<ELT>(ah, bl[s], acc[1]);
-            acc[2] = mfma16x16<ELT>(ah, bh[s], acc[2]);
-        }
+        for (int t = 0; t < RING; ++t)
+#pragma unroll
+            for (int cs = 0; cs < NCS; ++cs) {
+                const int ro = ((rr + t) % RING) * ROWB + cs * SLB;
+                const u32x4 ah = *(const u32x4 *)(ring + ro + aoff), al = *(const u32x4 *)(ring + ro + (aoff ^ 64));
+#pragma unroll
+                for (int j = 0; j < RPI; ++j) {
+                    const int ky = t - j;     // ring row t is filter row t - j of output row oy + j
+                    if (ky < 0 || ky >= KS) continue;
+                    const int s = ky * NCS + cs;
+                    acc[j][0] = mfma16x16<ELT>(al, bh[s], acc[j][0]);
+                    acc[j][1] = mfma16x16<ELT>(ah, bl[s], acc[j][1]);
+                    acc[j][2] = mfma16x16<ELT>(ah, bh[s], acc[j][2]);
+                }
+            }
         __builtin_amdgcn_s_setprio(0);
         // C layout: column lane & 15, rows 4 (lane >> 4) + r of the wave's 16-row block
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-            P[(mb * 16 + 4 * (lane >> 4) + r) * PLD + nb * 16 + l16] =
-                ((acc[0][r] + acc[1][r]) + acc[2][r]) * a.acc_scale;
-        __syncthreads();                      // P complete; ring row rr no longer read
-        if (owner) {
-            float v = 0.f;
+        for (int j = 0; j < RPI; ++j)
 #pragma unroll
-            for (int kx = 0; kx < KS; ++kx) v += P[(oq + kx) * PLD + oo * KS + kx];
-            bad |= !__builtin_isfinite(v);
-            if (wsp) wsp[(long long)((img * a.oh + oy) * a.ow + ox0 + oq) * a.cout + oo] = v;
-            else if (plain) yrow[(long long)oy * a.ow * a.ycs] = apply_act(v * esc + esh, e.act, e.alpha);
-            else store_epilogue(a, 0, (img * a.oh + oy) * a.ow + ox0 + oq, oo, v);
+            for (int r = 0; r < 4; ++r)
+                P[j][(mb * 16 + 4 * (lane >> 4) + r) * PLD + nb * 16 + l16] =
+                    ((acc[j][0][r] + acc[j][1][r]) + acc[j][2][r]) * a.acc_scale;
+        __syncthreads();                      // P complete; ring rows rr .. rr + RPI - 1 no longer read
+        if (owner) {
+#pragma unroll
+            for (int j = 0; j < RPI; ++j) {
+                if (oy + j >= oy1) break;
+                float v = 0.f;
+#pragma unroll
+                for (int kx = 0; kx < KS; ++kx) v += P[j][(oq + kx) * PLD + oo * KS + kx];
+                bad |= !__builtin_isfinite(v);
+                const int oyj = oy + j;
+                if (wsp) wsp[(long long)((img * a.oh + oyj) * a.ow + ox0 + oq) * a.cout + oo] = v;
+                else if (plain) yrow[(long long)oyj * a.ow * a.ycs] = apply_act(v * esc + esh, e.act, e.alpha);
+                else store_epilogue(a, 0, (img * a.oh + oyj) * a.ow + ox0 + oq, oo, v);
+            }
         }
-        if (more) store_row(rr + KS, nxt);    // into the ring slot of row rr (ky = 0 of this output row)
-        __syncthreads();                      // P reads done; the new ring row visible
+        if (more) {                           // into the ring slots of rows rr .. rr + RPI - 1
+#pragma unroll
+            for (int j = 0; j < RPI; ++j) store_row(rr + RING + j, nxt[j]);
+        }
+        __syncthreads();                      // P reads done; the new ring rows visible
     }
     if (bad && a.nonfinite) __hip_atomic_store(a.nonfinite, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     launch_stamp(a, true);
 }
 
-template <int ELT, int CO>
-static int launch_head_co(const ConvArgs &a, int ks, int ncs, dim3 grid, int strips, int th, hipStream_t s) {
-    if (ks == 7 && ncs == 2) conv_head_x3<ELT, CO, 7, 2><<<grid, kHeadT, 0, s>>>(a, strips, th);
-    else if (ks == 7 && ncs == 1) conv_head_x3<ELT, CO, 7, 1><<<grid, kHeadT, 0, s>>>(a, strips, th);
-    else if (ks == 5 && ncs == 2) conv_head_x3<ELT, CO, 5, 2><<<grid, kHeadT, 0, s>>>(a, strips, th);
-    else if (ks == 5 && ncs == 1) conv_head_x3<ELT, CO, 5, 1><<<grid, kHeadT, 0, s>>>(a, strips, th);
+template <int ELT, int CO, int RPI>
+static int launch_head_rpi(const ConvArgs &a, int ks, int ncs, dim3 grid, int strips, int th, hipStream_t s) {
+    if (ks == 7 && ncs == 2) conv_head_x3<ELT, CO, 7, 2, RPI><<<grid, kHeadT, 0, s>>>(a, strips, th);
+    else if (ks == 7 && ncs == 1) conv_head_x3<ELT, CO, 7, 1, RPI><<<grid, kHeadT, 0, s>>>(a, strips, th);
+    else if (ks == 5 && ncs == 2) conv_head_x3<ELT, CO, 5, 2, RPI><<<grid, kHeadT, 0, s>>>(a, strips, th);
+    else if (ks == 5 && ncs == 1) conv_head_x3<ELT, CO, 5, 1, RPI><<<grid, kHeadT, 0, s>>>(a, strips, th);
     else S2V_REQUIRE(false, "conv_head_x3: no kernel for a %dx%d filter over %d channels", ks, ks, 32 * ncs);
     return 0;
+}
+
+// S2V_HEAD_RPI: output rows per loop iteration (1 or 2, default 2)
+static int head_rpi() {
+    static const int r = [] { const char *e = getenv("S2V_HEAD_RPI"); return e && atoi(e) == 1 ? 1 : 2; }();
+    return r;
+}
+
+template <int ELT, int CO>
+static int launch_head_co(const ConvArgs &a, int ks, int ncs, dim3 grid, int strips, int th, hipStream_t s) {
+    return head_rpi() == 1 ? launch_head_rpi<ELT, CO, 1>(a, ks, ncs, grid, strips, th, s)
+                           : launch_head_rpi<ELT, CO, 2>(a, ks, ncs, grid, strips, th, s);
 }
 
 // host launcher (conv.hip): prec 1 = bf16x3, 2 = f16x3

@@ -48,6 +48,12 @@ ROWPACK0 = os.environ.get("S2V_ENET_ROWPACK0", "0") == "1"
 # where the style-encoder branch forks off the calling stream: 0 = before LNet (both from the start of
 # the step), h = before LNet's h x h decoder level (LNet's earlier levels then run on the whole chip)
 FORK_AT = int(os.environ.get("S2V_ENET_FORK_AT", "0"))
+# S2V_ENET_PAUSE="k:h": the style encoder runs its first conv and k down ResBlocks from the fork, then waits
+# for LNet to reach its h x h decoder level (h = 0: LNet's end) and runs the rest from there, so the LNet
+# levels in between (the latency-bound 12^2 FFC chain) have the whole chip.  Empty: no pause.
+PAUSE = tuple(int(v) for v in os.environ.get("S2V_ENET_PAUSE", "").split(":")) if os.environ.get("S2V_ENET_PAUSE") else None
+# persistent blocks of the resumed part (S2V_ENET_RESUME_GRID; default: as STYLE_GRID)
+RESUME_GRID = os.environ.get("S2V_ENET_RESUME_GRID", "")
 
 
 def style_grid(device) -> int:
@@ -219,13 +225,25 @@ class ENetEngine:
 
     def style_code(self, ctx, ref: torch.Tensor):
         """ref: NCHW [B,3,H,W] device tensor -> style [B,1,1,512] (ENet.py:94-101)."""
+        st = self.style_begin(ctx, ref)
+        self.style_down(ctx, st, len(self.down))
+        return self.style_end(ctx, st)
+
+    def style_begin(self, ctx, ref: torch.Tensor) -> dict:
+        """conv_body_first of the style encoder; returns the state style_down / style_end continue from."""
         dev, b = self.device, ref.shape[0]
         x = NHWC.empty(b, 256, 256, 4, dev)
         ops.fill(ctx, x.t)
         ops.nchw_to_nhwc(ctx, ref, x.slice(0, 3))                  # F.interpolate(ref, 256, bilinear)
         f = NHWC.empty(b, 256, 256, self.first.cout, dev)
         ops.conv2d(ctx, x, self.first, f, act=ops.ACT_LRELU, alpha=LRELU)
-        for c1, c2, sk in self.down:                                # ResBlock(mode='down'), base_blocks.py:40-49
+        return {"f": f, "i": 0}
+
+    def style_down(self, ctx, st: dict, upto: int):
+        """The down ResBlocks st["i"] .. upto - 1 (ResBlock(mode='down'), base_blocks.py:40-49)."""
+        f, b, dev = st["f"], st["f"].n, self.device
+        while st["i"] < min(upto, len(self.down)):
+            c1, c2, sk = self.down[st["i"]]
             h, w = f.h, f.w
             td = NHWC.empty(b, h // 2, w // 2, c1.cout, dev)         # interpolate(lrelu(conv1(x)), 0.5):
             ops.conv2d(ctx, f, c1, td, act=ops.ACT_LRELU, alpha=LRELU, pool=True)   # pooled in the epilogue
@@ -233,6 +251,11 @@ class ENetEngine:
             ops.conv2d(ctx, f, sk, out)                             # skip(interpolate(x, 0.5))
             ops.conv2d(ctx, td, c2, out, act=ops.ACT_LRELU, alpha=LRELU, res=out, res_after=True)
             f = out
+            st["i"] += 1
+        st["f"] = f
+
+    def style_end(self, ctx, st: dict):
+        f, b, dev = st["f"], st["f"].n, self.device
         g = NHWC.empty(b, f.h, f.w, self.final_conv.cout, dev)
         ops.conv2d(ctx, f, self.final_conv, g, act=ops.ACT_LRELU, alpha=LRELU)
         style = NHWC.empty(b, 1, 1, self.final_linear.cout, dev)
@@ -248,19 +271,38 @@ class ENetEngine:
         side = self._side(ctx) if OVERLAP else None
         enc = {}
 
+        def finish(sctx):
+            enc["style"] = self.style_end(sctx, enc.pop("st"))
+            ops.conv2d(sctx, enc["style"], self.mod, svec)
+            enc["d"] = self._demods(sctx, svec.t.view(b, -1))       # off the tail: beside LNet
+
         def fork():
             sst, sctx = side
             sst.wait_stream(torch.cuda.current_stream(dev))
             with ops.x3_grid_cap(sctx, style_grid(dev)), ops.side_stream(sst, ctx.keep):
-                enc["style"] = self.style_code(sctx, face[:, 3:])
-                ops.conv2d(sctx, enc["style"], self.mod, svec)
-                enc["d"] = self._demods(sctx, svec.t.view(b, -1))   # off the tail: beside LNet
+                enc["st"] = self.style_begin(sctx, face[:, 3:])
+                self.style_down(sctx, enc["st"], PAUSE[0] if PAUSE else len(self.down))
+                if not PAUSE:
+                    finish(sctx)
+
+        def resume():
+            # the rest of the encoder after LNet's calling stream reached this point (stream order on the
+            # side stream keeps it behind the first part)
+            sst, sctx = side
+            sst.wait_stream(torch.cuda.current_stream(dev))
+            grid = int(RESUME_GRID) if RESUME_GRID else style_grid(dev)
+            with ops.x3_grid_cap(sctx, grid), ops.side_stream(sst, ctx.keep):
+                self.style_down(sctx, enc["st"], len(self.down))
+                finish(sctx)
+
         on_level = None
         if side is not None:
             if FORK_AT:
                 on_level = lambda h: fork() if h == FORK_AT and not enc else None  # noqa: E731
             else:
                 fork()
+                if PAUSE and PAUSE[1]:
+                    on_level = lambda h: resume() if h == PAUSE[1] and "st" in enc else None  # noqa: E731
         else:
             enc["style"] = self.style_code(ctx, face[:, 3:])
             ops.conv2d(ctx, enc["style"], self.mod, svec)
@@ -273,6 +315,8 @@ class ENetEngine:
         self.lnet.forward(ctx, audio, x6, lo, pad_rgb=True, on_level=on_level)
         if side is not None and not enc:
             fork()                                             # FORK_AT names no LNet level
+        if side is not None and "st" in enc:
+            resume()                                           # PAUSE resumes at LNet's end
         ops.nhwc_to_nchw(ctx, lo.slice(0, 3), low)
         if side is not None:
             torch.cuda.current_stream(dev).wait_stream(side[0])    # style code ready for the StyleConvs
