@@ -95,12 +95,14 @@ def _worker(rank, world, port, n, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n", [7, 16, 1])
-def test_broadcast_and_gather_world2_gloo(n):
+@pytest.mark.parametrize("n,world", [(7, 2), (16, 2), (1, 2), (13, 4), (3, 4)])
+def test_broadcast_and_gather_world2_gloo(n, world):
+    """World 2 and 4: at 4, rank 0's batch_isend_irecv pairs three receives with three peers' sends (13
+    frames: shards of 4 / 3 / 3 / 3), and at n = 3 one rank holds no frames and sends nothing."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, n, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, q)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
