@@ -370,7 +370,7 @@ std::vector<int64_t> modulated_conv2d_(const Tensor &x, const Tensor &y, const T
                                        double pix_w, const OptT &res, bool res_after_act, int64_t act, double alpha,
                                        const OptT &ws, int64_t force_splits, const OptT &stamps, const OptT &stamp_ctr,
                                        at::IntArrayRef stamp_pos, double x_scale, const OptT &nonfinite, bool dry,
-                                       int64_t d2s, int64_t force_tile) {
+                                       int64_t d2s, int64_t force_tile, double premod) {
     const c10::DeviceGuard guard(x.device());
     const at::Device dev = x.device();
     TORCH_CHECK(!g_recording, "conv group: modulated convs cannot be group members");
@@ -437,16 +437,50 @@ std::vector<int64_t> modulated_conv2d_(const Tensor &x, const Tensor &y, const T
     p.ws = (float *)w.p; p.ws_bytes = w.bytes;
     auto out = plan_list(p, 0);
     const float *dp = has(d) ? d->data_ptr<float>() : nullptr;
-    if (x3)
+    // premod != 0: wbuf already holds the modulated weights (modulate_weights_, e.g. written on a side stream
+    // ahead of the conv): > 0 the split layout at that pre-scale, < 0 fp32; they must be the layout this plan reads
+    TORCH_CHECK(premod == 0.0 || (x3 ? premod == (double)wscale : premod < 0.0),
+                "modconv: the pre-modulated weights (premod ", premod, ") are not the layout this conv reads (",
+                x3 ? "split, pre-scale " : "fp32", x3 ? wscale : 0.f, ")");
+    if (premod == 0.0 && x3)
         check(s2v_modulate_weights_split(wt.data_ptr<float>(), npad, kpad, K, p.cin, (int)cout, s.data_ptr<float>(),
                                          s_ns, dp, d_ns, B, (int)prec, wscale, wbuf.data_ptr(), stream()),
               "s2v_modulate_weights_split");
-    else
+    else if (premod == 0.0)
         check(s2v_modulate_weights(wt.data_ptr<float>(), npad, kpad, K, p.cin, (int)cout, s.data_ptr<float>(), s_ns, dp,
                                    d_ns, B, wbuf.data_ptr<float>(), stream()),
               "s2v_modulate_weights");
     check(s2v_conv2d(&p, stream()), "s2v_conv2d");
     return out;
+}
+
+// The per-sample modulation alone (W * s[b, c] (* d[b, o]) into wbuf [B, npad, kpad]): prec != f32 writes the
+// split layout at pre-scale wscale (what modulated_conv2d_ plans for a split-precision conv), f32 plain fp32.  A
+// later modulated_conv2d_(..., premod) reads it instead of modulating again.
+void modulate_weights_(const Tensor &wt, const Tensor &s, const OptT &d, const Tensor &wbuf, int64_t cout, int64_t cin,
+                       int64_t taps, int64_t prec, double wscale) {
+    const c10::DeviceGuard guard(wt.device());
+    const at::Device dev = wt.device();
+    f32(wt, dev, "modulate wt");
+    TORCH_CHECK(wt.dim() == 2 && wt.is_contiguous() && wt.size(0) >= cout, "modulate wt: packed [npad, kpad]");
+    const int npad = (int)wt.size(0), kpad = (int)wt.size(1), K = (int)(taps * cin);
+    TORCH_CHECK(kpad >= K && cin > 0 && cout > 0, "modulate: kpad < taps * cin");
+    f32(wbuf, dev, "modulate wbuf");
+    TORCH_CHECK(wbuf.dim() == 3 && wbuf.is_contiguous() && wbuf.size(1) == npad && wbuf.size(2) == kpad,
+                "modulate wbuf: [B, npad, kpad]");
+    const int B = (int)wbuf.size(0);
+    const int s_ns = (int)rows_view(s, dev, B, cin, "modulate s");
+    int d_ns = 0;
+    if (has(d)) d_ns = (int)rows_view(*d, dev, B, cout, "modulate d");
+    const float *dp = has(d) ? d->data_ptr<float>() : nullptr;
+    if (prec != S2V_PREC_F32)
+        check(s2v_modulate_weights_split(wt.data_ptr<float>(), npad, kpad, K, (int)cin, (int)cout, s.data_ptr<float>(),
+                                         s_ns, dp, d_ns, B, (int)prec, (float)wscale, wbuf.data_ptr(), stream()),
+              "s2v_modulate_weights_split");
+    else
+        check(s2v_modulate_weights(wt.data_ptr<float>(), npad, kpad, K, (int)cin, (int)cout, s.data_ptr<float>(), s_ns,
+                                   dp, d_ns, B, wbuf.data_ptr<float>(), stream()),
+              "s2v_modulate_weights");
 }
 
 // batched activation GEMM out[z] = a[z] @ b[z] (+ res[z]): a [.., M, K], b [.., K, N], out [.., M, N]
@@ -1046,7 +1080,10 @@ TORCH_LIBRARY_FRAGMENT(s2v, m) {
           "Tensor? pix_add, "
           "float pix_w, Tensor? res, "
           "bool res_after_act, int act, float alpha, Tensor? ws, int force_splits, Tensor(s!)? stamps, Tensor? stamp_ctr, "
-          "int[3] stamp_pos, float x_scale, Tensor(f!)? nonfinite, bool dry, int d2s=0, int force_tile=0) -> int[]");
+          "int[3] stamp_pos, float x_scale, Tensor(f!)? nonfinite, bool dry, int d2s=0, int force_tile=0, "
+          "float premod=0.) -> int[]");
+    m.def("modulate_weights_(Tensor wt, Tensor s, Tensor? d, Tensor(a!) wbuf, int cout, int cin, int taps, int prec, "
+          "float wscale) -> ()");
     m.def("amax_(Tensor x, Tensor(a!) out) -> ()");
     // conv groups: host-side recording, no tensor to dispatch on (catch-all kernels)
     m.def("group_begin_() -> ()", &group_begin_);
@@ -1099,6 +1136,7 @@ TORCH_LIBRARY_FRAGMENT(s2v, m) {
 TORCH_LIBRARY_IMPL(s2v, CUDA, m) {
     m.impl("conv2d_", &conv2d_);
     m.impl("modulated_conv2d_", &modulated_conv2d_);
+    m.impl("modulate_weights_", &modulate_weights_);
     m.impl("gemm_kn_", &gemm_kn_);
     m.impl("split_weights_", &split_weights_);
     m.impl("amax_", &amax_);

@@ -52,6 +52,10 @@ FORK_AT = int(os.environ.get("S2V_ENET_FORK_AT", "0"))
 # for LNet to reach its h x h decoder level (h = 0: LNet's end) and runs the rest from there, so the LNet
 # levels in between (the latency-bound 12^2 FFC chain) have the whole chip.  Empty: no pause.
 PAUSE = tuple(int(v) for v in os.environ.get("S2V_ENET_PAUSE", "").split(":")) if os.environ.get("S2V_ENET_PAUSE") else None
+# S2V_ENET_PREMOD=1: the tail's StyleConv weights are modulated (W * s * d, ops.modulate_weights) on the style
+# encoder's side stream right after the style code, beside LNet, instead of inside each StyleConv launch of the
+# critical tail (the four polyphase edge strips then share one modulation)
+PREMOD = os.environ.get("S2V_ENET_PREMOD", "1") == "1"
 # persistent blocks of the resumed part (S2V_ENET_RESUME_GRID; default: as STYLE_GRID)
 RESUME_GRID = os.environ.get("S2V_ENET_RESUME_GRID", "")
 
@@ -183,7 +187,25 @@ class ENetEngine:
         ops.modconv_demod_rows(ctx, s2, t, dall, eps=1e-8, post=math.sqrt(2.0))
         return t, dall
 
-    def _poly_styleconv(self, ctx, L, cur: NHWC, s, d4, idx, noises, ctr):
+    def _premodulate(self, ctx, s2, dtab, dall, b) -> dict:
+        """PREMOD: the per-sample weights of the tail's StyleConvs, {layer index: {"conv4" / "conv": (wbuf,
+        premod)}} (row-packed layers keep their in-launch modulation)."""
+        wb = {}
+        for st in range(2):
+            for li in range(2):
+                L, idx = self.layers[3 * st + li], 2 * st + li
+                off = self.mod_offs[3 * st + li]
+                r0, wd = dtab.r0[idx], dtab.width[idx]
+                sv = s2[:, off: off + L.cin]
+                if POLY_UP and L.conv4 is not None:
+                    d4 = dall[:, r0: r0 + wd]
+                    wb[idx] = {"conv4": ops.modulate_weights(ctx, L.conv4, sv, d4, b),
+                               "conv": ops.modulate_weights(ctx, L.conv, sv, d4[:, : L.cout], b)}
+                elif L.rp is None:
+                    wb[idx] = {"conv": ops.modulate_weights(ctx, L.conv, sv, dall[:, r0: r0 + L.cout], b)}
+        return wb
+
+    def _poly_styleconv(self, ctx, L, cur: NHWC, s, d4, idx, noises, ctr, wb=None):
         """StyleConv(sample_mode='upsample') (base_blocks.py:500-533): F.interpolate(x, 2, bilinear) then
         the modulated 3x3 conv + noise + bias + LeakyReLU, as one depth-to-space conv over ``cur`` with
         the folded parity-class filters (L.conv4).  The fold assumes every upsampled row / column is an
@@ -204,7 +226,8 @@ class ENetEngine:
                 self.last_noises[idx] = noise
         y = NHWC.empty(b, h2, w2, L.cout, dev)
         kw = dict(act=ops.ACT_LRELU, alpha=LRELU, pix_w=L.noise_w or 0.0)
-        ops.modulated_conv2d(ctx, cur, L.conv4, y, s, d4, pix_add=noise, d2s=True, **kw)
+        wb = wb or {}
+        ops.modulated_conv2d(ctx, cur, L.conv4, y, s, d4, pix_add=noise, d2s=True, premod=wb.get("conv4"), **kw)
         c = cur.c
         # (x strip, its noise, the strip output lines kept, where they go): each strip's x2 upsample is
         # exact on the lines the kept outputs read (the clamped source row / column is the image's own)
@@ -219,7 +242,7 @@ class ENetEngine:
             ops.resize_nhwc(ctx, xs, up, scale_factor=2)
             ys = NHWC.empty(b, up.h, up.w, L.cout, dev)
             nz = None if noise is None else nsel(noise).contiguous()
-            ops.modulated_conv2d(ctx, up, L.conv, ys, s, d, pix_add=nz, **kw)
+            ops.modulated_conv2d(ctx, up, L.conv, ys, s, d, pix_add=nz, premod=wb.get("conv"), **kw)
             ysel(y.t).copy_(ssel(ys.t))
         return y
 
@@ -275,6 +298,8 @@ class ENetEngine:
             enc["style"] = self.style_end(sctx, enc.pop("st"))
             ops.conv2d(sctx, enc["style"], self.mod, svec)
             enc["d"] = self._demods(sctx, svec.t.view(b, -1))       # off the tail: beside LNet
+            if PREMOD:
+                enc["wb"] = self._premodulate(sctx, svec.t.view(b, -1), enc["d"][0], enc["d"][1], b)
 
         def fork():
             sst, sctx = side
@@ -342,7 +367,7 @@ class ENetEngine:
                 r0, wd = dtab.r0[2 * st + li], dtab.width[2 * st + li]
                 if POLY_UP and L.conv4 is not None:
                     cur = self._poly_styleconv(ctx, L, cur, s2[:, off: off + L.cin], dall[:, r0: r0 + wd],
-                                               2 * st + li, noises, ctr)
+                                               2 * st + li, noises, ctr, wb=enc.get("wb", {}).get(2 * st + li))
                     continue
                 x = cur
                 if L.upsample:
@@ -363,8 +388,9 @@ class ENetEngine:
                         noise = torch.empty((b, x.h, x.w), device=dev)
                         ops.gaussian_noise(ctx, noise, self.noise_seed, (2 * st + li) << 36, ctr=ctr, shift=40)
                         self.last_noises[2 * st + li] = noise
+                pm = enc.get("wb", {}).get(2 * st + li, {}).get("conv") if L.rp is None else None
                 ops.modulated_conv2d(ctx, x, conv, y, s2[:, off: off + cin], d, act=ops.ACT_LRELU, alpha=LRELU,
-                                     pix_add=noise, pix_w=L.noise_w or 0.0)
+                                     pix_add=noise, pix_w=L.noise_w or 0.0, premod=pm)
                 cur = y
             R = self.layers[3 * st + 2]
             off = self.mod_offs[3 * st + 2]

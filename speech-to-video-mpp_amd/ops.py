@@ -825,15 +825,29 @@ def _run_conv(ctx, launch, x, cw, yv, pool, in_scale=None, nc_scale=None, pix_ad
         CONV_HOOK(ctx, info, flops, go)
 
 
+def modulate_weights(ctx: Ctx, cw: ConvW, s: torch.Tensor, d: torch.Tensor | None, batch: int):
+    """The per-sample weights W * s[b, c] (* d[b, o]) of ``cw`` alone (``s2v::modulate_weights_``), in the layout a
+    split-precision modulated conv reads (pre-scale 2^11 when demodulated in f16x3), or fp32 in f32 mode: the
+    (wbuf, premod) pair modulated_conv2d(premod=) takes, so the modulation can run ahead of the conv (e.g. on a
+    side stream as soon as the style code exists)."""
+    prec = prec_code()
+    wbuf = empty((batch, cw.npad, cw.kpad), cw.wt.device)      # (calling-stream memory on a side branch)
+    wscale = 2048.0 if (prec == PREC_F16X3 and d is not None) else 1.0
+    S2V.modulate_weights_(cw.wt, s, d, wbuf, cw.cout, cw.cin, cw.kh * cw.kw, prec, wscale)
+    return wbuf, (wscale if prec != PREC_F32 else -1.0)
+
+
 def modulated_conv2d(ctx: Ctx, x: NHWC, cw: ConvW, y: NHWC, s: torch.Tensor, d: torch.Tensor | None = None, *,
                      act=ACT_NONE, alpha=0.0, res: NHWC | None = None, res_after=False, pix_add=None, pix_w=0.0,
-                     shift=None, force_splits=0, d2s=False):
+                     shift=None, force_splits=0, d2s=False, premod=None):
     """StyleGAN2 modulated conv with per-sample weights W * s[b, c] (* d[b, o]) written by the
     ``s2v::modulated_conv2d_`` op in the form its planned kernel reads (split layout with a 2^11 f16
     pre-scale when demodulated, or fp32), then one batched conv (no prologue / epilogue scaling in
     the GEMM).  s: [B, cin] (row stride s.stride(0)); d: [B, cout] demodulation or None.
     ``d2s``: cw holds the 4 parity classes of a x2-upsampled conv (cout = 4 classes x c, class-major)
-    and y is the full [B, 2H, 2W, c] output (s2v_conv_params.d2s_cout); pix_add is then [B, 2H, 2W]."""
+    and y is the full [B, 2H, 2W, c] output (s2v_conv_params.d2s_cout); pix_add is then [B, 2H, 2W].
+    ``premod``: a (wbuf, premod) pair from modulate_weights for the same (cw, s, d): the conv reads those weights
+    instead of modulating them again (the op refuses a layout its plan does not read)."""
     oh, ow = cw.out_hw(x.h, x.w)
     assert cw.in_mode != IN_TRANSPOSED and cw.poly is None and (cw.sh, cw.sw, cw.dh, cw.dw) == (1, 1, 1, 1), \
         "modulated_conv2d: direct stride-1 convs only"
@@ -842,7 +856,11 @@ def modulated_conv2d(ctx: Ctx, x: NHWC, cw: ConvW, y: NHWC, s: torch.Tensor, d: 
                                                                                              cw.cout // 4)
     else:
         assert x.c == cw.cin and (y.n, y.h, y.w, y.c) == (x.n, oh, ow, cw.cout)
-    wbuf = torch.empty((x.n, cw.npad, cw.kpad), device=cw.wt.device)
+    if premod is not None:
+        wbuf, pm = premod
+        assert tuple(wbuf.shape) == (x.n, cw.npad, cw.kpad), "modulated_conv2d: premod weights of another shape"
+    else:
+        wbuf, pm = torch.empty((x.n, cw.npad, cw.kpad), device=cw.wt.device), 0.0
     yv, resv = y.v, None if res is None else res.v
     prec = prec_code()
     x_split = int(getattr(x, "split", 0))
@@ -862,7 +880,7 @@ def modulated_conv2d(ctx: Ctx, x: NHWC, cw: ConvW, y: NHWC, s: torch.Tensor, d: 
                                      prec,
                                      x_split != 0, cw.scale, sh, pix_add, pix_w, resv, res_after, act, alpha, ws,
                                      force_splits if fs is None else fs, st[0], st[1], st[2], xscale, flag, dry, int(d2s),
-                                     force_tile if ft is None else ft)
+                                     force_tile if ft is None else ft, pm)
     if TUNE is not None and key is not None:
         TUNE(ctx, key, lambda ft, fs: _with_ws(ctx, lambda ws: launch(ws, False, _NOSTAMP, ft, fs)[0]),
              lambda ft, fs: launch(ctx.ws.tensor(), True, _NOSTAMP, ft, fs)[1:], yv, resv)

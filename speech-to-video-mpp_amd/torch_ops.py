@@ -30,7 +30,7 @@ OPS = ("fused_bias_act", "upfirdn2d", "conv2d_nhwc", "layernorm2d", "instnorm_ad
        "resize_bilinear", "flow_warp", "mel_spectrogram")
 # the launch ops every kernel of the model forwards is dispatched through (csrc/torch_launch.cpp,
 # called by s2v_amd.ops): in-place on caller-owned views, capturable
-LAUNCH_OPS = ("conv2d_", "modulated_conv2d_", "gemm_kn_", "split_weights_", "split_act_", "layernorm2d_", "instnorm_",
+LAUNCH_OPS = ("conv2d_", "modulated_conv2d_", "modulate_weights_", "gemm_kn_", "split_weights_", "split_act_", "layernorm2d_", "instnorm_",
               "adain_params_", "modconv_demod_", "row_layernorm_", "attention_", "resize_", "pad_reflect_",
               "flow_warp_", "flow_warp_cat_", "fill_value_", "gaussian_noise_", "counter_add_", "rfft2_", "irfft2_", "eltwise_", "fir2d_",
               "lipsync_inputs_", "to_u8_", "mel_chunks_", "melspectrogram_")

@@ -378,6 +378,21 @@ def test_modulated_conv_per_sample_weights(ctx, prec, n, cin, h, w, cout, k, mod
                          alpha=0.2, pix_add=noise.float().to(DEV).contiguous(), pix_w=0.3)
     err = (to_nchw(y) - ref).abs()
     assert (err <= 2 * REL[prec] * bound + 1e-6).all(), f"max err {err.max():.3e}"
+    # the modulation run ahead (ops.modulate_weights, engine/enet.py PREMOD) and read by the conv: bit-identical,
+    # with and without the demodulation; a pre-modulated layout the conv does not read is refused.  (Cout <= 4
+    # layers run the fp32 direct kernels, whose layout modulate_weights writes in f32 mode only.)
+    for dd in ((d, None) if cout > 4 else ()):
+        dv = None if dd is None else dd.float().to(DEV)
+        kw = dict(act=ops.ACT_LRELU, alpha=0.2, pix_add=noise.float().to(DEV).contiguous(), pix_w=0.3)
+        y1 = NHWC.empty(n, oh, ow, cout, DEV)
+        ops.modulated_conv2d(ctx, nhwc(x.float()), cw, y1, s.float().to(DEV), dv, **kw)
+        pm = ops.modulate_weights(ctx, cw, s.float().to(DEV), dv, n)
+        y2 = NHWC.empty(n, oh, ow, cout, DEV)
+        ops.modulated_conv2d(ctx, nhwc(x.float()), cw, y2, s.float().to(DEV), dv, premod=pm, **kw)
+        torch.cuda.synchronize()
+        assert torch.equal(y1.t, y2.t)
+        with pytest.raises(Exception, match="pre-modulated"):
+            ops.modulated_conv2d(ctx, nhwc(x.float()), cw, y2, s.float().to(DEV), dv, premod=(pm[0], -pm[1]), **kw)
 
 
 @pytest.mark.parametrize("tile", [0, 4, 5, 6, 8, 9, 10, 11, 12])
