@@ -56,6 +56,9 @@ PAUSE = tuple(int(v) for v in os.environ.get("S2V_ENET_PAUSE", "").split(":")) i
 # encoder's side stream right after the style code, beside LNet, instead of inside each StyleConv launch of the
 # critical tail (the four polyphase edge strips then share one modulation)
 PREMOD = os.environ.get("S2V_ENET_PREMOD", "1") == "1"
+# S2V_ENET_STACK_STRIPS=1: the polyphase StyleConv's edge strips (the two outermost output lines per side) as one
+# stacked strip image per axis: two upsample + conv launches instead of four
+STACK_STRIPS = os.environ.get("S2V_ENET_STACK_STRIPS", "1") == "1"
 # persistent blocks of the resumed part (S2V_ENET_RESUME_GRID; default: as STYLE_GRID)
 RESUME_GRID = os.environ.get("S2V_ENET_RESUME_GRID", "")
 
@@ -229,6 +232,23 @@ class ENetEngine:
         wb = wb or {}
         ops.modulated_conv2d(ctx, cur, L.conv4, y, s, d4, pix_add=noise, d2s=True, premod=wb.get("conv4"), **kw)
         c = cur.c
+        if STACK_STRIPS:
+            # the two strips of one axis stacked into one 4-line image (first two lines | last two lines): one
+            # upsample and one conv per axis instead of two.  The lines the kept outputs read never straddle the
+            # seam: output lines 0, 1 read upsampled lines <= 2 (from source lines 0, 1 only) and 6, 7 read
+            # lines >= 5 (source lines 2, 3 = the image's last two) or the conv's zero padding past line 7,
+            # exactly as the separate strips do
+            for axis, n_src, n_out in ((1, cur.h, h2), (2, cur.w, w2)):
+                xs = NHWC(torch.cat([cur.t.narrow(axis, 0, 2), cur.t.narrow(axis, n_src - 2, 2)], axis))
+                up = NHWC.empty(b, 2 * xs.h, 2 * xs.w, c, dev)
+                ops.resize_nhwc(ctx, xs, up, scale_factor=2)
+                ys = NHWC.empty(b, up.h, up.w, L.cout, dev)
+                nz = None if noise is None else torch.cat([noise.narrow(axis, 0, 4), noise.narrow(axis, n_out - 4, 4)],
+                                                          axis)
+                ops.modulated_conv2d(ctx, up, L.conv, ys, s, d, pix_add=nz, premod=wb.get("conv"), **kw)
+                y.t.narrow(axis, 0, 2).copy_(ys.t.narrow(axis, 0, 2))
+                y.t.narrow(axis, n_out - 2, 2).copy_(ys.t.narrow(axis, 6, 2))
+            return y
         # (x strip, its noise, the strip output lines kept, where they go): each strip's x2 upsample is
         # exact on the lines the kept outputs read (the clamped source row / column is the image's own)
         strips = ((cur.t[:, 0:2], lambda t: t[:, 0:4], lambda t: t[:, 0:2], lambda t: t[:, 0:2]),
