@@ -2,7 +2,8 @@
 """Phase timeline of graph-replayed ENet(+LNet) steps from a rocprofv3 --kernel-trace database.
 
 A step starts at its ``fill_kernel`` (the style encoder's input, first kernel of ENet.forward) and
-its StyleConv tail at the first ``modulate_weights`` kernel after it.  Per phase: wall time, busy
+its StyleConv tail at the first kernel launched after LNet's last FourierUnit transform and the style
+encoder's last persistent conv have ended.  Per phase: wall time, busy
 time (union of kernel intervals) and the summed kernel time (> busy when kernels overlap), plus the
 top kernels of each phase.  Usage: timeline.py run_results.db [--steps N]"""
 import sqlite3
@@ -44,7 +45,13 @@ def main():
         i0, i2 = starts[si], starts[si + 1]
         step = ks[i0:i2]
         t0, t2 = step[0][1], ks[i2][1]
-        i1 = next((i for i, (n, a, b) in enumerate(step) if "modulate_weights" in n), None)
+        # the tail starts with the first kernel launched after both branches ended: LNet's last FourierUnit
+        # transform and the style encoder's last persistent conv (the StyleConv weights are modulated on the
+        # encoder's side stream since r06, so a modulate_weights kernel no longer marks the tail)
+        ends = [b for n, a, b in step if "fft2" in n or n.startswith("void s2v::conv_igemm_x3_persist<")]
+        i1 = next((i for i, (n, a, b) in enumerate(step) if ends and a >= max(ends)), None)
+        if i1 is None:
+            i1 = next((i for i, (n, a, b) in enumerate(step) if "modulate_weights" in n), None)
         t1 = step[i1][1] if i1 is not None else t2
         print(f"step {si}: {(t2 - t0) / 1e3:8.1f} us, {len(step)} kernels")
         for name, lo, hi in (("encoder+LNet", t0, t1), ("StyleConv tail", t1, t2)):
