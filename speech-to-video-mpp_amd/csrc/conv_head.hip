@@ -93,12 +93,15 @@ __global__ __launch_bounds__(kHeadT) void conv_head_x3(ConvArgs a, int strips, i
     if (refl) gx = reflect_idx(gx, a.w);
     const bool xok = (unsigned)gx < (unsigned)a.w && sact;
     const float *__restrict__ xcol = xb + (long long)gx * a.xcs + 32 * scs + 8 * sq;
+    // the last ring row an output row of this band reads: with RPI = 2 an odd band's last iteration stages one
+    // row past it, which is never read and (under reflect padding of a small image) may reflect out of range
+    const int rlast = (oy1 - oy0 - 1) + KS - 1;
     auto load_row = [&](int r, f4 (&v)[2]) {  // ring row r = input row base + r
         int gy = base + r;
         if (refl) gy = reflect_idx(gy, a.h);
         v[0] = f4{0.f, 0.f, 0.f, 0.f};
         v[1] = f4{0.f, 0.f, 0.f, 0.f};
-        if (xok && (unsigned)gy < (unsigned)a.h) {
+        if (xok && r <= rlast && (unsigned)gy < (unsigned)a.h) {
             const float *src = xcol + (long long)gy * a.w * a.xcs;
             v[0] = *(const f4 *)src;
             v[1] = *(const f4 *)(src + 4);

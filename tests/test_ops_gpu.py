@@ -714,7 +714,8 @@ def test_small_cout_conv(ctx, prec, cin, k, cout):
     (1, 32, 20, 64, 5, 4, "zero", ops.ACT_NONE),          # 5x5 over one 32-channel slice
     (2, 32, 9, 61, 7, 1, "reflect", ops.ACT_NONE),
     (2, 256, 20, 64, 7, 2, "zero", ops.ACT_NONE),          # DNet flow head form: 4 channel groups, split-K fold
-    (1, 128, 9, 70, 5, 3, "reflect", ops.ACT_TANH)])
+    (1, 128, 9, 70, 5, 3, "reflect", ops.ACT_TANH),
+    (2, 64, 5, 40, 7, 3, "reflect", ops.ACT_NONE)])        # 5 rows (odd band): the 2-row loop's unread extra
 def test_conv_head_x3(ctx, prec, n, cin, h, w, k, cout, pad_mode, act):
     """Cout <= 4 wide-filter heads (conv_head.hip: kx in N, ky in K, an LDS ring of split input rows)
     in the split precisions; exact fp32 VALU (conv_halo_small / conv_small_cpar) in f32.  Against the
