@@ -54,7 +54,8 @@ def main():
     for (r, slot, s0, s1), (a, b) in zip(head, tr):
         t0, t1 = off + k * s0, off + k * s1
         per.append({"replay": r, "trace_us": (b - a) / 1e3, "stamp_us": (s1 - s0) * tick / 1e3,
-                    "head_us": (t0 - a) / 1e3, "tail_us": (b - t1) / 1e3})
+                    "head_us": (t0 - a) / 1e3, "tail_us": (b - t1) / 1e3,
+                    "fit_resid_us": ((a + b) / 2 - (off + k * (s0 + s1) / 2)) / 1e3})
     avg = lambda key: sum(p[key] for p in per) / len(per)  # noqa: E731
     res = {"kernel": sym, "flops_per_launch": fl_head, "grid": list(grid), "launches": len(per),
            "launches_per_replay": per_rep, "clock_ns_per_tick_fit": k, "trace_us": avg("trace_us"),
