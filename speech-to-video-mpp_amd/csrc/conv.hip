@@ -15,6 +15,8 @@
 // ``splitk_reduce`` folds with the same epilogue.
 #include "common.hpp"
 
+#include <vector>
+
 #include "conv_impl.hpp"
 
 #include <cmath>
@@ -1515,7 +1517,21 @@ static int group_plan(const s2v_conv_params *ps, int n, GroupPlan &gp) {
         if (rc) return rc;
         S2V_REQUIRE(ps[i].prec == ps[0].prec, "conv2d_group: members of one precision");
     }
-    static const int cands[] = {4, 3, 1};
+    // candidate tiles (kX3Tiles indices; S2V_GROUP_TILES overrides, e.g. "0,6,4,3,1")
+    static const std::vector<int> cands = [] {
+        std::vector<int> v;
+        const char *e = getenv("S2V_GROUP_TILES");
+        if (e && *e) {
+            for (const char *q = e; *q;) {
+                const int t = atoi(q);
+                if (t == 0 || t == 1 || t == 3 || t == 4 || t == 6) v.push_back(t);
+                while (*q && *q != ',') ++q;
+                if (*q == ',') ++q;
+            }
+        }
+        if (v.empty()) v = {4, 3, 1};
+        return v;
+    }();
     const int cus = plan_cus();
     double best = 1e30;
     gp.cfg = -1;

@@ -811,7 +811,9 @@ constexpr bool x3_has_group(int cfg) { return cfg == 1 || cfg == 3 || cfg == 4; 
 template <int ELT>
 int launch_conv_x3_group(int cfg, const ConvGroup &g, dim3 grid, hipStream_t s) {
     switch (cfg) {
+        case 0: conv_igemm_x3_group<256, 256, 2, 8, 1, 1, ELT><<<grid, 512, 0, s>>>(g); break;
         case 1: conv_igemm_x3_group<128, 128, 2, 8, 1, 1, ELT><<<grid, 512, 0, s>>>(g); break;
+        case 6: conv_igemm_x3_group<256, 128, 4, 8, 1, 1, ELT><<<grid, 512, 0, s>>>(g); break;
         case 3: conv_igemm_x3_group<128, 64, 2, 4, 1, 1, ELT><<<grid, 256, 0, s>>>(g); break;
         case 4: conv_igemm_x3_group<64, 64, 2, 4, 1, 1, ELT><<<grid, 256, 0, s>>>(g); break;
         default: S2V_REQUIRE(false, "conv2d_group: x3 configuration %d has no grouped kernel", cfg);
