@@ -974,6 +974,24 @@ static int epi_vec4(const s2v_conv_params *p) {
 
 static bool use_direct(const s2v_conv_params *p) { return p->cout <= 4 && !p->b_kn; }
 
+// 4-channel 1x1 / 3x3 convs on the exact-fp32 MFMA kernel (conv_k4.hip) in every precision mode: stride 1,
+// zero "same" padding, 32k <= 256 output channels, a plain epilogue (scale, shift, per-pixel add, activation);
+// S2V_K4=0: the split-precision tiles / conv_smallk4 instead
+int launch_conv_k4(const ConvArgs &a, int batch, int kt, hipStream_t s);
+static bool k4_ok(const s2v_conv_params *p) {
+    static const int on = [] { const char *e = getenv("S2V_K4"); return e ? atoi(e) : 1; }();
+    if (!on || p->cin != 4 || p->kh != p->kw || (p->kh != 1 && p->kh != 3) || p->force_tile || p->b_kn || p->x_split)
+        return false;
+    if (p->in_mode != S2V_IN_DIRECT || p->pad_mode != S2V_PAD_ZERO || p->sh != 1 || p->sw != 1 || p->dh != 1 ||
+        p->dw != 1 || p->ph != p->kh / 2 || p->pw != p->kw / 2)
+        return false;
+    if (p->cout % 32 || p->cout > 256 || p->in_scale || p->pre_act != S2V_ACT_NONE || p->nc_scale || p->res ||
+        p->post_mul || p->dup_src || p->out_pool || p->out_step > 1 || p->d2s_cout > 0)
+        return false;
+    if (!p->wt || p->kpad < p->kh * p->kw * 4 || p->xcs % 4 || ((uintptr_t)p->x % 16) || p->x_bs % 4) return false;
+    return (long long)p->n * p->oh * p->ow < (1LL << 31);
+}
+
 static bool vec4_input(const s2v_conv_params *p) {
     return (p->cin % 4 == 0) && (p->xcs % 4 == 0) && (((uintptr_t)p->x % 16) == 0) && (p->x_bs % 4 == 0) &&
            (!p->in_scale || (p->in_scale_ns % 4 == 0 && ((uintptr_t)p->in_scale % 16) == 0));
@@ -1024,7 +1042,7 @@ static bool is_smallk(const s2v_conv_params *p) {
     return m < (1LL << 31) && k <= 64 && smallk_cfg(p, (int)m, (int)k, tppx, qpt);
 }
 static bool tiled_x3(const s2v_conv_params *p) {
-    return p->prec != S2V_PREC_F32 && !(use_direct(p) && !p->force_tile) && !is_smallk(p);
+    return p->prec != S2V_PREC_F32 && !(use_direct(p) && !p->force_tile) && !is_smallk(p) && !k4_ok(p);
 }
 static bool uses_x3(const s2v_conv_params *p) { return tiled_x3(p) && !p->b_kn; }
 
@@ -1203,6 +1221,12 @@ static Plan make_plan(const s2v_conv_params *p_in, int M, int K) {
         pl.splits = 1;
         pl.tps = pl.ktiles;
         if (halo_ks(p)) pl.splits = halo_splits(p, pl.tps);   // tps: channels per split
+        return pl;
+    }
+    if (k4_ok(p)) {                                   // conv_k4_mfma (fp32 MFMA, no split-K)
+        pl.tile = -4;
+        pl.splits = 1;
+        pl.tps = pl.ktiles;
         return pl;
     }
     int tppx, qpt;
@@ -1684,7 +1708,7 @@ extern "C" size_t s2v_conv2d_ws_bytes(const s2v_conv_params *p) {
     int M, K;
     if (validate(p, M, K) != 0) return 0;
     Plan pl = make_plan(p, M, K);
-    if (pl.splits <= 1 || pl.tile == -2) return 0;
+    if (pl.splits <= 1 || pl.tile == -2 || pl.tile == -4) return 0;
     const int batch = p->batch > 0 ? p->batch : 1;
     return (size_t)batch * pl.splits * (size_t)M * p->cout * sizeof(float);
 }
@@ -1699,6 +1723,11 @@ extern "C" int s2v_conv2d_plan(const s2v_conv_params *p, int *out6) {
         const GldsCfg &c = kGlds[pl.tile];
         out6[0] = c.bm; out6[1] = c.bn; out6[2] = c.wm; out6[3] = 5; out6[4] = 0; out6[5] = pl.splits;
         out6[6] = p->prec; out6[7] = 8; out6[8] = c.nst; out6[9] = 0;
+        return 0;
+    }
+    if (pl.tile == -4) {                                // conv_k4_mfma<KT> (reported as 4000 + KT)
+        out6[0] = 0; out6[1] = p->cout; out6[2] = 0; out6[3] = 0;
+        out6[4] = 4000 + p->kh * p->kw; out6[5] = 1;
         return 0;
     }
     if (pl.tile == -2) {
@@ -1753,6 +1782,11 @@ extern "C" int s2v_conv2d(const s2v_conv_params *p, s2v_stream_t stream) {
     const int batch = p->batch > 0 ? p->batch : 1;
     Plan pl = make_plan(p, M, K);
     ConvArgs a = make_args(p, M, K, pl);
+    if (pl.tile == -4) {
+        rc = launch_conv_k4(a, batch, p->kh * p->kw, s);
+        if (rc) return rc;
+        return check_launch("conv_k4");
+    }
     if (pl.tile == -2) {
         int tppx, qpt;
         smallk_cfg(p, M, K, tppx, qpt);

@@ -200,6 +200,8 @@ class ENetEngine:
                 off = self.mod_offs[3 * st + li]
                 r0, wd = dtab.r0[idx], dtab.width[idx]
                 sv = s2[:, off: off + L.cin]
+                if L.cin <= 4:
+                    continue      # the 4-channel first StyleConv runs exact fp32 (conv_k4.hip): modulated in-launch
                 if POLY_UP and L.conv4 is not None:
                     d4 = dall[:, r0: r0 + wd]
                     wb[idx] = {"conv4": ops.modulate_weights(ctx, L.conv4, sv, d4, b),

@@ -381,7 +381,7 @@ def test_modulated_conv_per_sample_weights(ctx, prec, n, cin, h, w, cout, k, mod
     # the modulation run ahead (ops.modulate_weights, engine/enet.py PREMOD) and read by the conv: bit-identical,
     # with and without the demodulation; a pre-modulated layout the conv does not read is refused.  (Cout <= 4
     # layers run the fp32 direct kernels, whose layout modulate_weights writes in f32 mode only.)
-    for dd in ((d, None) if cout > 4 else ()):
+    for dd in ((d, None) if cout > 4 and cin > 4 else ()):     # (4-channel layers: exact fp32, conv_k4.hip)
         dv = None if dd is None else dd.float().to(DEV)
         kw = dict(act=ops.ACT_LRELU, alpha=0.2, pix_add=noise.float().to(DEV).contiguous(), pix_w=0.3)
         y1 = NHWC.empty(n, oh, ow, cout, DEV)
