@@ -70,9 +70,11 @@ NOISE_DESC = (f"on: NoiseInjection weight {NOISE_W} on all four StyleConvs, fres
 
 
 ARITH = {"f16x3": "f16x3: fp32 tensors, conv products as split-fp32 hi*hi+hi*lo+lo*hi on f16 MFMA "
-                   "(22 significant bits per operand, <= 3*2^-22 per product), fp32 accumulate; all other ops fp32",
+                   "(22 significant bits per operand, <= 3*2^-22 per product), fp32 accumulate; 4-channel-input convs and "
+                   "Cout <= 4 VALU heads in exact fp32; all other ops fp32",
          "bf16x3": "bf16x3: fp32 tensors, conv products as split-fp32 hi*hi+hi*lo+lo*hi on bf16 MFMA "
-                    "(16 significant bits per operand), fp32 accumulate; all other ops fp32",
+                    "(16 significant bits per operand), fp32 accumulate; 4-channel-input convs and Cout <= 4 VALU heads in "
+                    "exact fp32; all other ops fp32",
          "f32": "f32: exact fp32 MFMA (v_mfma_f32_32x32x2_f32) convs; all other ops fp32"}
 
 
