@@ -923,7 +923,7 @@ def plan_symbol(plan) -> str:
                 return f"void s2v::conv_smallk4<{-wm}, {bkn - 2000}>(s2v::ConvArgs, int, int, int, int)"
             return f"void s2v::conv_smallk<{-wm}, {avec}>(s2v::ConvArgs, int, int, int, int)"
         if bkn >= 4000:
-            return f"void s2v::conv_k4_mfma<{bkn - 4000}>(s2v::ConvArgs, int)"
+            return f"void s2v::conv_k4_mfma<{bkn - 4000}, false>(s2v::ConvArgs, int)"
         if bkn >= 3000:
             return f"void s2v::conv_head_x3<{x3 - 1}, {bn}, {bkn - 3000}, {wm}>(s2v::ConvArgs, int, int)"
         if bkn >= 1000:
