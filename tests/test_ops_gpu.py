@@ -1157,3 +1157,35 @@ def test_conv2d_post_and_dup_epilogue(ctx, prec, tile, splits, nc):
     assert (err <= REL[prec] * (bound + 1) + 1e-6).all(), f"main: max err {err.max():.3e}"
     dref = F.leaky_relu(0.7 * ds + db[None, :, None, None], 0.2)
     assert (got[:, cout:] - dref).abs().max() < 1e-6
+
+
+@pytest.mark.parametrize("n,h,w,cout,k,noise", [(3, 7, 9, 32, 3, False), (2, 16, 16, 96, 3, True),
+                                                 (2, 20, 24, 256, 3, True), (3, 11, 13, 64, 1, False),
+                                                 (1, 33, 40, 256, 1, True)])
+def test_conv_k4_exact_fp32(ctx, prec, n, h, w, cout, k, noise):
+    """4-channel "same" convs run on conv_k4_mfma (csrc/conv_k4.hip) in every precision mode, in exact fp32 (MFMA
+    v_mfma_f32_32x32x2f32): against fp64 at the fp32 bound, including partial last tiles (h*w not a multiple of 32),
+    Cout of one / three / eight 32-channel blocks, bias + noise + LeakyReLU in the epilogue, and the plan names the
+    kernel."""
+    wt = rnd(cout, 4, k, k, seed=81) / math.sqrt(4 * k * k)
+    bias = rnd(cout, seed=82)
+    x = rnd(n, 4, h, w, seed=83)
+    nz = rnd(n, h, w, seed=84)
+    cw = ConvW(wt.float(), bias.float(), DEV, padding=k // 2)
+    seen = {}
+
+    def hook(c_, p, flops, launch):
+        seen["plan"] = p.plan
+        launch()
+    ops.CONV_HOOK = hook
+    try:
+        y = NHWC.empty(n, h, w, cout + 8, DEV).slice(4, cout)
+        kw = dict(pix_add=nz.float().to(DEV).contiguous(), pix_w=0.3) if noise else {}
+        ops.conv2d(ctx, nhwc(x.float()), cw, y, act=ops.ACT_LRELU, alpha=0.2, **kw)
+    finally:
+        ops.CONV_HOOK = None
+    assert ops.plan_symbol(seen["plan"]).startswith("void s2v::conv_k4_mfma<"), ops.plan_symbol(seen["plan"])
+    ref = F.conv2d(x, wt, bias, padding=k // 2) + (0.3 * nz[:, None] if noise else 0)
+    ref = F.leaky_relu(ref, 0.2)
+    err = (to_nchw(y) - ref).abs()
+    assert (err <= REL["f32"] * (conv_bound(x, wt, 1, k // 2, 1) + 1) + 1e-6).all(), f"max err {err.max():.3e}"
