@@ -28,8 +28,12 @@ __global__ __launch_bounds__(256) void conv_k4_mfma(ConvArgs a, int chunks) {
     const int g = blockIdx.x / chunks, chunk = blockIdx.x - (blockIdx.x / chunks) * chunks;   // image, pixel chunk
     const int bidx = g / a.n, img = g - (g / a.n) * a.n;
     const int hw = a.oh * a.ow;
-    const int n0 = wave * 64;                         // this wave's 64 output channels: blocks n0 .. n0 + 31, + 32 ..
-    if (n0 >= a.cout) return;                         // (no barriers below)
+    // waves over channels (64 each) x waves over the block's tiles: a narrow layer (Cout <= 64: GFPGAN's / GPEN's
+    // 1x1 RGB input convs) gives all four waves their own tiles instead of leaving three idle
+    const int WN = (a.cout + 63) / 64, WM = 4 / WN;
+    const int wn = wave % WN, wm = wave / WN;
+    if (wm >= WM) return;                             // (no barriers below)
+    const int n0 = wn * 64;                           // this wave's 64 output channels: blocks n0 .. n0 + 31, + 32 ..
     // filter fragments: B[k][n] = W[n][k] for k = 2 s + lh, the wave's two 32-column blocks
     const float *__restrict__ w = a.wt + (long long)bidx * a.w_bs;
     float b[KS][2];
@@ -66,16 +70,16 @@ __global__ __launch_bounds__(256) void conv_k4_mfma(ConvArgs a, int chunks) {
         }
     };
     f4 vn[KT];
-    if (PF) load_a(chunk * kK4Tiles * 32, vn);
+    if (PF) load_a((chunk * kK4Tiles + wm) * 32, vn);
 #pragma unroll 1
-    for (int t = 0; t < kK4Tiles; ++t) {
+    for (int t = wm; t < kK4Tiles; t += WM) {
         const int p0 = (chunk * kK4Tiles + t) * 32;
         if (p0 >= hw) break;
         f4 vc[KT];
         if (PF) {
 #pragma unroll
             for (int tap = 0; tap < KT; ++tap) vc[tap] = vn[tap];
-            if (t + 1 < kK4Tiles && p0 + 32 < hw) load_a(p0 + 32, vn);
+            if (t + WM < kK4Tiles && p0 + 32 * WM < hw) load_a(p0 + 32 * WM, vn);
         } else {
             load_a(p0, vc);
         }
