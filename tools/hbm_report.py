@@ -53,6 +53,11 @@ _LNET = [
      "LNet 7x7 64->3 sigmoid head (LNet.py:77): in 16x96^2x64, out 16x96^2x3"),
 ]
 _ENET = [
+    ("conv_k4_mfma<1,", _b(16 * 256 * 256 * 4 * F, 16 * 256 * 256 * 256 * F),
+     "ENet conv_body_first 1x1 4->256 (ENet.py:94), exact fp32 MFMA: in 16x256^2x4, out 16x256^2x256"),
+    ("conv_k4_mfma<9,", _b(16 * 200 * 200 * 4 * F, 16 * 200 * 200 * F, 16 * 200 * 200 * 256 * F),
+     "ENet first StyleConv 3x3 4->256 at 200^2 (ENet.py:122), exact fp32 MFMA: in 16x200^2x4, noise 16x200^2, "
+     "out 16x200^2x256"),
     ("torgb_up2_kernel<8, 4>", _b(16 * 400 * 400 * 128 * F, 16 * 200 * 200 * 4 * F, 16 * 400 * 400 * 4 * F),
      "ENet 400^2 ToRGB + x2 skip (base_blocks.py:540-554): x 16x400^2x128, skip 16x200^2x4, out 16x400^2x4"),
     ("torgb_up2_kernel<8, 2>", _b(16 * 200 * 200 * 256 * F, 16 * 100 * 100 * 4 * F, 16 * 200 * 200 * 4 * F),
